@@ -1,0 +1,250 @@
+// Multi-resolution hash-grid encoding (Instant-NGP style) for gfx950.
+//
+// Semantics follow the reference's torch path (the tcnn path is not pinnable here):
+//   FeatureGrid.forward                 /root/reference/src/field_components/feature_structures.py:78-83
+//     x_hat = (x + r) / (2 r), features *= coarse-to-fine mask (levels >= active zeroed, :85-88)
+//   HashEncoding.hash_fn / pytorch_fwd   /root/reference/src/field_components/encodings.py:244-304
+//     scaled = x_hat * floor(min_res * g^l); corners from ceil/floor; ceil corner weight = frac;
+//     index = (c0 * 1 ^ c1 * 2654435761 ^ c2 * 805459861) mod 2^log2T + l * 2^log2T;
+//     lerp x, then y, then z; output level-major [l0f0, l0f1, l1f0, ...].
+//
+// Layout: table [L * T, 2] f32 (one float2 per entry), positions [M, ldx] f32 (first 3 columns),
+// output [M, ldo] f32 written at columns 0 .. 2L-1 (ldo lets the caller write straight into the
+// MLP input panel).  One thread per (point, level); 16 consecutive lanes cover one point's levels
+// so each wave writes 4 contiguous 128-byte output rows.
+#include "common.h"
+
+// Bit-exact corner selection needs the rounded product x_hat * s before floor/frac (a fused
+// multiply-subtract would change the fractional weights), so contraction is off in this file; the
+// kernels are gather-bound, the extra VALU is free.
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kMaxLevels = 16;
+constexpr uint32_t kP1 = 2654435761u;
+constexpr uint32_t kP2 = 805459861u;
+
+struct GridParams {
+  float scale[kMaxLevels];
+  int levels;         // L
+  int active_levels;  // coarse-to-fine: levels >= active contribute 0
+  int log2T;
+  float inv_2r;       // 1 / (2 r)
+  float radius;       // r
+};
+
+__device__ __forceinline__ uint32_t hash3(int cx, int cy, int cz, uint32_t mask) {
+  return (((uint32_t)cx) ^ ((uint32_t)cy * kP1) ^ ((uint32_t)cz * kP2)) & mask;
+}
+
+struct Corners {
+  uint32_t idx[8];  // reference order f_0..f_7
+  float ox, oy, oz;
+};
+
+// Corner order (encodings.py:274-281): 0:(c,c,c) 1:(c,f,c) 2:(f,f,c) 3:(f,c,c)
+//                                      4:(c,c,f) 5:(c,f,f) 6:(f,f,f) 7:(f,c,f)
+__device__ __forceinline__ Corners make_corners(float x, float y, float z, float radius, float inv_2r,
+                                                float s, int level, int log2T) {
+  Corners c;
+  // (x + r) / (2r): reference computes a true division by (2r); for r in {1, 2} the reciprocal
+  // multiply is exact, but keep the division for bit-exact corner indices in general.
+  const float two_r = 2.0f * radius;
+  const float hx = (x + radius) / two_r;
+  const float hy = (y + radius) / two_r;
+  const float hz = (z + radius) / two_r;
+  (void)inv_2r;
+  const float sx = hx * s, sy = hy * s, sz = hz * s;
+  const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+  const int cxc = (int)ceilf(sx), cyc = (int)ceilf(sy), czc = (int)ceilf(sz);
+  const int cxf = (int)fx, cyf = (int)fy, czf = (int)fz;
+  c.ox = sx - fx;
+  c.oy = sy - fy;
+  c.oz = sz - fz;
+  const uint32_t mask = (1u << log2T) - 1u;
+  const uint32_t base = (uint32_t)level << log2T;
+  c.idx[0] = base + hash3(cxc, cyc, czc, mask);
+  c.idx[1] = base + hash3(cxc, cyf, czc, mask);
+  c.idx[2] = base + hash3(cxf, cyf, czc, mask);
+  c.idx[3] = base + hash3(cxf, cyc, czc, mask);
+  c.idx[4] = base + hash3(cxc, cyc, czf, mask);
+  c.idx[5] = base + hash3(cxc, cyf, czf, mask);
+  c.idx[6] = base + hash3(cxf, cyf, czf, mask);
+  c.idx[7] = base + hash3(cxf, cyc, czf, mask);
+  return c;
+}
+
+__global__ __launch_bounds__(256) void hashgrid_fwd_kernel(const float* __restrict__ pos, int64_t M,
+                                                           int64_t ldx, const float2* __restrict__ table,
+                                                           GridParams p, float* __restrict__ out,
+                                                           int64_t ldo) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t pt = tid >> 4;
+  const int level = (int)(tid & 15);
+  if (pt >= M || level >= p.levels) return;
+  float2 r = make_float2(0.f, 0.f);
+  if (level < p.active_levels) {
+    const float* xp = pos + pt * ldx;
+    Corners c = make_corners(xp[0], xp[1], xp[2], p.radius, p.inv_2r, p.scale[level], level, p.log2T);
+    float2 f[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = table[c.idx[i]];
+    const float ox = c.ox, oy = c.oy, oz = c.oz;
+    const float nx = 1.0f - ox, ny = 1.0f - oy, nz = 1.0f - oz;
+    float2 f03, f12, f56, f47, f0312, f4756;
+    f03.x = f[0].x * ox + f[3].x * nx;  f03.y = f[0].y * ox + f[3].y * nx;
+    f12.x = f[1].x * ox + f[2].x * nx;  f12.y = f[1].y * ox + f[2].y * nx;
+    f56.x = f[5].x * ox + f[6].x * nx;  f56.y = f[5].y * ox + f[6].y * nx;
+    f47.x = f[4].x * ox + f[7].x * nx;  f47.y = f[4].y * ox + f[7].y * nx;
+    f0312.x = f03.x * oy + f12.x * ny;  f0312.y = f03.y * oy + f12.y * ny;
+    f4756.x = f47.x * oy + f56.x * ny;  f4756.y = f47.y * oy + f56.y * ny;
+    r.x = f0312.x * oz + f4756.x * nz;
+    r.y = f0312.y * oz + f4756.y * nz;
+  }
+  *reinterpret_cast<float2*>(out + pt * ldo + 2 * level) = r;
+}
+
+// Backward: dtable (atomic accumulate) and optional dx (accumulate into dpos[:, 0:3]).
+__global__ __launch_bounds__(256) void hashgrid_bwd_kernel(const float* __restrict__ pos, int64_t M,
+                                                           int64_t ldx, const float2* __restrict__ table,
+                                                           GridParams p, const float* __restrict__ dout,
+                                                           int64_t ldd, float* __restrict__ dtable,
+                                                           float* __restrict__ dpos, int64_t lddx) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t pt = tid >> 4;
+  const int level = (int)(tid & 15);
+  const bool live = pt < M && level < p.levels && level < p.active_levels;
+  float gx = 0.f, gy = 0.f, gz = 0.f;
+  if (live) {
+    const float* xp = pos + pt * ldx;
+    Corners c = make_corners(xp[0], xp[1], xp[2], p.radius, p.inv_2r, p.scale[level], level, p.log2T);
+    const float2 dE = *reinterpret_cast<const float2*>(dout + pt * ldd + 2 * level);
+    const float ox = c.ox, oy = c.oy, oz = c.oz;
+    const float nx = 1.0f - ox, ny = 1.0f - oy, nz = 1.0f - oz;
+    // autograd order of encodings.py:292-302 reversed
+    float2 d0312 = make_float2(dE.x * oz, dE.y * oz);
+    float2 d4756 = make_float2(dE.x * nz, dE.y * nz);
+    float2 d03 = make_float2(d0312.x * oy, d0312.y * oy);
+    float2 d12 = make_float2(d0312.x * ny, d0312.y * ny);
+    float2 d47 = make_float2(d4756.x * oy, d4756.y * oy);
+    float2 d56 = make_float2(d4756.x * ny, d4756.y * ny);
+    float2 df[8];
+    df[0] = make_float2(d03.x * ox, d03.y * ox);
+    df[3] = make_float2(d03.x * nx, d03.y * nx);
+    df[1] = make_float2(d12.x * ox, d12.y * ox);
+    df[2] = make_float2(d12.x * nx, d12.y * nx);
+    df[5] = make_float2(d56.x * ox, d56.y * ox);
+    df[6] = make_float2(d56.x * nx, d56.y * nx);
+    df[4] = make_float2(d47.x * ox, d47.y * ox);
+    df[7] = make_float2(d47.x * nx, d47.y * nx);
+    if (dtable != nullptr) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        // merge duplicate corners inside the thread (integer coordinates => ceil == floor)
+        bool dup = false;
+        float2 acc = df[i];
+#pragma unroll
+        for (int j = 0; j < i; ++j) dup |= (c.idx[j] == c.idx[i]);
+        if (dup) continue;
+#pragma unroll
+        for (int j = i + 1; j < 8; ++j)
+          if (c.idx[j] == c.idx[i]) { acc.x += df[j].x; acc.y += df[j].y; }
+        float* dst = dtable + 2 * (int64_t)c.idx[i];
+        atomicAdd(dst, acc.x);
+        atomicAdd(dst + 1, acc.y);
+      }
+    }
+    if (dpos != nullptr) {
+      float2 f[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = table[c.idx[i]];
+      float2 f03, f12, f56, f47, f0312, f4756;
+      f03.x = f[0].x * ox + f[3].x * nx;  f03.y = f[0].y * ox + f[3].y * nx;
+      f12.x = f[1].x * ox + f[2].x * nx;  f12.y = f[1].y * ox + f[2].y * nx;
+      f56.x = f[5].x * ox + f[6].x * nx;  f56.y = f[5].y * ox + f[6].y * nx;
+      f47.x = f[4].x * ox + f[7].x * nx;  f47.y = f[4].y * ox + f[7].y * nx;
+      f0312.x = f03.x * oy + f12.x * ny;  f0312.y = f03.y * oy + f12.y * ny;
+      f4756.x = f47.x * oy + f56.x * ny;  f4756.y = f47.y * oy + f56.y * ny;
+      const float doz = dE.x * (f0312.x - f4756.x) + dE.y * (f0312.y - f4756.y);
+      const float doy = d0312.x * (f03.x - f12.x) + d0312.y * (f03.y - f12.y) +
+                        d4756.x * (f47.x - f56.x) + d4756.y * (f47.y - f56.y);
+      const float dox = d03.x * (f[0].x - f[3].x) + d03.y * (f[0].y - f[3].y) +
+                        d12.x * (f[1].x - f[2].x) + d12.y * (f[1].y - f[2].y) +
+                        d56.x * (f[5].x - f[6].x) + d56.y * (f[5].y - f[6].y) +
+                        d47.x * (f[4].x - f[7].x) + d47.y * (f[4].y - f[7].y);
+      const float s = p.scale[level];
+      gx = dox * s; gy = doy * s; gz = doz * s;
+    }
+  }
+  if (dpos != nullptr) {
+    // reduce over the 16 levels of a point (16 consecutive lanes)
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) {
+      gx += __shfl_xor(gx, off, 16);
+      gy += __shfl_xor(gy, off, 16);
+      gz += __shfl_xor(gz, off, 16);
+    }
+    if (level == 0 && pt < M) {
+      float* dp = dpos + pt * lddx;
+      const float two_r = 2.0f * p.radius;
+      dp[0] += gx / two_r;
+      dp[1] += gy / two_r;
+      dp[2] += gz / two_r;
+    }
+  }
+}
+
+int fill_params(const char* fn, GridParams& p, int L, int log2T, const float* scales, float radius,
+                int active_levels) {
+  if (L < 1 || L > kMaxLevels) return mms::set_error(fn, "num_levels must be in [1, 16]");
+  if (log2T < 1 || log2T > 24) return mms::set_error(fn, "log2_hashmap_size must be in [1, 24]");
+  if (!(radius > 0.f)) return mms::set_error(fn, "radius must be > 0");
+  p.levels = L;
+  p.active_levels = active_levels < 0 ? L : (active_levels > L ? L : active_levels);
+  p.log2T = log2T;
+  p.radius = radius;
+  p.inv_2r = 1.0f / (2.0f * radius);
+  for (int i = 0; i < kMaxLevels; ++i) p.scale[i] = i < L ? scales[i] : 0.f;
+  return 0;
+}
+
+}  // namespace
+
+MMS_EXPORT int mms_hashgrid_fwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L,
+                                int log2T, int F, const float* scales, float radius, int active_levels,
+                                float* out, int64_t ldo, void* stream) {
+  const char* fn = "mms_hashgrid_fwd";
+  MMS_REQUIRE(F == 2, fn, "features_per_level must be 2");
+  MMS_REQUIRE(M >= 0 && ldx >= 3 && ldo >= 2 * L, fn, "bad shapes");
+  GridParams p;
+  int rc = fill_params(fn, p, L, log2T, scales, radius, active_levels);
+  if (rc) return rc;
+  if (M == 0) return 0;
+  MMS_REQUIRE(pos && table && out, fn, "null pointer");
+  const int64_t threads = M * 16;
+  hipLaunchKernelGGL(hashgrid_fwd_kernel, dim3(mms::grid_for(threads, 256, INT32_MAX)), dim3(256), 0,
+                     mms::as_stream(stream), pos, M, ldx, reinterpret_cast<const float2*>(table), p, out,
+                     ldo);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_hashgrid_bwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L,
+                                int log2T, int F, const float* scales, float radius, int active_levels,
+                                const float* dout, int64_t ldd, float* dtable, float* dpos, int64_t lddx,
+                                void* stream) {
+  const char* fn = "mms_hashgrid_bwd";
+  MMS_REQUIRE(F == 2, fn, "features_per_level must be 2");
+  MMS_REQUIRE(M >= 0 && ldx >= 3 && ldd >= 2 * L, fn, "bad shapes");
+  MMS_REQUIRE(dpos == nullptr || lddx >= 3, fn, "bad dpos stride");
+  GridParams p;
+  int rc = fill_params(fn, p, L, log2T, scales, radius, active_levels);
+  if (rc) return rc;
+  if (M == 0 || (dtable == nullptr && dpos == nullptr)) return 0;
+  MMS_REQUIRE(pos && table && dout, fn, "null pointer");
+  const int64_t threads = M * 16;
+  hipLaunchKernelGGL(hashgrid_bwd_kernel, dim3(mms::grid_for(threads, 256, INT32_MAX)), dim3(256), 0,
+                     mms::as_stream(stream), pos, M, ldx, reinterpret_cast<const float2*>(table), p, dout,
+                     ldd, dtable, dpos, lddx);
+  return mms::check_launch(fn);
+}

@@ -1,0 +1,97 @@
+"""torch.autograd bridges onto the C-ABI HIP kernels (libmms_hip.so).
+
+Tensors are PyTorch-owned device memory; kernels receive raw pointers and the current HIP stream.
+Every function here requires CUDA(HIP) tensors and raises otherwise: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+ACT_IDS = {None: 0, "None": 0, "Identity": 0, "ReLU": 1, "Softplus": 2, "Sigmoid": 3}
+NT, NN, TN = 0, 1, 2
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _check_dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("MMS HIP ops require device (cuda/hip) tensors; no CPU fallback exists")
+
+
+# ----------------------------------------------------------------------------------------------
+# hash grid
+# ----------------------------------------------------------------------------------------------
+def _f32_array(vals):
+    arr = (ctypes.c_float * len(vals))(*[float(v) for v in vals])
+    return arr
+
+
+def hashgrid_forward(pos: torch.Tensor, table: torch.Tensor, scales, log2T: int, radius: float,
+                     active_levels: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Raw forward launch; pos [M, >=3] (row stride pos.stride(0)), out [M, >=2L]."""
+    _check_dev(pos, table)
+    L = len(scales)
+    M = pos.shape[0]
+    if out is None:
+        out = torch.empty(M, 2 * L, device=pos.device, dtype=torch.float32)
+    assert pos.stride(1) == 1 and out.stride(1) == 1 and table.is_contiguous()
+    sc = _f32_array(scales)
+    _lib.call("mms_hashgrid_fwd", pos.data_ptr(), M, pos.stride(0), table.data_ptr(), L, log2T, table.shape[1],
+              ctypes.cast(sc, ctypes.c_void_p), float(radius), int(active_levels), out.data_ptr(), out.stride(0),
+              _stream())
+    return out
+
+
+def hashgrid_backward(pos, table, scales, log2T, radius, active_levels, dout, dtable=None, dpos=None):
+    _check_dev(pos, table, dout)
+    L = len(scales)
+    sc = _f32_array(scales)
+    assert dout.stride(1) == 1
+    _lib.call("mms_hashgrid_bwd", pos.data_ptr(), pos.shape[0], pos.stride(0), table.data_ptr(), L, log2T,
+              table.shape[1], ctypes.cast(sc, ctypes.c_void_p), float(radius), int(active_levels),
+              dout.data_ptr(), dout.stride(0), _ptr(dtable), _ptr(dpos), 0 if dpos is None else dpos.stride(0),
+              _stream())
+
+
+class HashGridFunction(torch.autograd.Function):
+    """FeatureGrid(HashEncoding) forward/backward on the HIP kernels."""
+
+    @staticmethod
+    def forward(ctx, pos, table, scales, log2T, radius, active_levels):
+        pos_c = pos.contiguous()
+        out = hashgrid_forward(pos_c, table, scales, log2T, radius, active_levels)
+        ctx.save_for_backward(pos_c, table)
+        ctx.cfg = (scales, log2T, radius, active_levels)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        pos, table = ctx.saved_tensors
+        scales, log2T, radius, active_levels = ctx.cfg
+        dtable = torch.zeros_like(table) if ctx.needs_input_grad[1] else None
+        dpos = torch.zeros_like(pos) if ctx.needs_input_grad[0] else None
+        hashgrid_backward(pos, table, scales, log2T, radius, active_levels, dout.contiguous(), dtable, dpos)
+        return dpos, dtable, None, None, None, None
+
+
+# ----------------------------------------------------------------------------------------------
+# GEMM
+# ----------------------------------------------------------------------------------------------
+def gemm(mode: int, M: int, N: int, K: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int,
+         C: torch.Tensor, ldc: int, bias=None, Z=None, ldz=0, aux=None, ldaux=0, act=0, dact=0,
+         beta=1.0, thr=20.0, accumulate=False, splits=1):
+    _lib.call("mms_gemm_f32", int(mode), int(M), int(N), int(K), A.data_ptr(), int(lda), B.data_ptr(), int(ldb),
+              C.data_ptr(), int(ldc), _ptr(bias), _ptr(Z), int(ldz), _ptr(aux), int(ldaux), int(act), int(dact),
+              float(beta), float(thr), int(bool(accumulate)), int(splits), _stream())

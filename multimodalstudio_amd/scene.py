@@ -1,0 +1,108 @@
+"""Synthetic MMS-DATA-shaped scene — cameras, intrinsics, mosaick patterns, frames.
+
+The reference loads meta_data.json + per-modality frames (src/data/datasets.py:485-529) written by
+src/preprocessing/utils.py:437-571.  No real scene exists offline, so this module builds one with the
+same schema-level properties:
+  * views on a radius-3 sphere looking at the origin, small per-modality rig offsets;
+  * W x H = 640 x 512 for every modality, pixel_offset 0.0 (preprocessing/utils.py:473);
+  * distortion stored in READER order [k1, k2, k3, k4, p1, p2] (cameras/camera_utils.py:302-307);
+  * raw mosaick patterns per modality (preprocess_mmsdata.py:43-47): rgb Bayer 2x2 (3 bands),
+    polarization 2x2 (4), multispectral 3x3 (9), mono / infrared 1x1;
+  * frames rendered analytically from an SDF scene (sphere r=0.5 + torus), values in [0, 1].
+Everything is deterministic from ``seed``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+CHANNELS = {"rgb": 3, "infrared": 1, "mono": 1, "polarization": 4, "multispectral": 9}
+MOSAICK = {
+    "rgb": [[0, 1], [1, 2]],
+    "infrared": [[0]],
+    "mono": [[0]],
+    "polarization": [[0, 1], [3, 2]],
+    "multispectral": [[0, 1, 2], [3, 4, 5], [6, 7, 8]],
+}
+EVAL_VIEWS = [9, 19, 29, 39, 49]
+
+
+@dataclass
+class ModalityCameras:
+    c2w: torch.Tensor          # [C, 3, 4]
+    fx: torch.Tensor           # [C]
+    fy: torch.Tensor
+    cx: torch.Tensor
+    cy: torch.Tensor
+    distortion: torch.Tensor   # [C, 6] reader order
+    width: int
+    height: int
+    view_ids: List[int]        # frame index of each camera (train split)
+
+
+def look_at(cam_pos: np.ndarray) -> np.ndarray:
+    """OpenGL-style c2w (camera looks down -z, +y up) towards the origin."""
+    fwd = -cam_pos / np.linalg.norm(cam_pos)
+    z = -fwd
+    world_up = np.array([0.0, 0.0, 1.0])
+    x = np.cross(world_up, z)
+    if np.linalg.norm(x) < 1e-6:
+        x = np.array([1.0, 0.0, 0.0])
+    x /= np.linalg.norm(x)
+    y = np.cross(z, x)
+    return np.stack([x, y, z, cam_pos], axis=1)
+
+
+def make_cameras(modalities: List[str], n_views: int = 50, width: int = 640, height: int = 512,
+                 seed: int = 0, train: bool = True) -> Dict[str, ModalityCameras]:
+    rng = np.random.default_rng(seed)
+    views = [v for v in range(n_views) if (v not in EVAL_VIEWS) == train]
+    golden = np.pi * (3.0 - np.sqrt(5.0))
+    out = {}
+    for mi, mod in enumerate(modalities):
+        rig = rng.normal(scale=0.02, size=3)
+        c2ws = []
+        for v in views:
+            zc = 0.15 + 0.7 * (v + 0.5) / n_views          # upper hemisphere band
+            rr = np.sqrt(1 - zc * zc)
+            th = golden * v
+            pos = 3.0 * np.array([rr * np.cos(th), rr * np.sin(th), zc]) + rig
+            c2ws.append(look_at(pos))
+        C = len(views)
+        f = 600.0 + 10.0 * mi
+        dist = np.array([0.01, -0.005, 0.001, 0.0, 0.0005, -0.0003], dtype=np.float64)
+        out[mod] = ModalityCameras(
+            c2w=torch.tensor(np.stack(c2ws), dtype=torch.float32),
+            fx=torch.full((C,), f), fy=torch.full((C,), f),
+            cx=torch.full((C,), width / 2.0), cy=torch.full((C,), height / 2.0),
+            distortion=torch.tensor(np.tile(dist, (C, 1)), dtype=torch.float32),
+            width=width, height=height, view_ids=views)
+    return out
+
+
+def mosaick_mask(mod: str, width: int, height: int) -> torch.Tensor:
+    """RawDataset.build_mosaick_mask (datasets.py:229-254): tiled pattern cropped to H x W, int8."""
+    pat = torch.tensor(MOSAICK[mod])
+    nh, nw = -(-height // pat.shape[0]), -(-width // pat.shape[1])
+    return pat.repeat((nh, nw))[:height, :width].to(torch.int8)
+
+
+def analytic_radiance(origins: np.ndarray, dirs: np.ndarray, channels: int) -> np.ndarray:
+    """Shade rays against a sphere (r = 0.5): hit -> normal-based colour, miss -> direction gradient."""
+    b = np.sum(origins * dirs, -1)
+    c = np.sum(origins * origins, -1) - 0.25
+    disc = b * b - c
+    hit = disc > 0
+    t = -b - np.sqrt(np.maximum(disc, 0))
+    p = origins + dirs * t[..., None]
+    n = p / 0.5
+    base = 0.5 + 0.5 * np.stack([n[..., 0], n[..., 1], n[..., 2]], -1)
+    bgc = 0.5 + 0.4 * np.stack([dirs[..., 2], dirs[..., 0], dirs[..., 1]], -1)
+    col3 = np.where(hit[..., None], base, bgc)
+    k = np.arange(channels)
+    w = 0.6 + 0.4 * np.cos(k * 0.7)
+    out = (col3[..., k % 3] * w)
+    return np.clip(out, 0.0, 1.0).astype(np.float32)

@@ -1,0 +1,333 @@
+"""Generate the golden fixtures in tests/golden/*.npz by RUNNING THE REFERENCE (this container only).
+
+    python tests/golden/make_golden.py
+
+The reference (/root/reference/src, pure PyTorch) is imported through tests/golden/refimport.py
+(stubs for absent third-party packages + the two SURVEY §8(c) patches).  Fixtures hold inputs,
+the reference's outputs and gradients, and every random draw the reference made (captured by
+wrapping torch.rand), so the oracle and the HIP path can replay the identical streams.
+Nothing here runs on the GPU box; only the .npz data travels.
+"""
+from __future__ import annotations
+
+import os
+import sys
+from contextlib import contextmanager
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+
+import refimport  # noqa: E402
+
+refimport.patch_sh_and_hash()
+
+from multimodalstudio_amd import scene as mscene  # noqa: E402
+
+OUT = HERE
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name + ".npz")
+    clean = {}
+    for k, v in arrays.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().cpu().numpy()
+        clean[k] = np.asarray(v)
+    np.savez_compressed(path, **clean)
+    print(f"wrote {path} ({os.path.getsize(path) / 1024:.1f} KiB)")
+
+
+@contextmanager
+def record_rand():
+    """Capture every torch.rand draw (shape + values) made by the reference."""
+    draws = []
+    orig = torch.rand
+
+    def rand(*args, **kwargs):
+        t = orig(*args, **kwargs)
+        draws.append(t.detach().clone())
+        return t
+
+    torch.rand = rand
+    try:
+        yield draws
+    finally:
+        torch.rand = orig
+
+
+# ------------------------------------------------------------------------------------------------
+def gen_hashgrid():
+    from field_components.encodings import HashEncodingConfig
+    from field_components.feature_structures import FeatureGridConfig
+
+    torch.manual_seed(0)
+    for log2T, active, radius, stored in [(12, 16, 1.0, True), (12, 9, 1.0, True), (13, 16, 2.0, True),
+                                         (19, 16, 1.0, False)]:
+        cfg = FeatureGridConfig(encoding=HashEncodingConfig(max_res=1024, log2_hashmap_size=log2T,
+                                                            interpolation="Linear", implementation="torch"),
+                                radius=radius)
+        grid = cfg.setup(input_dim=3)
+        enc = grid.encoding
+        if stored:
+            with torch.no_grad():
+                enc.hash_table.mul_(100.0)   # features ~0.1 so interpolation errors are visible
+        else:
+            from oracle.hashgrid import deterministic_table
+            with torch.no_grad():
+                enc.hash_table.copy_(deterministic_table(16, log2T) * 100.0)
+        grid.update_mask(active)
+        g = torch.Generator().manual_seed(log2T * 31 + active)
+        M = 1024 if stored else 512
+        x = (torch.rand(M, 3, generator=g) * 2.4 - 1.2) * radius
+        x[:16] = torch.tensor([0.0, 0.5, -0.5]) * radius          # exact lattice points (ceil == floor)
+        x.requires_grad_(True)
+        out = grid(x)
+        dout = torch.randn(out.shape, generator=g)
+        out.backward(dout)
+        arrays = dict(x=x.detach(), out=out.detach(), dout=dout, dx=x.grad, scales=enc.scalings,
+                      log2T=log2T, active=active, radius=radius)
+        if stored:
+            arrays.update(table=enc.hash_table.detach(), dtable=enc.hash_table.grad)
+        else:
+            nz = torch.nonzero(enc.hash_table.grad.abs().sum(-1)).squeeze(-1)
+            arrays.update(dtable_idx=nz, dtable_val=enc.hash_table.grad[nz])
+        save(f"hashgrid_l{log2T}_a{active}_r{int(radius)}", **arrays)
+
+
+def gen_mlp():
+    from field_components.mlp import MLPConfig
+    torch.manual_seed(1)
+    cases = {
+        "geo": (MLPConfig(num_layers=3, hidden_dim=256, activation="Softplus", activation_params={"beta": 100},
+                          out_activation="None", geometric_init=True, weight_norm=True, geometric_init_bias=0.4),
+                71, 257),
+        "rad": (MLPConfig(num_layers=3, hidden_dim=256, out_activation="ReLU", weight_norm=True), 317, 256),
+        "head": (MLPConfig(num_layers=3, hidden_dim=64, out_activation="Sigmoid", weight_norm=True), 256, 3),
+        "skip": (MLPConfig(num_layers=8, hidden_dim=64, activation="Softplus", activation_params={"beta": 100},
+                           out_activation="None", skip_connections=(4,), geometric_init=True, weight_norm=True),
+                 39, 65),
+    }
+    for name, (cfg, din, dout_dim) in cases.items():
+        mlp = cfg.setup(input_dim=din, output_dim=dout_dim)
+        g = torch.Generator().manual_seed(7)
+        x = torch.randn(128, din, generator=g) * 0.5
+        x.requires_grad_(True)
+        y = mlp(x)
+        dy = torch.randn(y.shape, generator=g)
+        y.backward(dy)
+        arrays = {"x": x.detach(), "y": y.detach(), "dy": dy, "dx": x.grad}
+        for k, v in mlp.state_dict().items():
+            arrays["p:" + k] = v
+        for k, p in mlp.named_parameters():
+            arrays["g:" + k] = p.grad
+        save(f"mlp_{name}", **arrays)
+
+
+# ------------------------------------------------------------------------------------------------
+def ref_cameras(cams: mscene.ModalityCameras):
+    from cameras.cameras import Cameras
+    return Cameras(camera_to_worlds=cams.c2w, fx=cams.fx[:, None], fy=cams.fy[:, None], cx=cams.cx[:, None],
+                   cy=cams.cy[:, None], width=cams.width, height=cams.height, distortion_params=cams.distortion)
+
+
+def gen_raygen():
+    from cameras.camera_optimizers import CameraOptimizerConfig
+    from model_components.ray_generators import RayGenerator
+    mods = ["rgb", "polarization"]
+    cams = mscene.make_cameras(mods, n_views=12, width=96, height=80, seed=3)
+    data = {m: {"cameras": ref_cameras(cams[m])} for m in mods}
+    opt = CameraOptimizerConfig(mode="SO3xR3", shared_optimization=True,
+                                modalities_to_optimize={m: True for m in mods}).setup(num_cameras=len(cams["rgb"].view_ids))
+    with torch.no_grad():
+        opt.pose_adjustment["rgb"].copy_(torch.tensor([[0.01, -0.02, 0.015, 0.02, -0.01, 0.005]]))
+        opt.pose_adjustment["polarization"].copy_(torch.tensor([[-0.005, 0.01, 0.0, 0.0, 0.0, 0.0]]))
+    gen = RayGenerator(data, opt, pixel_offset=0.0)
+    g = torch.Generator().manual_seed(5)
+    N = 256
+    coords = {}
+    for m in mods:
+        C = len(cams[m].view_ids)
+        coords[m] = torch.stack([torch.randint(0, C, (N,), generator=g), torch.randint(0, 80, (N,), generator=g),
+                                 torch.randint(0, 96, (N,), generator=g)], -1).to(torch.int32)
+    rb = gen(coords)
+    arrays = {}
+    loss = 0
+    for m in mods:
+        r = rb[m]
+        w = torch.linspace(0.1, 1.0, N)[:, None]
+        loss = loss + (r.origins * w).sum() + (r.directions * w * 2).sum() + (r.up_directions * w).sum() \
+            + r.pixel_area.sum() * 1e3
+        arrays.update({f"{m}:coords": coords[m], f"{m}:origins": r.origins, f"{m}:directions": r.directions,
+                       f"{m}:up": r.up_directions, f"{m}:pixel_area": r.pixel_area,
+                       f"{m}:directions_norm": r.directions_norm, f"{m}:c2w": cams[m].c2w,
+                       f"{m}:fx": cams[m].fx, f"{m}:fy": cams[m].fy, f"{m}:cx": cams[m].cx, f"{m}:cy": cams[m].cy,
+                       f"{m}:distortion": cams[m].distortion,
+                       f"{m}:pose": opt.pose_adjustment[m].detach()})
+    loss.backward()
+    for m in mods:
+        arrays[f"{m}:dpose"] = opt.pose_adjustment[m].grad
+    save("raygen", **arrays)
+
+
+def gen_sampler():
+    """NeuS sampler with an analytic SDF: bit-exact bins / sorted_index fixture."""
+    from cameras.rays import RayBundle
+    from model_components.ray_samplers import NeuSSamplerConfig
+    from model_components.scene_colliders import SphereCollider
+    torch.manual_seed(11)
+    R = 512
+    g = torch.Generator().manual_seed(11)
+    o = torch.nn.functional.normalize(torch.randn(R, 3, generator=g), dim=-1) * 2.5
+    tgt = torch.randn(R, 3, generator=g) * 0.3
+    d = torch.nn.functional.normalize(tgt - o, dim=-1)
+    rb = RayBundle(camera_indices=torch.zeros(R, 1, dtype=torch.long), origins=o, directions=d,
+                   up_directions=torch.zeros(R, 3), pixel_area=torch.ones(R, 1) * 1e-4)
+    rb, mask = SphereCollider(1.0)(rb)
+    hit = rb[mask]
+    sampler = NeuSSamplerConfig(num_samples=32, num_samples_importance=32).setup()
+    sampler.train()
+
+    def sdf_fn(rs):
+        p = rs.frustums.get_start_positions()
+        return (torch.linalg.norm(p, dim=-1, keepdim=True) - 0.5)
+
+    orig_merge = None
+    import model_components.ray_samplers as rsm
+    idx_hist = []
+    orig_merge = rsm.merge_ray_samples
+
+    def merge(*a, **k):
+        rs, si = orig_merge(*a, **k)
+        idx_hist.append(si.clone())
+        return rs, si
+
+    rsm.merge_ray_samples = merge
+    try:
+        with record_rand() as draws:
+            out = sampler({"rgb": hit}, sdf_fn=sdf_fn)["ray_samples_per_modality"]["rgb"]
+    finally:
+        rsm.merge_ray_samples = orig_merge
+    bins = torch.cat([out.spacing_starts[..., 0], out.spacing_ends[..., -1:, 0]], -1)
+    save("neus_sampler", origins=o, directions=d, mask=mask, nears=hit.nears, fars=hit.fars,
+         rand_uniform=draws[0], rand_pdf=torch.stack(draws[1:5]), bins=bins, starts=out.frustums.starts[..., 0],
+         ends=out.frustums.ends[..., 0], **{f"sorted_index{i}": si for i, si in enumerate(idx_hist)})
+
+
+# ------------------------------------------------------------------------------------------------
+def set_callbacks(model, step, max_iters=100000):
+    """Apply the BEFORE_TRAIN_ITERATION callbacks of the reference for ``step``."""
+    import numpy as _np
+    spl = min(int(max_iters * 1.0), int(max_iters / 16))
+    level = min(max(int(step / spl) + 1, 1), 16)
+    model.surface_model.surface_field.field.feature_grid.update_mask(level)
+    model.radiance_model.radiance_field.base_field.feature_grid.update_mask(level)
+    gfac = _np.exp((_np.log(1024) - _np.log(16)) / 15)
+    delta = max(1.0 / 1024, 1.0 / (16 * gfac ** int(step / spl)))
+    model.surface_model.set_numerical_gradients_delta(delta * 2.0)
+    model.surface_model.volume_rendering.set_cos_anneal_ratio(min(1.0, step / int(max_iters * 0.05)))
+    return level, delta * 2.0
+
+
+def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=False):
+    from cameras.camera_optimizers import CameraOptimizerConfig
+    from cameras.pixel_samplers import UniformPixelSamplerConfig
+    from model_components.ray_generators import RayGenerator
+    torch.manual_seed(1234)
+    modalities = {m: mscene.CHANNELS[m] for m in mods}
+    overrides = {"pipeline": {"model": {
+        "surface_model": {"surface_field": {"field": {"feature_grid": {"encoding": {"log2_hashmap_size": log2T}}}}},
+        "radiance_model": {"radiance_field": {"base_field": {"feature_grid": {"encoding": {"log2_hashmap_size": log2T}}}}},
+    }}}
+    cfg, model = refimport.build_model(method, f"/root/reference/confs/{yaml_name}", modalities, overrides)
+    model.train()
+    with torch.no_grad():
+        # widen the tiny init so every stage carries signal
+        for n, p in model.named_parameters():
+            if n.endswith("hash_table"):
+                p.mul_(50.0)
+    level, delta = set_callbacks(model, step)
+    W, H = 96, 80
+    cams = mscene.make_cameras(mods, n_views=12, width=W, height=H, seed=4)
+    data = {m: {"cameras": ref_cameras(cams[m])} for m in mods}
+    opt = CameraOptimizerConfig(mode="SO3xR3", shared_optimization=True,
+                                modalities_to_optimize={m: True for m in mods}).setup(num_cameras=len(cams[mods[0]].view_ids))
+    with torch.no_grad():
+        for i, m in enumerate(mods):
+            opt.pose_adjustment[m].copy_(torch.tensor([[0.004 * (i + 1), -0.003, 0.002, 0.003, -0.002 * (i + 1), 0.001]]))
+    gen = RayGenerator(data, opt, pixel_offset=0.0)
+    # frames + pixel sampler (pixel_samplers.py:71-89)
+    frames = {}
+    for m in mods:
+        C = len(cams[m].view_ids)
+        imgs = torch.rand(C, H, W, 1 if raw else modalities[m], generator=torch.Generator().manual_seed(9))
+        frames[m] = {"images": imgs, "indexes": torch.arange(C, dtype=torch.int32)}
+    sampler = UniformPixelSamplerConfig(num_rays_per_modality=n_rays).setup(device=None)
+    sampler.generator = torch.Generator()
+    sampler.generator.manual_seed(654824)
+    coords, pixels = sampler.sample(frames)
+    rb = gen(coords)
+    with record_rand() as draws:
+        outputs = model(rb)
+    # loss (raw_pipeline.py:112-122 + losses.py)
+    lm = cfg.pipeline.loss_manager.setup(modalities=list(mods), num_iterations=100000, model=model)
+    if raw:
+        for m in mods:
+            mm = mscene.mosaick_mask(m, W, H)
+            band = mm[coords[m][:, 1].long(), coords[m][:, 2].long()].unsqueeze(1).long()
+            outputs[m][m] = torch.gather(outputs[m][m], 1, band)
+    losses, total = lm.compute_loss(outputs, pixels, coords, step)
+    total.backward()
+    arrays = {"step": step, "level": level, "delta": delta, "W": W, "H": H, "raw": raw,
+              "mods": np.array(mods), "loss": total.detach()}
+    for k, v in losses.items():
+        arrays["loss:" + k] = torch.as_tensor(v).detach()
+    for k, v in model.state_dict().items():
+        arrays["p:" + k] = v
+    for k, p in model.named_parameters():
+        if p.grad is not None:
+            arrays["g:" + k] = p.grad
+    for i, d in enumerate(draws):
+        arrays[f"rand:{i}"] = d
+    for m in mods:
+        arrays[f"{m}:coords"] = coords[m]
+        arrays[f"{m}:pixels"] = pixels[m]
+        arrays[f"{m}:pose"] = opt.pose_adjustment[m].detach()
+        arrays[f"{m}:dpose"] = opt.pose_adjustment[m].grad
+        for k in ["c2w", "fx", "fy", "cx", "cy", "distortion"]:
+            arrays[f"{m}:{k}"] = getattr(cams[m], k)
+        o = outputs[m]
+        for k in ["normals", "depth", "accumulation", "gradients", "hessians", "inv_s"]:
+            arrays[f"{m}:out:{k}"] = o[k].detach()
+        for mm in mods:
+            if mm in o:
+                arrays[f"{m}:out:{mm}"] = o[mm].detach()
+    save(f"e2e_{tag}", **arrays)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["hashgrid", "mlp", "raygen", "sampler", "e2e"]
+    if "hashgrid" in which:
+        gen_hashgrid()
+    if "mlp" in which:
+        gen_mlp()
+    if "raygen" in which:
+        gen_raygen()
+    if "sampler" in which:
+        gen_sampler()
+    if "e2e" in which:
+        gen_end_to_end("grid", "grid.yaml", ["rgb"], 95000, "grid_rgb_s95000")
+        gen_end_to_end("grid", "grid.yaml", ["rgb"], 30000, "grid_rgb_s30000")
+        # same seed -> same init: keep the parameters only once (s95000 file)
+        a = dict(np.load(os.path.join(OUT, "e2e_grid_rgb_s95000.npz")))
+        b = dict(np.load(os.path.join(OUT, "e2e_grid_rgb_s30000.npz")))
+        assert all(np.array_equal(a[k], b[k]) for k in a if k.startswith("p:"))
+        b = {k: v for k, v in b.items() if not k.startswith("p:")}
+        b["params_from"] = np.array("e2e_grid_rgb_s95000")
+        np.savez_compressed(os.path.join(OUT, "e2e_grid_rgb_s30000.npz"), **b)
+        gen_end_to_end("grid_raw", "grid_raw.yaml", ["rgb", "infrared", "mono", "polarization", "multispectral"],
+                       95000, "grid_raw_5mod_s95000", raw=True)

@@ -1,0 +1,73 @@
+"""GPU parity: hash grid and fp32 GEMM kernels vs the CPU oracle / fp64 references."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hashgrid as ohg
+
+pytestmark = pytest.mark.gpu
+
+
+def _pts(M, lo=-1.1, hi=1.1, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(M, 3, generator=g) * (hi - lo) + lo
+
+
+@pytest.mark.parametrize("log2T,active,radius", [(12, 16, 1.0), (19, 16, 1.0), (19, 7, 1.0), (14, 16, 2.0)])
+def test_hashgrid_fwd_bwd(dev, log2T, active, radius):
+    from multimodalstudio_amd import hip_ops
+    L = 16
+    scales = ohg.level_scales(16, 1024, L)
+    g = torch.Generator().manual_seed(1)
+    table = (torch.rand(L << log2T, 2, generator=g) * 2 - 1) * 1e-1
+    x = _pts(3000, seed=log2T)
+    # oracle
+    xr = x.clone().requires_grad_(True)
+    tr = table.clone().requires_grad_(True)
+    ref = ohg.feature_grid(xr, tr, scales, log2T, radius, active)
+    dout = torch.randn(ref.shape, generator=g)
+    ref.backward(dout)
+    # hip
+    xd = x.to(dev).requires_grad_(True)
+    td = table.to(dev).requires_grad_(True)
+    out = hip_ops.HashGridFunction.apply(xd, td, scales.tolist(), log2T, radius, active)
+    out.backward(dout.to(dev))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(td.grad.cpu().numpy(), tr.grad.numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(xd.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 257, 71), (300, 3, 64), (4096, 256, 256), (77, 130, 317)])
+def test_gemm_modes(dev, M, N, K):
+    from multimodalstudio_amd import hip_ops
+    g = torch.Generator().manual_seed(M + N + K)
+    X = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g)
+    b = torch.randn(N, generator=g)
+    dY = torch.randn(M, N, generator=g)
+    Xd, Wd, bd, dYd = X.to(dev), W.to(dev), b.to(dev), dY.to(dev)
+    # forward NT with softplus + Z
+    Y = torch.empty(M, N, device=dev)
+    Z = torch.empty(M, N, device=dev)
+    hip_ops.gemm(hip_ops.NT, M, N, K, Xd, K, Wd, K, Y, N, bias=bd, Z=Z, ldz=N, act=2, beta=100.0, thr=20.0)
+    z_ref = X.double() @ W.double().T + b.double()
+    y_ref = torch.nn.functional.softplus(z_ref, beta=100, threshold=20)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(Z.cpu().numpy(), z_ref.numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(Y.cpu().numpy(), y_ref.numpy(), rtol=1e-4, atol=1e-4)
+    # backward data NN: dX = (dY * sp'(Z)) W
+    dX = torch.empty(M, K, device=dev)
+    dZ = torch.empty(M, N, device=dev)
+    # dZ via epilogue aux: treat as NN with identity: use gemm with K=N? compute dZ on host ref instead
+    dz_ref = dY.double() * torch.sigmoid(100 * z_ref).where(100 * z_ref <= 20, torch.ones_like(z_ref))
+    dZd = dz_ref.float().to(dev)
+    hip_ops.gemm(hip_ops.NN, M, K, N, dZd, N, Wd, K, dX, K)
+    dx_ref = dz_ref @ W.double()
+    # backward weights TN (split-K): dW = dZ^T X
+    dW = torch.zeros(N, K, device=dev)
+    hip_ops.gemm(hip_ops.TN, N, K, M, dZd, N, Xd, K, dW, K, accumulate=True, splits=7)
+    dw_ref = dz_ref.T @ X.double()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(dX.cpu().numpy(), dx_ref.numpy(), rtol=1e-4, atol=2e-3)
+    np.testing.assert_allclose(dW.cpu().numpy(), dw_ref.numpy(), rtol=1e-4, atol=5e-3)
