@@ -1,0 +1,177 @@
+/*
+ * mms_hip.h — C ABI of libmms_hip.so, the MI355X (gfx950) kernels of MultimodalStudio's per-ray
+ * training hot path.  This is the drop-in boundary: the reference's Python plugin classes
+ * (Encoding / FieldComponent / fields / samplers / renderer, /root/reference/src) bind it through
+ * ctypes (multimodalstudio_amd/_lib.py; INTEGRATION.md shows the stubs a maintainer would add).
+ *
+ * Conventions:
+ *   - every pointer is a device pointer to fp32 (or int) memory owned by the caller (PyTorch);
+ *     row-major matrices take an explicit leading dimension (elements);
+ *   - `stream` is a hipStream_t passed as void*; calls are stream-ordered, never synchronise and
+ *     never allocate (graph-capturable);
+ *   - return 0 on success, negative on error; mms_last_error() gives the thread-local message;
+ *   - "accumulate" outputs (+=) are marked; the library never owns parameters.
+ *
+ * Each entry point names the reference interface it replaces (file:line under /root/reference/src).
+ */
+#ifndef MMS_HIP_H
+#define MMS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* mms_version(void);
+const char* mms_last_error(void);
+
+/* ---- multires hash grid: HashEncoding (field_components/encodings.py:184-310) inside FeatureGrid
+ * (field_components/feature_structures.py:78-88).  pos [M, ldx] (cols 0..2), table [L*2^log2T, F=2],
+ * scales [L] host array (floor(min_res*g^l)), out [M, ldo] cols 0..2L-1.  Levels >= active_levels are
+ * zero (coarse-to-fine mask).  bwd: dtable += (atomic), dpos[:, 0:3] += (either may be NULL). */
+int mms_hashgrid_fwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L, int log2T, int F,
+                     const float* scales, float radius, int active_levels, float* out, int64_t ldo, void* stream);
+int mms_hashgrid_bwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L, int log2T, int F,
+                     const float* scales, float radius, int active_levels, const float* dout, int64_t ldd,
+                     float* dtable, float* dpos, int64_t lddx, void* stream);
+
+/* ---- fp32 MFMA GEMM with fused MLP epilogue: nn.Linear + activation (field_components/mlp.py:152-171).
+ * mode 0 NT: C = A[M,K] B[N,K]^T ; 1 NN: C = A[M,K] B[K,N] ; 2 TN: C = A[K,M]^T B[K,N].
+ * Epilogue: v = acc + bias[n]; Z[m,n] = v (optional); v = act(v); v *= dact'(aux[m,n]) (optional);
+ * C = v or C += v (accumulate; atomic when splits > 1).  act/dact: 0 none, 1 ReLU, 2 Softplus(beta,thr),
+ * 3 Sigmoid. */
+int mms_gemm_f32(int mode, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
+                 int64_t ldb, float* C, int64_t ldc, const float* bias, float* Z, int64_t ldz, const float* aux,
+                 int64_t ldaux, int act, int dact, float beta, float thr, int accumulate, int splits, void* stream);
+
+/* ---- weight norm (mlp.py:206-209; torch weight_norm dim=0): W = v * (g / ||v||_row); bwd dg += , dv += */
+int mms_weight_norm_fwd(const float* g, const float* v, int64_t N, int64_t K, float* W, int64_t ldw, float* norms,
+                        void* stream);
+int mms_weight_norm_bwd(const float* g, const float* v, const float* norms, int64_t N, int64_t K, const float* dW,
+                        int64_t lddw, float* dg, float* dv, void* stream);
+/* bias gradient: out[n] += sum_m A[m, n] */
+int mms_colsum(const float* A, int64_t M, int64_t N, int64_t lda, float* out, void* stream);
+/* dZ = dY * act'(Z) */
+int mms_act_bwd(const float* dY, int64_t ldy, const float* Z, int64_t ldz, int64_t M, int64_t N, int act,
+                float beta, float thr, float* dZ, int64_t lddz, void* stream);
+
+/* ---- SDF-field input panel [x, PE(x)] (NeRFEncoding encodings.py:161-182; SDFField surface_field.py:99-116)
+ * for the centre rows [0, M) and, with ntaps = 4, the 4 numerical-gradient taps x + k_t * delta
+ * (SurfaceModel.gradient, surface_model.py:137-153) at rows [M (t+1), M (t+2)).  bwd: dpos += */
+int mms_geo_input_fwd(const float* pos, int64_t ldp, int64_t M, int ntaps, float delta, int F, float* X, int64_t ldx,
+                      void* stream);
+int mms_geo_input_bwd(const float* X, int64_t ldx, const float* dX, int64_t lddx, const float* dP, int64_t lddp,
+                      int64_t M, int ntaps, int F, float* dpos, int64_t lddpos, void* stream);
+/* gradients / hessians / normals from the 5 SDF evaluations (surface_model.py:143-151, :91);
+ * four_delta = 4 delta, delta_sq = delta^2.  bwd writes d sdf into column 0 of dout rows (all 5M). */
+int mms_taps_combine_fwd(const float* out, int64_t ldo, int64_t M, float four_delta, float delta_sq, float* grads,
+                         float* hess, float* normals, void* stream);
+int mms_taps_combine_bwd(const float* grads, const float* dgrads, const float* dhess, const float* dnormals,
+                         int64_t M, float four_delta, float delta_sq, float* dout, int64_t lddo, void* stream);
+
+/* ---- radiance input panel [x, SH4(d), geo, n.v, (grid)] (RadianceModel.forward radiance_model.py:94-151,
+ * RadianceField radiance_field.py:72-77, SH utils/math.py:21-83).  One ray = S consecutive rows. */
+int mms_rad_input_fwd(const float* pos, int64_t ldp, const float* dirs, const float* normals, const float* geo,
+                      int64_t ldg, int64_t M, int S, int G, float* X, int64_t ldx, void* stream);
+int mms_rad_input_bwd(const float* dX, int64_t lddx, const float* dP, int64_t lddp, const float* dirs,
+                      const float* normals, int64_t R, int S, int G, float* dpos, int64_t lddpos, float* dgeo,
+                      int64_t lddg, float* ddirs, void* stream);
+
+/* ---- background NeRF inputs: L-inf SceneContraction (spatial_distortions.py:90-97), PE6(pos) -> X[:, 0:39],
+ * PE4(dir) -> D[:, dcol:dcol+27] (NeRFField nerf_field.py:92-105).  bwd: dpos = , ddirs += */
+int mms_bg_input_fwd(const float* pos, int64_t M, const float* dirs, int S, float* X, int64_t ldx, float* D,
+                     int64_t ldd, int64_t dcol, void* stream);
+int mms_bg_input_bwd(const float* pos, const float* X, int64_t ldx, const float* dX, int64_t lddx, const float* dirs,
+                     const float* dD, int64_t lddd, int64_t dcol, int64_t R, int S, float* dpos, float* ddirs,
+                     void* stream);
+
+/* ---- NeuS alpha + transmittance weights (NeuSVolumeRendering volume_rendering.py:177-213), one wave per ray,
+ * S <= 64.  bwd: dsdf = (strided), dgrads +=, ddirs +=, ddeltas +=, ds_param += (atomic). */
+int mms_neus_weights_fwd(const float* sdf, int64_t lds, const float* grads, const float* dirs, const float* deltas,
+                         const float* s_param, float cos_anneal, int64_t R, int S, float* alpha, float* weights,
+                         void* stream);
+int mms_neus_weights_bwd(const float* sdf, int64_t lds, const float* grads, const float* dirs, const float* deltas,
+                         const float* s_param, float cos_anneal, int64_t R, int S, const float* alpha,
+                         const float* dweights, float* dsdf, int64_t ldds, float* dgrads, float* ddirs,
+                         float* ddeltas, float* ds_param, void* stream);
+/* density -> alpha -> weights (RaySamples.get_alphas + get_weights_from_alphas, cameras/rays.py:138-217) */
+int mms_density_weights_fwd(const float* density, int64_t ldd, const float* deltas, int64_t R, int S, float* alpha,
+                            float* weights, void* stream);
+int mms_density_weights_bwd(const float* density, int64_t ldd, const float* deltas, int64_t R, int S,
+                            const float* alpha, const float* dweights, float* ddensity, int64_t lddd, float* ddeltas,
+                            void* stream);
+/* composite sum_s w c (+ bg (1 - sum w)), scattering compacted rays to rows idx[r]
+ * (Renderer.render / RadianceRenderer renderers.py:75-174; BackgroundModel sum background_model.py:101-109) */
+int mms_composite_fwd(const float* w, const float* vals, int64_t ldv, int C, const float* bg, int64_t R, int S,
+                      const int64_t* idx, float* out, void* stream);
+int mms_composite_bwd(const float* w, const float* vals, int64_t ldv, int C, const float* bg, int64_t R, int S,
+                      const int64_t* idx, const float* dout, float* dvals, int64_t lddv, float* dw, float* dbg,
+                      void* stream);
+
+/* ---- PolarizationHead Stokes alignment + intensities (field_heads.py:90-106; polarizer.py:54-101).
+ * stokes [M,3] (MLP output), dirs/ups per ray [M/S, 3]; out [M,4]; bwd dstokes =, ddirs +=, dups += */
+int mms_polarizer_fwd(const float* stokes, const float* dirs, const float* ups, int64_t M, int S, float* out,
+                      void* stream);
+int mms_polarizer_bwd(const float* stokes, const float* dirs, const float* ups, int64_t R, int S, const float* dout,
+                      float* dstokes, float* ddirs, float* dups, void* stream);
+
+/* ---- samplers (model_components/ray_samplers.py) */
+/* stratified jittered bins (SpacedSampler :209-221): lin [nb] host-computed torch.linspace values (device copy),
+ * t [R, tcols] (tcols = 1 single jitter, nb per-bin jitter) or NULL (eval) */
+int mms_stratified_bins(const float* lin, int nb, const float* t, int tcols, int64_t R, float* bins, void* stream);
+/* spacing bins -> euclidean starts/ends/deltas/positions (spacing_to_euclidean_fn :178-181, rays.py:69-81,
+ * 304-349); kind 0 uniform, 1 linear disparity.  bwd: d near/far/origins/dirs += */
+int mms_samples_fwd(const float* bins, int64_t ldb, int nb, const float* nears, const float* fars,
+                    const float* origins, const float* dirs, int kind, int64_t R, float* starts, float* ends,
+                    float* deltas, float* pos, void* stream);
+int mms_samples_bwd(const float* bins, int64_t ldb, int nb, const float* nears, const float* fars, const float* dirs,
+                    int kind, int64_t R, const float* dpos, const float* ddeltas, const float* dstarts,
+                    float* dnears, float* dfars, float* dorigins, float* ddirs, void* stream);
+/* one NeuS up-sampling iteration (NeuSSampler :480-511): sdf gather-merge, fixed-inv_s alpha (:516-551),
+ * weights, PDF inverse CDF (PDFSampler :357-403), stable merge (merge_ray_samples :38-68). */
+int mms_neus_step(int64_t R, int S, const float* bins, const float* sdf_prev, int s_prev, const float* sdf_new,
+                  int n_prev_new, const int* prev_idx, const float* nears, const float* fars, float inv_s,
+                  const float* rand, const float* u_lin, int n_new, float* sdf_out, float* new_bins,
+                  float* merged_bins, int* sorted_idx, void* stream);
+
+/* ---- rays (cameras/cameras.py:460-703, camera_utils.py:280-383, poses.py:53-67, ray_generators.py:54-81).
+ * coords int [N, 3] = (camera, y, x); mats = camera_opt_to_camera [C or 1, 3, 4]; bwd dmats += (atomic). */
+int mms_raygen_fwd(const int* coords, int64_t N, const float* fx, const float* fy, const float* cx, const float* cy,
+                   const float* c2w, const float* dist, const float* mats, int mat_per_cam, float pixel_offset,
+                   float* origins, float* dirs, float* ups, float* area, float* dnorm, void* stream);
+int mms_raygen_bwd(const int* coords, int64_t N, const float* fx, const float* fy, const float* cx, const float* cy,
+                   const float* c2w, const float* dist, const float* mats, int mat_per_cam, float pixel_offset,
+                   const float* dorig, const float* ddirs, const float* dups, float* dmats, void* stream);
+/* SphereCollider (scene_colliders.py:60-80) + background near/far (:107-113); mask uint8 */
+int mms_collider_fwd(const float* origins, const float* dirs, int64_t N, float radius, float* nears, float* fars,
+                     unsigned char* mask, float* bg_nears, float* bg_fars, void* stream);
+int mms_collider_bwd(const float* origins, const float* dirs, int64_t N, float radius, const float* dnears,
+                     const float* dfars, const float* dbg_nears, const float* dbg_fars, float* dorig, float* ddirs,
+                     void* stream);
+/* order-preserving mask compaction (TensorDataclass.__getitem__ with a bool mask, base_model.py:88-93) */
+int mms_compact(const unsigned char* mask, int64_t N, int64_t* idx, int64_t* count, void* stream);
+
+/* ---- losses (model_components/losses.py): L1 (+ SkipSaturation fill), eikonal, curvature; scalars on device */
+int mms_l1_loss_fwd(const float* out, int64_t ldo, const float* tgt, int64_t N, int C, float sat_thr,
+                    unsigned long long* first_scratch, float* loss, void* stream);
+int mms_l1_loss_bwd(const float* out, int64_t ldo, const float* tgt, int64_t N, int C, float sat_thr,
+                    const unsigned long long* first_scratch, const float* dloss, float scale, float* dout,
+                    int64_t lddo, void* stream);
+int mms_geo_loss_fwd(const float* grads, const float* hess, int64_t M, float inv_total, float* eik, float* curv,
+                     void* stream);
+int mms_geo_loss_bwd(const float* grads, const float* hess, int64_t M, float inv_total, const float* deik,
+                     float eik_scale, const float* dcurv, float curv_scale, float* dgrads, float* dhess,
+                     void* stream);
+
+/* ---- optimizer (pipelines/base_pipeline.py:232-248 clip_gradients, torch.optim.AdamW): acc += sum x^2 ;
+ * AdamW with clip coefficient min(1, max_norm / (sqrt(*sumsq) + 1e-6)) read on device */
+int mms_sumsq(const float* x, int64_t n, float* acc, void* stream);
+int mms_adamw(float* p, const float* g, float* m, float* v, int64_t n, const float* sumsq, float max_norm, float lr,
+              float wd, float beta1, float beta2, float eps, float step_size, float bc2_sqrt, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MMS_HIP_H */

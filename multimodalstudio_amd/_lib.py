@@ -1,6 +1,8 @@
-"""ctypes binding of the C-ABI library ``libmms_hip.so`` (declared in include/mms_hip.h).
+"""ctypes binding of the C-ABI library ``libmms_hip.so``.
 
-The product path has no fallback: if the library is missing or fails to load, every op raises.
+The argument types are derived from the declarations in ``include/mms_hip.h`` (the single source of
+truth for the boundary), so the header and the binding cannot drift apart.  There is no fallback:
+if the library or header is missing every op raises.
 Streams: each call passes ``torch.cuda.current_stream().cuda_stream`` (a hipStream_t) so kernels
 are ordered with PyTorch's own work; the library never synchronises or allocates.
 """
@@ -8,23 +10,38 @@ from __future__ import annotations
 
 import ctypes
 import os
+import re
 from pathlib import Path
 
 _PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("MMS_HIP_LIB", _PKG / "libmms_hip.so"))
+HEADER = _PKG.parent / "include" / "mms_hip.h"
 
-_p = ctypes.c_void_p
-_i64 = ctypes.c_int64
-_i32 = ctypes.c_int
-_f32 = ctypes.c_float
+_DECL = re.compile(r"^\s*(int|const char\*)\s+(mms_\w+)\s*\(([^;]*?)\)\s*;", re.S | re.M)
 
-# name -> argtypes (restype is always int status, except mms_last_error / mms_version)
-SIGNATURES = {
-    "mms_hashgrid_fwd": [_p, _i64, _i64, _p, _i32, _i32, _i32, _p, _f32, _i32, _p, _i64, _p],
-    "mms_hashgrid_bwd": [_p, _i64, _i64, _p, _i32, _i32, _i32, _p, _f32, _i32, _p, _i64, _p, _p, _i64, _p],
-    "mms_gemm_f32": [_i32, _i64, _i64, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _p, _i64,
-                     _i32, _i32, _f32, _f32, _i32, _i32, _p],
-}
+
+def _ctype(arg: str):
+    a = arg.strip()
+    if a == "void" or not a:
+        return None
+    if "*" in a:
+        return ctypes.c_void_p
+    t = a.rsplit(" ", 1)[0].strip()
+    return {"int64_t": ctypes.c_int64, "int": ctypes.c_int, "float": ctypes.c_float}[t]
+
+
+def parse_header(path: Path = HEADER):
+    """Return {name: (restype, [argtypes])} for every mms_* declaration in the header."""
+    text = path.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    out = {}
+    for ret, name, args in _DECL.findall(text):
+        argtypes = [t for t in (_ctype(x) for x in args.replace("\n", " ").split(",")) if t is not None]
+        out[name] = (ctypes.c_char_p if ret.startswith("const char") else ctypes.c_int, argtypes)
+    return out
+
+
+SIGNATURES = parse_header() if HEADER.exists() else {}
 
 _lib = None
 
@@ -42,15 +59,13 @@ def lib():
         raise HipLibraryError(
             f"{LIB_PATH} not found: build it with `python -m multimodalstudio_amd.build` "
             "(there is no CPU or PyTorch fallback for the MMS hot path)")
+    if not SIGNATURES:
+        raise HipLibraryError(f"C-ABI header {HEADER} not found")
     L = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
-    for name, argtypes in SIGNATURES.items():
+    for name, (restype, argtypes) in SIGNATURES.items():
         fn = getattr(L, name)
         fn.argtypes = argtypes
-        fn.restype = ctypes.c_int
-    L.mms_last_error.argtypes = []
-    L.mms_last_error.restype = ctypes.c_char_p
-    L.mms_version.argtypes = []
-    L.mms_version.restype = ctypes.c_char_p
+        fn.restype = restype
     _lib = L
     return L
 
@@ -65,4 +80,4 @@ def call(name: str, *args) -> None:
 
 
 def exported_symbols():
-    return list(SIGNATURES.keys()) + ["mms_last_error", "mms_version"]
+    return list(SIGNATURES.keys())

@@ -1,0 +1,226 @@
+// Loss terms and the fused optimizer step.
+//
+// Losses (/root/reference/src/model_components/losses.py):
+//   L1 radiance loss (nn.L1Loss, mean)                       :68-90
+//   SkipSaturationLoss: saturated targets -> output := first saturated target value   :152-164
+//   EikonalLoss: MSE(||grad||, 1)                             :107-119
+//   CurvatureLoss: L1(sum(hessian), 0)                        :121-150
+// Optimizer (pipelines/base_pipeline.py:232-248 + torch.optim.AdamW, method_configs.py:260-269):
+//   clip_grad_norm_(max_norm) over an optimizer's parameters, then AdamW (decoupled weight decay).
+// Every scalar stays on the device (no host synchronisation inside a step).
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ float block_reduce_sum(float v) {
+  __shared__ float red[16];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+  }
+  return t;  // valid on thread 0
+}
+
+// first flattened index with target > thr (atomicMin), init must be INT64 max
+__global__ void first_saturated_kernel(const float* __restrict__ tgt, int64_t n, float thr,
+                                       unsigned long long* __restrict__ first) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (tgt[i] > thr) atomicMin(first, (unsigned long long)i);
+  }
+}
+
+// out/tgt are [N, C] with row strides; loss += sum |o - t| / (N C)
+__global__ __launch_bounds__(256) void l1_fwd_kernel(const float* __restrict__ out, int64_t ldo,
+                                                     const float* __restrict__ tgt, int64_t N, int C, float thr,
+                                                     const unsigned long long* __restrict__ first,
+                                                     float* __restrict__ loss) {
+  const int64_t n = N * C;
+  float fill = 0.f;
+  bool sat = false;
+  if (first != nullptr && first[0] < (unsigned long long)n) { sat = true; fill = tgt[first[0]]; }
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / C, c = i - r * C;
+    const float t = tgt[i];
+    float o = out[r * ldo + c];
+    if (sat && t > thr) o = fill;
+    s += fabsf(o - t);
+  }
+  s = block_reduce_sum(s);
+  if (threadIdx.x == 0) atomicAdd(loss, s / (float)n);
+}
+
+__global__ void l1_bwd_kernel(const float* __restrict__ out, int64_t ldo, const float* __restrict__ tgt, int64_t N,
+                              int C, float thr, const unsigned long long* __restrict__ first,
+                              const float* __restrict__ dloss, float scale, float* __restrict__ dout, int64_t lddo) {
+  const int64_t n = N * C;
+  const bool sat = first != nullptr && first[0] < (unsigned long long)n;
+  const float g = dloss[0] * scale / (float)n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / C, c = i - r * C;
+    const float t = tgt[i];
+    const float o = out[r * ldo + c];
+    float d = (o > t) ? g : ((o < t) ? -g : 0.f);
+    if (sat && t > thr) d = 0.f;  // masked_fill: output replaced by a constant
+    dout[r * lddo + c] += d;
+  }
+}
+
+// eikonal: sum over rows of (||g|| - 1)^2 / M_total ; curvature: sum |h0 + h1 + h2| / M_total
+__global__ __launch_bounds__(256) void geo_loss_fwd_kernel(const float* __restrict__ grads,
+                                                           const float* __restrict__ hess, int64_t M, float inv_total,
+                                                           float* __restrict__ eik, float* __restrict__ curv) {
+  float se = 0.f, sc = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
+    if (grads) {
+      const float g0 = grads[i * 3], g1 = grads[i * 3 + 1], g2 = grads[i * 3 + 2];
+      const float n = sqrtf(g0 * g0 + g1 * g1 + g2 * g2);
+      se += (n - 1.0f) * (n - 1.0f);
+    }
+    if (hess) sc += fabsf(hess[i * 3] + hess[i * 3 + 1] + hess[i * 3 + 2]);
+  }
+  se = block_reduce_sum(se);
+  __syncthreads();
+  sc = block_reduce_sum(sc);
+  if (threadIdx.x == 0) {
+    if (eik) atomicAdd(eik, se * inv_total);
+    if (curv) atomicAdd(curv, sc * inv_total);
+  }
+}
+
+__global__ void geo_loss_bwd_kernel(const float* __restrict__ grads, const float* __restrict__ hess, int64_t M,
+                                    float inv_total, const float* __restrict__ deik, float eik_scale,
+                                    const float* __restrict__ dcurv, float curv_scale, float* __restrict__ dgrads,
+                                    float* __restrict__ dhess) {
+  const float ge = deik ? deik[0] * eik_scale * inv_total : 0.f;
+  const float gc = dcurv ? dcurv[0] * curv_scale * inv_total : 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
+    if (grads && dgrads && deik) {
+      const float g0 = grads[i * 3], g1 = grads[i * 3 + 1], g2 = grads[i * 3 + 2];
+      const float n = sqrtf(g0 * g0 + g1 * g1 + g2 * g2);
+      const float f = n > 0.f ? 2.0f * (n - 1.0f) * ge / n : 0.f;
+      dgrads[i * 3] += f * g0;
+      dgrads[i * 3 + 1] += f * g1;
+      dgrads[i * 3 + 2] += f * g2;
+    }
+    if (hess && dhess && dcurv) {
+      const float l = hess[i * 3] + hess[i * 3 + 1] + hess[i * 3 + 2];
+      const float d = l > 0.f ? gc : (l < 0.f ? -gc : 0.f);
+      dhess[i * 3] += d;
+      dhess[i * 3 + 1] += d;
+      dhess[i * 3 + 2] += d;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ optimizer
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ acc) {
+  float s = 0.f;
+  const int64_t n4 = n / 4;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = x4[i];
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    s += x[i] * x[i];
+  s = block_reduce_sum(s);
+  if (threadIdx.x == 0) atomicAdd(acc, s);
+}
+
+// AdamW with the clip coefficient coef = min(1, max_norm / (sqrt(sumsq) + 1e-6)) applied to g.
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                    const float* __restrict__ sumsq, float max_norm, float lr, float wd,
+                                                    float beta1, float beta2, float eps, float step_size,
+                                                    float bc2_sqrt) {
+  float coef = 1.0f;
+  if (sumsq != nullptr && max_norm > 0.f) {
+    const float total = sqrtf(sumsq[0]);
+    coef = fminf(max_norm / (total + 1e-6f), 1.0f);
+  }
+  const float decay = 1.0f - lr * wd;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i] * coef;
+    float pi = p[i] * decay;
+    float mi = m[i];
+    mi = mi + (1.0f - beta1) * (gi - mi);
+    float vi = v[i] * beta2 + (1.0f - beta2) * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi - step_size * (mi / denom);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+}  // namespace
+
+MMS_EXPORT int mms_l1_loss_fwd(const float* out, int64_t ldo, const float* tgt, int64_t N, int C, float sat_thr,
+                               unsigned long long* first_scratch, float* loss, void* stream) {
+  const char* fn = "mms_l1_loss_fwd";
+  if (N == 0) return 0;
+  hipStream_t s = mms::as_stream(stream);
+  if (first_scratch) {
+    if (hipMemsetAsync(first_scratch, 0xFF, sizeof(unsigned long long), s) != hipSuccess)
+      return mms::set_error(fn, "memset failed");
+    hipLaunchKernelGGL(first_saturated_kernel, dim3(mms::grid_for(N * C, 256, 1024)), dim3(256), 0, s, tgt, N * C,
+                       sat_thr, first_scratch);
+  }
+  hipLaunchKernelGGL(l1_fwd_kernel, dim3(mms::grid_for(N * C, 256, 1024)), dim3(256), 0, s, out, ldo, tgt, N, C,
+                     sat_thr, first_scratch, loss);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_l1_loss_bwd(const float* out, int64_t ldo, const float* tgt, int64_t N, int C, float sat_thr,
+                               const unsigned long long* first_scratch, const float* dloss, float scale, float* dout,
+                               int64_t lddo, void* stream) {
+  const char* fn = "mms_l1_loss_bwd";
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(l1_bwd_kernel, dim3(mms::grid_for(N * C, 256, 4096)), dim3(256), 0, mms::as_stream(stream), out,
+                     ldo, tgt, N, C, sat_thr, first_scratch, dloss, scale, dout, lddo);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_geo_loss_fwd(const float* grads, const float* hess, int64_t M, float inv_total, float* eik,
+                                float* curv, void* stream) {
+  const char* fn = "mms_geo_loss_fwd";
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(geo_loss_fwd_kernel, dim3(mms::grid_for(M, 256, 1024)), dim3(256), 0, mms::as_stream(stream),
+                     grads, hess, M, inv_total, eik, curv);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_geo_loss_bwd(const float* grads, const float* hess, int64_t M, float inv_total, const float* deik,
+                                float eik_scale, const float* dcurv, float curv_scale, float* dgrads, float* dhess,
+                                void* stream) {
+  const char* fn = "mms_geo_loss_bwd";
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(geo_loss_bwd_kernel, dim3(mms::grid_for(M, 256, 8192)), dim3(256), 0, mms::as_stream(stream),
+                     grads, hess, M, inv_total, deik, eik_scale, dcurv, curv_scale, dgrads, dhess);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_sumsq(const float* x, int64_t n, float* acc, void* stream) {
+  const char* fn = "mms_sumsq";
+  if (n == 0) return 0;
+  MMS_REQUIRE(((uintptr_t)x & 15) == 0, fn, "buffer must be 16-byte aligned");
+  hipLaunchKernelGGL(sumsq_kernel, dim3(mms::grid_for(n / 4 + 1, 256, 2048)), dim3(256), 0, mms::as_stream(stream), x,
+                     n, acc);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_adamw(float* p, const float* g, float* m, float* v, int64_t n, const float* sumsq, float max_norm,
+                         float lr, float wd, float beta1, float beta2, float eps, float step_size, float bc2_sqrt,
+                         void* stream) {
+  const char* fn = "mms_adamw";
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(adamw_kernel, dim3(mms::grid_for(n, 256, 8192)), dim3(256), 0, mms::as_stream(stream), p, g, m, v,
+                     n, sumsq, max_norm, lr, wd, beta1, beta2, eps, step_size, bc2_sqrt);
+  return mms::check_launch(fn);
+}

@@ -1,0 +1,335 @@
+// Ray generation (pinhole + OpenCV undistortion + pose refinement) and the sphere collider.
+//
+// Reference (paths under /root/reference/src):
+//   RayGenerator.forward                model_components/ray_generators.py:54-81
+//   Cameras._generate_rays_from_coords  cameras/cameras.py:460-703 (perspective cameras)
+//   radial_and_tangential_undistort     cameras/camera_utils.py:280-383 (params read [k1,k2,k3,k4,p1,p2])
+//   pose_utils.multiply                 utils/poses.py:53-67   (c2w o camera_opt_to_camera)
+//   SphereCollider.forward              model_components/scene_colliders.py:60-80
+//   update_ray_bundles_for_background   model_components/scene_colliders.py:107-113
+// The SO(3)xR^3 exponential map of the (1 x 6) pose delta is O(1) work and stays in PyTorch autograd on
+// the host side; these kernels take the resulting 3x4 matrices and return dL/dmatrix (atomics).
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+__device__ void undistort(float& x, float& y, const float* dp) {
+  const float xd = x, yd = y;
+  const float k1 = dp[0], k2 = dp[1], k3 = dp[2], k4 = dp[3], p1 = dp[4], p2 = dp[5];
+  for (int it = 0; it < 10; ++it) {
+    const float r = x * x + y * y;
+    const float d = 1.0f + r * (k1 + r * (k2 + r * (k3 + r * k4)));
+    const float fx = d * x + 2 * p1 * x * y + p2 * (r + 2 * x * x) - xd;
+    const float fy = d * y + 2 * p2 * x * y + p1 * (r + 2 * y * y) - yd;
+    const float d_r = k1 + r * (2.0f * k2 + r * (3.0f * k3 + r * 4.0f * k4));
+    const float d_x = 2.0f * x * d_r;
+    const float d_y = 2.0f * y * d_r;
+    const float fx_x = d + d_x * x + 2.0f * p1 * y + 6.0f * p2 * x;
+    const float fx_y = d_y * x + 2.0f * p1 * x + 2.0f * p2 * y;
+    const float fy_x = d_x * y + 2.0f * p2 * y + 2.0f * p1 * x;
+    const float fy_y = d + d_y * y + 2.0f * p2 * x + 6.0f * p1 * y;
+    const float den = fy_x * fx_y - fx_x * fy_y;
+    const float xn = fx * fy_y - fy * fx_y;
+    const float yn = fy * fx_x - fx * fy_x;
+    const bool ok = fabsf(den) > 1e-3f;
+    x = x + (ok ? xn / den : 0.0f);
+    y = y + (ok ? yn / den : 0.0f);
+  }
+}
+
+struct Pose {
+  float R[3][3];
+  float t[3];
+};
+
+// c2w o mat (poses.py:53-67): R = R1 R2, t = t1 + R1 t2
+__device__ __forceinline__ Pose compose(const float* c2w, const float* mat) {
+  Pose P;
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) {
+      float s = c2w[i * 4 + 0] * mat[0 * 4 + j];
+      s = s + c2w[i * 4 + 1] * mat[1 * 4 + j];
+      s = s + c2w[i * 4 + 2] * mat[2 * 4 + j];
+      P.R[i][j] = s;
+    }
+    float s = c2w[i * 4 + 0] * mat[0 * 4 + 3];
+    s = s + c2w[i * 4 + 1] * mat[1 * 4 + 3];
+    s = s + c2w[i * 4 + 2] * mat[2 * 4 + 3];
+    P.t[i] = c2w[i * 4 + 3] + s;
+  }
+  return P;
+}
+
+__device__ __forceinline__ void cam_coords(int xi, int yi, float off, float fx, float fy, float cx, float cy,
+                                           const float* dp, float u[3], float v[3]) {
+  const float x = (float)xi + off, y = (float)yi + off;
+  u[0] = (x - cx) / fx;       v[0] = -(y - cy) / fy;
+  u[1] = (x - cx + 1) / fx;   v[1] = -(y - cy) / fy;
+  u[2] = (x - cx) / fx;       v[2] = -(y - cy + 1) / fy;
+  if (dp) {
+    for (int s = 0; s < 3; ++s) undistort(u[s], v[s], dp);
+  }
+}
+
+__device__ __forceinline__ void rotate(const Pose& P, float u, float v, float o[3]) {
+  for (int i = 0; i < 3; ++i) {
+    float s = u * P.R[i][0];
+    s = s + v * P.R[i][1];
+    s = s + (-1.0f) * P.R[i][2];
+    o[i] = s;
+  }
+}
+
+__global__ void raygen_fwd_kernel(const int* __restrict__ coords, int64_t N, const float* __restrict__ fxs,
+                                  const float* __restrict__ fys, const float* __restrict__ cxs,
+                                  const float* __restrict__ cys, const float* __restrict__ c2w,
+                                  const float* __restrict__ dist, const float* __restrict__ mats, int mat_per_cam,
+                                  float off, float* __restrict__ origins, float* __restrict__ dirs,
+                                  float* __restrict__ ups, float* __restrict__ area, float* __restrict__ dnorm) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < N; r += (int64_t)gridDim.x * blockDim.x) {
+    const int c = coords[r * 3], yi = coords[r * 3 + 1], xi = coords[r * 3 + 2];
+    float u[3], v[3];
+    cam_coords(xi, yi, off, fxs[c], fys[c], cxs[c], cys[c], dist ? dist + c * 6 : nullptr, u, v);
+    const Pose P = compose(c2w + c * 12, mats + (mat_per_cam ? c * 12 : 0));
+    float w[3][3];
+    for (int s = 0; s < 3; ++s) {
+      float o[3];
+      rotate(P, u[s], v[s], o);
+      const float n = sqrtf(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+      if (s == 0 && dnorm) dnorm[r] = n;
+      const float dn = fmaxf(n, 1e-12f);
+      for (int i = 0; i < 3; ++i) w[s][i] = o[i] / dn;
+    }
+    for (int i = 0; i < 3; ++i) {
+      dirs[r * 3 + i] = w[0][i];
+      origins[r * 3 + i] = P.t[i];
+      if (ups) ups[r * 3 + i] = P.R[i][1];
+    }
+    if (area) {
+      float ax = 0.f, ay = 0.f;
+      for (int i = 0; i < 3; ++i) {
+        const float a = w[0][i] - w[1][i], b = w[0][i] - w[2][i];
+        ax = ax + a * a;
+        ay = ay + b * b;
+      }
+      area[r] = sqrtf(ax) * sqrtf(ay);
+    }
+  }
+}
+
+// dL/dmat (accumulated with atomics; per camera when mat_per_cam, else one shared matrix)
+__global__ __launch_bounds__(256) void raygen_bwd_kernel(const int* __restrict__ coords, int64_t N,
+                                                         const float* __restrict__ fxs, const float* __restrict__ fys,
+                                                         const float* __restrict__ cxs, const float* __restrict__ cys,
+                                                         const float* __restrict__ c2w,
+                                                         const float* __restrict__ dist,
+                                                         const float* __restrict__ mats, int mat_per_cam, float off,
+                                                         const float* __restrict__ dorig,
+                                                         const float* __restrict__ ddirs,
+                                                         const float* __restrict__ dups, float* __restrict__ dmats) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float g[12];
+  for (int k = 0; k < 12; ++k) g[k] = 0.f;
+  int cam = 0;
+  if (r < N) {
+    const int c = coords[r * 3], yi = coords[r * 3 + 1], xi = coords[r * 3 + 2];
+    cam = c;
+    float u[3], v[3];
+    cam_coords(xi, yi, off, fxs[c], fys[c], cxs[c], cys[c], dist ? dist + c * 6 : nullptr, u, v);
+    const float* A = c2w + c * 12;
+    const Pose P = compose(A, mats + (mat_per_cam ? c * 12 : 0));
+    float dR[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    float dt[3] = {0.f, 0.f, 0.f};
+    if (ddirs) {
+      float o[3];
+      rotate(P, u[0], v[0], o);
+      const float n = sqrtf(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+      const float gd[3] = {ddirs[r * 3], ddirs[r * 3 + 1], ddirs[r * 3 + 2]};
+      float dv[3];
+      if (n > 1e-12f) {
+        const float dot = (gd[0] * o[0] + gd[1] * o[1] + gd[2] * o[2]) / (n * n);
+        for (int i = 0; i < 3; ++i) dv[i] = (gd[i] - dot * o[i]) / n;
+      } else {
+        for (int i = 0; i < 3; ++i) dv[i] = gd[i] / 1e-12f;
+      }
+      const float dc[3] = {u[0], v[0], -1.0f};
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) dR[i][j] += dv[i] * dc[j];
+    }
+    if (dups) {
+      for (int i = 0; i < 3; ++i) dR[i][1] += dups[r * 3 + i];
+    }
+    if (dorig) {
+      for (int i = 0; i < 3; ++i) dt[i] = dorig[r * 3 + i];
+    }
+    // R = A_R M_R -> dM_R = A_R^T dR ; t = A_t + A_R M_t -> dM_t = A_R^T dt
+    for (int i = 0; i < 3; ++i) {
+      for (int j = 0; j < 3; ++j) {
+        g[i * 4 + j] = A[0 * 4 + i] * dR[0][j] + A[1 * 4 + i] * dR[1][j] + A[2 * 4 + i] * dR[2][j];
+      }
+      g[i * 4 + 3] = A[0 * 4 + i] * dt[0] + A[1 * 4 + i] * dt[1] + A[2 * 4 + i] * dt[2];
+    }
+  }
+  if (mat_per_cam) {
+    if (r < N)
+      for (int k = 0; k < 12; ++k) atomicAdd(dmats + cam * 12 + k, g[k]);
+    return;
+  }
+  // shared: reduce the block, 12 atomics per block
+  __shared__ float red[4][12];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int k = 0; k < 12; ++k) {
+    float s = g[k];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) red[w][k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < 12) {
+    const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(dmats + threadIdx.x, s);
+  }
+}
+
+// ------------------------------------------------------------------ collider
+__global__ void collider_fwd_kernel(const float* __restrict__ origins, const float* __restrict__ dirs, int64_t N,
+                                    float radius, float* __restrict__ nears, float* __restrict__ fars,
+                                    unsigned char* __restrict__ mask, float* __restrict__ bg_nears,
+                                    float* __restrict__ bg_fars) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < N; r += (int64_t)gridDim.x * blockDim.x) {
+    const float* o = origins + r * 3;
+    const float* d = dirs + r * 3;
+    float dot = d[0] * o[0];
+    dot = dot + d[1] * o[1];
+    dot = dot + d[2] * o[2];
+    const float on = sqrtf(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+    const float under = dot * dot - (on * on - radius * radius);
+    const bool hit = under > 0.01f;
+    const float sq = sqrtf(fmaxf(under, 0.01f));
+    const float nr = fmaxf(sq * -1.0f - dot, 0.01f);
+    const float fr = fmaxf(sq * 1.0f - dot, 0.01f);
+    nears[r] = nr;
+    fars[r] = fr;
+    mask[r] = hit ? 1 : 0;
+    if (bg_nears) bg_nears[r] = hit ? fr : nr;
+    if (bg_fars) bg_fars[r] = fr + 3.0f;
+  }
+}
+
+// d near / d far (full-length [N] arrays, may be null) -> d origins, d dirs (accumulate)
+__global__ void collider_bwd_kernel(const float* __restrict__ origins, const float* __restrict__ dirs, int64_t N,
+                                    float radius, const float* __restrict__ dnears, const float* __restrict__ dfars,
+                                    const float* __restrict__ dbg_nears, const float* __restrict__ dbg_fars,
+                                    float* __restrict__ dorig, float* __restrict__ ddirs) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < N; r += (int64_t)gridDim.x * blockDim.x) {
+    const float* o = origins + r * 3;
+    const float* d = dirs + r * 3;
+    float dot = d[0] * o[0];
+    dot = dot + d[1] * o[1];
+    dot = dot + d[2] * o[2];
+    const float on = sqrtf(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+    const float under = dot * dot - (on * on - radius * radius);
+    const bool hit = under > 0.01f;
+    const float sq = sqrtf(fmaxf(under, 0.01f));
+    const float nraw = sq * -1.0f - dot, fraw = sq * 1.0f - dot;
+    float dn = dnears ? dnears[r] : 0.f;
+    float df = dfars ? dfars[r] : 0.f;
+    if (dbg_nears) { if (hit) df += dbg_nears[r]; else dn += dbg_nears[r]; }
+    if (dbg_fars) df += dbg_fars[r];
+    if (!(nraw >= 0.01f)) dn = 0.f;
+    if (!(fraw >= 0.01f)) df = 0.f;
+    const float dsq = -dn + df;
+    float ddot = -dn - df;
+    float dunder = (under >= 0.01f) ? dsq * 0.5f / sq : 0.f;
+    ddot += 2.0f * dot * dunder;
+    const float don = -2.0f * on * dunder;
+    for (int c = 0; c < 3; ++c) {
+      float go = ddot * d[c];
+      if (on > 0.f) go += don * o[c] / on;
+      dorig[r * 3 + c] += go;
+      ddirs[r * 3 + c] += ddot * o[c];
+    }
+  }
+}
+
+// order-preserving compaction of mask -> idx (int64), count; single block, chunked scan
+__global__ __launch_bounds__(1024) void compact_kernel(const unsigned char* __restrict__ mask, int64_t N,
+                                                       int64_t* __restrict__ idx, int64_t* __restrict__ count) {
+  __shared__ int64_t base;
+  __shared__ int wsum[16];
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int64_t start = 0; start < N; start += blockDim.x) {
+    const int64_t i = start + threadIdx.x;
+    const int f = (i < N && mask[i]) ? 1 : 0;
+    const unsigned long long bal = __ballot(f);
+    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int off = 0;
+    for (int k = 0; k < w; ++k) off += wsum[k];
+    if (f) idx[base + off + pre] = i;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int k = 0; k < (int)(blockDim.x >> 6); ++k) tot += wsum[k];
+      base += tot;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) count[0] = base;
+}
+
+}  // namespace
+
+MMS_EXPORT int mms_raygen_fwd(const int* coords, int64_t N, const float* fx, const float* fy, const float* cx,
+                              const float* cy, const float* c2w, const float* dist, const float* mats, int mat_per_cam,
+                              float pixel_offset, float* origins, float* dirs, float* ups, float* area, float* dnorm,
+                              void* stream) {
+  const char* fn = "mms_raygen_fwd";
+  if (N == 0) return 0;
+  MMS_REQUIRE(coords && c2w && mats && origins && dirs, fn, "null pointer");
+  hipLaunchKernelGGL(raygen_fwd_kernel, dim3(mms::grid_for(N, 256, 16384)), dim3(256), 0, mms::as_stream(stream),
+                     coords, N, fx, fy, cx, cy, c2w, dist, mats, mat_per_cam, pixel_offset, origins, dirs, ups, area,
+                     dnorm);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_raygen_bwd(const int* coords, int64_t N, const float* fx, const float* fy, const float* cx,
+                              const float* cy, const float* c2w, const float* dist, const float* mats, int mat_per_cam,
+                              float pixel_offset, const float* dorig, const float* ddirs, const float* dups,
+                              float* dmats, void* stream) {
+  const char* fn = "mms_raygen_bwd";
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(raygen_bwd_kernel, dim3(mms::grid_for(N, 256, INT32_MAX)), dim3(256), 0, mms::as_stream(stream),
+                     coords, N, fx, fy, cx, cy, c2w, dist, mats, mat_per_cam, pixel_offset, dorig, ddirs, dups, dmats);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_collider_fwd(const float* origins, const float* dirs, int64_t N, float radius, float* nears,
+                                float* fars, unsigned char* mask, float* bg_nears, float* bg_fars, void* stream) {
+  const char* fn = "mms_collider_fwd";
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(collider_fwd_kernel, dim3(mms::grid_for(N, 256, 16384)), dim3(256), 0, mms::as_stream(stream),
+                     origins, dirs, N, radius, nears, fars, mask, bg_nears, bg_fars);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_collider_bwd(const float* origins, const float* dirs, int64_t N, float radius, const float* dnears,
+                                const float* dfars, const float* dbg_nears, const float* dbg_fars, float* dorig,
+                                float* ddirs, void* stream) {
+  const char* fn = "mms_collider_bwd";
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(collider_bwd_kernel, dim3(mms::grid_for(N, 256, 16384)), dim3(256), 0, mms::as_stream(stream),
+                     origins, dirs, N, radius, dnears, dfars, dbg_nears, dbg_fars, dorig, ddirs);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_compact(const unsigned char* mask, int64_t N, int64_t* idx, int64_t* count, void* stream) {
+  const char* fn = "mms_compact";
+  hipLaunchKernelGGL(compact_kernel, dim3(1), dim3(1024), 0, mms::as_stream(stream), mask, N, idx, count);
+  return mms::check_launch(fn);
+}

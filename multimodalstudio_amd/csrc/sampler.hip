@@ -1,0 +1,288 @@
+// Ray-sampling kernels: stratified bins, spacing -> euclidean samples (+ backward to near/far and
+// the ray), and the NeuS importance up-sampling step.
+//
+// Reference (paths under /root/reference/src/model_components/ray_samplers.py):
+//   SpacedSampler.generate_ray_samples :183-233   (uniform: g = id, disparity: g = 1/x)
+//   spacing_to_euclidean_fn             :178-181   e = g^-1(g(far) b + g(near) (1 - b))
+//   NeuSSampler.generate_ray_samples    :464-514   4 iterations, inv_s = 64 * 2^i
+//   rendering_sdf_with_fixed_inv_s      :516-551
+//   PDFSampler.generate_ray_samples     :357-403   (include_original=False, padding 1e-5, single jitter)
+//   merge_ray_samples                   :38-68     (sort of the two start lists + max end)
+// and cameras/rays.py:201-217 (weights from alphas), :69-81 (start positions o + d * start).
+//
+// Bin values depend only on float32 arithmetic performed in the reference's order (no contraction);
+// the PDF cumulative sums and transmittance products are sequential like torch.cumsum / cumprod on
+// CPU, so searchsorted indices and merge order (sorted_index) match the reference.
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// stratified bins: lin [S+1]; t either per ray ([R,1], tstride=1, tcols=1) or per bin ([R, S+1])
+__global__ void stratified_bins_kernel(const float* __restrict__ lin, int nb, const float* __restrict__ t, int tcols,
+                                       int64_t R, float* __restrict__ bins) {
+  const int64_t total = R * nb;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / nb;
+    const int k = (int)(e - r * nb);
+    if (t == nullptr) { bins[e] = lin[k]; continue; }
+    const float tk = t[r * tcols + (tcols == 1 ? 0 : k)];
+    // centers c_k = (b_{k+1} + b_k) / 2 ; upper = [c_0..c_{n-2}, b_{n-1}] ; lower = [b_0, c_0..c_{n-2}]
+    const float upper = (k < nb - 1) ? (lin[k + 1] + lin[k]) / 2.0f : lin[nb - 1];
+    const float lower = (k > 0) ? (lin[k] + lin[k - 1]) / 2.0f : lin[0];
+    bins[e] = lower + (upper - lower) * tk;
+  }
+}
+
+__device__ __forceinline__ float to_euclid(float b, float nr, float fr, int kind) {
+  if (kind == 0) return fr * b + nr * (1 - b);
+  const float sn = 1.0f / nr, sf = 1.0f / fr;
+  return 1.0f / (sf * b + sn * (1 - b));
+}
+
+// de/dnear, de/dfar for a bin value b
+__device__ __forceinline__ void euclid_grad(float b, float nr, float fr, int kind, float& dn, float& df) {
+  if (kind == 0) { dn = 1 - b; df = b; return; }
+  const float sn = 1.0f / nr, sf = 1.0f / fr;
+  const float A = sf * b + sn * (1 - b);
+  const float iA2 = 1.0f / (A * A);
+  dn = iA2 * (1 - b) / (nr * nr);
+  df = iA2 * b / (fr * fr);
+}
+
+// bins [R, nb] (ldb) -> starts/ends/deltas [R, S = nb-1] and positions [R*S, 3]
+__global__ void samples_fwd_kernel(const float* __restrict__ bins, int64_t ldb, int nb, const float* __restrict__ nears,
+                                   const float* __restrict__ fars, const float* __restrict__ origins,
+                                   const float* __restrict__ dirs, int kind, int64_t R, float* __restrict__ starts,
+                                   float* __restrict__ ends, float* __restrict__ deltas, float* __restrict__ pos) {
+  const int S = nb - 1;
+  const int64_t total = R * S;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / S;
+    const int k = (int)(e - r * S);
+    const float nr = nears[r], fr = fars[r];
+    const float s0 = to_euclid(bins[r * ldb + k], nr, fr, kind);
+    const float s1 = to_euclid(bins[r * ldb + k + 1], nr, fr, kind);
+    if (starts) starts[e] = s0;
+    if (ends) ends[e] = s1;
+    if (deltas) deltas[e] = s1 - s0;
+    if (pos) {
+      const float* o = origins + r * 3;
+      const float* d = dirs + r * 3;
+      pos[e * 3] = o[0] + d[0] * s0;
+      pos[e * 3 + 1] = o[1] + d[1] * s0;
+      pos[e * 3 + 2] = o[2] + d[2] * s0;
+    }
+  }
+}
+
+// backward: one wave per ray, lane = bin edge (nb <= 65: the last edge handled by lane 0)
+__global__ __launch_bounds__(256) void samples_bwd_kernel(const float* __restrict__ bins, int64_t ldb, int nb,
+                                                          const float* __restrict__ nears,
+                                                          const float* __restrict__ fars,
+                                                          const float* __restrict__ dirs, int kind, int64_t R,
+                                                          const float* __restrict__ dpos,
+                                                          const float* __restrict__ ddeltas,
+                                                          const float* __restrict__ dstarts,
+                                                          float* __restrict__ dnears, float* __restrict__ dfars,
+                                                          float* __restrict__ dorigins, float* __restrict__ ddirs) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;
+  const int S = nb - 1;
+  const float nr = nears[r], fr = fars[r];
+  const float* d = dirs + r * 3;
+  float gn = 0.f, gf = 0.f, go0 = 0.f, go1 = 0.f, go2 = 0.f, gd0 = 0.f, gd1 = 0.f, gd2 = 0.f;
+  for (int k = lane; k < nb; k += 64) {
+    const float b = bins[r * ldb + k];
+    const float e = to_euclid(b, nr, fr, kind);
+    float de = 0.f;
+    if (k < S) {
+      const int64_t i = r * S + k;
+      if (dpos) {
+        const float p0 = dpos[i * 3], p1 = dpos[i * 3 + 1], p2 = dpos[i * 3 + 2];
+        go0 += p0; go1 += p1; go2 += p2;
+        gd0 += p0 * e; gd1 += p1 * e; gd2 += p2 * e;
+        de += p0 * d[0] + p1 * d[1] + p2 * d[2];
+      }
+      if (ddeltas) de -= ddeltas[i];
+      if (dstarts) de += dstarts[i];
+    }
+    if (k > 0 && ddeltas) de += ddeltas[r * S + k - 1];
+    float dn, df;
+    euclid_grad(b, nr, fr, kind, dn, df);
+    gn += de * dn;
+    gf += de * df;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    gn += __shfl_xor(gn, o); gf += __shfl_xor(gf, o);
+    go0 += __shfl_xor(go0, o); go1 += __shfl_xor(go1, o); go2 += __shfl_xor(go2, o);
+    gd0 += __shfl_xor(gd0, o); gd1 += __shfl_xor(gd1, o); gd2 += __shfl_xor(gd2, o);
+  }
+  if (lane == 0) {
+    if (dnears) dnears[r] += gn;
+    if (dfars) dfars[r] += gf;
+    if (dorigins) { dorigins[r * 3] += go0; dorigins[r * 3 + 1] += go1; dorigins[r * 3 + 2] += go2; }
+    if (ddirs) { ddirs[r * 3] += gd0; ddirs[r * 3 + 1] += gd1; ddirs[r * 3 + 2] += gd2; }
+  }
+}
+
+// ------------------------------------------------------------------ NeuS up-sampling step (one thread per ray)
+constexpr int kMaxBins = 80;
+
+__global__ __launch_bounds__(64) void neus_step_kernel(
+    int64_t R, int S, const float* __restrict__ bins, const float* __restrict__ sdf_prev, int s_prev,
+    const float* __restrict__ sdf_new, int n_prev_new, const int* __restrict__ prev_idx,
+    const float* __restrict__ nears, const float* __restrict__ fars, float inv_s, const float* __restrict__ rand,
+    const float* __restrict__ u_lin, int n_new, float* __restrict__ sdf_out, float* __restrict__ new_bins,
+    float* __restrict__ merged_bins, int* __restrict__ sorted_idx) {
+  __shared__ float s_cdf[64][kMaxBins + 1];
+  __shared__ float s_sdf[64][kMaxBins];
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  float* cdf = s_cdf[threadIdx.x];
+  float* sdf = s_sdf[threadIdx.x];
+  const float* b = bins + r * (S + 1);
+  // (a) merged sdf for the current samples
+  for (int j = 0; j < S; ++j) {
+    float v;
+    if (prev_idx) {
+      const int id = prev_idx[r * S + j];
+      v = id < s_prev ? sdf_prev[r * s_prev + id] : sdf_new[r * n_prev_new + (id - s_prev)];
+    } else {
+      v = sdf_new[r * S + j];
+    }
+    sdf[j] = v;
+    sdf_out[r * S + j] = v;
+  }
+  const float nr = nears[r], fr = fars[r];
+  // (b-d) fixed-inv_s alphas and weights (w_{S-1} = 0), sequential cumprod
+  // torch.cumprod / cumsum on CPU accumulate in double (at::acc_type<float, false>) and round each
+  // output to float: do the same so the CDF (and hence searchsorted) matches.
+  double T = 1.0;
+  float prev_cos = 0.0f;
+  float e_cur = fr * b[0] + nr * (1 - b[0]);
+  for (int k = 0; k < S - 1; ++k) {
+    const float e_nxt = fr * b[k + 1] + nr * (1 - b[k + 1]);
+    const float dl = e_nxt - e_cur;
+    e_cur = e_nxt;
+    const float pv = sdf[k], nx = sdf[k + 1];
+    const float mid = (pv + nx) * 0.5f;
+    float cs = (nx - pv) / (dl + 1e-5f);
+    float cmin = fminf(prev_cos, cs);
+    prev_cos = cs;
+    cmin = fminf(fmaxf(cmin, -1e3f), 0.0f);
+    const float pe = mid - cmin * dl * 0.5f;
+    const float ne = mid + cmin * dl * 0.5f;
+    const float pc = sigm(pe * inv_s), nc = sigm(ne * inv_s);
+    const float alpha = (pc - nc + 1e-5f) / (pc + 1e-5f);
+    const float w = alpha * (float)T;
+    T = T * (double)(1.0f - alpha + 1e-7f);
+    cdf[k + 1] = w;  // stash weights (shifted by one)
+  }
+  cdf[S] = 0.0f;
+  // (e) pdf / cdf with padding 1e-5 (histogram_padding) and eps 1e-5
+  float wsum = 0.f;
+  for (int k = 0; k < S; ++k) {
+    const float w = cdf[k + 1] + 1e-5f;
+    cdf[k + 1] = w;
+    wsum = wsum + w;
+  }
+  const float pad = fmaxf(1e-5f - wsum, 0.f);
+  const float padk = pad / (float)S;
+  wsum = wsum + pad;
+  double run = 0.0;
+  cdf[0] = 0.f;
+  for (int k = 0; k < S; ++k) {
+    const float w = cdf[k + 1] + padk;
+    run = run + (double)(w / wsum);
+    cdf[k + 1] = fminf(1.0f, (float)run);
+  }
+  // (f-g) inverse CDF at u_j = lin_j + rand / nb (searchsorted right)
+  const int nb = n_new + 1;
+  const float rj = rand ? rand[r] / (float)nb : 0.0f;
+  float* nbo = new_bins + r * nb;
+  for (int j = 0; j < nb; ++j) {
+    const float u = rand ? u_lin[j] + rj : u_lin[j];
+    int lo = 0, hi = S + 1;  // first index with cdf > u
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cdf[mid] > u) hi = mid; else lo = mid + 1;
+    }
+    const int inds = lo;
+    const int below = min(max(inds - 1, 0), S);
+    const int above = min(max(inds, 0), S);
+    const float c0 = cdf[below], c1 = cdf[above];
+    const float b0 = b[below], b1 = b[above];
+    float t = (u - c0) / (c1 - c0);
+    if (isnan(t)) t = 0.f;
+    t = fminf(fmaxf(t, 0.f), 1.f);
+    nbo[j] = b0 + t * (b1 - b0);
+  }
+  // (h) stable merge of the start lists; end = max of the ends
+  float* mb = merged_bins + r * (S + n_new + 1);
+  int* si = sorted_idx + r * (S + n_new);
+  int i1 = 0, i2 = 0, o = 0;
+  while (i1 < S || i2 < n_new) {
+    bool take1;
+    if (i1 >= S) take1 = false;
+    else if (i2 >= n_new) take1 = true;
+    else take1 = !(nbo[i2] < b[i1]);  // ties keep the first list first (stable)
+    if (take1) { mb[o] = b[i1]; si[o] = i1; ++i1; }
+    else { mb[o] = nbo[i2]; si[o] = S + i2; ++i2; }
+    ++o;
+  }
+  mb[S + n_new] = fmaxf(b[S], nbo[n_new]);
+}
+
+}  // namespace
+
+MMS_EXPORT int mms_stratified_bins(const float* lin, int nb, const float* t, int tcols, int64_t R, float* bins,
+                                   void* stream) {
+  const char* fn = "mms_stratified_bins";
+  if (R == 0) return 0;
+  hipLaunchKernelGGL(stratified_bins_kernel, dim3(mms::grid_for(R * nb, 256, 16384)), dim3(256), 0,
+                     mms::as_stream(stream), lin, nb, t, tcols, R, bins);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_samples_fwd(const float* bins, int64_t ldb, int nb, const float* nears, const float* fars,
+                               const float* origins, const float* dirs, int kind, int64_t R, float* starts, float* ends,
+                               float* deltas, float* pos, void* stream) {
+  const char* fn = "mms_samples_fwd";
+  MMS_REQUIRE(nb >= 2, fn, "need at least two bin edges");
+  if (R == 0) return 0;
+  hipLaunchKernelGGL(samples_fwd_kernel, dim3(mms::grid_for(R * (nb - 1), 256, 16384)), dim3(256), 0,
+                     mms::as_stream(stream), bins, ldb, nb, nears, fars, origins, dirs, kind, R, starts, ends, deltas,
+                     pos);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_samples_bwd(const float* bins, int64_t ldb, int nb, const float* nears, const float* fars,
+                               const float* dirs, int kind, int64_t R, const float* dpos, const float* ddeltas,
+                               const float* dstarts, float* dnears, float* dfars, float* dorigins, float* ddirs,
+                               void* stream) {
+  const char* fn = "mms_samples_bwd";
+  if (R == 0) return 0;
+  hipLaunchKernelGGL(samples_bwd_kernel, dim3(mms::grid_for(R * 64, 256, INT32_MAX)), dim3(256), 0,
+                     mms::as_stream(stream), bins, ldb, nb, nears, fars, dirs, kind, R, dpos, ddeltas, dstarts, dnears,
+                     dfars, dorigins, ddirs);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_neus_step(int64_t R, int S, const float* bins, const float* sdf_prev, int s_prev,
+                             const float* sdf_new, int n_prev_new, const int* prev_idx, const float* nears,
+                             const float* fars, float inv_s, const float* rand, const float* u_lin, int n_new,
+                             float* sdf_out, float* new_bins, float* merged_bins, int* sorted_idx, void* stream) {
+  const char* fn = "mms_neus_step";
+  MMS_REQUIRE(S >= 2 && S + n_new <= kMaxBins, fn, "sample count out of range");
+  if (R == 0) return 0;
+  hipLaunchKernelGGL(neus_step_kernel, dim3(mms::grid_for(R, 64, INT32_MAX)), dim3(64), 0, mms::as_stream(stream), R,
+                     S, bins, sdf_prev, s_prev, sdf_new, n_prev_new, prev_idx, nears, fars, inv_s, rand, u_lin, n_new,
+                     sdf_out, new_bins, merged_bins, sorted_idx);
+  return mms::check_launch(fn);
+}

@@ -1,0 +1,722 @@
+"""Fused autograd stages of the hot path, each a small chain of libmms_hip.so kernels.
+
+Every Function restates one stage of the reference's per-ray computation with an explicit backward
+(paths under /root/reference/src):
+
+  SurfaceFunction     SDFField + 4-tap numerical gradient (surface_model.py:66-153; surface_field.py:99-116)
+  RadianceFunction    RadianceModel input assembly + RadianceField (radiance_model.py:94-141; radiance_field.py:72-77)
+  BackgroundFunction  BackgroundModel NeRF field (background_model.py:73-99; nerf_field.py:92-105)
+  NeusWeightsFunction NeuSVolumeRendering (volume_rendering.py:171-213)
+  DensityWeightsFunction RaySamples.get_alphas + get_weights_from_alphas (rays.py:138-217)
+  CompositeFunction   RadianceRenderer / background sum (renderers.py:152-174; background_model.py:101-109)
+  SamplesFunction     spacing bins -> euclidean samples (ray_samplers.py:178-181; rays.py:69-81, 304-349)
+  RaysFunction        Cameras.generate_rays with pose refinement (cameras.py:460-703)
+  ColliderFunction    SphereCollider + background near/far (scene_colliders.py:60-113)
+  PolarizerFunction   PolarizationHead Stokes alignment (field_heads.py:90-106; polarizer.py:54-101)
+  L1LossFunction / GeoLossFunction   losses.py:68-164
+
+There is no CPU path: every function requires HIP device tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from .hip_ops import NN, NT, TN, _splits_for, act_bwd, colsum_, gemm, weight_norm_bwd, weight_norm_fwd
+
+ACT = {None: 0, "None": 0, "ReLU": 1, "Softplus": 2, "Sigmoid": 3}
+
+
+def _s() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _f32arr(vals):
+    return ctypes.cast((ctypes.c_float * len(vals))(*[float(v) for v in vals]), ctypes.c_void_p)
+
+
+class GridCfg:
+    """Static description of one FeatureGrid(HashEncoding) (encodings.py:48-67, feature_structures.py:28-45)."""
+
+    def __init__(self, scales: Sequence[float], log2T: int, radius: float, features: int = 2):
+        self.scales = [float(s) for s in scales]
+        self.L = len(self.scales)
+        self.log2T = int(log2T)
+        self.radius = float(radius)
+        self.F = int(features)
+        self._arr = (ctypes.c_float * self.L)(*self.scales)
+
+    @property
+    def scales_ptr(self):
+        return ctypes.cast(self._arr, ctypes.c_void_p)
+
+    @property
+    def out_dim(self):
+        return self.L * self.F
+
+
+def grid_fwd(g: GridCfg, pos: torch.Tensor, ldx: int, M: int, table, active: int, out: torch.Tensor, col: int):
+    _lib.call("mms_hashgrid_fwd", pos.data_ptr(), M, ldx, table.data_ptr(), g.L, g.log2T, g.F, g.scales_ptr,
+              g.radius, active, out.data_ptr() + 4 * col, out.stride(0), _s())
+
+
+def grid_bwd(g: GridCfg, pos, ldx, M, table, active, dout: torch.Tensor, col: int, dtable, dpos):
+    _lib.call("mms_hashgrid_bwd", pos.data_ptr(), M, ldx, table.data_ptr(), g.L, g.log2T, g.F, g.scales_ptr,
+              g.radius, active, dout.data_ptr() + 4 * col, dout.stride(0), _p(dtable), _p(dpos),
+              0 if dpos is None else dpos.stride(0), _s())
+
+
+# ------------------------------------------------------------------------------------------------
+# MLP core (shared by the fused field functions)
+# ------------------------------------------------------------------------------------------------
+class MLPRun:
+    """Forward activations of a weight-normed MLP kept for the explicit backward."""
+
+    def __init__(self, params: Sequence[torch.Tensor], acts: Sequence[Tuple[int, float, float]]):
+        self.params = list(params)
+        self.acts = list(acts)
+        self.L = len(self.params) // 3
+        self.Ws: List[torch.Tensor] = []
+        self.norms: List[torch.Tensor] = []
+        self.Zs: List[Optional[torch.Tensor]] = []
+        self.Ys: List[torch.Tensor] = []
+        self.x = None
+
+    def forward(self, x: torch.Tensor, keep: bool, last_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        M = x.shape[0]
+        self.x = x
+        h = x
+        dev = x.device
+        for l in range(self.L):
+            g, v, b = self.params[3 * l: 3 * l + 3]
+            N, K = v.shape
+            W = torch.empty(N, K, device=dev)
+            nrm = torch.empty(N, device=dev)
+            weight_norm_fwd(g.reshape(-1), v, W, nrm)
+            act, beta, thr = self.acts[l]
+            if l == self.L - 1 and last_out is not None:
+                Y = last_out
+            else:
+                Y = torch.empty(M, N, device=dev)
+            Z = torch.empty(M, N, device=dev) if (keep and act != 0) else None
+            gemm(NT, M, N, K, h, h.stride(0), W, W.stride(0), Y, Y.stride(0), bias=b, Z=Z, ldz=N, act=act, beta=beta,
+                 thr=thr)
+            if keep:
+                self.Ws.append(W)
+                self.norms.append(nrm)
+                self.Zs.append(Z)
+                self.Ys.append(Y)
+            h = Y
+        return h
+
+    def backward(self, dy: torch.Tensor, need_dx: bool) -> Tuple[Optional[torch.Tensor], List[torch.Tensor]]:
+        x = self.x
+        M = x.shape[0]
+        dev = x.device
+        grads: List[Optional[torch.Tensor]] = [None] * len(self.params)
+        act, beta, thr = self.acts[self.L - 1]
+        if act != 0:
+            dZ = torch.empty(M, dy.shape[1], device=dev)
+            act_bwd(dy, self.Zs[-1], act, beta, thr, dZ)
+        else:
+            dZ = dy
+        dx = None
+        for l in range(self.L - 1, -1, -1):
+            g, v, b = self.params[3 * l: 3 * l + 3]
+            N, K = v.shape
+            Xin = x if l == 0 else self.Ys[l - 1]
+            dW = torch.zeros(N, K, device=dev)
+            tiles = ((N + 127) // 128) * ((K + 127) // 128)
+            gemm(TN, N, K, M, dZ, dZ.stride(0), Xin, Xin.stride(0), dW, K, accumulate=True,
+                 splits=_splits_for(M, tiles))
+            db = torch.zeros(N, device=dev)
+            colsum_(dZ, db)
+            dg = torch.zeros(N, device=dev)
+            dv = torch.zeros(N, K, device=dev)
+            weight_norm_bwd(g.reshape(-1), v, self.norms[l], dW, dg, dv)
+            grads[3 * l], grads[3 * l + 1], grads[3 * l + 2] = dg.view_as(g), dv, db
+            if l > 0:
+                pa, pbeta, pthr = self.acts[l - 1]
+                dprev = torch.empty(M, K, device=dev)
+                gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[l], K, dprev, K,
+                     aux=self.Zs[l - 1] if pa != 0 else None, ldaux=K, dact=pa, beta=pbeta, thr=pthr)
+                dZ = dprev
+            elif need_dx:
+                dx = torch.empty(M, K, device=dev)
+                gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[0], K, dx, K)
+        return dx, grads
+
+
+# ------------------------------------------------------------------------------------------------
+# surface field (SDF + taps)
+# ------------------------------------------------------------------------------------------------
+SDF_ACTS = ((2, 100.0, 20.0), (2, 100.0, 20.0), (0, 1.0, 20.0))
+
+
+class SurfaceFunction(torch.autograd.Function):
+    """pos [M,3] -> (sdf [M,1], geo [M,G], grads [M,3], hess [M,3], normals [M,3]).
+
+    Rows of the MLP batch: [centre M | 4 x taps M]; panel columns [x(3), PE-tail(36), grid(32)].
+    `delta` is the tap offset numerical_gradients_delta / sqrt(3) (surface_model.py:138).
+    """
+
+    @staticmethod
+    def forward(ctx, pos, table, grid: GridCfg, active: int, delta: float, *params):
+        M = pos.shape[0]
+        dev = pos.device
+        pos = pos.contiguous()
+        K0 = 3 + 36 + grid.out_dim
+        X = torch.empty(5 * M, K0, device=dev)
+        d32 = float(torch.tensor(delta, dtype=torch.float32))
+        _lib.call("mms_geo_input_fwd", pos.data_ptr(), 3, M, 4, d32, 6, X.data_ptr(), K0, _s())
+        grid_fwd(grid, X, K0, 5 * M, table, active, X, 39)
+        run = MLPRun(params, SDF_ACTS)
+        out = run.forward(X, keep=True)
+        G = out.shape[1] - 1
+        four_delta = float(torch.tensor(4.0 * delta, dtype=torch.float32))
+        delta_sq = float(torch.tensor(delta ** 2, dtype=torch.float32))
+        grads = torch.empty(M, 3, device=dev)
+        hess = torch.empty(M, 3, device=dev)
+        normals = torch.empty(M, 3, device=dev)
+        _lib.call("mms_taps_combine_fwd", out.data_ptr(), out.stride(0), M, four_delta, delta_sq, grads.data_ptr(),
+                  hess.data_ptr(), normals.data_ptr(), _s())
+        sdf = out[:M, 0:1].contiguous()
+        geo = out[:M, 1:].contiguous()
+        ctx.grid, ctx.active, ctx.M, ctx.G = grid, active, M, G
+        ctx.four_delta, ctx.delta_sq = four_delta, delta_sq
+        ctx.run = run
+        ctx.X = X
+        ctx.save_for_backward(pos, table, grads, *params)
+        return sdf, geo, grads, hess, normals
+
+    @staticmethod
+    def backward(ctx, dsdf, dgeo, dgrads, dhess, dnormals):
+        pos, table, grads, *params = ctx.saved_tensors
+        M, G = ctx.M, ctx.G
+        dev = pos.device
+        dout = torch.zeros(5 * M, G + 1, device=dev)
+        _lib.call("mms_taps_combine_bwd", grads.data_ptr(), _p(dgrads if dgrads is not None else None),
+                  _p(dhess), _p(dnormals), M, ctx.four_delta, ctx.delta_sq, dout.data_ptr(), dout.stride(0), _s())
+        if dsdf is not None:
+            dout[:M, 0:1] += dsdf
+        if dgeo is not None:
+            dout[:M, 1:] = dgeo
+        need_table = ctx.needs_input_grad[1]
+        need_pos = ctx.needs_input_grad[0]
+        dX, pgrads = ctx.run.backward(dout, need_dx=True)
+        X = ctx.X
+        K0 = X.shape[1]
+        dtable = torch.zeros_like(table) if need_table else None
+        dP = torch.zeros(5 * M, 3, device=dev) if need_pos else None
+        grid_bwd(ctx.grid, X, K0, 5 * M, table, ctx.active, dX, 39, dtable, dP)
+        dpos = None
+        if need_pos:
+            dpos = torch.zeros(M, 3, device=dev)
+            _lib.call("mms_geo_input_bwd", X.data_ptr(), K0, dX.data_ptr(), dX.stride(0), dP.data_ptr(), 3, M, 4, 6,
+                      dpos.data_ptr(), 3, _s())
+        ctx.run = None
+        ctx.X = None
+        return (dpos, dtable, None, None, None, *pgrads)
+
+
+def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> torch.Tensor:
+    """Inference SDF (SurfaceModel.get_sdf, surface_model.py:213-226; evaluated under no_grad by the sampler)."""
+    M = pos.shape[0]
+    dev = pos.device
+    K0 = 3 + 36 + grid.out_dim
+    X = torch.empty(M, K0, device=dev)
+    _lib.call("mms_geo_input_fwd", pos.data_ptr(), pos.stride(0), M, 0, 0.0, 6, X.data_ptr(), K0, _s())
+    grid_fwd(grid, X, K0, M, table, active, X, 39)
+    # only the sdf column of the last layer is needed
+    last = list(params[-3:])
+    g, v, b = last
+    p2 = list(params[:-3]) + [g[:1], v[:1].contiguous(), b[:1]]
+    run = MLPRun(p2, SDF_ACTS)
+    out = run.forward(X, keep=False)
+    return out[:, 0]
+
+
+# ------------------------------------------------------------------------------------------------
+# radiance field
+# ------------------------------------------------------------------------------------------------
+RAD_ACTS = ((1, 1.0, 20.0), (1, 1.0, 20.0), (1, 1.0, 20.0))
+
+
+class RadianceFunction(torch.autograd.Function):
+    """(pos [M,3], dirs [R,3], normals [M,3] (detached), geo [M,G], table) -> feature [M,256]."""
+
+    @staticmethod
+    def forward(ctx, pos, dirs, normals, geo, table, grid: GridCfg, active: int, S: int, *params):
+        M = pos.shape[0]
+        G = geo.shape[1]
+        dev = pos.device
+        K0 = 3 + 25 + G + 1 + grid.out_dim
+        X = torch.empty(M, K0, device=dev)
+        pos = pos.contiguous()
+        dirs = dirs.contiguous()
+        normals = normals.contiguous()
+        geo = geo.contiguous()
+        _lib.call("mms_rad_input_fwd", pos.data_ptr(), 3, dirs.data_ptr(), normals.data_ptr(), geo.data_ptr(),
+                  geo.stride(0), M, S, G, X.data_ptr(), K0, _s())
+        grid_fwd(grid, X, K0, M, table, active, X, 29 + G)
+        run = MLPRun(params, RAD_ACTS)
+        feat = run.forward(X, keep=True)
+        ctx.run, ctx.X, ctx.grid, ctx.active, ctx.S, ctx.G = run, X, grid, active, S, G
+        ctx.save_for_backward(pos, dirs, normals, table, *params)
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        pos, dirs, normals, table, *params = ctx.saved_tensors
+        M, S, G = pos.shape[0], ctx.S, ctx.G
+        R = M // S
+        dev = pos.device
+        dX, pgrads = ctx.run.backward(dfeat.contiguous(), need_dx=True)
+        X = ctx.X
+        K0 = X.shape[1]
+        dtable = torch.zeros_like(table) if ctx.needs_input_grad[4] else None
+        need_pos = ctx.needs_input_grad[0]
+        dP = torch.zeros(M, 3, device=dev) if need_pos else None
+        grid_bwd(ctx.grid, X, K0, M, table, ctx.active, dX, 29 + G, dtable, dP)
+        dpos = torch.zeros(M, 3, device=dev) if need_pos else None
+        dgeo = torch.empty(M, G, device=dev) if ctx.needs_input_grad[3] else None
+        ddirs = torch.zeros(R, 3, device=dev) if ctx.needs_input_grad[1] else None
+        _lib.call("mms_rad_input_bwd", dX.data_ptr(), dX.stride(0), _p(dP), 3, dirs.data_ptr(), normals.data_ptr(), R,
+                  S, G, _p(dpos), 3, _p(dgeo), G, _p(ddirs), _s())
+        ctx.run = None
+        ctx.X = None
+        return (dpos, ddirs, None, dgeo, dtable, None, None, None, *pgrads)
+
+
+# ------------------------------------------------------------------------------------------------
+# plain MLP (heads)
+# ------------------------------------------------------------------------------------------------
+class MLPFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, acts, *params):
+        run = MLPRun(params, acts)
+        # grad mode is off inside Function.forward: decide from what the graph will need
+        y = run.forward(x.contiguous(), keep=any(ctx.needs_input_grad))
+        ctx.run = run
+        ctx.save_for_backward(*params)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx, grads = ctx.run.backward(dy.contiguous(), need_dx=ctx.needs_input_grad[0])
+        ctx.run = None
+        return (dx, None, *grads)
+
+
+# ------------------------------------------------------------------------------------------------
+# background NeRF field: contraction + PE -> base MLP -> density head ; [feat, PE(d)] -> head MLP
+# ------------------------------------------------------------------------------------------------
+BG_BASE_ACTS = ((1, 1.0, 20.0),) * 4
+BG_DENS_ACTS = ((2, 1.0, 20.0),)
+BG_HEAD_ACTS = ((1, 1.0, 20.0),) * 4
+
+
+class BackgroundFunction(torch.autograd.Function):
+    """pos [M,3] (raw sample starts), dirs [R,3] -> density [M,1], feature [M,128]."""
+
+    @staticmethod
+    def forward(ctx, pos, dirs, S: int, nb: int, nd: int, *params):
+        M = pos.shape[0]
+        dev = pos.device
+        base_p, dens_p, head_p = params[:3 * nb], params[3 * nb:3 * (nb + nd)], params[3 * (nb + nd):]
+        X = torch.empty(M, 39, device=dev)
+        Fb = base_p[-2].shape[0]
+        H = torch.empty(M, Fb + 27, device=dev)
+        pos = pos.contiguous()
+        dirs = dirs.contiguous()
+        _lib.call("mms_bg_input_fwd", pos.data_ptr(), M, dirs.data_ptr(), S, X.data_ptr(), 39, H.data_ptr(),
+                  H.stride(0), Fb, _s())
+        base = MLPRun(base_p, BG_BASE_ACTS[:nb])
+        base.forward(X, keep=True, last_out=H)          # writes cols [0, Fb) of the head panel
+        dens = MLPRun(dens_p, BG_DENS_ACTS)
+        density = _mlp_strided(dens, H, Fb)             # density head reads the base features in place
+        head = MLPRun(head_p, BG_HEAD_ACTS[:len(head_p) // 3])
+        feat = head.forward(H, keep=True)
+        ctx.base, ctx.dens, ctx.head, ctx.X, ctx.H = base, dens, head, X, H
+        ctx.S, ctx.nb, ctx.nd, ctx.Fb = S, nb, nd, Fb
+        ctx.save_for_backward(pos, dirs, *params)
+        return density, feat
+
+    @staticmethod
+    def backward(ctx, ddensity, dfeat):
+        pos, dirs, *params = ctx.saved_tensors
+        M, S, Fb = pos.shape[0], ctx.S, ctx.Fb
+        R = M // S
+        dev = pos.device
+        dH, hgrads = ctx.head.backward(dfeat.contiguous(), need_dx=True)          # [M, Fb+27]
+        if ddensity is None:
+            ddensity = torch.zeros(M, 1, device=dev)
+        dFb_d, dgrads_dens = _mlp_strided_bwd(ctx.dens, ddensity.contiguous(), ctx.H, Fb)
+        dbase_out = dH[:, :Fb] + dFb_d
+        dX, bgrads = ctx.base.backward(dbase_out.contiguous(), need_dx=True)
+        dpos = torch.empty(M, 3, device=dev) if ctx.needs_input_grad[0] else None
+        ddirs = torch.zeros(R, 3, device=dev) if ctx.needs_input_grad[1] else None
+        _lib.call("mms_bg_input_bwd", pos.data_ptr(), ctx.X.data_ptr(), 39, dX.data_ptr(), dX.stride(0),
+                  dirs.data_ptr(), dH.data_ptr(), dH.stride(0), Fb, R, S, _p(dpos), _p(ddirs), _s())
+        ctx.base = ctx.dens = ctx.head = ctx.X = ctx.H = None
+        return (dpos, ddirs, None, None, None, *bgrads, *dgrads_dens, *hgrads)
+
+
+def _mlp_strided(run: MLPRun, H: torch.Tensor, Fb: int) -> torch.Tensor:
+    """Run a 1-layer MLP on the first Fb columns of panel H (row stride H.stride(0))."""
+    g, v, b = run.params
+    N, K = v.shape
+    M = H.shape[0]
+    dev = H.device
+    W = torch.empty(N, K, device=dev)
+    nrm = torch.empty(N, device=dev)
+    weight_norm_fwd(g.reshape(-1), v, W, nrm)
+    act, beta, thr = run.acts[0]
+    Y = torch.empty(M, N, device=dev)
+    Z = torch.empty(M, N, device=dev)
+    gemm(NT, M, N, K, H, H.stride(0), W, K, Y, N, bias=b, Z=Z, ldz=N, act=act, beta=beta, thr=thr)
+    run.Ws, run.norms, run.Zs, run.Ys = [W], [nrm], [Z], [Y]
+    return Y
+
+
+def _mlp_strided_bwd(run: MLPRun, dy: torch.Tensor, H: torch.Tensor, Fb: int):
+    g, v, b = run.params
+    N, K = v.shape
+    M = H.shape[0]
+    dev = H.device
+    act, beta, thr = run.acts[0]
+    dZ = torch.empty(M, N, device=dev)
+    act_bwd(dy, run.Zs[0], act, beta, thr, dZ)
+    dW = torch.zeros(N, K, device=dev)
+    gemm(TN, N, K, M, dZ, N, H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1))
+    db = torch.zeros(N, device=dev)
+    colsum_(dZ, db)
+    dg = torch.zeros(N, device=dev)
+    dv = torch.zeros(N, K, device=dev)
+    weight_norm_bwd(g.reshape(-1), v, run.norms[0], dW, dg, dv)
+    dxin = torch.empty(M, K, device=dev)
+    gemm(NN, M, K, N, dZ, N, run.Ws[0], K, dxin, K)
+    return dxin, [dg.view_as(g), dv, db]
+
+
+# ------------------------------------------------------------------------------------------------
+# volume rendering
+# ------------------------------------------------------------------------------------------------
+class NeusWeightsFunction(torch.autograd.Function):
+    """(sdf [R*S,1], grads [R*S,3], dirs [R,3], deltas [R*S], s_param [1]) -> weights [R, S]."""
+
+    @staticmethod
+    def forward(ctx, sdf, grads, dirs, deltas, s_param, cos_anneal: float, S: int):
+        M = sdf.shape[0]
+        R = M // S
+        dev = sdf.device
+        sdf, grads, dirs, deltas = sdf.contiguous(), grads.contiguous(), dirs.contiguous(), deltas.contiguous()
+        alpha = torch.empty(R, S, device=dev)
+        w = torch.empty(R, S, device=dev)
+        _lib.call("mms_neus_weights_fwd", sdf.data_ptr(), 1, grads.data_ptr(), dirs.data_ptr(), deltas.data_ptr(),
+                  s_param.data_ptr(), float(cos_anneal), R, S, alpha.data_ptr(), w.data_ptr(), _s())
+        ctx.save_for_backward(sdf, grads, dirs, deltas, s_param, alpha)
+        ctx.cos_anneal, ctx.S = float(cos_anneal), S
+        return w
+
+    @staticmethod
+    def backward(ctx, dw):
+        sdf, grads, dirs, deltas, s_param, alpha = ctx.saved_tensors
+        S = ctx.S
+        R = sdf.shape[0] // S
+        dev = sdf.device
+        dsdf = torch.empty_like(sdf)
+        dgrads = torch.zeros_like(grads)
+        ddirs = torch.zeros_like(dirs)
+        ddeltas = torch.zeros_like(deltas)
+        ds = torch.zeros_like(s_param)
+        _lib.call("mms_neus_weights_bwd", sdf.data_ptr(), 1, grads.data_ptr(), dirs.data_ptr(), deltas.data_ptr(),
+                  s_param.data_ptr(), ctx.cos_anneal, R, S, alpha.data_ptr(), dw.contiguous().data_ptr(),
+                  dsdf.data_ptr(), 1, dgrads.data_ptr(), ddirs.data_ptr(), ddeltas.data_ptr(), ds.data_ptr(), _s())
+        return dsdf, dgrads, ddirs, ddeltas, ds, None, None
+
+
+class DensityWeightsFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, density, deltas, S: int):
+        M = density.shape[0]
+        R = M // S
+        density, deltas = density.contiguous(), deltas.contiguous()
+        alpha = torch.empty(R, S, device=density.device)
+        w = torch.empty(R, S, device=density.device)
+        _lib.call("mms_density_weights_fwd", density.data_ptr(), 1, deltas.data_ptr(), R, S, alpha.data_ptr(),
+                  w.data_ptr(), _s())
+        ctx.save_for_backward(density, deltas, alpha)
+        ctx.S = S
+        return w
+
+    @staticmethod
+    def backward(ctx, dw):
+        density, deltas, alpha = ctx.saved_tensors
+        S = ctx.S
+        R = density.shape[0] // S
+        dden = torch.empty_like(density)
+        ddel = torch.zeros_like(deltas)
+        _lib.call("mms_density_weights_bwd", density.data_ptr(), 1, deltas.data_ptr(), R, S, alpha.data_ptr(),
+                  dw.contiguous().data_ptr(), dden.data_ptr(), 1, ddel.data_ptr(), _s())
+        return dden, ddel, None
+
+
+class CompositeFunction(torch.autograd.Function):
+    """weights [R,S], vals [R*S, C] -> out [N, C] = bg with hit rows idx[r] replaced by sum w c + bg (1 - sum w).
+
+    With bg None the output has R rows (no scatter).  Renderer.render (renderers.py:94-106) semantics.
+    """
+
+    @staticmethod
+    def forward(ctx, w, vals, bg, idx, S: int):
+        R = w.shape[0]
+        C = vals.shape[1]
+        w, vals = w.contiguous(), vals.contiguous()
+        if bg is not None:
+            out = bg.detach().clone().contiguous()
+            bgc = bg.contiguous()
+        else:
+            out = torch.empty(R, C, device=w.device)
+            bgc = None
+        _lib.call("mms_composite_fwd", w.data_ptr(), vals.data_ptr(), C, C, _p(bgc), R, S, _p(idx), out.data_ptr(),
+                  _s())
+        ctx.save_for_backward(w, vals, bgc, idx)
+        ctx.S = S
+        ctx.has_bg = bg is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        w, vals, bgc, idx = ctx.saved_tensors
+        S = ctx.S
+        R, C = w.shape[0], vals.shape[1]
+        dout = dout.contiguous()
+        dvals = torch.empty_like(vals) if ctx.needs_input_grad[1] else None
+        dw = torch.zeros_like(w)
+        dbg = dout.clone() if ctx.has_bg else None
+        _lib.call("mms_composite_bwd", w.data_ptr(), vals.data_ptr(), C, C, _p(bgc), R, S, _p(idx), dout.data_ptr(),
+                  _p(dvals), C, dw.data_ptr(), _p(dbg), _s())
+        return dw, dvals, dbg, None, None
+
+
+# ------------------------------------------------------------------------------------------------
+# samples, rays, collider
+# ------------------------------------------------------------------------------------------------
+class SamplesFunction(torch.autograd.Function):
+    """bins [R, S+1] (detached) + nears/fars [R] + origins/dirs [R,3] -> positions [R*S,3], deltas [R*S],
+    starts [R*S], ends [R*S]."""
+
+    @staticmethod
+    def forward(ctx, bins, nears, fars, origins, dirs, kind: int):
+        R, nb = bins.shape
+        S = nb - 1
+        dev = bins.device
+        bins, nears, fars = bins.contiguous(), nears.contiguous(), fars.contiguous()
+        origins, dirs = origins.contiguous(), dirs.contiguous()
+        starts = torch.empty(R * S, device=dev)
+        ends = torch.empty(R * S, device=dev)
+        deltas = torch.empty(R * S, device=dev)
+        pos = torch.empty(R * S, 3, device=dev)
+        _lib.call("mms_samples_fwd", bins.data_ptr(), nb, nb, nears.data_ptr(), fars.data_ptr(), origins.data_ptr(),
+                  dirs.data_ptr(), kind, R, starts.data_ptr(), ends.data_ptr(), deltas.data_ptr(), pos.data_ptr(),
+                  _s())
+        ctx.save_for_backward(bins, nears, fars, dirs)
+        ctx.kind = kind
+        ctx.mark_non_differentiable(ends)
+        return pos, deltas, starts, ends
+
+    @staticmethod
+    def backward(ctx, dpos, ddeltas, dstarts, dends):
+        bins, nears, fars, dirs = ctx.saved_tensors
+        R, nb = bins.shape
+        dn = torch.zeros_like(nears)
+        df = torch.zeros_like(fars)
+        do = torch.zeros(R, 3, device=bins.device)
+        dd = torch.zeros(R, 3, device=bins.device)
+        _lib.call("mms_samples_bwd", bins.data_ptr(), nb, nb, nears.data_ptr(), fars.data_ptr(), dirs.data_ptr(),
+                  ctx.kind, R, _p(None if dpos is None else dpos.contiguous()),
+                  _p(None if ddeltas is None else ddeltas.contiguous()),
+                  _p(None if dstarts is None else dstarts.contiguous()), dn.data_ptr(), df.data_ptr(), do.data_ptr(),
+                  dd.data_ptr(), _s())
+        return None, dn, df, do, dd, None
+
+
+class RaysFunction(torch.autograd.Function):
+    """camera_opt_to_camera mats [C|1, 3, 4] -> origins, dirs, ups (+ pixel_area, directions_norm)."""
+
+    @staticmethod
+    def forward(ctx, mats, coords, cams, pixel_offset: float):
+        N = coords.shape[0]
+        dev = coords.device
+        mats = mats.contiguous()
+        o = torch.empty(N, 3, device=dev)
+        d = torch.empty(N, 3, device=dev)
+        u = torch.empty(N, 3, device=dev)
+        a = torch.empty(N, 1, device=dev)
+        dn = torch.empty(N, 1, device=dev)
+        per_cam = 1 if mats.shape[0] > 1 else 0
+        _lib.call("mms_raygen_fwd", coords.data_ptr(), N, cams.fx.data_ptr(), cams.fy.data_ptr(), cams.cx.data_ptr(),
+                  cams.cy.data_ptr(), cams.c2w.data_ptr(), _p(cams.distortion), mats.data_ptr(), per_cam,
+                  float(pixel_offset), o.data_ptr(), d.data_ptr(), u.data_ptr(), a.data_ptr(), dn.data_ptr(), _s())
+        ctx.save_for_backward(mats, coords)
+        ctx.cams, ctx.off, ctx.per_cam = cams, float(pixel_offset), per_cam
+        ctx.mark_non_differentiable(a, dn)
+        return o, d, u, a, dn
+
+    @staticmethod
+    def backward(ctx, do, dd, du, da, ddn):
+        mats, coords = ctx.saved_tensors
+        cams = ctx.cams
+        N = coords.shape[0]
+        dm = torch.zeros_like(mats)
+        _lib.call("mms_raygen_bwd", coords.data_ptr(), N, cams.fx.data_ptr(), cams.fy.data_ptr(), cams.cx.data_ptr(),
+                  cams.cy.data_ptr(), cams.c2w.data_ptr(), _p(cams.distortion), mats.data_ptr(), ctx.per_cam,
+                  ctx.off, _p(None if do is None else do.contiguous()), _p(None if dd is None else dd.contiguous()),
+                  _p(None if du is None else du.contiguous()), dm.data_ptr(), _s())
+        return dm, None, None, None
+
+
+class ColliderFunction(torch.autograd.Function):
+    """origins/dirs [N,3] -> nears, fars, bg_nears, bg_fars [N] (+ uint8 mask)."""
+
+    @staticmethod
+    def forward(ctx, origins, dirs, radius: float):
+        N = origins.shape[0]
+        dev = origins.device
+        origins, dirs = origins.contiguous(), dirs.contiguous()
+        n = torch.empty(N, device=dev)
+        f = torch.empty(N, device=dev)
+        bn = torch.empty(N, device=dev)
+        bf = torch.empty(N, device=dev)
+        mask = torch.empty(N, dtype=torch.uint8, device=dev)
+        _lib.call("mms_collider_fwd", origins.data_ptr(), dirs.data_ptr(), N, float(radius), n.data_ptr(),
+                  f.data_ptr(), mask.data_ptr(), bn.data_ptr(), bf.data_ptr(), _s())
+        ctx.save_for_backward(origins, dirs)
+        ctx.radius = float(radius)
+        ctx.mark_non_differentiable(mask)
+        return n, f, bn, bf, mask
+
+    @staticmethod
+    def backward(ctx, dn, df, dbn, dbf, dmask):
+        origins, dirs = ctx.saved_tensors
+        N = origins.shape[0]
+        do = torch.zeros_like(origins)
+        dd = torch.zeros_like(dirs)
+        c = lambda t: None if t is None else t.contiguous()
+        _lib.call("mms_collider_bwd", origins.data_ptr(), dirs.data_ptr(), N, ctx.radius, _p(c(dn)), _p(c(df)),
+                  _p(c(dbn)), _p(c(dbf)), do.data_ptr(), dd.data_ptr(), _s())
+        return do, dd, None
+
+
+def compact(mask: torch.Tensor) -> torch.Tensor:
+    """Order-preserving indices of mask != 0 (int64); one device->host read of the count."""
+    N = mask.shape[0]
+    idx = torch.empty(N, dtype=torch.int64, device=mask.device)
+    cnt = torch.empty(1, dtype=torch.int64, device=mask.device)
+    _lib.call("mms_compact", mask.data_ptr(), N, idx.data_ptr(), cnt.data_ptr(), _s())
+    return idx[: int(cnt.item())]
+
+
+# ------------------------------------------------------------------------------------------------
+# losses
+# ------------------------------------------------------------------------------------------------
+class L1LossFunction(torch.autograd.Function):
+    """nn.L1Loss(mean) with optional SkipSaturation fill (losses.py:152-164)."""
+
+    @staticmethod
+    def forward(ctx, out, target, sat_thr: Optional[float]):
+        N, C = target.shape
+        out_c = out.contiguous()
+        target = target.contiguous()
+        loss = torch.zeros((), device=out.device)
+        scratch = torch.empty(1, dtype=torch.int64, device=out.device) if sat_thr is not None else None
+        thr = float(sat_thr) if sat_thr is not None else 0.0
+        _lib.call("mms_l1_loss_fwd", out_c.data_ptr(), C, target.data_ptr(), N, C, thr, _p(scratch),
+                  loss.data_ptr(), _s())
+        ctx.save_for_backward(out_c, target, scratch)
+        ctx.thr = thr
+        return loss
+
+    @staticmethod
+    def backward(ctx, dl):
+        out, target, scratch = ctx.saved_tensors
+        N, C = target.shape
+        dout = torch.zeros_like(out)
+        _lib.call("mms_l1_loss_bwd", out.data_ptr(), C, target.data_ptr(), N, C, ctx.thr, _p(scratch),
+                  dl.contiguous().data_ptr(), 1.0, dout.data_ptr(), C, _s())
+        return dout, None, None
+
+
+class GeoLossFunction(torch.autograd.Function):
+    """Eikonal MSE(||g||, 1) and curvature L1(sum h, 0) over the concatenated modalities (losses.py:107-150)."""
+
+    @staticmethod
+    def forward(ctx, *tensors):
+        n = len(tensors) // 2
+        grads, hess = tensors[:n], tensors[n:]
+        total = sum(g.shape[0] for g in grads)
+        inv = 1.0 / float(total)
+        eik = torch.zeros((), device=grads[0].device)
+        curv = torch.zeros((), device=grads[0].device)
+        for g, h in zip(grads, hess):
+            _lib.call("mms_geo_loss_fwd", g.contiguous().data_ptr(), h.contiguous().data_ptr(), g.shape[0], inv,
+                      eik.data_ptr(), curv.data_ptr(), _s())
+        ctx.save_for_backward(*[t.contiguous() for t in tensors])
+        ctx.inv, ctx.n = inv, n
+        return eik, curv
+
+    @staticmethod
+    def backward(ctx, deik, dcurv):
+        ts = ctx.saved_tensors
+        n = ctx.n
+        outs = []
+        dg_list, dh_list = [], []
+        for g, h in zip(ts[:n], ts[n:]):
+            dg = torch.zeros_like(g)
+            dh = torch.zeros_like(h)
+            _lib.call("mms_geo_loss_bwd", g.data_ptr(), h.data_ptr(), g.shape[0], ctx.inv,
+                      _p(None if deik is None else deik.contiguous()), 1.0,
+                      _p(None if dcurv is None else dcurv.contiguous()), 1.0, dg.data_ptr(), dh.data_ptr(), _s())
+            dg_list.append(dg)
+            dh_list.append(dh)
+        return (*dg_list, *dh_list)
+
+
+class PolarizerFunction(torch.autograd.Function):
+    """Stokes [M,3] -> 4 polarised intensities [M,4] (field_heads.py:90-106, polarizer.py:54-101)."""
+
+    @staticmethod
+    def forward(ctx, stokes, dirs, ups, S: int):
+        M = stokes.shape[0]
+        stokes, dirs, ups = stokes.contiguous(), dirs.contiguous(), ups.contiguous()
+        out = torch.empty(M, 4, device=stokes.device)
+        _lib.call("mms_polarizer_fwd", stokes.data_ptr(), dirs.data_ptr(), ups.data_ptr(), M, S, out.data_ptr(), _s())
+        ctx.save_for_backward(stokes, dirs, ups)
+        ctx.S = S
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        stokes, dirs, ups = ctx.saved_tensors
+        S = ctx.S
+        R = stokes.shape[0] // S
+        ds = torch.empty_like(stokes)
+        dd = torch.zeros_like(dirs)
+        du = torch.zeros_like(ups)
+        _lib.call("mms_polarizer_bwd", stokes.data_ptr(), dirs.data_ptr(), ups.data_ptr(), R, S,
+                  dout.contiguous().data_ptr(), ds.data_ptr(), dd.data_ptr(), du.data_ptr(), _s())
+        return ds, dd, du, None
+
+
+def HashGridApply(x, table, cfg: GridCfg, active: int):
+    """Standalone FeatureGrid forward (feature_structures.py:78-83) with autograd to x and table."""
+    from .hip_ops import HashGridFunction
+    return HashGridFunction.apply(x, table, cfg.scales, cfg.log2T, cfg.radius, active)

@@ -95,3 +95,31 @@ def gemm(mode: int, M: int, N: int, K: int, A: torch.Tensor, lda: int, B: torch.
     _lib.call("mms_gemm_f32", int(mode), int(M), int(N), int(K), A.data_ptr(), int(lda), B.data_ptr(), int(ldb),
               C.data_ptr(), int(ldc), _ptr(bias), _ptr(Z), int(ldz), _ptr(aux), int(ldaux), int(act), int(dact),
               float(beta), float(thr), int(bool(accumulate)), int(splits), _stream())
+
+
+def weight_norm_fwd(g, v, W, norms):
+    N, K = v.shape
+    _lib.call("mms_weight_norm_fwd", g.data_ptr(), v.data_ptr(), N, K, W.data_ptr(), W.stride(0), norms.data_ptr(),
+              _stream())
+
+
+def weight_norm_bwd(g, v, norms, dW, dg, dv):
+    N, K = v.shape
+    _lib.call("mms_weight_norm_bwd", g.data_ptr(), v.data_ptr(), norms.data_ptr(), N, K, dW.data_ptr(), dW.stride(0),
+              dg.data_ptr(), dv.data_ptr(), _stream())
+
+
+def colsum_(A, out):
+    M, N = A.shape
+    _lib.call("mms_colsum", A.data_ptr(), M, N, A.stride(0), out.data_ptr(), _stream())
+
+
+def act_bwd(dY, Z, act, beta, thr, dZ):
+    M, N = dY.shape
+    _lib.call("mms_act_bwd", dY.data_ptr(), dY.stride(0), Z.data_ptr(), Z.stride(0), M, N, int(act), float(beta),
+              float(thr), dZ.data_ptr(), dZ.stride(0), _stream())
+
+
+def _splits_for(M_rows: int, tiles: int) -> int:
+    target = max(1, 1024 // max(1, tiles))
+    return int(max(1, min(target, M_rows // 512)))

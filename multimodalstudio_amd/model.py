@@ -1,0 +1,492 @@
+"""MMS model on the HIP kernels, with the reference's module tree and parameter names.
+
+``BaseModel(...).state_dict()`` has the same keys and shapes as the reference's
+``models.base_model.BaseModel`` (/root/reference/src/models/base_model.py:55-80), so reference
+checkpoints load unchanged and vice versa.  The orchestration in ``BaseModel.forward`` follows
+base_model.py:82-161 stage by stage; every stage runs in libmms_hip.so through functions.py.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib
+from . import functions as fx
+from .functions import GridCfg
+
+
+# ------------------------------------------------------------------------------------------------
+# field components
+# ------------------------------------------------------------------------------------------------
+class _WeightParams(nn.Module):
+    """Holds original0 (g) / original1 (v) like torch's weight_norm parametrization list."""
+
+    def __init__(self, g: torch.Tensor, v: torch.Tensor):
+        super().__init__()
+        self.original0 = nn.Parameter(g)
+        self.original1 = nn.Parameter(v)
+
+
+class WeightNormLinear(nn.Module):
+    """nn.Linear under parametrizations.weight_norm (mlp.py:206-209): keys bias, parametrizations.weight.original{0,1}."""
+
+    def __init__(self, in_features: int, out_features: int, weight: torch.Tensor, bias: torch.Tensor):
+        super().__init__()
+        g = torch.linalg.vector_norm(weight, dim=1, keepdim=True).detach().clone()
+        self.parametrizations = nn.ModuleDict({"weight": _WeightParams(g, weight.detach().clone())})
+        self.bias = nn.Parameter(bias.detach().clone())
+        self.in_features, self.out_features = in_features, out_features
+
+    def params(self):
+        w = self.parametrizations["weight"]
+        return [w.original0, w.original1, self.bias]
+
+
+@dataclass
+class MLPConfig:
+    """MLPConfig (mlp.py:36-58)."""
+    num_layers: int = 8
+    hidden_dim: int = 128
+    weight_norm: bool = True
+    activation: str = "ReLU"
+    activation_params: dict = field(default_factory=dict)
+    out_activation: Optional[str] = "Sigmoid"
+    skip_connections: Sequence[int] = ()
+    geometric_init: bool = False
+    geometric_init_bias: float = 0.5
+
+
+class MLP(nn.Module):
+    """Weight-normed MLP (mlp.py:99-209) with the reference's initialisers."""
+
+    def __init__(self, config: MLPConfig, input_dim: int, output_dim: Optional[int] = None):
+        super().__init__()
+        if config.skip_connections:
+            raise NotImplementedError("skip connections (mlp_raw surface field) are not on the HIP path yet")
+        if not config.weight_norm:
+            raise NotImplementedError("the HIP MLP implements the weight-normed layers used by every method config")
+        self.config = config
+        self.input_dim = input_dim
+        self.output_dim = output_dim if output_dim is not None else config.hidden_dim
+        dims = [input_dim] + [config.hidden_dim] * (config.num_layers - 1) + [self.output_dim]
+        weights, biases = [], []
+        for i in range(len(dims) - 1):
+            lin = nn.Linear(dims[i], dims[i + 1])
+            weights.append(lin.weight.data)
+            biases.append(lin.bias.data)
+        if config.geometric_init:
+            self._geometric_init(weights, biases, config.geometric_init_bias, input_dim > 3)
+        else:
+            for w, b in zip(weights, biases):
+                nn.init.kaiming_uniform_(w)
+                nn.init.zeros_(b)
+        self.layers = nn.ModuleList([WeightNormLinear(dims[i], dims[i + 1], weights[i], biases[i])
+                                     for i in range(len(dims) - 1)])
+        hidden = fx.ACT[config.activation]
+        beta = float(config.activation_params.get("beta", 1.0))
+        thr = float(config.activation_params.get("threshold", 20.0))
+        out = fx.ACT[config.out_activation if config.out_activation != "None" else None]
+        self.acts = tuple([(hidden, beta, thr)] * (len(dims) - 2) + [(out, 1.0, 20.0)])
+
+    @staticmethod
+    def _geometric_init(weights, biases, bias, additional_input):
+        """MLP.geometric_init (mlp.py:173-198)."""
+        L = len(weights)
+        for l in range(L):
+            out_dim, in_dim = weights[l].shape
+            if l == L - 1:
+                nn.init.normal_(weights[l], mean=np.sqrt(np.pi) / np.sqrt(in_dim), std=0.0001)
+                nn.init.constant_(biases[l], -bias)
+            elif additional_input and l == 0:
+                nn.init.constant_(biases[l], 0.0)
+                nn.init.constant_(weights[l][:, 3:], 0.0)
+                nn.init.normal_(weights[l][:, :3], 0.0, np.sqrt(2) / np.sqrt(out_dim))
+            else:
+                nn.init.constant_(biases[l], 0.0)
+                nn.init.normal_(weights[l], 0.0, np.sqrt(2) / np.sqrt(out_dim))
+
+    def params(self) -> List[torch.Tensor]:
+        out = []
+        for layer in self.layers:
+            out += layer.params()
+        return out
+
+    def forward(self, x):
+        return fx.MLPFunction.apply(x, self.acts, *self.params())
+
+
+class HashEncoding(nn.Module):
+    """HashEncoding (encodings.py:184-310) with implementation 'hip' (parameter hash_table [L*T, F])."""
+
+    def __init__(self, num_levels=16, features_per_level=2, min_res=16, max_res=2048, log2_hashmap_size=19,
+                 hash_init_scale=0.001):
+        super().__init__()
+        self.num_levels, self.features, self.log2T = num_levels, features_per_level, log2_hashmap_size
+        self.growth_factor = float(np.exp((np.log(max_res) - np.log(min_res)) / (num_levels - 1)))
+        levels = torch.arange(num_levels)
+        self.scalings = torch.floor(min_res * self.growth_factor ** levels)
+        T = 2 ** log2_hashmap_size
+        table = (torch.rand(size=(T * num_levels, features_per_level)) * 2 - 1) * hash_init_scale
+        self.hash_table = nn.Parameter(table)
+
+    def get_out_dim(self):
+        return self.num_levels * self.features
+
+
+class FeatureGrid(nn.Module):
+    """FeatureGrid (feature_structures.py:56-127): rescale by radius + coarse-to-fine level mask."""
+
+    def __init__(self, encoding: HashEncoding, radius: float = 1.0):
+        super().__init__()
+        self.encoding = encoding
+        self.radius = float(radius)
+        self.active_levels = encoding.num_levels
+        self.cfg = GridCfg(encoding.scalings.tolist(), encoding.log2T, self.radius, encoding.features)
+
+    def update_mask(self, level: int):
+        """feature_structures.py:85-88 (levels >= `level` contribute zero)."""
+        self.active_levels = int(level)
+
+    def forward(self, x):
+        return fx.HashGridApply(x, self.encoding.hash_table, self.cfg, self.active_levels)
+
+
+class FeatureGridAndMLP(nn.Module):
+    """FeatureGridAndMLP (feature_structures.py:130-173)."""
+
+    def __init__(self, grid: FeatureGrid, mlp: MLP):
+        super().__init__()
+        self.feature_grid = grid
+        self.mlp_head = mlp
+
+
+class SingleVarianceNetwork(nn.Module):
+    """single_variance.py:19-36."""
+
+    def __init__(self, init_val: float = 0.3):
+        super().__init__()
+        self.s = nn.Parameter(init_val * torch.ones(1))
+
+    def get_inv_variance(self):
+        return torch.exp(self.s * 10.0).clip(1e-6, 1e6)
+
+
+class _DensityFn(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.variance_network = SingleVarianceNetwork(0.3)
+
+
+class NeuSVolumeRendering(nn.Module):
+    """NeuSVolumeRendering (volume_rendering.py:161-239)."""
+
+    def __init__(self, anneal_end_ratio: float = 0.05):
+        super().__init__()
+        self.density_fn = _DensityFn()
+        self.anneal_end_ratio = anneal_end_ratio
+        self._cos_anneal_ratio = 1.0
+
+    def set_cos_anneal_ratio(self, anneal: float):
+        self._cos_anneal_ratio = float(anneal)
+
+
+class ModalityHead(nn.Module):
+    """ModalityHead / PolarizationHead (field_heads.py:55-106)."""
+
+    def __init__(self, kind: str, input_dim: int, output_dim: int, num_layers: int, hidden_dim: int,
+                 out_activation: Optional[str]):
+        super().__init__()
+        self.kind = kind
+        cfg = MLPConfig(num_layers=num_layers, hidden_dim=hidden_dim, out_activation=out_activation)
+        self.field = MLP(cfg, input_dim, 3 if kind == "polarization" else output_dim)
+
+    def forward(self, x, directions=None, up_directions=None, S: int = 1):
+        y = self.field(x)
+        if self.kind == "polarization":
+            return fx.PolarizerFunction.apply(y, directions, up_directions, S)
+        return y
+
+
+class SDFField(nn.Module):
+    """SDFField (surface_field.py:80-116) around FeatureGridAndMLP (attribute `field`)."""
+
+    def __init__(self, field: FeatureGridAndMLP):
+        super().__init__()
+        self.field = field
+
+
+class SurfaceModel(nn.Module):
+    """SurfaceModel (surface_model.py:51-285): numerical 4-tap gradients + hessian."""
+
+    def __init__(self, surface_field: SDFField):
+        super().__init__()
+        self.surface_field = surface_field
+        self.volume_rendering = NeuSVolumeRendering()
+        self.numerical_gradients_delta = 2.0 / 1024
+
+    def set_numerical_gradients_delta(self, delta: float):
+        self.numerical_gradients_delta = float(delta)
+
+    def _grid_and_params(self):
+        f = self.surface_field.field
+        return f.feature_grid, f.mlp_head.params()
+
+    def forward(self, pos: torch.Tensor):
+        grid, params = self._grid_and_params()
+        delta = self.numerical_gradients_delta / np.sqrt(3)
+        return fx.SurfaceFunction.apply(pos, grid.encoding.hash_table, grid.cfg, grid.active_levels, float(delta),
+                                        *params)
+
+    def get_sdf(self, pos: torch.Tensor) -> torch.Tensor:
+        grid, params = self._grid_and_params()
+        with torch.no_grad():
+            return fx.sdf_only(pos, grid.encoding.hash_table, grid.cfg, grid.active_levels, params)
+
+
+class RadianceField(nn.Module):
+    def __init__(self, base_field: FeatureGridAndMLP):
+        super().__init__()
+        self.base_field = base_field
+
+
+class RadianceModel(nn.Module):
+    """RadianceModel (radiance_model.py:57-169) with SH(4) directions and n.v (grid.yaml)."""
+
+    def __init__(self, radiance_field: RadianceField, heads: Dict[str, ModalityHead]):
+        super().__init__()
+        self.radiance_field = radiance_field
+        self.modality_heads = nn.ModuleDict(heads)
+
+    def features(self, pos, dirs, normals, geo, S):
+        bf = self.radiance_field.base_field
+        g = bf.feature_grid
+        return fx.RadianceFunction.apply(pos, dirs, normals, geo, g.encoding.hash_table, g.cfg, g.active_levels, S,
+                                         *bf.mlp_head.params())
+
+
+class NeRFField(nn.Module):
+    """NeRFField (nerf_field.py:47-105): base MLP, density head (Softplus), head MLP."""
+
+    def __init__(self, base_field: MLP, head_field: MLP, density_head: ModalityHead):
+        super().__init__()
+        self.base_field = base_field
+        self.head_field = head_field
+        self.density_head = density_head
+
+
+class BackgroundModel(nn.Module):
+    """BackgroundModel (background_model.py:46-129) with L-inf scene contraction."""
+
+    def __init__(self, background_field: NeRFField, heads: Dict[str, ModalityHead]):
+        super().__init__()
+        self.background_field = background_field
+        self.modality_heads = nn.ModuleDict(heads)
+
+    def field(self, pos, dirs, S):
+        bf = self.background_field
+        base = bf.base_field.params()
+        dens = bf.density_head.field.params()
+        head = bf.head_field.params()
+        return fx.BackgroundFunction.apply(pos, dirs, S, len(base) // 3, len(dens) // 3, *base, *dens, *head)
+
+
+# ------------------------------------------------------------------------------------------------
+# model
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class ModelSpec:
+    """The fields of method_configs 'grid' / 'grid_raw' that shape the hot path (method_configs.py:59-260)."""
+    modalities: Dict[str, int]
+    log2T: int = 19
+    num_levels: int = 16
+    min_res: int = 16
+    max_res: int = 1024
+    radius: float = 1.0
+    num_samples: int = 32
+    num_importance: int = 32
+    upsample_steps: int = 4
+    base_variance: float = 64.0
+    bg_samples: int = 16
+
+
+@dataclass
+class RNG:
+    """Uniform draws in the reference's order; None entries are drawn on the device."""
+    uniform: Dict[str, torch.Tensor] = field(default_factory=dict)
+    pdf: Dict[str, List[torch.Tensor]] = field(default_factory=dict)
+    background: Dict[str, torch.Tensor] = field(default_factory=dict)
+
+
+def _linspace(n: int, lo: float = 0.0, hi: float = 1.0) -> torch.Tensor:
+    """torch.linspace on the host (the reference's CPU values), for upload."""
+    return torch.linspace(lo, hi, n)
+
+
+class BaseModel(nn.Module):
+    """BaseModel (base_model.py:38-199) — collider -> NeuS sampler -> background -> surface -> radiance -> render."""
+
+    def __init__(self, spec: ModelSpec):
+        super().__init__()
+        self.spec = spec
+        mods = spec.modalities
+
+        def grid(radius=1.0):
+            enc = HashEncoding(spec.num_levels, 2, spec.min_res, spec.max_res, spec.log2T)
+            return FeatureGrid(enc, radius)
+
+        sdf_mlp = MLP(MLPConfig(num_layers=3, hidden_dim=256, activation="Softplus", activation_params={"beta": 100},
+                                out_activation="None", geometric_init=True, geometric_init_bias=0.4),
+                      3 + 36 + 32, 257)
+        self.surface_model = SurfaceModel(SDFField(FeatureGridAndMLP(grid(), sdf_mlp)))
+        rad_mlp = MLP(MLPConfig(num_layers=3, hidden_dim=256, out_activation="ReLU"), 3 + 25 + 257 + 32, 256)
+        heads = {}
+        for m, c in mods.items():
+            if m == "polarization":
+                heads[m] = ModalityHead("polarization", 256, c, 3, 256, "None")
+            else:
+                heads[m] = ModalityHead("plain", 256, c, 3, 64, "Sigmoid")
+        self.radiance_model = RadianceModel(RadianceField(FeatureGridAndMLP(grid(), rad_mlp)), heads)
+        bg_base = MLP(MLPConfig(num_layers=4, hidden_dim=256, out_activation="ReLU"), 39, 256)
+        bg_head = MLP(MLPConfig(num_layers=4, hidden_dim=256, out_activation="ReLU"), 256 + 27, 128)
+        dens = ModalityHead("plain", 256, 1, 1, 64, "Softplus")
+        bg_heads = {}
+        for m, c in mods.items():
+            if m == "polarization":
+                bg_heads[m] = ModalityHead("polarization", 128, c, 1, 64, "None")
+            else:
+                bg_heads[m] = ModalityHead("plain", 128, c, 1, 64, "Sigmoid")
+        self.background_model = BackgroundModel(NeRFField(bg_base, bg_head, dens), bg_heads)
+        self._lin = {}
+
+    # -- callbacks (BEFORE_TRAIN_ITERATION), restated from the reference schedules --------------------
+    def set_step(self, step: int, max_iters: int = 100000):
+        spl = min(int(max_iters * 1.0), int(max_iters / self.spec.num_levels))
+        level = min(max(int(step / spl) + 1, 1), self.spec.num_levels)
+        self.surface_model.surface_field.field.feature_grid.update_mask(level)
+        self.radiance_model.radiance_field.base_field.feature_grid.update_mask(level)
+        g = float(np.exp((np.log(self.spec.max_res) - np.log(self.spec.min_res)) / (self.spec.num_levels - 1)))
+        delta = max(1.0 / self.spec.max_res, 1.0 / (self.spec.min_res * g ** int(step / spl)))
+        self.surface_model.set_numerical_gradients_delta(delta * (self.spec.radius * 2.0))
+        self.surface_model.volume_rendering.set_cos_anneal_ratio(min(1.0, step / int(max_iters * 0.05)))
+
+    def _lin_dev(self, n: int, hi: float, device) -> torch.Tensor:
+        key = (n, hi, str(device))
+        if key not in self._lin:
+            self._lin[key] = _linspace(n, 0.0, hi).to(device)
+        return self._lin[key]
+
+    # -- NeuS sampler (ray_samplers.py:448-514), no autograd ------------------------------------------
+    @torch.no_grad()
+    def neus_bins(self, n_h, f_h, o_h, d_h, t_rand, pdf_rands):
+        sp = self.spec
+        R = n_h.shape[0]
+        dev = n_h.device
+        S = sp.num_samples
+        lin = self._lin_dev(S + 1, 1.0, dev)
+        bins = torch.empty(R, S + 1, device=dev)
+        _lib.call("mms_stratified_bins", lin.data_ptr(), S + 1, fx._p(t_rand), 1, R, bins.data_ptr(), fx._s())
+        n_new = sp.num_importance // sp.upsample_steps
+        u_lin = self._lin_dev(n_new + 1, 1.0 - 1.0 / (n_new + 1), dev)
+        pos = self._positions(bins, n_h, f_h, o_h, d_h)
+        sdf_new = self.surface_model.get_sdf(pos)
+        sdf_prev, prev_idx, s_prev, n_prev_new = None, None, 0, S
+        new_bins = None
+        for it in range(sp.upsample_steps):
+            if it > 0:
+                sdf_new = self.surface_model.get_sdf(self._positions(new_bins, n_h, f_h, o_h, d_h))
+            sdf_out = torch.empty(R, S, device=dev)
+            new_bins = torch.empty(R, n_new + 1, device=dev)
+            merged = torch.empty(R, S + n_new + 1, device=dev)
+            sidx = torch.empty(R, S + n_new, dtype=torch.int32, device=dev)
+            rnd = pdf_rands[it] if pdf_rands is not None else None
+            _lib.call("mms_neus_step", R, S, bins.data_ptr(), fx._p(sdf_prev), s_prev, sdf_new.data_ptr(), n_prev_new,
+                      fx._p(prev_idx), n_h.data_ptr(), f_h.data_ptr(), float(sp.base_variance * 2 ** it),
+                      fx._p(rnd), u_lin.data_ptr(), n_new, sdf_out.data_ptr(), new_bins.data_ptr(), merged.data_ptr(),
+                      sidx.data_ptr(), fx._s())
+            sdf_prev, prev_idx, s_prev, n_prev_new = sdf_out, sidx, S, n_new
+            bins = merged
+            S += n_new
+        return bins
+
+    def _positions(self, bins, n, f, o, d):
+        R, nb = bins.shape
+        pos = torch.empty(R * (nb - 1), 3, device=bins.device)
+        _lib.call("mms_samples_fwd", bins.data_ptr(), nb, nb, n.data_ptr(), f.data_ptr(), o.data_ptr(), d.data_ptr(),
+                  0, R, None, None, None, pos.data_ptr(), fx._s())
+        return pos
+
+    # -- forward ----------------------------------------------------------------------------------------
+    def forward(self, rays: Dict[str, Dict[str, torch.Tensor]], rng: Optional[RNG] = None):
+        """rays[mod] = {"origins", "directions", "up_directions"} ([N,3] device); returns per-modality outputs."""
+        rng = rng or RNG()
+        sp = self.spec
+        outputs = {}
+        s_param = self.surface_model.volume_rendering.density_fn.variance_network.s
+        for mod in sp.modalities:
+            r = rays[mod]
+            o, d, up = r["origins"], r["directions"], r["up_directions"]
+            N = o.shape[0]
+            dev = o.device
+            nears, fars, bnears, bfars, mask = fx.ColliderFunction.apply(o, d, 1.0)
+            idx = fx.compact(mask)
+            R = idx.shape[0]
+            o_h, d_h, up_h = o.index_select(0, idx), d.index_select(0, idx), up.index_select(0, idx)
+            n_h, f_h = nears.index_select(0, idx), fars.index_select(0, idx)
+            t_rand = rng.uniform.get(mod)
+            if t_rand is None and self.training:
+                t_rand = torch.rand(R, 1, device=dev)
+            pdf = rng.pdf.get(mod)
+            if pdf is None and self.training:
+                pdf = [torch.rand(R, 1, device=dev) for _ in range(sp.upsample_steps)]
+            bins = self.neus_bins(n_h.detach(), f_h.detach(), o_h.detach(), d_h.detach(), t_rand, pdf)
+            S = bins.shape[1] - 1
+            pos, deltas, starts, ends = fx.SamplesFunction.apply(bins, n_h, f_h, o_h, d_h, 0)
+            # background (background_model.py:73-111) on all N rays
+            bt = rng.background.get(mod)
+            if bt is None and self.training:
+                bt = torch.rand(N, sp.bg_samples + 1, device=dev)
+            blin = self._lin_dev(sp.bg_samples + 1, 1.0, dev)
+            bbins = torch.empty(N, sp.bg_samples + 1, device=dev)
+            _lib.call("mms_stratified_bins", blin.data_ptr(), sp.bg_samples + 1, fx._p(bt), sp.bg_samples + 1, N,
+                      bbins.data_ptr(), fx._s())
+            bpos, bdeltas, _, _ = fx.SamplesFunction.apply(bbins, bnears, bfars, o, d, 1)
+            density, bfeat = self.background_model.field(bpos, d, sp.bg_samples)
+            bw = fx.DensityWeightsFunction.apply(density, bdeltas, sp.bg_samples)
+            bg_out = {}
+            for m, head in self.background_model.modality_heads.items():
+                vals = head(bfeat, d, up, sp.bg_samples)
+                bg_out[m] = fx.CompositeFunction.apply(bw, vals, None, None, sp.bg_samples)
+            # surface + radiance
+            sdf, geo, grads, hess, normals = self.surface_model(pos)
+            vr = self.surface_model.volume_rendering
+            w = fx.NeusWeightsFunction.apply(sdf, grads, d_h, deltas, s_param, vr._cos_anneal_ratio, S)
+            feat = self.radiance_model.features(pos, d_h, normals.detach(), geo, S)
+            out = {}
+            for m, head in self.radiance_model.modality_heads.items():
+                vals = head(feat, d_h, up_h, S)
+                out[m] = fx.CompositeFunction.apply(w, vals, bg_out[m], idx, S)
+            with torch.no_grad():
+                acc = torch.zeros(N, 1, device=dev)
+                acc.index_copy_(0, idx, w.sum(-1, keepdim=True))
+                nrm = torch.zeros(N, 3, device=dev)
+                nrm.index_copy_(0, idx, (w[..., None] * normals.view(R, S, 3)).sum(1))
+                steps = ((starts + ends) / 2).view(R, S)
+                dep = torch.zeros(N, 1, device=dev)
+                if R > 0:
+                    dep.index_copy_(0, idx, torch.clip((w * steps).sum(-1, keepdim=True), steps.min(), steps.max()))
+            out["normals"] = nrm
+            out["depth"] = dep
+            out["accumulation"] = acc
+            out["gradients"] = grads.view(R, S, 3)
+            out["hessians"] = hess.view(R, S, 3)
+            out["inv_s"] = 1.0 / self.surface_model.volume_rendering.density_fn.variance_network.get_inv_variance()
+            out["weights"] = w
+            out["bins"] = bins
+            out["mask"] = mask
+            outputs[mod] = out
+        return outputs

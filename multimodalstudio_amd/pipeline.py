@@ -1,0 +1,321 @@
+"""Training step around the hot path: pixel sampling, ray generation with pose refinement, the model,
+losses and the optimizer step — the MI355X counterpart of RawPipeline/BasePipeline.train_step
+(/root/reference/src/pipelines/raw_pipeline.py:67-82, base_pipeline.py:138-153).
+
+Parameters of each optimizer group live in ONE flat fp32 buffer (params are views into it) and so do
+their gradients, so grad-norm clipping is one reduction, AdamW is one launch, and the data-parallel
+gradient all-reduce (ddp.py) is a handful of large RCCL calls instead of one per tensor.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib
+from . import functions as fx
+from . import scene as mscene
+from .model import RNG, BaseModel, ModelSpec
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+# ------------------------------------------------------------------------------------------------
+# cameras / rays
+# ------------------------------------------------------------------------------------------------
+class DeviceCameras:
+    """Per-modality camera tensors on the device (Cameras fields used by cameras.py:460-703)."""
+
+    def __init__(self, cams: mscene.ModalityCameras, device):
+        self.c2w = cams.c2w.reshape(-1, 12).contiguous().to(device)
+        self.fx = cams.fx.contiguous().to(device)
+        self.fy = cams.fy.contiguous().to(device)
+        self.cx = cams.cx.contiguous().to(device)
+        self.cy = cams.cy.contiguous().to(device)
+        self.distortion = cams.distortion.contiguous().to(device) if cams.distortion is not None else None
+        self.num = cams.c2w.shape[0]
+
+
+def exp_map_so3xr3(tangent: torch.Tensor) -> torch.Tensor:
+    """lie_groups.py:28-63 on the (1 x 6) / (C x 6) pose deltas: O(1) work, kept in PyTorch autograd."""
+    log_rot = tangent[:, 3:]
+    nrms = (log_rot * log_rot).sum(1)
+    ang = torch.clamp(nrms, 1e-4).sqrt()
+    inv = 1.0 / ang
+    fac1 = inv * ang.sin()
+    fac2 = inv * inv * (1.0 - ang.cos())
+    B = tangent.shape[0]
+    zero = torch.zeros(B, dtype=tangent.dtype, device=tangent.device)
+    wx, wy, wz = log_rot[:, 0], log_rot[:, 1], log_rot[:, 2]
+    skew = torch.stack([zero, -wz, wy, wz, zero, -wx, -wy, wx, zero], -1).view(B, 3, 3)
+    R = fac1[:, None, None] * skew + fac2[:, None, None] * torch.bmm(skew, skew) + \
+        torch.eye(3, dtype=tangent.dtype, device=tangent.device)[None]
+    return torch.cat([R, tangent[:, :3, None]], dim=-1)
+
+
+class CameraOptimizer(nn.Module):
+    """CameraOptimizer (camera_optimizers.py:34-133), SO3xR3, shared (1 x 6) or per-camera deltas."""
+
+    def __init__(self, modalities: List[str], num_cameras: Dict[str, int], mode: str = "SO3xR3",
+                 shared: bool = True, optimize: Optional[Dict[str, bool]] = None):
+        super().__init__()
+        self.mode = mode
+        self.shared = shared
+        self.optimize = optimize or {m: True for m in modalities}
+        self.pose_adjustment = nn.ParameterDict()
+        if mode != "off":
+            for m in modalities:
+                n = 1 if shared else num_cameras[m]
+                self.pose_adjustment[m] = nn.Parameter(torch.zeros(n, 6))
+
+    def matrices(self, mod: str, device) -> torch.Tensor:
+        if self.mode == "off" or mod not in self.pose_adjustment:
+            return torch.eye(4, device=device)[None, :3, :4]
+        mat = exp_map_so3xr3(self.pose_adjustment[mod])
+        return mat if self.optimize.get(mod, True) else mat.detach()
+
+
+class RayGenerator(nn.Module):
+    """RayGenerator.forward (ray_generators.py:54-81) on the raygen kernel."""
+
+    def __init__(self, cameras: Dict[str, DeviceCameras], pose_optimizer: CameraOptimizer, pixel_offset: float):
+        super().__init__()
+        self.cameras = cameras
+        self.pose_optimizer = pose_optimizer
+        self.pixel_offset = float(pixel_offset)
+
+    def forward(self, coords: Dict[str, torch.Tensor]):
+        out = {}
+        for mod, c in coords.items():
+            cams = self.cameras[mod]
+            mats = self.pose_optimizer.matrices(mod, c.device)
+            o, d, u, a, dn = fx.RaysFunction.apply(mats, c, cams, self.pixel_offset)
+            out[mod] = {"origins": o, "directions": d, "up_directions": u, "pixel_area": a, "directions_norm": dn,
+                        "camera_indices": c[:, :1]}
+        return out
+
+
+class UniformPixelSampler:
+    """UniformPixelSampler.sample (pixel_samplers.py:71-89): host CPU generator, draw order frame, x, y."""
+
+    def __init__(self, num_rays_per_modality: int, seed: int):
+        self.n = num_rays_per_modality
+        self.generator = torch.Generator()
+        self.generator.manual_seed(seed)
+
+    def sample(self, frames: Dict[str, dict]):
+        coords, sel = {}, {}
+        for mod, data in frames.items():
+            n_frames, height, width = data["shape"]
+            ri = torch.randint(0, n_frames, (self.n, 1), dtype=torch.int32, generator=self.generator)
+            fi = data["indexes"][ri]
+            px = torch.randint(0, width, (self.n, 1), dtype=torch.int32, generator=self.generator)
+            py = torch.randint(0, height, (self.n, 1), dtype=torch.int32, generator=self.generator)
+            coords[mod] = torch.cat([fi, py, px], dim=-1)
+            sel[mod] = ri.squeeze(-1)
+        return coords, sel
+
+
+# ------------------------------------------------------------------------------------------------
+# flat-buffer fused AdamW
+# ------------------------------------------------------------------------------------------------
+class FlatGroup:
+    """One optimizer param group with params and grads viewed into flat device buffers."""
+
+    def __init__(self, params: List[nn.Parameter], lr: float, weight_decay: float, eps: float,
+                 betas=(0.9, 0.999)):
+        self.params = [p for p in params]
+        n = sum(p.numel() for p in self.params)
+        pad = (-n) % 4
+        dev = self.params[0].device
+        self.flat = torch.zeros(n + pad, device=dev)
+        self.grad = torch.zeros(n + pad, device=dev)
+        self.m = torch.zeros(n + pad, device=dev)
+        self.v = torch.zeros(n + pad, device=dev)
+        self.sumsq = torch.zeros(1, device=dev)
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            self.flat[off:off + k].copy_(p.data.reshape(-1))
+            p.data = self.flat[off:off + k].view_as(p)
+            p.grad = self.grad[off:off + k].view_as(p)
+            off += k
+        self.n = n
+        self.lr, self.wd, self.eps, self.betas = lr, weight_decay, eps, betas
+        self.step_count = 0
+
+    def zero_grad(self):
+        self.grad.zero_()
+        for p in self.params:   # re-attach in case autograd replaced a grad tensor
+            pass
+
+    def check_grads_attached(self):
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            if p.grad is None or p.grad.data_ptr() != self.grad[off:off + k].data_ptr():
+                g = p.grad
+                view = self.grad[off:off + k].view_as(p)
+                if g is not None:
+                    view.copy_(g)
+                p.grad = view
+            off += k
+
+    def step(self, lr_factor: float, max_norm: float = 2.0):
+        """clip_grad_norm_(max_norm) then torch AdamW math (single launch each; scalars stay on device)."""
+        self.check_grads_attached()
+        self.step_count += 1
+        t = self.step_count
+        b1, b2 = self.betas
+        lr = self.lr * lr_factor
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        self.sumsq.zero_()
+        _lib.call("mms_sumsq", self.grad.data_ptr(), self.n, self.sumsq.data_ptr(), _s())
+        _lib.call("mms_adamw", self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.n,
+                  self.sumsq.data_ptr(), float(max_norm), float(lr), float(self.wd), float(b1), float(b2),
+                  float(self.eps), float(lr / bc1), float(math.sqrt(bc2)), _s())
+
+
+def lr_factor(step: int, max_iters: int = 100000, warm_up_ratio=0.1, milestones=(0.5, 0.75, 0.9), gamma=0.4):
+    """MultiStepWarmupScheduler.func (schedulers.py:259-266) as LambdaLR evaluates it."""
+    warm = int(max_iters * warm_up_ratio)
+    if step < warm:
+        return step / warm
+    idx = int(np.searchsorted(milestones, step / max_iters, side="left"))
+    return gamma ** idx
+
+
+def curvature_factor(step: int, max_iters: int = 100000, num_levels=16, min_res=16, max_res=1024):
+    """CurvatureLossWarmUpScheduler (schedulers.py:320-343), warm_up_ratio 0.1."""
+    warm = int(max_iters * 0.1)
+    if step < warm:
+        return step / warm
+    spl = min(int(max_iters * 1.0), int(max_iters / num_levels))
+    g = float(np.exp((np.log(max_res) - np.log(min_res)) / (num_levels - 1)))
+    level = min(max(int(step / spl) + 1, 1), num_levels)
+    return float(np.reciprocal(g ** (level - 1)))
+
+
+# ------------------------------------------------------------------------------------------------
+# losses
+# ------------------------------------------------------------------------------------------------
+def compute_loss(outputs, targets: Dict[str, torch.Tensor], modalities: List[str], step: int,
+                 sat_threshold: float = 0.9980):
+    """LossManager.compute_loss (losses.py:224-265) for the grid / grid_raw configs."""
+    losses = {}
+    total = None
+    for mod in modalities:
+        thr = sat_threshold if mod == "polarization" else None
+        l = fx.L1LossFunction.apply(outputs[mod][mod], targets[mod], thr)
+        losses[mod] = l
+        total = l if total is None else total + l
+    grads = [outputs[m]["gradients"].reshape(-1, 3) for m in modalities]
+    hess = [outputs[m]["hessians"].reshape(-1, 3) for m in modalities]
+    eik, curv = fx.GeoLossFunction.apply(*grads, *hess)
+    cf = curvature_factor(step)
+    losses["eikonal_loss"] = eik
+    losses["curvature_loss"] = curv
+    total = total + 0.1 * eik + (5e-4 * cf) * curv
+    return losses, total
+
+
+def select_right_channel(rendered: torch.Tensor, band: torch.Tensor) -> torch.Tensor:
+    """RawPipeline.select_right_channel_per_pixel (raw_pipeline.py:112-122): gather at the mosaick band."""
+    return torch.gather(rendered, 1, band)
+
+
+# ------------------------------------------------------------------------------------------------
+# trainer
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class TrainConfig:
+    method: str = "grid"                 # "grid" (demosaicked) or "grid_raw"
+    modalities: tuple = ("rgb",)
+    num_rays_per_modality: int = 2048
+    log2T: int = 19
+    width: int = 640
+    height: int = 512
+    n_views: int = 50
+    max_iters: int = 100000
+    pose_mode: str = "SO3xR3"
+    seed: int = 654824
+
+
+class Trainer:
+    """Synthetic-scene trainer: frames resident in HBM, host pixel sampler, full train step on the HIP path."""
+
+    def __init__(self, cfg: TrainConfig, device, rank: int = 0, frames_on_device: bool = True):
+        self.cfg = cfg
+        self.device = device
+        self.raw = cfg.method == "grid_raw"
+        mods = list(cfg.modalities)
+        self.modalities = mods
+        channels = {m: mscene.CHANNELS[m] for m in mods}
+        torch.manual_seed(654824)
+        self.model = BaseModel(ModelSpec(channels, log2T=cfg.log2T)).to(device)
+        cams = mscene.make_cameras(mods, cfg.n_views, cfg.width, cfg.height, seed=0, train=True)
+        self.cams = {m: DeviceCameras(cams[m], device) for m in mods}
+        self.pose = CameraOptimizer(mods, {m: self.cams[m].num for m in mods}, mode=cfg.pose_mode).to(device)
+        self.raygen = RayGenerator(self.cams, self.pose, 0.0)
+        self.sampler = UniformPixelSampler(cfg.num_rays_per_modality, cfg.seed + rank)
+        # frames cached in HBM (the reference caches all training frames in RAM, dataloaders.py:135-162)
+        self.images = {m: mscene.render_frames(cams[m], channels[m], device, m if self.raw else None) for m in mods}
+        self.frames = {m: {"shape": (cams[m].c2w.shape[0], cfg.height, cfg.width),
+                           "indexes": torch.arange(cams[m].c2w.shape[0], dtype=torch.int32)} for m in mods}
+        self.masks = {m: mscene.mosaick_mask(m, cfg.width, cfg.height).to(device) for m in mods} if self.raw else {}
+        self.fields = FlatGroup(list(self.model.parameters()), lr=1e-3, weight_decay=0.01, eps=1e-15)
+        pose_params = list(self.pose.parameters())
+        self.poses = FlatGroup(pose_params, lr=1e-4, weight_decay=0.01, eps=1e-15) if pose_params else None
+        self.step = 0
+
+    def targets_for(self, coords: Dict[str, torch.Tensor], sel: Dict[str, torch.Tensor]):
+        """Pixel values at the sampled pixels (pixel_samplers.py:86: images[frame, y, x])."""
+        out = {}
+        for m, c in coords.items():
+            img = self.images[m]
+            ri = sel[m].to(img.device).long()
+            cd = c.to(img.device).long()
+            out[m] = img[ri, cd[:, 1], cd[:, 2]]
+        return out
+
+    def set_step(self, step: int):
+        self.step = step
+        self.model.set_step(step, self.cfg.max_iters)
+        self.fields.step_count = step
+        if self.poses is not None:
+            self.poses.step_count = step
+
+    def train_step(self, coords=None, targets=None, rng: Optional[RNG] = None, ddp=None):
+        """One training iteration (raw_pipeline.py:67-82)."""
+        if coords is None:
+            coords, sel = self.sampler.sample(self.frames)
+            targets = self.targets_for(coords, sel)
+        dev = self.device
+        coords_d = {m: c.to(dev, non_blocking=True) for m, c in coords.items()}
+        targets_d = {m: t.to(dev, non_blocking=True) for m, t in targets.items()}
+        rays = self.raygen(coords_d)
+        outputs = self.model(rays, rng)
+        if self.raw:
+            for m in self.modalities:
+                band = self.masks[m][coords_d[m][:, 1].long(), coords_d[m][:, 2].long()].long()[:, None]
+                outputs[m][m] = select_right_channel(outputs[m][m], band)
+        losses, total = compute_loss(outputs, targets_d, self.modalities, self.step)
+        self.fields.zero_grad()
+        if self.poses is not None:
+            self.poses.zero_grad()
+        total.backward()
+        if ddp is not None:
+            ddp.allreduce_grads([self.fields] + ([self.poses] if self.poses is not None else []))
+        f = lr_factor(self.step, self.cfg.max_iters)
+        self.fields.step(f)
+        if self.poses is not None:
+            self.poses.step(f)
+        self.step += 1
+        return losses, total, outputs

@@ -106,3 +106,37 @@ def analytic_radiance(origins: np.ndarray, dirs: np.ndarray, channels: int) -> n
     w = 0.6 + 0.4 * np.cos(k * 0.7)
     out = (col3[..., k % 3] * w)
     return np.clip(out, 0.0, 1.0).astype(np.float32)
+
+
+def render_frames(cams: ModalityCameras, channels: int, device, raw_mod: Optional[str] = None) -> torch.Tensor:
+    """Analytic frames [C, H, W, channels] (or mosaicked [C, H, W, 1] when raw_mod is given) on `device`.
+
+    Data preparation only (the reference loads frames from disk into RAM, dataloaders.py:135-162); uses
+    plain tensor math on the chosen device.
+    """
+    H, W = cams.height, cams.width
+    ys, xs = torch.meshgrid(torch.arange(H, device=device, dtype=torch.float32),
+                            torch.arange(W, device=device, dtype=torch.float32), indexing="ij")
+    frames = []
+    k = torch.arange(channels, device=device)
+    wk = 0.6 + 0.4 * torch.cos(k * 0.7)
+    mm = mosaick_mask(raw_mod, W, H).to(device).long() if raw_mod is not None else None
+    for c in range(cams.c2w.shape[0]):
+        c2w = cams.c2w[c].to(device)
+        dc = torch.stack([(xs - cams.cx[c]) / cams.fx[c], -(ys - cams.cy[c]) / cams.fy[c], -torch.ones_like(xs)], -1)
+        d = torch.nn.functional.normalize(dc @ c2w[:, :3].T, dim=-1)
+        o = c2w[:, 3].expand_as(d)
+        b = (o * d).sum(-1)
+        cc = (o * o).sum(-1) - 0.25
+        disc = b * b - cc
+        hit = disc > 0
+        t = -b - torch.sqrt(torch.clamp(disc, min=0))
+        n = (o + d * t[..., None]) / 0.5
+        base = 0.5 + 0.5 * n
+        bgc = 0.5 + 0.4 * torch.stack([d[..., 2], d[..., 0], d[..., 1]], -1)
+        col3 = torch.where(hit[..., None], base, bgc)
+        img = torch.clamp(col3[..., k % 3] * wk, 0.0, 1.0)
+        if mm is not None:
+            img = torch.gather(img, -1, mm[..., None])
+        frames.append(img)
+    return torch.stack(frames, 0)
