@@ -1,0 +1,203 @@
+#!/usr/bin/env python
+"""Train-rays/s benchmark of the MMS hot path on MI355X (BASELINE.json metric, configs[1] by default).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config grid_rgb|grid_raw5] [--rays R]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = one full training iteration of RawPipeline/BasePipeline.train_step on synthetic data of the
+MMS-DATA shape: host pixel sampling (reference RNG), ray generation with SO3xR3 pose refinement, the
+collider, the 4-iteration NeuS sampler, hash grids, SDF MLP with 4 numerical-gradient taps, radiance
+MLP, heads, background NeRF, NeuS compositing, losses, backward, grad clipping, AdamW.  Random-init
+weights; model state at step 95000 (all 16 grid levels active).  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import statistics
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (method, modalities, workload description)
+    "grid_rgb": ("grid", ("rgb",), "confs/grid.yaml, RGB-only (modalities: [rgb]), hash grid + MLPs, 1 GPU"),
+    "grid_raw5": ("grid_raw", ("rgb", "infrared", "mono", "polarization", "multispectral"),
+                  "confs/grid_raw.yaml, 5-modality mosaicked, per-modality heads"),
+}
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+F32_MFMA_PEAK_TF = 157.3   # dense f32-input MFMA (v_mfma_f32_32x32x2_f32) peak, MI355X_MICROARCH.md
+HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per lookup, forward
+HASH_BWD_B = 128 + 12 + 16 * 8 * 2 * (4 + 4)    # bytes per lookup, backward (table grads)
+
+
+def work_fns():
+    return {
+        "mms_gemm_f32": lambda a: 2.0 * a[1] * a[2] * a[3],
+        "mms_hashgrid_fwd": lambda a: float(a[1]) * HASH_FWD_B,
+        "mms_hashgrid_bwd": lambda a: float(a[1]) * HASH_BWD_B,
+    }
+
+
+def cpu_baseline(trainer, cfg, seconds: float):
+    """The fixture-pinned CPU restatement (oracle/) of the same workload, bounded sample, on host cores."""
+    from oracle.train import OracleTrainer
+    from multimodalstudio_amd import scene as ms
+    mods = list(cfg.modalities)
+    channels = {m: ms.CHANNELS[m] for m in mods}
+    sd = {k: v.detach().cpu() for k, v in trainer.model.state_dict().items()}
+    ot = OracleTrainer(sd, channels, trainer.host_cams, cfg.log2T, trainer.step, raw=False)
+    n_rays = 256
+    g = torch.Generator().manual_seed(1)
+
+    def batch():
+        coords, targets = {}, {}
+        for m in mods:
+            cams = trainer.host_cams[m]
+            C = cams.c2w.shape[0]
+            c = torch.stack([torch.randint(0, C, (n_rays,), generator=g), torch.randint(0, cfg.height, (n_rays,),
+                            generator=g), torch.randint(0, cfg.width, (n_rays,), generator=g)], -1).to(torch.int32)
+            coords[m] = c
+            targets[m] = torch.rand(n_rays, channels[m], generator=g)
+        return coords, targets
+
+    ot.train_step(*batch())   # warmup
+    times = []
+    t_start = time.perf_counter()
+    while (time.perf_counter() - t_start < seconds and len(times) < 50) or len(times) < 3:
+        c, t = batch()
+        t0 = time.perf_counter()
+        ot.train_step(c, t)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {
+        "value": round(n_rays * len(mods) / med, 2),
+        "unit": "rays/s",
+        "cores": torch.get_num_threads(),
+        "kind": "port",
+        "sample": f"{len(times)} timed steps (median) of the CPU restatement (oracle/, bit-exact to the reference "
+                  f"torch path) at {n_rays} rays/modality, same config, log2T={cfg.log2T}, fwd+bwd+AdamW; "
+                  f"host {platform.processor() or platform.machine()}",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="grid_rgb", choices=list(CONFIGS))
+    ap.add_argument("--rays", type=int, default=2048, help="num_rays_per_modality (grid.yaml: 2048)")
+    ap.add_argument("--log2T", type=int, default=19)
+    ap.add_argument("--start-step", type=int, default=95000)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    from multimodalstudio_amd import _lib
+    from multimodalstudio_amd import ddp as mddp
+    from multimodalstudio_amd.pipeline import Trainer, TrainConfig
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    ddp = mddp.init_from_env("nccl") if world > 1 else None
+
+    method, mods, desc = CONFIGS[args.config]
+    cfg = TrainConfig(method=method, modalities=mods, num_rays_per_modality=args.rays, log2T=args.log2T)
+    trainer = Trainer(cfg, dev, rank=rank)
+    trainer.set_step(args.start_step)
+
+    for _ in range(args.warmup):
+        trainer.train_step(ddp=ddp)
+    torch.cuda.synchronize()
+    if ddp:
+        ddp.barrier()
+    torch.cuda.synchronize()
+    if not args.no_kernel_timing:
+        _lib.TIMER.start(work_fns())
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.train_step(ddp=ddp)
+    torch.cuda.synchronize()
+    if ddp:
+        ddp.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    _lib.TIMER.stop()
+    if ddp:
+        elapsed = ddp.max_over_ranks(elapsed, dev)
+
+    rays_per_step = args.rays * len(mods) * world
+    value = rays_per_step * args.steps / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    roof = None
+    kernels = []
+    if not args.no_kernel_timing:
+        summ = _lib.TIMER.summary()
+        for name, (n, ms, work) in summ.items():
+            launches_per_step = n / args.steps
+            if name == "mms_gemm_f32":
+                ach = work / (ms * 1e-3) / 1e12
+                kernels.append({"kernel": name, "bound": "mfma", "achieved": round(ach, 3), "peak": F32_MFMA_PEAK_TF,
+                                "unit": "TFLOP/s", "frac": round(ach / F32_MFMA_PEAK_TF, 4),
+                                "avg_ms": round(ms, 5), "launches_per_step": launches_per_step,
+                                "ms_per_step": round(ms * launches_per_step, 4), "traffic": None})
+            else:
+                ach = work / (ms * 1e-3) / 1e9
+                kernels.append({"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "avg_ms": round(ms, 5),
+                                "launches_per_step": launches_per_step,
+                                "ms_per_step": round(ms * launches_per_step, 4), "traffic": None})
+        kernels.sort(key=lambda k: -k["ms_per_step"])
+        if kernels:
+            top = kernels[0]
+            roof = {k: top[k] for k in ["bound", "achieved", "peak", "unit", "frac", "traffic"]}
+            roof["kernel"] = top["kernel"]
+            roof["avg_ms"] = top["avg_ms"]
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(trainer, cfg, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "train rays/sec (grid.yaml MMS-DATA-shaped synthetic scene)",
+            "value": round(value, 1),
+            "unit": "rays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (analytic MMS-DATA-shaped scene, 45 train views 640x512, random-init weights)",
+            "config": {"workload": desc, "num_rays_per_modality": args.rays, "modalities": list(mods),
+                       "rays_per_step": rays_per_step, "log2_hashmap_size": args.log2T,
+                       "model_step": args.start_step, "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "roofline_kernels": kernels,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if ddp:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

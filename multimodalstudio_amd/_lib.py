@@ -70,10 +70,52 @@ def lib():
     return L
 
 
+class KernelTimer:
+    """Live per-launch timing of selected entry points with HIP events on the launching stream.
+
+    ``watch[name] = work_fn(args) -> algorithmic bytes or flops of that launch``.  Used by bench.py for
+    the roofline fractions; disabled (zero overhead beyond a dict lookup) unless ``active``.
+    """
+
+    def __init__(self):
+        self.active = False
+        self.watch = {}
+        self.records = []
+
+    def start(self, watch):
+        self.watch = dict(watch)
+        self.records = []
+        self.active = True
+
+    def stop(self):
+        self.active = False
+
+    def summary(self):
+        """{name: (launches, mean_ms, mean_work)} — call after a device synchronise."""
+        out = {}
+        for name, ev0, ev1, work in self.records:
+            ms = ev0.elapsed_time(ev1)
+            n, t, w = out.get(name, (0, 0.0, 0.0))
+            out[name] = (n + 1, t + ms, w + work)
+        return {k: (n, t / n, w / n) for k, (n, t, w) in out.items()}
+
+
+TIMER = KernelTimer()
+
+
 def call(name: str, *args) -> None:
     """Invoke ``name`` and raise RuntimeError with mms_last_error() on a non-zero status."""
     L = lib()
+    timed = TIMER.active and name in TIMER.watch
+    if timed:
+        import torch
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
     rc = getattr(L, name)(*args)
+    if timed:
+        e1.record()
+        TIMER.records.append((name, e0, e1, float(TIMER.watch[name](args))))
     if rc != 0:
         msg = L.mms_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed ({rc}): {msg}")

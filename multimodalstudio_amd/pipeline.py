@@ -267,6 +267,7 @@ class Trainer:
         self.sampler = UniformPixelSampler(cfg.num_rays_per_modality, cfg.seed + rank)
         # frames cached in HBM (the reference caches all training frames in RAM, dataloaders.py:135-162)
         self.images = {m: mscene.render_frames(cams[m], channels[m], device, m if self.raw else None) for m in mods}
+        self.host_cams = cams
         self.frames = {m: {"shape": (cams[m].c2w.shape[0], cfg.height, cfg.width),
                            "indexes": torch.arange(cams[m].c2w.shape[0], dtype=torch.int32)} for m in mods}
         self.masks = {m: mscene.mosaick_mask(m, cfg.width, cfg.height).to(device) for m in mods} if self.raw else {}
