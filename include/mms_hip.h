@@ -45,6 +45,15 @@ int mms_gemm_f32(int mode, int64_t M, int64_t N, int64_t K, const float* A, int6
                  int64_t ldb, float* C, int64_t ldc, const float* bias, float* Z, int64_t ldz, const float* aux,
                  int64_t ldaux, int act, int dact, float beta, float thr, int accumulate, int splits, void* stream);
 
+/* ---- MLP GEMM engine (field_components/mlp.py:152-171): C = epilogue(op(A) op(B)^T).
+ * trans_a = 0: A is [M, K] (lda); 1: A is stored [K, M].  trans_b = 0: B is [N, K]; 1: B is stored [K, N].
+ * prec 0 = exact fp32 MFMA, 1 = bf16 MFMA (fp32 accumulate), 2 = split bf16x3 (near-fp32 operands).
+ * Epilogue as mms_gemm_f32; ones_col >= 0 also writes 1.0 at column ones_col of every output row. */
+int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+             const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, float* Z, int64_t ldz,
+             const float* aux, int64_t ldaux, int act, int dact, float beta, float thr, int accumulate, int splits,
+             int ones_col, void* stream);
+
 /* ---- weight norm (mlp.py:206-209; torch weight_norm dim=0): W = v * (g / ||v||_row); bwd dg += , dv += */
 int mms_weight_norm_fwd(const float* g, const float* v, int64_t N, int64_t K, float* W, int64_t ldw, float* norms,
                         void* stream);

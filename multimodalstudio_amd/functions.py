@@ -29,6 +29,21 @@ from .hip_ops import NN, NT, TN, _splits_for, act_bwd, colsum_, gemm, weight_nor
 
 ACT = {None: 0, "None": 0, "ReLU": 1, "Softplus": 2, "Sigmoid": 3}
 
+# GEMM operand precision per MLP family: 0 exact fp32 MFMA (parity mode), 1 bf16, 2 split bf16x3.
+PRECISION = {"sdf": 0, "radiance": 0, "heads": 0, "background": 0}
+PRESETS = {
+    "fp32": {"sdf": 0, "radiance": 0, "heads": 0, "background": 0},
+    # throughput mode: the SDF MLP keeps ~fp32 operand precision (its 4-tap finite differences divide
+    # sdf differences by 4 delta ~ 4.5e-3), everything else runs bf16 MFMA with fp32 accumulation
+    "fast": {"sdf": 2, "radiance": 1, "heads": 1, "background": 1},
+    "bf16x3": {"sdf": 2, "radiance": 2, "heads": 2, "background": 2},
+}
+
+
+def set_precision(mode: str) -> None:
+    """Select the MLP GEMM precision preset ('fp32' parity | 'fast' | 'bf16x3')."""
+    PRECISION.update(PRESETS[mode])
+
 
 def _s() -> int:
     return torch.cuda.current_stream().cuda_stream
@@ -79,7 +94,8 @@ def grid_bwd(g: GridCfg, pos, ldx, M, table, active, dout: torch.Tensor, col: in
 class MLPRun:
     """Forward activations of a weight-normed MLP kept for the explicit backward."""
 
-    def __init__(self, params: Sequence[torch.Tensor], acts: Sequence[Tuple[int, float, float]]):
+    def __init__(self, params: Sequence[torch.Tensor], acts: Sequence[Tuple[int, float, float]], prec: int = 0):
+        self.prec = int(prec)
         self.params = list(params)
         self.acts = list(acts)
         self.L = len(self.params) // 3
@@ -107,7 +123,7 @@ class MLPRun:
                 Y = torch.empty(M, N, device=dev)
             Z = torch.empty(M, N, device=dev) if (keep and act != 0) else None
             gemm(NT, M, N, K, h, h.stride(0), W, W.stride(0), Y, Y.stride(0), bias=b, Z=Z, ldz=N, act=act, beta=beta,
-                 thr=thr)
+                 thr=thr, prec=self.prec)
             if keep:
                 self.Ws.append(W)
                 self.norms.append(nrm)
@@ -135,7 +151,7 @@ class MLPRun:
             dW = torch.zeros(N, K, device=dev)
             tiles = ((N + 127) // 128) * ((K + 127) // 128)
             gemm(TN, N, K, M, dZ, dZ.stride(0), Xin, Xin.stride(0), dW, K, accumulate=True,
-                 splits=_splits_for(M, tiles))
+                 splits=_splits_for(M, tiles), prec=self.prec)
             db = torch.zeros(N, device=dev)
             colsum_(dZ, db)
             dg = torch.zeros(N, device=dev)
@@ -146,11 +162,11 @@ class MLPRun:
                 pa, pbeta, pthr = self.acts[l - 1]
                 dprev = torch.empty(M, K, device=dev)
                 gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[l], K, dprev, K,
-                     aux=self.Zs[l - 1] if pa != 0 else None, ldaux=K, dact=pa, beta=pbeta, thr=pthr)
+                     aux=self.Zs[l - 1] if pa != 0 else None, ldaux=K, dact=pa, beta=pbeta, thr=pthr, prec=self.prec)
                 dZ = dprev
             elif need_dx:
                 dx = torch.empty(M, K, device=dev)
-                gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[0], K, dx, K)
+                gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[0], K, dx, K, prec=self.prec)
         return dx, grads
 
 
@@ -177,7 +193,7 @@ class SurfaceFunction(torch.autograd.Function):
         d32 = float(torch.tensor(delta, dtype=torch.float32))
         _lib.call("mms_geo_input_fwd", pos.data_ptr(), 3, M, 4, d32, 6, X.data_ptr(), K0, _s())
         grid_fwd(grid, X, K0, 5 * M, table, active, X, 39)
-        run = MLPRun(params, SDF_ACTS)
+        run = MLPRun(params, SDF_ACTS, PRECISION["sdf"])
         out = run.forward(X, keep=True)
         G = out.shape[1] - 1
         four_delta = float(torch.tensor(4.0 * delta, dtype=torch.float32))
@@ -238,7 +254,7 @@ def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> to
     last = list(params[-3:])
     g, v, b = last
     p2 = list(params[:-3]) + [g[:1], v[:1].contiguous(), b[:1]]
-    run = MLPRun(p2, SDF_ACTS)
+    run = MLPRun(p2, SDF_ACTS, PRECISION["sdf"])
     out = run.forward(X, keep=False)
     return out[:, 0]
 
@@ -266,7 +282,7 @@ class RadianceFunction(torch.autograd.Function):
         _lib.call("mms_rad_input_fwd", pos.data_ptr(), 3, dirs.data_ptr(), normals.data_ptr(), geo.data_ptr(),
                   geo.stride(0), M, S, G, X.data_ptr(), K0, _s())
         grid_fwd(grid, X, K0, M, table, active, X, 29 + G)
-        run = MLPRun(params, RAD_ACTS)
+        run = MLPRun(params, RAD_ACTS, PRECISION["radiance"])
         feat = run.forward(X, keep=True)
         ctx.run, ctx.X, ctx.grid, ctx.active, ctx.S, ctx.G = run, X, grid, active, S, G
         ctx.save_for_backward(pos, dirs, normals, table, *params)
@@ -301,7 +317,7 @@ class RadianceFunction(torch.autograd.Function):
 class MLPFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, acts, *params):
-        run = MLPRun(params, acts)
+        run = MLPRun(params, acts, PRECISION["heads"])
         # grad mode is off inside Function.forward: decide from what the graph will need
         y = run.forward(x.contiguous(), keep=any(ctx.needs_input_grad))
         ctx.run = run
@@ -338,11 +354,11 @@ class BackgroundFunction(torch.autograd.Function):
         dirs = dirs.contiguous()
         _lib.call("mms_bg_input_fwd", pos.data_ptr(), M, dirs.data_ptr(), S, X.data_ptr(), 39, H.data_ptr(),
                   H.stride(0), Fb, _s())
-        base = MLPRun(base_p, BG_BASE_ACTS[:nb])
+        base = MLPRun(base_p, BG_BASE_ACTS[:nb], PRECISION["background"])
         base.forward(X, keep=True, last_out=H)          # writes cols [0, Fb) of the head panel
-        dens = MLPRun(dens_p, BG_DENS_ACTS)
+        dens = MLPRun(dens_p, BG_DENS_ACTS, PRECISION["background"])
         density = _mlp_strided(dens, H, Fb)             # density head reads the base features in place
-        head = MLPRun(head_p, BG_HEAD_ACTS[:len(head_p) // 3])
+        head = MLPRun(head_p, BG_HEAD_ACTS[:len(head_p) // 3], PRECISION["background"])
         feat = head.forward(H, keep=True)
         ctx.base, ctx.dens, ctx.head, ctx.X, ctx.H = base, dens, head, X, H
         ctx.S, ctx.nb, ctx.nd, ctx.Fb = S, nb, nd, Fb
@@ -381,7 +397,7 @@ def _mlp_strided(run: MLPRun, H: torch.Tensor, Fb: int) -> torch.Tensor:
     act, beta, thr = run.acts[0]
     Y = torch.empty(M, N, device=dev)
     Z = torch.empty(M, N, device=dev)
-    gemm(NT, M, N, K, H, H.stride(0), W, K, Y, N, bias=b, Z=Z, ldz=N, act=act, beta=beta, thr=thr)
+    gemm(NT, M, N, K, H, H.stride(0), W, K, Y, N, bias=b, Z=Z, ldz=N, act=act, beta=beta, thr=thr, prec=run.prec)
     run.Ws, run.norms, run.Zs, run.Ys = [W], [nrm], [Z], [Y]
     return Y
 
@@ -395,14 +411,14 @@ def _mlp_strided_bwd(run: MLPRun, dy: torch.Tensor, H: torch.Tensor, Fb: int):
     dZ = torch.empty(M, N, device=dev)
     act_bwd(dy, run.Zs[0], act, beta, thr, dZ)
     dW = torch.zeros(N, K, device=dev)
-    gemm(TN, N, K, M, dZ, N, H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1))
+    gemm(TN, N, K, M, dZ, N, H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1), prec=run.prec)
     db = torch.zeros(N, device=dev)
     colsum_(dZ, db)
     dg = torch.zeros(N, device=dev)
     dv = torch.zeros(N, K, device=dev)
     weight_norm_bwd(g.reshape(-1), v, run.norms[0], dW, dg, dv)
     dxin = torch.empty(M, K, device=dev)
-    gemm(NN, M, K, N, dZ, N, run.Ws[0], K, dxin, K)
+    gemm(NN, M, K, N, dZ, N, run.Ws[0], K, dxin, K, prec=run.prec)
     return dxin, [dg.view_as(g), dv, db]
 
 

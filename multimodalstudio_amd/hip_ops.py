@@ -89,12 +89,27 @@ class HashGridFunction(torch.autograd.Function):
 # ----------------------------------------------------------------------------------------------
 # GEMM
 # ----------------------------------------------------------------------------------------------
+_MODE_TRANS = {NT: (0, 0), NN: (0, 1), TN: (1, 1)}
+PREC_IDS = {"fp32": 0, "bf16": 1, "bf16x3": 2}
+
+
 def gemm(mode: int, M: int, N: int, K: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int,
          C: torch.Tensor, ldc: int, bias=None, Z=None, ldz=0, aux=None, ldaux=0, act=0, dact=0,
-         beta=1.0, thr=20.0, accumulate=False, splits=1):
-    _lib.call("mms_gemm_f32", int(mode), int(M), int(N), int(K), A.data_ptr(), int(lda), B.data_ptr(), int(ldb),
+         beta=1.0, thr=20.0, accumulate=False, splits=1, prec: int = 0, ones_col: int = -1):
+    """NT: C = A B^T (A [M,K], B [N,K]); NN: C = A B (B [K,N]); TN: C = A^T B (A [K,M], B [K,N])."""
+    ta, tb = _MODE_TRANS[mode]
+    _lib.call("mms_gemm", int(prec), ta, tb, int(M), int(N), int(K), A.data_ptr(), int(lda), B.data_ptr(), int(ldb),
               C.data_ptr(), int(ldc), _ptr(bias), _ptr(Z), int(ldz), _ptr(aux), int(ldaux), int(act), int(dact),
-              float(beta), float(thr), int(bool(accumulate)), int(splits), _stream())
+              float(beta), float(thr), int(bool(accumulate)), int(splits), int(ones_col), _stream())
+
+
+def gemm_f32_legacy(mode: int, M: int, N: int, K: int, A, lda, B, ldb, C, ldc, **kw):
+    """The first-generation fp32 GEMM (mms_gemm_f32), kept for A/B comparisons."""
+    _lib.call("mms_gemm_f32", int(mode), int(M), int(N), int(K), A.data_ptr(), int(lda), B.data_ptr(), int(ldb),
+              C.data_ptr(), int(ldc), _ptr(kw.get("bias")), _ptr(kw.get("Z")), int(kw.get("ldz", 0)),
+              _ptr(kw.get("aux")), int(kw.get("ldaux", 0)), int(kw.get("act", 0)), int(kw.get("dact", 0)),
+              float(kw.get("beta", 1.0)), float(kw.get("thr", 20.0)), int(bool(kw.get("accumulate", False))),
+              int(kw.get("splits", 1)), _stream())
 
 
 def weight_norm_fwd(g, v, W, norms):

@@ -71,3 +71,31 @@ def test_gemm_modes(dev, M, N, K):
     torch.cuda.synchronize()
     np.testing.assert_allclose(dX.cpu().numpy(), dx_ref.numpy(), rtol=1e-4, atol=2e-3)
     np.testing.assert_allclose(dW.cpu().numpy(), dw_ref.numpy(), rtol=1e-4, atol=5e-3)
+
+
+@pytest.mark.parametrize("prec,tol", [(0, 2e-6), (2, 2e-5), (1, 2e-2)])
+@pytest.mark.parametrize("M,N,K", [(1000, 257, 71), (300, 3, 64), (4096, 256, 256), (77, 130, 317), (2000, 128, 283)])
+def test_gemm_precisions(dev, prec, tol, M, N, K):
+    """mms_gemm (f32 / bf16 / bf16x3) in all three layouts vs fp64; tolerance relative to max|ref|."""
+    from multimodalstudio_amd import hip_ops
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    X = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) * 0.1
+    b = torch.randn(N, generator=g)
+    dZ = torch.randn(M, N, generator=g)
+    Xd, Wd, bd, dZd = X.to(dev), W.to(dev), b.to(dev), dZ.to(dev)
+
+    def chk(out, ref, what):
+        ref = ref.numpy()
+        err = np.abs(out.cpu().double().numpy() - ref).max() / np.abs(ref).max()
+        assert err < tol, f"{what} prec={prec}: rel err {err:.2e}"
+
+    Y = torch.empty(M, N, device=dev)
+    hip_ops.gemm(hip_ops.NT, M, N, K, Xd, K, Wd, K, Y, N, bias=bd, prec=prec)
+    chk(Y, X.double() @ W.double().T + b.double(), "NT")
+    dX = torch.empty(M, K, device=dev)
+    hip_ops.gemm(hip_ops.NN, M, K, N, dZd, N, Wd, K, dX, K, prec=prec)
+    chk(dX, dZ.double() @ W.double(), "NN")
+    dW = torch.zeros(N, K, device=dev)
+    hip_ops.gemm(hip_ops.TN, N, K, M, dZd, N, Xd, K, dW, K, accumulate=True, splits=3, prec=prec)
+    chk(dW, dZ.double().T @ X.double(), "TN")
