@@ -35,13 +35,19 @@ CONFIGS = {
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F32_MFMA_PEAK_TF = 157.3   # dense f32-input MFMA (v_mfma_f32_32x32x2_f32) peak, MI355X_MICROARCH.md
+BF16_MFMA_PEAK_TF = 2500.0  # dense bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
+# split-bf16x3 runs 3 bf16 MFMAs per f32 product: its ceiling for the algorithmic 2MNK flops is a third
+MFMA_PEAK_TF = {"fp32": F32_MFMA_PEAK_TF, "bf16": BF16_MFMA_PEAK_TF, "bf16x3": BF16_MFMA_PEAK_TF / 3}
+PREC_NAMES = {0: "fp32", 1: "bf16", 2: "bf16x3"}
+DTYPES = {"fp32": "fp32", "fast": "bf16 MFMA (fp32 accumulate; SDF MLP split-bf16x3), fp32 elsewhere",
+          "bf16x3": "split-bf16x3 MFMA (fp32-accurate), fp32 elsewhere"}
 HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per lookup, forward
 HASH_BWD_B = 128 + 12 + 16 * 8 * 2 * (4 + 4)    # bytes per lookup, backward (table grads)
 
 
 def work_fns():
     return {
-        "mms_gemm_f32": lambda a: 2.0 * a[1] * a[2] * a[3],
+        "mms_gemm": lambda a: (PREC_NAMES[a[0]], 2.0 * a[3] * a[4] * a[5]),
         "mms_hashgrid_fwd": lambda a: float(a[1]) * HASH_FWD_B,
         "mms_hashgrid_bwd": lambda a: float(a[1]) * HASH_BWD_B,
     }
@@ -101,11 +107,15 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--precision", default="fp32", choices=list(DTYPES),
+                    help="MLP GEMM precision preset (functions.PRESETS); fp32 = reference-parity mode")
     args = ap.parse_args()
 
     from multimodalstudio_amd import _lib
     from multimodalstudio_amd import ddp as mddp
     from multimodalstudio_amd.pipeline import Trainer, TrainConfig
+    from multimodalstudio_amd import functions as mfn
+    mfn.set_precision(args.precision)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -149,10 +159,11 @@ def main():
         summ = _lib.TIMER.summary()
         for name, (n, ms, work) in summ.items():
             launches_per_step = n / args.steps
-            if name == "mms_gemm_f32":
+            if name.startswith("mms_gemm"):
+                peak = MFMA_PEAK_TF[name.split(":")[1]]
                 ach = work / (ms * 1e-3) / 1e12
-                kernels.append({"kernel": name, "bound": "mfma", "achieved": round(ach, 3), "peak": F32_MFMA_PEAK_TF,
-                                "unit": "TFLOP/s", "frac": round(ach / F32_MFMA_PEAK_TF, 4),
+                kernels.append({"kernel": name, "bound": "mfma", "achieved": round(ach, 3), "peak": peak,
+                                "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                                 "avg_ms": round(ms, 5), "launches_per_step": launches_per_step,
                                 "ms_per_step": round(ms * launches_per_step, 4), "traffic": None})
             else:
@@ -184,11 +195,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": DTYPES[args.precision],
             "data": "synthetic (analytic MMS-DATA-shaped scene, 45 train views 640x512, random-init weights)",
             "config": {"workload": desc, "num_rays_per_modality": args.rays, "modalities": list(mods),
                        "rays_per_step": rays_per_step, "log2_hashmap_size": args.log2T,
-                       "model_step": args.start_step, "parallelism": f"dp{world}"},
+                       "model_step": args.start_step, "precision": args.precision, "parallelism": f"dp{world}"},
             "roofline": roof,
             "roofline_kernels": kernels,
             "cpu_baseline": cpu,

@@ -73,7 +73,8 @@ def lib():
 class KernelTimer:
     """Live per-launch timing of selected entry points with HIP events on the launching stream.
 
-    ``watch[name] = work_fn(args) -> algorithmic bytes or flops of that launch``.  Used by bench.py for
+    ``watch[name] = work_fn(args) -> algorithmic bytes or flops of that launch`` (or ``(label, work)`` to
+    split one entry point into several records, e.g. the GEMM per precision).  Used by bench.py for
     the roofline fractions; disabled (zero overhead beyond a dict lookup) unless ``active``.
     """
 
@@ -115,7 +116,11 @@ def call(name: str, *args) -> None:
     rc = getattr(L, name)(*args)
     if timed:
         e1.record()
-        TIMER.records.append((name, e0, e1, float(TIMER.watch[name](args))))
+        w = TIMER.watch[name](args)
+        key = name
+        if isinstance(w, tuple):
+            key, w = f"{name}:{w[0]}", w[1]
+        TIMER.records.append((key, e0, e1, float(w)))
     if rc != 0:
         msg = L.mms_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed ({rc}): {msg}")

@@ -8,31 +8,49 @@
 // Precision modes (template PREC):
 //   F32    v_mfma_f32_32x32x2_f32  — exact fp32 (bitwise an fmaf chain); the parity mode
 //   BF16   v_mfma_f32_32x32x16_bf16 on RNE-rounded operands, fp32 accumulate
-//   BF16X3 split operands x = hi + lo (both bf16); acc += hi.hi + hi.lo + lo.hi  (~2^-16 relative
+//   BF16X3 split operands x = hi + lo (both bf16); acc += lo.hi + hi.lo + hi.hi  (~2^-16 relative
 //          operand precision, fp32 accumulate) — 16x/3 the f32-MFMA rate at near-fp32 accuracy, used
 //          for the SDF MLP whose 4-tap finite differences need the extra mantissa.
 //
-// Tiling: 128x128 block tile, BK = 32, 256 threads = 2x2 waves of 64x64 (2x2 MFMA 32x32 tiles/wave).
-// Operands are register-prefetched one k-step ahead with 16-byte loads and staged in LDS k-contiguous
-// per row ([row][BK+pad]); fragments are one ds_read_b32 (F32, pad 1: conflict-free) or two
-// ds_read_b128 (BF16*, pad 4: 16-B aligned, conflict-free per 16-lane group).  The block -> tile map
-// keeps the N-tiles of one M panel on one XCD (ids b and b+8), so the A panel is fetched into one L2.
-// Split-K over grid.z accumulates with hardware f32 atomics (tall-skinny weight gradients).
+// Tiling: 128x128 block tile, 256 threads = 2x2 waves of 64x64 (2x2 MFMA 32x32 tiles per wave).
+// Operands are register-prefetched one k-step ahead with 16-byte loads and staged in LDS already in
+// the MFMA input format (f32, or bf16 / bf16 hi+lo converted once per element at staging):
+//   N source -> [row][BK + pad] image, fragments by ds_read_b32 (F32) / ds_read_b128 (bf16)
+//   T source -> [k][128 + pad] image (no transpose on the way in), fragments by ds_read_b32 (F32:
+//               consecutive lanes read consecutive rows) / ds_read_b64_tr_b16 (bf16: the hardware
+//               transposing read delivers 4 k-values of one row per lane; two reads per 32x32x16 fragment).
+// BK = 32 (F32, BF16X3) or 64 (BF16).  The block -> tile map keeps the N-tiles of one M panel on one XCD
+// (ids b and b+8); split-K (small outputs, long K: weight gradients) folds the K slice into blockIdx.x
+// and accumulates with hardware f32 atomics.
 #include "common.h"
+
+#include <type_traits>
 
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short short4_ __attribute__((ext_vector_type(4)));
+typedef short short8_ __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) short4_ lds_short4;
 
 enum Prec { P_F32 = 0, P_BF16 = 1, P_BF16X3 = 2 };
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SOFTPLUS = 2, ACT_SIGMOID = 3 };
 
-constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int BM = 128, BN = 128;
 
+// ---------------------------------------------------------------------------- per-precision geometry
 template <int PREC>
-struct LdsK {
-  static constexpr int v = (PREC == P_F32) ? (BK + 1) : (BK + 4);
+struct Geo {
+  static constexpr int BK = (PREC == P_BF16) ? 64 : 32;
+  using elem = typename std::conditional<PREC == P_F32, float, __bf16>::type;
+  static constexpr int NIMG = (PREC == P_BF16X3) ? 2 : 1;          // hi (+ lo) images per operand
+  // N image: [128][LDN]; T image: [BK][LDT]  (elements)
+  static constexpr int LDN = (PREC == P_F32) ? BK + 1 : BK + 8;     // f32: odd stride; bf16: 16-B rows
+  static constexpr int LDT = (PREC == P_F32) ? 128 + 4 : 128 + 32;  // bf16: 320-B rows, tr reads conflict-free
+  template <bool T>
+  static constexpr int img_elems() { return T ? BK * LDT : 128 * LDN; }
 };
 
 struct Epi {
@@ -45,6 +63,7 @@ struct Epi {
   float beta, thr;
   int accumulate;
   int ones_col;  // >= 0: also write 1.0 at C[row, ones_col] (bias-gradient column for the next TN GEMM)
+  int splits;    // K slices folded into blockIdx.x
 };
 
 __device__ __forceinline__ float act_fwd(int act, float v, float beta, float thr) {
@@ -65,20 +84,20 @@ __device__ __forceinline__ float act_grad(int act, float z, float beta, float th
   }
 }
 
-// ---------------------------------------------------------------------------- staging
-// N source ([rows][K], k contiguous): 1024 float4 per 128x32 tile, thread t covers idx = t + 256 i:
-//   row = idx >> 3, kc = idx & 7  -> 8 lanes read one row's 128 contiguous bytes.
-// T source ([K][rows], rows contiguous): kr = (idx & 7) | ((idx >> 8) << 3), cc = (idx >> 3) & 31.
-template <bool T, bool VEC>
+// ---------------------------------------------------------------------------- global -> registers
+// NV = float4 per thread per operand tile = 128 * BK / 4 / 256 = BK / 8.
+// N source ([rows][K]): idx = t + 256 i -> row = idx / (BK/4), kc = idx % (BK/4)  (a row's BK floats by BK/4 lanes)
+// T source ([K][rows]): idx -> k = idx / 32, c = idx % 32                         (a k-row's 128 floats by 32 lanes)
+template <int BK, bool T, bool VEC>
 __device__ __forceinline__ void stage_load(const float* __restrict__ src, int64_t ld, int64_t r0, int64_t rmax,
-                                           int64_t k0, int64_t kmax, float4 (&reg)[4]) {
+                                           int64_t k0, int64_t kmax, float4 (&reg)[BK / 8]) {
   const int t = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < BK / 8; ++i) {
     const int idx = t + 256 * i;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (!T) {
-      const int64_t r = r0 + (idx >> 3), k = k0 + 4 * (idx & 7);
+      const int64_t r = r0 + idx / (BK / 4), k = k0 + 4 * (idx % (BK / 4));
       if (VEC) {
         if (r < rmax && k < kmax) v = *reinterpret_cast<const float4*>(src + r * ld + k);
       } else if (r < rmax) {
@@ -89,7 +108,7 @@ __device__ __forceinline__ void stage_load(const float* __restrict__ src, int64_
         if (k + 3 < kmax) v.w = p[3];
       }
     } else {
-      const int64_t k = k0 + ((idx & 7) | ((idx >> 8) << 3)), r = r0 + 4 * ((idx >> 3) & 31);
+      const int64_t k = k0 + idx / 32, r = r0 + 4 * (idx % 32);
       if (VEC) {
         if (k < kmax && r < rmax) v = *reinterpret_cast<const float4*>(src + k * ld + r);
       } else if (k < kmax) {
@@ -104,166 +123,198 @@ __device__ __forceinline__ void stage_load(const float* __restrict__ src, int64_
   }
 }
 
-template <bool T, int LDK>
-__device__ __forceinline__ void stage_store(float* lds, const float4 (&reg)[4]) {
+__device__ __forceinline__ bf16x4 cvt4(const float4 v) {
+  bf16x4 r;
+  r[0] = (__bf16)v.x; r[1] = (__bf16)v.y; r[2] = (__bf16)v.z; r[3] = (__bf16)v.w;
+  return r;
+}
+
+__device__ __forceinline__ float4 resid4(const float4 v, const bf16x4 h) {
+  return make_float4(v.x - (float)h[0], v.y - (float)h[1], v.z - (float)h[2], v.w - (float)h[3]);
+}
+
+// ---------------------------------------------------------------------------- registers -> LDS image(s)
+template <int PREC, bool T>
+__device__ __forceinline__ void stage_store(typename Geo<PREC>::elem* img, const float4 (&reg)[Geo<PREC>::BK / 8]) {
+  using G = Geo<PREC>;
+  constexpr int BK = G::BK;
   const int t = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < BK / 8; ++i) {
     const int idx = t + 256 * i;
-    if (!T) {
-      float* p = lds + (idx >> 3) * LDK + 4 * (idx & 7);
-      if (LDK % 4 == 0) {
+    const int off = T ? (idx / 32) * G::LDT + 4 * (idx % 32) : (idx / (BK / 4)) * G::LDN + 4 * (idx % (BK / 4));
+    if constexpr (PREC == P_F32) {
+      float* p = img + off;
+      if (T) {
         *reinterpret_cast<float4*>(p) = reg[i];
       } else {
         p[0] = reg[i].x; p[1] = reg[i].y; p[2] = reg[i].z; p[3] = reg[i].w;
       }
     } else {
-      const int kr = (idx & 7) | ((idx >> 8) << 3), c = 4 * ((idx >> 3) & 31);
-      float* p = lds + c * LDK + kr;
-      p[0] = reg[i].x; p[LDK] = reg[i].y; p[2 * LDK] = reg[i].z; p[3 * LDK] = reg[i].w;
+      const bf16x4 hi = cvt4(reg[i]);
+      *reinterpret_cast<bf16x4*>(img + off) = hi;
+      if constexpr (PREC == P_BF16X3) {
+        *reinterpret_cast<bf16x4*>(img + G::template img_elems<T>() + off) = cvt4(resid4(reg[i], hi));
+      }
     }
   }
 }
 
-__device__ __forceinline__ bf16x8 to_bf16(const float4 lo, const float4 hi) {
-  bf16x8 r;
-  r[0] = (__bf16)lo.x; r[1] = (__bf16)lo.y; r[2] = (__bf16)lo.z; r[3] = (__bf16)lo.w;
-  r[4] = (__bf16)hi.x; r[5] = (__bf16)hi.y; r[6] = (__bf16)hi.z; r[7] = (__bf16)hi.w;
-  return r;
+// ---------------------------------------------------------------------------- LDS -> MFMA fragments
+// bf16 32x32x16 operand fragment for rows [row0, row0+32), k-step ks: lane l holds X[row0 + (l&31)][ks + 8(l>>5) + j].
+template <bool T, int LDN, int LDT>
+__device__ __forceinline__ bf16x8 frag_bf16(const __bf16* img, int row0, int ks) {
+  const int lane = threadIdx.x & 63;
+  if (!T) {
+    return *reinterpret_cast<const bf16x8*>(img + (row0 + (lane & 31)) * LDN + ks + 8 * (lane >> 5));
+  } else {
+    // ds_read_b64_tr_b16: per 16-lane group g, lane 4q+p addresses k-row (kb + q), columns 4p..4p+3 of the
+    // group's 16-row block; lane i of the group receives row (block + i) at k = kb + 0..3.
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int kb = ks + 8 * (g >> 1);
+    const __bf16* a = img + (kb + q) * LDT + row0 + 16 * (g & 1) + 4 * p;
+    const short4_ lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(a));
+    const short4_ hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4*)(a + 4 * LDT));
+    const short8_ v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
 }
 
-__device__ __forceinline__ void split_bf16(const float4 lo, const float4 hi, bf16x8& h, bf16x8& l) {
-  h = to_bf16(lo, hi);
-  float4 rlo, rhi;
-  rlo.x = lo.x - (float)h[0]; rlo.y = lo.y - (float)h[1]; rlo.z = lo.z - (float)h[2]; rlo.w = lo.w - (float)h[3];
-  rhi.x = hi.x - (float)h[4]; rhi.y = hi.y - (float)h[5]; rhi.z = hi.z - (float)h[6]; rhi.w = hi.w - (float)h[7];
-  l = to_bf16(rlo, rhi);
+// f32 32x32x2 operand: lane l holds X[row0 + (l&31)][kk + (l>>5)]
+template <bool T, int LDN, int LDT>
+__device__ __forceinline__ float frag_f32(const float* img, int row0, int kk) {
+  const int lane = threadIdx.x & 63;
+  if (!T) return img[(row0 + (lane & 31)) * LDN + kk + (lane >> 5)];
+  return img[(kk + (lane >> 5)) * LDT + row0 + (lane & 31)];
 }
 
+// ---------------------------------------------------------------------------- epilogue
+// one 32x32 accumulator tile -> C (bias, Z = pre-activation, activation, aux act-grad, store/accumulate/atomic).
+// C/D map (all dtypes): col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5).
+__device__ __forceinline__ void epi_tile(const floatx16& a, int64_t rbase, int64_t col, int64_t M, int64_t N,
+                                         float* __restrict__ C, int64_t ldc, const Epi& ep) {
+  if (col >= N) return;
+  const bool split = ep.splits > 1;
+  const float bval = (ep.bias != nullptr && !split) ? ep.bias[col] : 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int64_t row = rbase + (e & 3) + 8 * (e >> 2);
+    if (row < M) {
+      float v = a[e] + bval;
+      if (ep.Z != nullptr) ep.Z[row * ep.ldz + col] = v;
+      if (ep.act != ACT_NONE) v = act_fwd(ep.act, v, ep.beta, ep.thr);
+      if (ep.aux != nullptr) v *= act_grad(ep.dact, ep.aux[row * ep.ldaux + col], ep.beta, ep.thr);
+      float* dst = C + row * ldc + col;
+      if (split) atomicAdd(dst, v);
+      else if (ep.accumulate) *dst += v;
+      else *dst = v;
+      if (ep.ones_col >= 0 && col == 0) C[row * ldc + ep.ones_col] = 1.0f;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- kernel
 template <int PREC, bool TA, bool TB, bool VEC>
 __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A,
                                                    int64_t lda, const float* __restrict__ B, int64_t ldb,
                                                    float* __restrict__ C, int64_t ldc, Epi ep, int64_t k_per_split,
                                                    int m_tiles_pad, int n_tiles) {
-  constexpr int LDK = LdsK<PREC>::v;
-  __shared__ __attribute__((aligned(16))) float lds[(BM + BN) * LDK];
-  float* As = lds;
-  float* Bs = lds + BM * LDK;
+  using G = Geo<PREC>;
+  using E = typename G::elem;
+  constexpr int BK = G::BK;
+  constexpr int A_ELEMS = G::NIMG * G::template img_elems<TA>();
+  constexpr int B_ELEMS = G::NIMG * G::template img_elems<TB>();
+  __shared__ __attribute__((aligned(16))) E lds[A_ELEMS + B_ELEMS];
+  E* As = lds;
+  E* Bs = lds + A_ELEMS;
 
-  // XCD-aware tile map: ids b and b + 8 (same XCD under round-robin dispatch) take the N-tiles of one M panel
+  // tile map.  Unsplit: XCD-aware -- ids b and b + 8 (same XCD under round-robin dispatch) take the N-tiles
+  // of one M panel, so the panel is fetched into one L2.  Split-K: id -> (tile, slice), consecutive ids on
+  // different tiles/slices, spreading the work over all 8 XCDs.
   const int id = blockIdx.x;
-  const int nt = (id >> 3) % n_tiles;
-  const int mt = (id & 7) + 8 * (id / (8 * n_tiles));
-  if (mt >= m_tiles_pad) return;
+  int mt, nt, slice = 0;
+  if (ep.splits > 1) {
+    const int tiles = m_tiles_pad * n_tiles;
+    const int t = id % tiles;
+    slice = id / tiles;
+    mt = t % m_tiles_pad;
+    nt = t / m_tiles_pad;
+  } else {
+    nt = (id >> 3) % n_tiles;
+    mt = (id & 7) + 8 * (id / (8 * n_tiles));
+    if (mt >= m_tiles_pad) return;
+  }
   const int64_t m0 = (int64_t)mt * BM;
   const int64_t n0 = (int64_t)nt * BN;
   if (m0 >= M) return;
-  const int64_t kbeg = (int64_t)blockIdx.z * k_per_split;
+  const int64_t kbeg = (int64_t)slice * k_per_split;
   const int64_t kend = (kbeg + k_per_split < K) ? kbeg + k_per_split : K;
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int r = lane & 31, h = lane >> 5;
 
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  floatx16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
 
-  float4 ra[4], rb[4];
+  float4 ra[BK / 8], rb[BK / 8];
   if (kbeg < kend) {
-    stage_load<TA, VEC>(A, lda, m0, M, kbeg, kend, ra);
-    stage_load<TB, VEC>(B, ldb, n0, N, kbeg, kend, rb);
+    stage_load<BK, TA, VEC>(A, lda, m0, M, kbeg, kend, ra);
+    stage_load<BK, TB, VEC>(B, ldb, n0, N, kbeg, kend, rb);
   }
   for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
     __syncthreads();
-    stage_store<TA, LDK>(As, ra);
-    stage_store<TB, LDK>(Bs, rb);
+    stage_store<PREC, TA>(As, ra);
+    stage_store<PREC, TB>(Bs, rb);
     __syncthreads();
     if (k0 + BK < kend) {
-      stage_load<TA, VEC>(A, lda, m0, M, k0 + BK, kend, ra);
-      stage_load<TB, VEC>(B, ldb, n0, N, k0 + BK, kend, rb);
+      stage_load<BK, TA, VEC>(A, lda, m0, M, k0 + BK, kend, ra);
+      stage_load<BK, TB, VEC>(B, ldb, n0, N, k0 + BK, kend, rb);
     }
-    const float* a0p = As + (wm * 64 + r) * LDK;
-    const float* a1p = As + (wm * 64 + 32 + r) * LDK;
-    const float* b0p = Bs + (wn * 64 + r) * LDK;
-    const float* b1p = Bs + (wn * 64 + 32 + r) * LDK;
-    if (PREC == P_F32) {
+    const int ar0 = wm * 64, br0 = wn * 64;
+    if constexpr (PREC == P_F32) {
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 2) {
-        const float a0 = a0p[kk + h], a1 = a1p[kk + h], b0 = b0p[kk + h], b1 = b1p[kk + h];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        const float a0 = frag_f32<TA, G::LDN, G::LDT>(As, ar0, kk), a1 = frag_f32<TA, G::LDN, G::LDT>(As, ar0 + 32, kk);
+        const float b0 = frag_f32<TB, G::LDN, G::LDT>(Bs, br0, kk), b1 = frag_f32<TB, G::LDN, G::LDT>(Bs, br0 + 32, kk);
+        acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc00, 0, 0, 0);
+        acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc01, 0, 0, 0);
+        acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc10, 0, 0, 0);
+        acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc11, 0, 0, 0);
       }
     } else {
 #pragma unroll
       for (int ks = 0; ks < BK; ks += 16) {
-        const int kb = ks + 8 * h;
-        const float4 a0l = *reinterpret_cast<const float4*>(a0p + kb), a0h = *reinterpret_cast<const float4*>(a0p + kb + 4);
-        const float4 a1l = *reinterpret_cast<const float4*>(a1p + kb), a1h = *reinterpret_cast<const float4*>(a1p + kb + 4);
-        const float4 b0l = *reinterpret_cast<const float4*>(b0p + kb), b0h = *reinterpret_cast<const float4*>(b0p + kb + 4);
-        const float4 b1l = *reinterpret_cast<const float4*>(b1p + kb), b1h = *reinterpret_cast<const float4*>(b1p + kb + 4);
-        if (PREC == P_BF16) {
-          const bf16x8 A0 = to_bf16(a0l, a0h), A1 = to_bf16(a1l, a1h);
-          const bf16x8 B0 = to_bf16(b0l, b0h), B1 = to_bf16(b1l, b1h);
-          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0, acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B1, acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B0, acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B1, acc[1][1], 0, 0, 0);
-        } else {
-          bf16x8 A0h, A0l, A1h, A1l, B0h, B0l, B1h, B1l;
-          split_bf16(a0l, a0h, A0h, A0l);
-          split_bf16(a1l, a1h, A1h, A1l);
-          split_bf16(b0l, b0h, B0h, B0l);
-          split_bf16(b1l, b1h, B1h, B1l);
-          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0l, B0h, acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0l, B1h, acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1l, B0h, acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1l, B1h, acc[1][1], 0, 0, 0);
-          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0h, B0l, acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0h, B1l, acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1h, B0l, acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1h, B1l, acc[1][1], 0, 0, 0);
-          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0h, B0h, acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0h, B1h, acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1h, B0h, acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1h, B1h, acc[1][1], 0, 0, 0);
+        const bf16x8 a0 = frag_bf16<TA, G::LDN, G::LDT>(As, ar0, ks), a1 = frag_bf16<TA, G::LDN, G::LDT>(As, ar0 + 32, ks);
+        const bf16x8 b0 = frag_bf16<TB, G::LDN, G::LDT>(Bs, br0, ks), b1 = frag_bf16<TB, G::LDN, G::LDT>(Bs, br0 + 32, ks);
+        if constexpr (PREC == P_BF16X3) {
+          constexpr int AO = G::template img_elems<TA>(), BO = G::template img_elems<TB>();
+          const bf16x8 a0l = frag_bf16<TA, G::LDN, G::LDT>(As + AO, ar0, ks);
+          const bf16x8 a1l = frag_bf16<TA, G::LDN, G::LDT>(As + AO, ar0 + 32, ks);
+          const bf16x8 b0l = frag_bf16<TB, G::LDN, G::LDT>(Bs + BO, br0, ks);
+          const bf16x8 b1l = frag_bf16<TB, G::LDN, G::LDT>(Bs + BO, br0 + 32, ks);
+          acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0l, b0, acc00, 0, 0, 0);
+          acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0l, b1, acc01, 0, 0, 0);
+          acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1l, b0, acc10, 0, 0, 0);
+          acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1l, b1, acc11, 0, 0, 0);
+          acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0l, acc00, 0, 0, 0);
+          acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1l, acc01, 0, 0, 0);
+          acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0l, acc10, 0, 0, 0);
+          acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1l, acc11, 0, 0, 0);
         }
+        acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc00, 0, 0, 0);
+        acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc01, 0, 0, 0);
+        acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc10, 0, 0, 0);
+        acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc11, 0, 0, 0);
       }
     }
   }
 
-  // epilogue: 32x32 C/D map (all dtypes): col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
-  const bool split = gridDim.z > 1;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t col = n0 + wn * 64 + j * 32 + r;
-      if (col >= N) continue;
-      const float bval = (ep.bias != nullptr && !split) ? ep.bias[col] : 0.f;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int64_t row = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (row >= M) continue;
-        float v = acc[i][j][e] + bval;
-        if (ep.Z != nullptr) ep.Z[row * ep.ldz + col] = v;
-        if (ep.act != ACT_NONE) v = act_fwd(ep.act, v, ep.beta, ep.thr);
-        if (ep.aux != nullptr) v *= act_grad(ep.dact, ep.aux[row * ep.ldaux + col], ep.beta, ep.thr);
-        float* dst = C + row * ldc + col;
-        if (split) atomicAdd(dst, v);
-        else if (ep.accumulate) *dst += v;
-        else *dst = v;
-        if (ep.ones_col >= 0 && col == 0) C[row * ldc + ep.ones_col] = 1.0f;
-      }
-    }
-  }
+  const int64_t rbase = m0 + wm * 64 + 4 * (lane >> 5);
+  const int64_t cbase = n0 + wn * 64 + (lane & 31);
+  epi_tile(acc00, rbase, cbase, M, N, C, ldc, ep);
+  epi_tile(acc01, rbase, cbase + 32, M, N, C, ldc, ep);
+  epi_tile(acc10, rbase + 32, cbase, M, N, C, ldc, ep);
+  epi_tile(acc11, rbase + 32, cbase + 32, M, N, C, ldc, ep);
 }
 
 template <int PREC, bool TA, bool TB>
@@ -309,22 +360,23 @@ MMS_EXPORT int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N
   // vector path: 16-B aligned bases, contiguous dims and leading dims multiples of 4
   const int64_t acont = trans_a ? M : K, bcont = trans_b ? N : K;
   const bool vec = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 && acont % 4 == 0 && bcont % 4 == 0;
+  const int BK = prec == P_BF16 ? Geo<P_BF16>::BK : Geo<P_F32>::BK;
   int64_t kps = (K + splits - 1) / splits;
   kps = ((kps + BK - 1) / BK) * BK;
   if (kps < BK) kps = BK;
   const int64_t zs = K == 0 ? 1 : (K + kps - 1) / kps;
-  MMS_REQUIRE(zs <= 65535, fn, "too many K splits");
   const int64_t mt = (M + BM - 1) / BM;
-  const int64_t mtp = ((mt + 7) / 8) * 8;
+  const int64_t mtp = zs > 1 ? mt : ((mt + 7) / 8) * 8;
   const int64_t nt = (N + BN - 1) / BN;
-  MMS_REQUIRE(mtp * nt <= INT32_MAX, fn, "grid too large");
-  Epi ep{bias, Z, ldz, aux, ldaux, act, dact, beta, thr, accumulate, ones_col};
-  dim3 grid((unsigned)(mtp * nt), 1, (unsigned)zs);
+  MMS_REQUIRE(mtp * nt * zs <= INT32_MAX, fn, "grid too large");
+  Epi ep{bias, Z, ldz, aux, ldaux, act, dact, beta, thr, accumulate, ones_col, (int)zs};
+  dim3 grid((unsigned)(mtp * nt * zs), 1, 1);
   hipStream_t s = mms::as_stream(stream);
+  const int64_t kp = K == 0 ? 0 : kps;
   switch (prec) {
-    case P_F32: dispatch_ta_tb<P_F32>(trans_a, trans_b, vec, grid, s, M, N, K, A, lda, B, ldb, C, ldc, ep, K == 0 ? 0 : kps, (int)mtp, (int)nt); break;
-    case P_BF16: dispatch_ta_tb<P_BF16>(trans_a, trans_b, vec, grid, s, M, N, K, A, lda, B, ldb, C, ldc, ep, K == 0 ? 0 : kps, (int)mtp, (int)nt); break;
-    default: dispatch_ta_tb<P_BF16X3>(trans_a, trans_b, vec, grid, s, M, N, K, A, lda, B, ldb, C, ldc, ep, K == 0 ? 0 : kps, (int)mtp, (int)nt); break;
+    case P_F32: dispatch_ta_tb<P_F32>(trans_a, trans_b, vec, grid, s, M, N, K, A, lda, B, ldb, C, ldc, ep, kp, (int)mtp, (int)nt); break;
+    case P_BF16: dispatch_ta_tb<P_BF16>(trans_a, trans_b, vec, grid, s, M, N, K, A, lda, B, ldb, C, ldc, ep, kp, (int)mtp, (int)nt); break;
+    default: dispatch_ta_tb<P_BF16X3>(trans_a, trans_b, vec, grid, s, M, N, K, A, lda, B, ldb, C, ldc, ep, kp, (int)mtp, (int)nt); break;
   }
   return mms::check_launch(fn);
 }
