@@ -52,7 +52,7 @@ int mms_gemm_f32(int mode, int64_t M, int64_t N, int64_t K, const float* A, int6
 int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
              const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, float* Z, int64_t ldz,
              const float* aux, int64_t ldaux, int act, int dact, float beta, float thr, int accumulate, int splits,
-             int ones_col, void* stream);
+             int ones_col, float* colsum, void* stream);
 
 /* ---- weight norm (mlp.py:206-209; torch weight_norm dim=0): W = v * (g / ||v||_row); bwd dg += , dv += */
 int mms_weight_norm_fwd(const float* g, const float* v, int64_t N, int64_t K, float* W, int64_t ldw, float* norms,

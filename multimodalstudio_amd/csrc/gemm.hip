@@ -64,6 +64,7 @@ struct Epi {
   int accumulate;
   int ones_col;  // >= 0: also write 1.0 at C[row, ones_col] (bias-gradient column for the next TN GEMM)
   int splits;    // K slices folded into blockIdx.x
+  float* colsum; // TA only: colsum[m] += sum_k A[k][m] (bias gradient of the weight-gradient GEMM), or null
 };
 
 __device__ __forceinline__ float act_fwd(int act, float v, float beta, float thr) {
@@ -256,6 +257,16 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t
 
   floatx16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
 
+  // fused bias gradient (TA): a T-source thread always holds columns 4 (t % 32) .. +3 of its k-rows
+  const bool do_cs = TA && ep.colsum != nullptr && nt == 0;
+  float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto colsum_acc = [&](const float4 (&reg)[BK / 8]) {
+#pragma unroll
+    for (int i = 0; i < BK / 8; ++i) {
+      cs.x += reg[i].x; cs.y += reg[i].y; cs.z += reg[i].z; cs.w += reg[i].w;
+    }
+  };
+
   float4 ra[BK / 8], rb[BK / 8];
   if (kbeg < kend) {
     stage_load<BK, TA, VEC>(A, lda, m0, M, kbeg, kend, ra);
@@ -265,6 +276,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t
     __syncthreads();
     stage_store<PREC, TA>(As, ra);
     stage_store<PREC, TB>(Bs, rb);
+    if (do_cs) colsum_acc(ra);
     __syncthreads();
     if (k0 + BK < kend) {
       stage_load<BK, TA, VEC>(A, lda, m0, M, k0 + BK, kend, ra);
@@ -309,6 +321,20 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t
     }
   }
 
+  if (do_cs) {  // reduce the 8 threads sharing t % 32 through LDS, then one atomic per column
+    float* red = reinterpret_cast<float*>(lds);
+    __syncthreads();
+    const int t = threadIdx.x;
+    *reinterpret_cast<float4*>(red + (t >> 5) * 128 + 4 * (t & 31)) = cs;
+    __syncthreads();
+    if (t < 128 && m0 + t < M) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v += red[j * 128 + t];
+      atomicAdd(ep.colsum + m0 + t, v);
+    }
+  }
+
   const int64_t rbase = m0 + wm * 64 + 4 * (lane >> 5);
   const int64_t cbase = n0 + wn * 64 + (lane & 31);
   epi_tile(acc00, rbase, cbase, M, N, C, ldc, ep);
@@ -346,8 +372,9 @@ inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 MMS_EXPORT int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
                         int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, float* Z,
                         int64_t ldz, const float* aux, int64_t ldaux, int act, int dact, float beta, float thr,
-                        int accumulate, int splits, int ones_col, void* stream) {
+                        int accumulate, int splits, int ones_col, float* colsum, void* stream) {
   const char* fn = "mms_gemm";
+  MMS_REQUIRE(colsum == nullptr || trans_a, fn, "the fused column sum needs a transposed (T-source) A");
   MMS_REQUIRE(prec >= 0 && prec <= 2, fn, "prec must be 0 (f32), 1 (bf16) or 2 (bf16x3)");
   MMS_REQUIRE(M >= 0 && N >= 0 && K >= 0, fn, "negative size");
   MMS_REQUIRE(act >= 0 && act <= 3 && dact >= 0 && dact <= 3, fn, "bad activation id");
@@ -369,7 +396,7 @@ MMS_EXPORT int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N
   const int64_t mtp = zs > 1 ? mt : ((mt + 7) / 8) * 8;
   const int64_t nt = (N + BN - 1) / BN;
   MMS_REQUIRE(mtp * nt * zs <= INT32_MAX, fn, "grid too large");
-  Epi ep{bias, Z, ldz, aux, ldaux, act, dact, beta, thr, accumulate, ones_col, (int)zs};
+  Epi ep{bias, Z, ldz, aux, ldaux, act, dact, beta, thr, accumulate, ones_col, (int)zs, colsum};
   dim3 grid((unsigned)(mtp * nt * zs), 1, 1);
   hipStream_t s = mms::as_stream(stream);
   const int64_t kp = K == 0 ? 0 : kps;

@@ -25,7 +25,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from . import _lib
-from .hip_ops import NN, NT, TN, _splits_for, act_bwd, colsum_, gemm, weight_norm_bwd, weight_norm_fwd
+from .hip_ops import NN, NT, TN, _splits_for, act_bwd, gemm, weight_norm_bwd, weight_norm_fwd
 
 ACT = {None: 0, "None": 0, "ReLU": 1, "Softplus": 2, "Sigmoid": 3}
 
@@ -149,11 +149,10 @@ class MLPRun:
             N, K = v.shape
             Xin = x if l == 0 else self.Ys[l - 1]
             dW = torch.zeros(N, K, device=dev)
+            db = torch.zeros(N, device=dev)
             tiles = ((N + 127) // 128) * ((K + 127) // 128)
             gemm(TN, N, K, M, dZ, dZ.stride(0), Xin, Xin.stride(0), dW, K, accumulate=True,
-                 splits=_splits_for(M, tiles), prec=self.prec)
-            db = torch.zeros(N, device=dev)
-            colsum_(dZ, db)
+                 splits=_splits_for(M, tiles), prec=self.prec, colsum=db)
             dg = torch.zeros(N, device=dev)
             dv = torch.zeros(N, K, device=dev)
             weight_norm_bwd(g.reshape(-1), v, self.norms[l], dW, dg, dv)
@@ -411,9 +410,9 @@ def _mlp_strided_bwd(run: MLPRun, dy: torch.Tensor, H: torch.Tensor, Fb: int):
     dZ = torch.empty(M, N, device=dev)
     act_bwd(dy, run.Zs[0], act, beta, thr, dZ)
     dW = torch.zeros(N, K, device=dev)
-    gemm(TN, N, K, M, dZ, N, H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1), prec=run.prec)
     db = torch.zeros(N, device=dev)
-    colsum_(dZ, db)
+    gemm(TN, N, K, M, dZ, N, H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1), prec=run.prec,
+         colsum=db)
     dg = torch.zeros(N, device=dev)
     dv = torch.zeros(N, K, device=dev)
     weight_norm_bwd(g.reshape(-1), v, run.norms[0], dW, dg, dv)

@@ -95,12 +95,14 @@ PREC_IDS = {"fp32": 0, "bf16": 1, "bf16x3": 2}
 
 def gemm(mode: int, M: int, N: int, K: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int,
          C: torch.Tensor, ldc: int, bias=None, Z=None, ldz=0, aux=None, ldaux=0, act=0, dact=0,
-         beta=1.0, thr=20.0, accumulate=False, splits=1, prec: int = 0, ones_col: int = -1):
-    """NT: C = A B^T (A [M,K], B [N,K]); NN: C = A B (B [K,N]); TN: C = A^T B (A [K,M], B [K,N])."""
+         beta=1.0, thr=20.0, accumulate=False, splits=1, prec: int = 0, ones_col: int = -1, colsum=None):
+    """NT: C = A B^T (A [M,K], B [N,K]); NN: C = A B (B [K,N]); TN: C = A^T B (A [K,M], B [K,N]).
+
+    ``colsum`` (TN only): colsum[m] += sum_k A[k, m] fused into the same pass (bias gradients)."""
     ta, tb = _MODE_TRANS[mode]
     _lib.call("mms_gemm", int(prec), ta, tb, int(M), int(N), int(K), A.data_ptr(), int(lda), B.data_ptr(), int(ldb),
               C.data_ptr(), int(ldc), _ptr(bias), _ptr(Z), int(ldz), _ptr(aux), int(ldaux), int(act), int(dact),
-              float(beta), float(thr), int(bool(accumulate)), int(splits), int(ones_col), _stream())
+              float(beta), float(thr), int(bool(accumulate)), int(splits), int(ones_col), _ptr(colsum), _stream())
 
 
 def gemm_f32_legacy(mode: int, M: int, N: int, K: int, A, lda, B, ldb, C, ldc, **kw):

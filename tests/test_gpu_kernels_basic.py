@@ -97,5 +97,9 @@ def test_gemm_precisions(dev, prec, tol, M, N, K):
     hip_ops.gemm(hip_ops.NN, M, K, N, dZd, N, Wd, K, dX, K, prec=prec)
     chk(dX, dZ.double() @ W.double(), "NN")
     dW = torch.zeros(N, K, device=dev)
-    hip_ops.gemm(hip_ops.TN, N, K, M, dZd, N, Xd, K, dW, K, accumulate=True, splits=3, prec=prec)
+    db = torch.full((N,), 0.5, device=dev)
+    hip_ops.gemm(hip_ops.TN, N, K, M, dZd, N, Xd, K, dW, K, accumulate=True, splits=3, prec=prec, colsum=db)
     chk(dW, dZ.double().T @ X.double(), "TN")
+    ref_db = dZ.double().sum(0) + 0.5
+    err = (db.cpu().double() - ref_db).abs().max() / dZ.double().abs().sum(0).max()
+    assert err < 1e-6, f"fused colsum rel err {err:.2e}"
