@@ -49,7 +49,7 @@ def work_fns():
     return {
         "mms_gemm": lambda a: (PREC_NAMES[a[0]], 2.0 * a[3] * a[4] * a[5]),
         "mms_hashgrid_fwd": lambda a: float(a[1]) * HASH_FWD_B,
-        "mms_hashgrid_bwd": lambda a: float(a[1]) * HASH_BWD_B,
+        "mms_hashgrid_bwd_grouped": lambda a: float(a[1]) * a[2] * HASH_BWD_B,
     }
 
 

@@ -35,6 +35,13 @@ int mms_hashgrid_fwd(const float* pos, int64_t M, int64_t ldx, const float* tabl
 int mms_hashgrid_bwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L, int log2T, int F,
                      const float* scales, float radius, int active_levels, const float* dout, int64_t ldd,
                      float* dtable, float* dpos, int64_t lddx, void* stream);
+/* Same, for Mg groups of `group` rows (row = g + j * gstride, j < group; group 1 or 5): the SDF batch
+ * [centre | 4 taps] (surface_model.py:138-160) -- the taps' shared-cell corner gradients are merged
+ * in-thread before the table atomics. */
+int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx,
+                             const float* table, int L, int log2T, int F, const float* scales, float radius,
+                             int active_levels, const float* dout, int64_t ldd, float* dtable, float* dpos,
+                             int64_t lddx, void* stream);
 
 /* ---- fp32 MFMA GEMM with fused MLP epilogue: nn.Linear + activation (field_components/mlp.py:152-171).
  * mode 0 NT: C = A[M,K] B[N,K]^T ; 1 NN: C = A[M,K] B[K,N] ; 2 TN: C = A[K,M]^T B[K,N].

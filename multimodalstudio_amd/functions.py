@@ -82,9 +82,11 @@ def grid_fwd(g: GridCfg, pos: torch.Tensor, ldx: int, M: int, table, active: int
               g.radius, active, out.data_ptr() + 4 * col, out.stride(0), _s())
 
 
-def grid_bwd(g: GridCfg, pos, ldx, M, table, active, dout: torch.Tensor, col: int, dtable, dpos):
-    _lib.call("mms_hashgrid_bwd", pos.data_ptr(), M, ldx, table.data_ptr(), g.L, g.log2T, g.F, g.scales_ptr,
-              g.radius, active, dout.data_ptr() + 4 * col, dout.stride(0), _p(dtable), _p(dpos),
+def grid_bwd(g: GridCfg, pos, ldx, M, table, active, dout: torch.Tensor, col: int, dtable, dpos, group: int = 1):
+    """Table / position gradients; group=5 for the [centre | 4 taps] SDF batch (M = 5 x centres)."""
+    Mg = M // group
+    _lib.call("mms_hashgrid_bwd_grouped", pos.data_ptr(), Mg, group, Mg, ldx, table.data_ptr(), g.L, g.log2T, g.F,
+              g.scales_ptr, g.radius, active, dout.data_ptr() + 4 * col, dout.stride(0), _p(dtable), _p(dpos),
               0 if dpos is None else dpos.stride(0), _s())
 
 
@@ -230,7 +232,7 @@ class SurfaceFunction(torch.autograd.Function):
         K0 = X.shape[1]
         dtable = torch.zeros_like(table) if need_table else None
         dP = torch.zeros(5 * M, 3, device=dev) if need_pos else None
-        grid_bwd(ctx.grid, X, K0, 5 * M, table, ctx.active, dX, 39, dtable, dP)
+        grid_bwd(ctx.grid, X, K0, 5 * M, table, ctx.active, dX, 39, dtable, dP, group=5)
         dpos = None
         if need_pos:
             dpos = torch.zeros(M, 3, device=dev)

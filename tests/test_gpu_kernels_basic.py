@@ -38,6 +38,32 @@ def test_hashgrid_fwd_bwd(dev, log2T, active, radius):
     np.testing.assert_allclose(xd.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("log2T", [12, 19])
+def test_hashgrid_bwd_grouped_taps(dev, log2T):
+    """[centre | 4 taps] batch: the grouped backward (in-thread merge of shared-cell corners) vs the oracle."""
+    from multimodalstudio_amd import functions as F
+    L, Mc, delta = 16, 2000, 2.0 / 1024 / 3 ** 0.5
+    scales = ohg.level_scales(16, 2048, L)
+    g = torch.Generator().manual_seed(7)
+    table = (torch.rand(L << log2T, 2, generator=g) * 2 - 1) * 1e-1
+    c = _pts(Mc, seed=3)
+    dirs = torch.tensor([[1., -1., -1.], [-1., -1., 1.], [-1., 1., -1.], [1., 1., 1.]])
+    x = torch.cat([c] + [c + delta * d for d in dirs], 0).contiguous()
+    xr = x.clone().requires_grad_(True)
+    tr = table.clone().requires_grad_(True)
+    ref = ohg.feature_grid(xr, tr, scales, log2T, 1.0, L)
+    dout = torch.randn(ref.shape, generator=g)
+    ref.backward(dout)
+    cfg = F.GridCfg(scales.tolist(), log2T, 1.0)
+    xd, td, dd = x.to(dev), table.to(dev), dout.to(dev).contiguous()
+    dtable = torch.zeros_like(td)
+    dpos = torch.zeros_like(xd)
+    F.grid_bwd(cfg, xd, 3, 5 * Mc, td, L, dd, 0, dtable, dpos, group=5)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(dtable.cpu().numpy(), tr.grad.numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(dpos.cpu().numpy(), xr.grad.numpy(), rtol=1e-3, atol=1e-3)
+
+
 @pytest.mark.parametrize("M,N,K", [(1000, 257, 71), (300, 3, 64), (4096, 256, 256), (77, 130, 317)])
 def test_gemm_modes(dev, M, N, K):
     from multimodalstudio_amd import hip_ops
