@@ -26,6 +26,12 @@
 
 #include <type_traits>
 
+// Diagnostic ablation builds only (scripts/gemm_ablate.py compiles them separately; the product library is
+// built with 0): bit 0 drops the epilogue stores, bit 1 the MFMAs, bit 2 the global loads.
+#ifndef MMS_GEMM_ABLATE
+#define MMS_GEMM_ABLATE 0
+#endif
+
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -92,32 +98,26 @@ __device__ __forceinline__ float act_grad(int act, float z, float beta, float th
 template <int BK, bool T, bool VEC>
 __device__ __forceinline__ void stage_load(const float* __restrict__ src, int64_t ld, int64_t r0, int64_t rmax,
                                            int64_t k0, int64_t kmax, float4 (&reg)[BK / 8]) {
+  // VEC: 16-B aligned rows (ld % 4 == 0); a float4 that straddles the end of the contiguous dimension
+  // falls back to masked scalar loads, so odd widths (71, 257, ...) keep the vector path elsewhere.
   const int t = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < BK / 8; ++i) {
     const int idx = t + 256 * i;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (!T) {
-      const int64_t r = r0 + idx / (BK / 4), k = k0 + 4 * (idx % (BK / 4));
-      if (VEC) {
-        if (r < rmax && k < kmax) v = *reinterpret_cast<const float4*>(src + r * ld + k);
-      } else if (r < rmax) {
-        const float* p = src + r * ld + k;
-        if (k < kmax) v.x = p[0];
-        if (k + 1 < kmax) v.y = p[1];
-        if (k + 2 < kmax) v.z = p[2];
-        if (k + 3 < kmax) v.w = p[3];
-      }
-    } else {
-      const int64_t k = k0 + idx / 32, r = r0 + 4 * (idx % 32);
-      if (VEC) {
-        if (k < kmax && r < rmax) v = *reinterpret_cast<const float4*>(src + k * ld + r);
-      } else if (k < kmax) {
-        const float* p = src + k * ld + r;
-        if (r < rmax) v.x = p[0];
-        if (r + 1 < rmax) v.y = p[1];
-        if (r + 2 < rmax) v.z = p[2];
-        if (r + 3 < rmax) v.w = p[3];
+    // (outer, inner): N source (row, k) with inner bound kmax; T source (k, row) with inner bound rmax
+    const int64_t o = T ? k0 + idx / 32 : r0 + idx / (BK / 4);
+    const int64_t in = T ? r0 + 4 * (idx % 32) : k0 + 4 * (idx % (BK / 4));
+    const int64_t omax = T ? kmax : rmax, inmax = T ? rmax : kmax;
+    if ((MMS_GEMM_ABLATE & 4) == 0 && o < omax) {
+      const float* p = src + o * ld + in;
+      if (VEC && in + 4 <= inmax) {
+        v = *reinterpret_cast<const float4*>(p);
+      } else {
+        if (in < inmax) v.x = p[0];
+        if (in + 1 < inmax) v.y = p[1];
+        if (in + 2 < inmax) v.z = p[2];
+        if (in + 3 < inmax) v.w = p[3];
       }
     }
     reg[i] = v;
@@ -202,10 +202,11 @@ __device__ __forceinline__ void epi_tile(const floatx16& a, int64_t rbase, int64
     const int64_t row = rbase + (e & 3) + 8 * (e >> 2);
     if (row < M) {
       float v = a[e] + bval;
-      if (ep.Z != nullptr) ep.Z[row * ep.ldz + col] = v;
+      if (ep.Z != nullptr && ((MMS_GEMM_ABLATE & 1) == 0 || v == 1234.5f)) ep.Z[row * ep.ldz + col] = v;
       if (ep.act != ACT_NONE) v = act_fwd(ep.act, v, ep.beta, ep.thr);
       if (ep.aux != nullptr) v *= act_grad(ep.dact, ep.aux[row * ep.ldaux + col], ep.beta, ep.thr);
       float* dst = C + row * ldc + col;
+      if ((MMS_GEMM_ABLATE & 1) && v != 1234.5f) continue;
       if (split) atomicAdd(dst, v);
       else if (ep.accumulate) *dst += v;
       else *dst = v;
@@ -283,7 +284,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t
       stage_load<BK, TB, VEC>(B, ldb, n0, N, k0 + BK, kend, rb);
     }
     const int ar0 = wm * 64, br0 = wn * 64;
-    if constexpr (PREC == P_F32) {
+    if constexpr ((MMS_GEMM_ABLATE & 2) != 0) {
+      acc00[0] += (float)As[lane] + (float)Bs[lane];  // keep the staging alive
+    } else if constexpr (PREC == P_F32) {
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 2) {
         const float a0 = frag_f32<TA, G::LDN, G::LDT>(As, ar0, kk), a1 = frag_f32<TA, G::LDN, G::LDT>(As, ar0 + 32, kk);
@@ -384,9 +387,8 @@ MMS_EXPORT int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N
   MMS_REQUIRE(splits == 1 || (accumulate && Z == nullptr && aux == nullptr && act == ACT_NONE && bias == nullptr &&
                               ones_col < 0),
               fn, "split-K requires a plain accumulating epilogue");
-  // vector path: 16-B aligned bases, contiguous dims and leading dims multiples of 4
-  const int64_t acont = trans_a ? M : K, bcont = trans_b ? N : K;
-  const bool vec = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0 && acont % 4 == 0 && bcont % 4 == 0;
+  // vector path: 16-B aligned bases and leading dims multiples of 4 (ragged contiguous dims are masked per float4)
+  const bool vec = aligned16(A) && aligned16(B) && lda % 4 == 0 && ldb % 4 == 0;
   const int BK = prec == P_BF16 ? Geo<P_BF16>::BK : Geo<P_F32>::BK;
   int64_t kps = (K + splits - 1) / splits;
   kps = ((kps + BK - 1) / BK) * BK;

@@ -45,6 +45,14 @@ def set_precision(mode: str) -> None:
     PRECISION.update(PRESETS[mode])
 
 
+def _alloc(rows: int, cols: int, dev, zero: bool = False) -> torch.Tensor:
+    """[rows, cols] view of a [rows, cols rounded up to 4] buffer: 16-byte aligned rows keep the GEMM and
+    panel kernels on their float4 paths for odd widths (71, 257, 317, ...)."""
+    ld = (cols + 3) // 4 * 4
+    buf = torch.zeros(rows, ld, device=dev) if zero else torch.empty(rows, ld, device=dev)
+    return buf[:, :cols]
+
+
 def _s() -> int:
     return torch.cuda.current_stream().cuda_stream
 
@@ -115,17 +123,17 @@ class MLPRun:
         for l in range(self.L):
             g, v, b = self.params[3 * l: 3 * l + 3]
             N, K = v.shape
-            W = torch.empty(N, K, device=dev)
+            W = _alloc(N, K, dev)
             nrm = torch.empty(N, device=dev)
             weight_norm_fwd(g.reshape(-1), v, W, nrm)
             act, beta, thr = self.acts[l]
             if l == self.L - 1 and last_out is not None:
                 Y = last_out
             else:
-                Y = torch.empty(M, N, device=dev)
-            Z = torch.empty(M, N, device=dev) if (keep and act != 0) else None
-            gemm(NT, M, N, K, h, h.stride(0), W, W.stride(0), Y, Y.stride(0), bias=b, Z=Z, ldz=N, act=act, beta=beta,
-                 thr=thr, prec=self.prec)
+                Y = _alloc(M, N, dev)
+            Z = _alloc(M, N, dev) if (keep and act != 0) else None
+            gemm(NT, M, N, K, h, h.stride(0), W, W.stride(0), Y, Y.stride(0), bias=b, Z=Z,
+                 ldz=0 if Z is None else Z.stride(0), act=act, beta=beta, thr=thr, prec=self.prec)
             if keep:
                 self.Ws.append(W)
                 self.norms.append(nrm)
@@ -141,7 +149,7 @@ class MLPRun:
         grads: List[Optional[torch.Tensor]] = [None] * len(self.params)
         act, beta, thr = self.acts[self.L - 1]
         if act != 0:
-            dZ = torch.empty(M, dy.shape[1], device=dev)
+            dZ = _alloc(M, dy.shape[1], dev)
             act_bwd(dy, self.Zs[-1], act, beta, thr, dZ)
         else:
             dZ = dy
@@ -161,13 +169,16 @@ class MLPRun:
             grads[3 * l], grads[3 * l + 1], grads[3 * l + 2] = dg.view_as(g), dv, db
             if l > 0:
                 pa, pbeta, pthr = self.acts[l - 1]
-                dprev = torch.empty(M, K, device=dev)
-                gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[l], K, dprev, K,
-                     aux=self.Zs[l - 1] if pa != 0 else None, ldaux=K, dact=pa, beta=pbeta, thr=pthr, prec=self.prec)
+                dprev = _alloc(M, K, dev)
+                zaux = self.Zs[l - 1] if pa != 0 else None
+                gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[l], self.Ws[l].stride(0), dprev, dprev.stride(0),
+                     aux=zaux, ldaux=0 if zaux is None else zaux.stride(0), dact=pa, beta=pbeta, thr=pthr,
+                     prec=self.prec)
                 dZ = dprev
             elif need_dx:
-                dx = torch.empty(M, K, device=dev)
-                gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[0], K, dx, K, prec=self.prec)
+                dx = _alloc(M, K, dev)
+                gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[0], self.Ws[0].stride(0), dx, dx.stride(0),
+                     prec=self.prec)
         return dx, grads
 
 
@@ -190,10 +201,10 @@ class SurfaceFunction(torch.autograd.Function):
         dev = pos.device
         pos = pos.contiguous()
         K0 = 3 + 36 + grid.out_dim
-        X = torch.empty(5 * M, K0, device=dev)
+        X = _alloc(5 * M, K0, dev)
         d32 = float(torch.tensor(delta, dtype=torch.float32))
-        _lib.call("mms_geo_input_fwd", pos.data_ptr(), 3, M, 4, d32, 6, X.data_ptr(), K0, _s())
-        grid_fwd(grid, X, K0, 5 * M, table, active, X, 39)
+        _lib.call("mms_geo_input_fwd", pos.data_ptr(), 3, M, 4, d32, 6, X.data_ptr(), X.stride(0), _s())
+        grid_fwd(grid, X, X.stride(0), 5 * M, table, active, X, 39)
         run = MLPRun(params, SDF_ACTS, PRECISION["sdf"])
         out = run.forward(X, keep=True)
         G = out.shape[1] - 1
@@ -218,7 +229,7 @@ class SurfaceFunction(torch.autograd.Function):
         pos, table, grads, *params = ctx.saved_tensors
         M, G = ctx.M, ctx.G
         dev = pos.device
-        dout = torch.zeros(5 * M, G + 1, device=dev)
+        dout = _alloc(5 * M, G + 1, dev, zero=True)
         _lib.call("mms_taps_combine_bwd", grads.data_ptr(), _p(dgrads if dgrads is not None else None),
                   _p(dhess), _p(dnormals), M, ctx.four_delta, ctx.delta_sq, dout.data_ptr(), dout.stride(0), _s())
         if dsdf is not None:
@@ -229,7 +240,7 @@ class SurfaceFunction(torch.autograd.Function):
         need_pos = ctx.needs_input_grad[0]
         dX, pgrads = ctx.run.backward(dout, need_dx=True)
         X = ctx.X
-        K0 = X.shape[1]
+        K0 = X.stride(0)
         dtable = torch.zeros_like(table) if need_table else None
         dP = torch.zeros(5 * M, 3, device=dev) if need_pos else None
         grid_bwd(ctx.grid, X, K0, 5 * M, table, ctx.active, dX, 39, dtable, dP, group=5)
@@ -248,9 +259,9 @@ def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> to
     M = pos.shape[0]
     dev = pos.device
     K0 = 3 + 36 + grid.out_dim
-    X = torch.empty(M, K0, device=dev)
-    _lib.call("mms_geo_input_fwd", pos.data_ptr(), pos.stride(0), M, 0, 0.0, 6, X.data_ptr(), K0, _s())
-    grid_fwd(grid, X, K0, M, table, active, X, 39)
+    X = _alloc(M, K0, dev)
+    _lib.call("mms_geo_input_fwd", pos.data_ptr(), pos.stride(0), M, 0, 0.0, 6, X.data_ptr(), X.stride(0), _s())
+    grid_fwd(grid, X, X.stride(0), M, table, active, X, 39)
     # only the sdf column of the last layer is needed
     last = list(params[-3:])
     g, v, b = last
@@ -275,14 +286,14 @@ class RadianceFunction(torch.autograd.Function):
         G = geo.shape[1]
         dev = pos.device
         K0 = 3 + 25 + G + 1 + grid.out_dim
-        X = torch.empty(M, K0, device=dev)
+        X = _alloc(M, K0, dev)
         pos = pos.contiguous()
         dirs = dirs.contiguous()
         normals = normals.contiguous()
         geo = geo.contiguous()
         _lib.call("mms_rad_input_fwd", pos.data_ptr(), 3, dirs.data_ptr(), normals.data_ptr(), geo.data_ptr(),
-                  geo.stride(0), M, S, G, X.data_ptr(), K0, _s())
-        grid_fwd(grid, X, K0, M, table, active, X, 29 + G)
+                  geo.stride(0), M, S, G, X.data_ptr(), X.stride(0), _s())
+        grid_fwd(grid, X, X.stride(0), M, table, active, X, 29 + G)
         run = MLPRun(params, RAD_ACTS, PRECISION["radiance"])
         feat = run.forward(X, keep=True)
         ctx.run, ctx.X, ctx.grid, ctx.active, ctx.S, ctx.G = run, X, grid, active, S, G
@@ -297,7 +308,7 @@ class RadianceFunction(torch.autograd.Function):
         dev = pos.device
         dX, pgrads = ctx.run.backward(dfeat.contiguous(), need_dx=True)
         X = ctx.X
-        K0 = X.shape[1]
+        K0 = X.stride(0)
         dtable = torch.zeros_like(table) if ctx.needs_input_grad[4] else None
         need_pos = ctx.needs_input_grad[0]
         dP = torch.zeros(M, 3, device=dev) if need_pos else None
@@ -348,12 +359,12 @@ class BackgroundFunction(torch.autograd.Function):
         M = pos.shape[0]
         dev = pos.device
         base_p, dens_p, head_p = params[:3 * nb], params[3 * nb:3 * (nb + nd)], params[3 * (nb + nd):]
-        X = torch.empty(M, 39, device=dev)
+        X = _alloc(M, 39, dev)
         Fb = base_p[-2].shape[0]
-        H = torch.empty(M, Fb + 27, device=dev)
+        H = _alloc(M, Fb + 27, dev)
         pos = pos.contiguous()
         dirs = dirs.contiguous()
-        _lib.call("mms_bg_input_fwd", pos.data_ptr(), M, dirs.data_ptr(), S, X.data_ptr(), 39, H.data_ptr(),
+        _lib.call("mms_bg_input_fwd", pos.data_ptr(), M, dirs.data_ptr(), S, X.data_ptr(), X.stride(0), H.data_ptr(),
                   H.stride(0), Fb, _s())
         base = MLPRun(base_p, BG_BASE_ACTS[:nb], PRECISION["background"])
         base.forward(X, keep=True, last_out=H)          # writes cols [0, Fb) of the head panel
@@ -380,7 +391,7 @@ class BackgroundFunction(torch.autograd.Function):
         dX, bgrads = ctx.base.backward(dbase_out.contiguous(), need_dx=True)
         dpos = torch.empty(M, 3, device=dev) if ctx.needs_input_grad[0] else None
         ddirs = torch.zeros(R, 3, device=dev) if ctx.needs_input_grad[1] else None
-        _lib.call("mms_bg_input_bwd", pos.data_ptr(), ctx.X.data_ptr(), 39, dX.data_ptr(), dX.stride(0),
+        _lib.call("mms_bg_input_bwd", pos.data_ptr(), ctx.X.data_ptr(), ctx.X.stride(0), dX.data_ptr(), dX.stride(0),
                   dirs.data_ptr(), dH.data_ptr(), dH.stride(0), Fb, R, S, _p(dpos), _p(ddirs), _s())
         ctx.base = ctx.dens = ctx.head = ctx.X = ctx.H = None
         return (dpos, ddirs, None, None, None, *bgrads, *dgrads_dens, *hgrads)
@@ -392,13 +403,14 @@ def _mlp_strided(run: MLPRun, H: torch.Tensor, Fb: int) -> torch.Tensor:
     N, K = v.shape
     M = H.shape[0]
     dev = H.device
-    W = torch.empty(N, K, device=dev)
+    W = _alloc(N, K, dev)
     nrm = torch.empty(N, device=dev)
     weight_norm_fwd(g.reshape(-1), v, W, nrm)
     act, beta, thr = run.acts[0]
-    Y = torch.empty(M, N, device=dev)
-    Z = torch.empty(M, N, device=dev)
-    gemm(NT, M, N, K, H, H.stride(0), W, K, Y, N, bias=b, Z=Z, ldz=N, act=act, beta=beta, thr=thr, prec=run.prec)
+    Y = _alloc(M, N, dev)
+    Z = _alloc(M, N, dev)
+    gemm(NT, M, N, K, H, H.stride(0), W, W.stride(0), Y, Y.stride(0), bias=b, Z=Z, ldz=Z.stride(0), act=act,
+         beta=beta, thr=thr, prec=run.prec)
     run.Ws, run.norms, run.Zs, run.Ys = [W], [nrm], [Z], [Y]
     return Y
 
@@ -409,17 +421,17 @@ def _mlp_strided_bwd(run: MLPRun, dy: torch.Tensor, H: torch.Tensor, Fb: int):
     M = H.shape[0]
     dev = H.device
     act, beta, thr = run.acts[0]
-    dZ = torch.empty(M, N, device=dev)
+    dZ = _alloc(M, N, dev)
     act_bwd(dy, run.Zs[0], act, beta, thr, dZ)
     dW = torch.zeros(N, K, device=dev)
     db = torch.zeros(N, device=dev)
-    gemm(TN, N, K, M, dZ, N, H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1), prec=run.prec,
-         colsum=db)
+    gemm(TN, N, K, M, dZ, dZ.stride(0), H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1),
+         prec=run.prec, colsum=db)
     dg = torch.zeros(N, device=dev)
     dv = torch.zeros(N, K, device=dev)
     weight_norm_bwd(g.reshape(-1), v, run.norms[0], dW, dg, dv)
-    dxin = torch.empty(M, K, device=dev)
-    gemm(NN, M, K, N, dZ, N, run.Ws[0], K, dxin, K, prec=run.prec)
+    dxin = _alloc(M, K, dev)
+    gemm(NN, M, K, N, dZ, dZ.stride(0), run.Ws[0], run.Ws[0].stride(0), dxin, dxin.stride(0), prec=run.prec)
     return dxin, [dg.view_as(g), dv, db]
 
 
