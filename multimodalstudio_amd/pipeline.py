@@ -294,7 +294,10 @@ class Trainer:
             self.poses.step_count = step
 
     def train_step(self, coords=None, targets=None, rng: Optional[RNG] = None, ddp=None):
-        """One training iteration (raw_pipeline.py:67-82)."""
+        """One training iteration (raw_pipeline.py:67-82); the BEFORE_TRAIN_ITERATION callbacks (coarse-to-fine
+        mask, tap delta, cos anneal: feature_structures.py:97-108, surface_model.py:254-271,
+        volume_rendering.py:227-230) are applied for the current step first, as the reference's trainer does."""
+        self.model.set_step(self.step, self.cfg.max_iters)
         if coords is None:
             coords, sel = self.sampler.sample(self.frames)
             targets = self.targets_for(coords, sel)
