@@ -45,9 +45,20 @@ HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per looku
 HASH_BWD_B = 128 + 12 + 16 * 8 * 2 * (4 + 4)    # bytes per lookup, backward (table grads)
 
 
+def gemm_work(a):
+    """(precision label, (algorithmic flops, algorithmic HBM bytes)) of one mms_gemm launch (argument order of
+    include/mms_hip.h): 2MNK flops; bytes = operands once + C written (+ Z, aux, read-modify-write)."""
+    prec, M, N, K = a[0], a[3], a[4], a[5]
+    Z, aux, accumulate, splits = a[13], a[15], a[21], a[22]
+    mn = float(M) * N
+    nbytes = 4.0 * (float(M) * K + float(N) * K + mn * (1 + (Z is not None) + (aux is not None) +
+                                                         (bool(accumulate) and splits <= 1)))
+    return PREC_NAMES[prec], (2.0 * M * N * K, nbytes)
+
+
 def work_fns():
     return {
-        "mms_gemm": lambda a: (PREC_NAMES[a[0]], 2.0 * a[3] * a[4] * a[5]),
+        "mms_gemm": gemm_work,
         "mms_hashgrid_fwd": lambda a: float(a[1]) * HASH_FWD_B,
         "mms_hashgrid_bwd_grouped": lambda a: float(a[1]) * a[2] * HASH_BWD_B,
     }
@@ -98,8 +109,8 @@ def cpu_baseline(trainer, cfg, seconds: float):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="grid_rgb", choices=list(CONFIGS))
     ap.add_argument("--rays", type=int, default=2048, help="num_rays_per_modality (grid.yaml: 2048)")
     ap.add_argument("--log2T", type=int, default=19)
@@ -160,12 +171,24 @@ def main():
         for name, (n, ms, work) in summ.items():
             launches_per_step = n / args.steps
             if name.startswith("mms_gemm"):
+                # roofline = the slower of the MFMA and the HBM bound for this launch mix
+                flops, nbytes = work
                 peak = MFMA_PEAK_TF[name.split(":")[1]]
-                ach = work / (ms * 1e-3) / 1e12
-                kernels.append({"kernel": name, "bound": "mfma", "achieved": round(ach, 3), "peak": peak,
-                                "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                                "avg_ms": round(ms, 5), "launches_per_step": launches_per_step,
-                                "ms_per_step": round(ms * launches_per_step, 4), "traffic": None})
+                t_mfma = flops / (peak * 1e12)
+                t_hbm = nbytes / (HBM_PEAK_GBS * 1e9)
+                if t_mfma >= t_hbm:
+                    ach = flops / (ms * 1e-3) / 1e12
+                    rec = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+                           "frac": round(ach / peak, 4)}
+                else:
+                    ach = nbytes / (ms * 1e-3) / 1e9
+                    rec = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(ach / HBM_PEAK_GBS, 4)}
+                rec.update({"kernel": name, "avg_ms": round(ms, 5), "launches_per_step": launches_per_step,
+                            "ms_per_step": round(ms * launches_per_step, 4), "traffic": None,
+                            "tflops": round(flops / (ms * 1e-3) / 1e12, 3),
+                            "gbs": round(nbytes / (ms * 1e-3) / 1e9, 1)})
+                kernels.append(rec)
             else:
                 ach = work / (ms * 1e-3) / 1e9
                 kernels.append({"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,

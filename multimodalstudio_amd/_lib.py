@@ -92,13 +92,21 @@ class KernelTimer:
         self.active = False
 
     def summary(self):
-        """{name: (launches, mean_ms, mean_work)} — call after a device synchronise."""
+        """{name: (launches, mean_ms, mean_work)} — call after a device synchronise.  ``mean_work`` is a
+        float, or a tuple of floats when the work function returns several quantities (e.g. flops, bytes)."""
         out = {}
         for name, ev0, ev1, work in self.records:
             ms = ev0.elapsed_time(ev1)
-            n, t, w = out.get(name, (0, 0.0, 0.0))
-            out[name] = (n + 1, t + ms, w + work)
-        return {k: (n, t / n, w / n) for k, (n, t, w) in out.items()}
+            n, t, w = out.get(name, (0, 0.0, None))
+            if isinstance(work, tuple):
+                w = work if w is None else tuple(a + b for a, b in zip(w, work))
+            else:
+                w = work if w is None else w + work
+            out[name] = (n + 1, t + ms, w)
+        res = {}
+        for k, (n, t, w) in out.items():
+            res[k] = (n, t / n, tuple(x / n for x in w) if isinstance(w, tuple) else w / n)
+        return res
 
 
 TIMER = KernelTimer()
@@ -118,9 +126,9 @@ def call(name: str, *args) -> None:
         e1.record()
         w = TIMER.watch[name](args)
         key = name
-        if isinstance(w, tuple):
+        if isinstance(w, tuple) and isinstance(w[0], str):
             key, w = f"{name}:{w[0]}", w[1]
-        TIMER.records.append((key, e0, e1, float(w)))
+        TIMER.records.append((key, e0, e1, tuple(float(x) for x in w) if isinstance(w, tuple) else float(w)))
     if rc != 0:
         msg = L.mms_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed ({rc}): {msg}")

@@ -96,32 +96,40 @@ __device__ __forceinline__ float act_grad(int act, float z, float beta, float th
 // N source ([rows][K]): idx = t + 256 i -> row = idx / (BK/4), kc = idx % (BK/4)  (a row's BK floats by BK/4 lanes)
 // T source ([K][rows]): idx -> k = idx / 32, c = idx % 32                         (a k-row's 128 floats by 32 lanes)
 template <int BK, bool T, bool VEC>
-__device__ __forceinline__ void stage_load(const float* __restrict__ src, int64_t ld, int64_t r0, int64_t rmax,
-                                           int64_t k0, int64_t kmax, float4 (&reg)[BK / 8]) {
-  // VEC: 16-B aligned rows (ld % 4 == 0); a float4 that straddles the end of the contiguous dimension
-  // falls back to masked scalar loads, so odd widths (71, 257, ...) keep the vector path elsewhere.
+__device__ __forceinline__ uint32_t stage_load(const float* __restrict__ src, int64_t ld, int64_t r0, int64_t rmax,
+                                               int64_t k0, int64_t kmax, float4 (&reg)[BK / 8]) {
+  // Branch-free: every load is issued unconditionally from a clamped (always valid) address; the validity of
+  // each element is returned as a bit mask and applied by stage_store, i.e. at the consumer, so the loads stay
+  // in flight across the compute phase.  (A load under a per-element condition makes hipcc wait vmcnt(0)
+  // inside each branch, and a select right after the load waits for it: both serialise the tile's loads.)
+  // VEC: 16-B aligned rows (ld % 4 == 0, so a float4 starting below the row length stays inside the row).
   const int t = threadIdx.x;
+  uint32_t mask = 0;
 #pragma unroll
   for (int i = 0; i < BK / 8; ++i) {
     const int idx = t + 256 * i;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     // (outer, inner): N source (row, k) with inner bound kmax; T source (k, row) with inner bound rmax
     const int64_t o = T ? k0 + idx / 32 : r0 + idx / (BK / 4);
     const int64_t in = T ? r0 + 4 * (idx % 32) : k0 + 4 * (idx % (BK / 4));
     const int64_t omax = T ? kmax : rmax, inmax = T ? rmax : kmax;
-    if ((MMS_GEMM_ABLATE & 4) == 0 && o < omax) {
-      const float* p = src + o * ld + in;
-      if (VEC && in + 4 <= inmax) {
-        v = *reinterpret_cast<const float4*>(p);
-      } else {
-        if (in < inmax) v.x = p[0];
-        if (in + 1 < inmax) v.y = p[1];
-        if (in + 2 < inmax) v.z = p[2];
-        if (in + 3 < inmax) v.w = p[3];
-      }
+    const bool ok = o < omax;
+    const float* row = src + (ok ? o : omax - 1) * ld;
+    float4 v;
+    if (VEC) {
+      const int64_t last = (inmax - 1) & ~(int64_t)3;
+      v = *reinterpret_cast<const float4*>(row + (in < inmax ? in : last));
+    } else {
+      v.x = row[in < inmax ? in : inmax - 1];
+      v.y = row[in + 1 < inmax ? in + 1 : inmax - 1];
+      v.z = row[in + 2 < inmax ? in + 2 : inmax - 1];
+      v.w = row[in + 3 < inmax ? in + 3 : inmax - 1];
     }
+    const int64_t nin = ok ? inmax - in : 0;   // valid elements in this float4
+    const uint32_t m4 = nin >= 4 ? 15u : (nin <= 0 ? 0u : ((1u << nin) - 1u));
+    mask |= m4 << (4 * i);
     reg[i] = v;
   }
+  return mask;
 }
 
 __device__ __forceinline__ bf16x4 cvt4(const float4 v) {
@@ -136,10 +144,21 @@ __device__ __forceinline__ float4 resid4(const float4 v, const bf16x4 h) {
 
 // ---------------------------------------------------------------------------- registers -> LDS image(s)
 template <int PREC, bool T>
-__device__ __forceinline__ void stage_store(typename Geo<PREC>::elem* img, const float4 (&reg)[Geo<PREC>::BK / 8]) {
+__device__ __forceinline__ void stage_store(typename Geo<PREC>::elem* img, float4 (&reg)[Geo<PREC>::BK / 8],
+                                            uint32_t mask) {
   using G = Geo<PREC>;
   constexpr int BK = G::BK;
   const int t = threadIdx.x;
+  if (mask != (BK / 8 == 8 ? 0xffffffffu : ((1u << (4 * (BK / 8))) - 1u))) {   // edge tile: zero invalid elements
+#pragma unroll
+    for (int i = 0; i < BK / 8; ++i) {
+      const uint32_t m = mask >> (4 * i);
+      reg[i].x = (m & 1u) ? reg[i].x : 0.f;
+      reg[i].y = (m & 2u) ? reg[i].y : 0.f;
+      reg[i].z = (m & 4u) ? reg[i].z : 0.f;
+      reg[i].w = (m & 8u) ? reg[i].w : 0.f;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < BK / 8; ++i) {
     const int idx = t + 256 * i;
@@ -197,6 +216,19 @@ __device__ __forceinline__ void epi_tile(const floatx16& a, int64_t rbase, int64
   if (col >= N) return;
   const bool split = ep.splits > 1;
   const float bval = (ep.bias != nullptr && !split) ? ep.bias[col] : 0.f;
+  // operands the epilogue reads (activation-gradient aux, or C for a read-modify-write) are loaded for all
+  // 16 rows first, unconditionally from clamped rows, so they issue back to back (see stage_load)
+  float rd[16];
+  const bool rmw = ep.accumulate && !split;
+  if (ep.aux != nullptr || rmw) {
+    const float* base = ep.aux != nullptr ? ep.aux : C;
+    const int64_t ld = ep.aux != nullptr ? ep.ldaux : ldc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int64_t row = rbase + (e & 3) + 8 * (e >> 2);
+      rd[e] = base[(row < M ? row : M - 1) * ld + col];
+    }
+  }
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int64_t row = rbase + (e & 3) + 8 * (e >> 2);
@@ -204,11 +236,11 @@ __device__ __forceinline__ void epi_tile(const floatx16& a, int64_t rbase, int64
       float v = a[e] + bval;
       if (ep.Z != nullptr && ((MMS_GEMM_ABLATE & 1) == 0 || v == 1234.5f)) ep.Z[row * ep.ldz + col] = v;
       if (ep.act != ACT_NONE) v = act_fwd(ep.act, v, ep.beta, ep.thr);
-      if (ep.aux != nullptr) v *= act_grad(ep.dact, ep.aux[row * ep.ldaux + col], ep.beta, ep.thr);
+      if (ep.aux != nullptr) v *= act_grad(ep.dact, rd[e], ep.beta, ep.thr);
       float* dst = C + row * ldc + col;
       if ((MMS_GEMM_ABLATE & 1) && v != 1234.5f) continue;
       if (split) atomicAdd(dst, v);
-      else if (ep.accumulate) *dst += v;
+      else if (rmw) *dst = rd[e] + v;
       else *dst = v;
       if (ep.ones_col >= 0 && col == 0) C[row * ldc + ep.ones_col] = 1.0f;
     }
@@ -269,19 +301,20 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t
   };
 
   float4 ra[BK / 8], rb[BK / 8];
+  uint32_t ma = 0, mb = 0;
   if (kbeg < kend) {
-    stage_load<BK, TA, VEC>(A, lda, m0, M, kbeg, kend, ra);
-    stage_load<BK, TB, VEC>(B, ldb, n0, N, kbeg, kend, rb);
+    ma = stage_load<BK, TA, VEC>(A, lda, m0, M, kbeg, kend, ra);
+    mb = stage_load<BK, TB, VEC>(B, ldb, n0, N, kbeg, kend, rb);
   }
   for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
     __syncthreads();
-    stage_store<PREC, TA>(As, ra);
-    stage_store<PREC, TB>(Bs, rb);
+    stage_store<PREC, TA>(As, ra, ma);
+    stage_store<PREC, TB>(Bs, rb, mb);
     if (do_cs) colsum_acc(ra);
     __syncthreads();
     if (k0 + BK < kend) {
-      stage_load<BK, TA, VEC>(A, lda, m0, M, k0 + BK, kend, ra);
-      stage_load<BK, TB, VEC>(B, ldb, n0, N, k0 + BK, kend, rb);
+      ma = stage_load<BK, TA, VEC>(A, lda, m0, M, k0 + BK, kend, ra);
+      mb = stage_load<BK, TB, VEC>(B, ldb, n0, N, k0 + BK, kend, rb);
     }
     const int ar0 = wm * 64, br0 = wn * 64;
     if constexpr ((MMS_GEMM_ABLATE & 2) != 0) {

@@ -109,66 +109,47 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(const float* __restri
 //
 // Points come in groups of G rows (row = g + j * gstride, j < G): the SDF batch is [centre | 4 taps]
 // with the taps a few 1e-3 apart (surface_model.py:138-160), so at all but the finest levels the G points
-// of a group fall into one grid cell.  One thread per (group, level) walks its G points and merges the
-// corner gradients of consecutive points that share the cell before issuing the atomics: the table
-// gradient is atomic-throughput bound (scattered f32 atomics), and this removes up to (G-1)/G of them.
-__device__ __forceinline__ void corner_grads(const float2 dE, float ox, float oy, float oz, float2 (&df)[8],
-                                             float2& d0312, float2& d4756, float2& d03, float2& d12, float2& d47,
-                                             float2& d56) {
-  const float nx = 1.0f - ox, ny = 1.0f - oy, nz = 1.0f - oz;
-  // autograd order of encodings.py:292-302 reversed
-  d0312 = make_float2(dE.x * oz, dE.y * oz);
-  d4756 = make_float2(dE.x * nz, dE.y * nz);
-  d03 = make_float2(d0312.x * oy, d0312.y * oy);
-  d12 = make_float2(d0312.x * ny, d0312.y * ny);
-  d47 = make_float2(d4756.x * oy, d4756.y * oy);
-  d56 = make_float2(d4756.x * ny, d4756.y * ny);
-  df[0] = make_float2(d03.x * ox, d03.y * ox);
-  df[3] = make_float2(d03.x * nx, d03.y * nx);
-  df[1] = make_float2(d12.x * ox, d12.y * ox);
-  df[2] = make_float2(d12.x * nx, d12.y * nx);
-  df[5] = make_float2(d56.x * ox, d56.y * ox);
-  df[6] = make_float2(d56.x * nx, d56.y * nx);
-  df[4] = make_float2(d47.x * ox, d47.y * ox);
-  df[7] = make_float2(d47.x * nx, d47.y * nx);
-}
-
-__device__ __forceinline__ void flush_corners(float* __restrict__ dtable, const uint32_t (&idx)[8],
-                                              const float2 (&acc)[8]) {
+// of a group fall into one grid cell.  Each lane walks the G points of its group and merges the corner
+// gradients of consecutive points that share the cell before issuing the atomics: the table gradient is
+// bound by scattered f32 atomics, and this removes up to (G-1)/G of them.
+// One lane per (group, level, feature): the two features of a table entry are added by lanes 2j, 2j+1 of the
+// same atomic instruction, i.e. in one 64-B memory-side atomic request instead of two (scattered f32 atomics
+// cost per request, MI355X_MICROARCH.md §Global float atomics).
+__device__ __forceinline__ void flush_corners(float* __restrict__ dtable, int feat, const uint32_t (&idx)[8],
+                                              const float (&acc)[8]) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     // merge duplicate corners inside the cell (integer coordinates => ceil == floor)
     bool dup = false;
-    float2 a = acc[i];
+    float a = acc[i];
 #pragma unroll
     for (int j = 0; j < i; ++j) dup |= (idx[j] == idx[i]);
     if (dup) continue;
 #pragma unroll
     for (int j = i + 1; j < 8; ++j)
-      if (idx[j] == idx[i]) { a.x += acc[j].x; a.y += acc[j].y; }
-    float* dst = dtable + 2 * (int64_t)idx[i];
-    atomicAdd(dst, a.x);
-    atomicAdd(dst + 1, a.y);
+      if (idx[j] == idx[i]) a += acc[j];
+    atomicAdd(dtable + 2 * (int64_t)idx[i] + feat, a);
   }
 }
 
 template <int G>
 __global__ __launch_bounds__(256) void hashgrid_bwd_kernel(const float* __restrict__ pos, int64_t Mg,
                                                            int64_t gstride, int64_t ldx,
-                                                           const float2* __restrict__ table, GridParams p,
+                                                           const float* __restrict__ table, GridParams p,
                                                            const float* __restrict__ dout, int64_t ldd,
                                                            float* __restrict__ dtable, float* __restrict__ dpos,
                                                            int64_t lddx) {
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t grp = tid >> 4;
-  const int level = (int)(tid & 15);
+  const int64_t grp = tid >> 5;
+  const int level = (int)((tid >> 1) & 15);
+  const int feat = (int)(tid & 1);
   const bool live = grp < Mg && level < p.levels && level < p.active_levels;
   const float s = p.scale[level];
   uint32_t pidx[8];
-  float2 pacc[8];
+  float pacc[8];
   bool pending = false;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { pidx[i] = 0; pacc[i] = make_float2(0.f, 0.f); }
+  for (int i = 0; i < 8; ++i) { pidx[i] = 0; pacc[i] = 0.f; }
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     const int64_t pt = grp + (int64_t)j * gstride;
@@ -176,10 +157,17 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_kernel(const float* __restri
     if (live) {
       const float* xp = pos + pt * ldx;
       const Corners c = make_corners(xp[0], xp[1], xp[2], p.radius, p.inv_2r, s, level, p.log2T);
-      const float2 dE = *reinterpret_cast<const float2*>(dout + pt * ldd + 2 * level);
+      const float dE = dout[pt * ldd + 2 * level + feat];
       const float ox = c.ox, oy = c.oy, oz = c.oz;
-      float2 df[8], d0312, d4756, d03, d12, d47, d56;
-      corner_grads(dE, ox, oy, oz, df, d0312, d4756, d03, d12, d47, d56);
+      const float nx = 1.0f - ox, ny = 1.0f - oy, nz = 1.0f - oz;
+      // autograd order of encodings.py:292-302 reversed (per feature)
+      const float d0312 = dE * oz, d4756 = dE * nz;
+      const float d03 = d0312 * oy, d12 = d0312 * ny, d47 = d4756 * oy, d56 = d4756 * ny;
+      float df[8];
+      df[0] = d03 * ox; df[3] = d03 * nx;
+      df[1] = d12 * ox; df[2] = d12 * nx;
+      df[5] = d56 * ox; df[6] = d56 * nx;
+      df[4] = d47 * ox; df[7] = d47 * nx;
       if (dtable != nullptr) {
         // same 8 table entries as the pending point (same cell) -> merge, else flush the pending set
         bool same = pending;
@@ -187,45 +175,35 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_kernel(const float* __restri
         for (int i = 0; i < 8; ++i) same &= (pidx[i] == c.idx[i]);
         if (same) {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) { pacc[i].x += df[i].x; pacc[i].y += df[i].y; }
+          for (int i = 0; i < 8; ++i) pacc[i] += df[i];
         } else {
-          if (pending) flush_corners(dtable, pidx, pacc);
+          if (pending) flush_corners(dtable, feat, pidx, pacc);
 #pragma unroll
           for (int i = 0; i < 8; ++i) { pidx[i] = c.idx[i]; pacc[i] = df[i]; }
           pending = true;
         }
       }
       if (dpos != nullptr) {
-        float2 f[8];
+        float f[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) f[i] = table[c.idx[i]];
-        const float nx = 1.0f - ox, ny = 1.0f - oy, nz = 1.0f - oz;
-        float2 f03, f12, f56, f47, f0312, f4756;
-        f03.x = f[0].x * ox + f[3].x * nx;  f03.y = f[0].y * ox + f[3].y * nx;
-        f12.x = f[1].x * ox + f[2].x * nx;  f12.y = f[1].y * ox + f[2].y * nx;
-        f56.x = f[5].x * ox + f[6].x * nx;  f56.y = f[5].y * ox + f[6].y * nx;
-        f47.x = f[4].x * ox + f[7].x * nx;  f47.y = f[4].y * ox + f[7].y * nx;
-        f0312.x = f03.x * oy + f12.x * ny;  f0312.y = f03.y * oy + f12.y * ny;
-        f4756.x = f47.x * oy + f56.x * ny;  f4756.y = f47.y * oy + f56.y * ny;
-        const float doz = dE.x * (f0312.x - f4756.x) + dE.y * (f0312.y - f4756.y);
-        const float doy = d0312.x * (f03.x - f12.x) + d0312.y * (f03.y - f12.y) +
-                          d4756.x * (f47.x - f56.x) + d4756.y * (f47.y - f56.y);
-        const float dox = d03.x * (f[0].x - f[3].x) + d03.y * (f[0].y - f[3].y) +
-                          d12.x * (f[1].x - f[2].x) + d12.y * (f[1].y - f[2].y) +
-                          d56.x * (f[5].x - f[6].x) + d56.y * (f[5].y - f[6].y) +
-                          d47.x * (f[4].x - f[7].x) + d47.y * (f[4].y - f[7].y);
-        gx = dox * s; gy = doy * s; gz = doz * s;
+        for (int i = 0; i < 8; ++i) f[i] = table[2 * (int64_t)c.idx[i] + feat];
+        const float f03 = f[0] * ox + f[3] * nx, f12 = f[1] * ox + f[2] * nx;
+        const float f56 = f[5] * ox + f[6] * nx, f47 = f[4] * ox + f[7] * nx;
+        const float f0312 = f03 * oy + f12 * ny, f4756 = f47 * oy + f56 * ny;
+        gz = dE * (f0312 - f4756) * s;
+        gy = (d0312 * (f03 - f12) + d4756 * (f47 - f56)) * s;
+        gx = (d03 * (f[0] - f[3]) + d12 * (f[1] - f[2]) + d56 * (f[5] - f[6]) + d47 * (f[4] - f[7])) * s;
       }
     }
     if (dpos != nullptr) {
-      // reduce over the 16 levels of a point (16 consecutive lanes)
+      // reduce over the 16 levels x 2 features of a point (32 consecutive lanes)
 #pragma unroll
-      for (int off = 8; off >= 1; off >>= 1) {
-        gx += __shfl_xor(gx, off, 16);
-        gy += __shfl_xor(gy, off, 16);
-        gz += __shfl_xor(gz, off, 16);
+      for (int off = 16; off >= 1; off >>= 1) {
+        gx += __shfl_xor(gx, off, 32);
+        gy += __shfl_xor(gy, off, 32);
+        gz += __shfl_xor(gz, off, 32);
       }
-      if (level == 0 && grp < Mg) {
+      if ((tid & 31) == 0 && grp < Mg) {
         float* dp = dpos + pt * lddx;
         const float two_r = 2.0f * p.radius;
         dp[0] += gx / two_r;
@@ -234,7 +212,7 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_kernel(const float* __restri
       }
     }
   }
-  if (pending) flush_corners(dtable, pidx, pacc);
+  if (pending) flush_corners(dtable, feat, pidx, pacc);
 }
 
 int fill_params(const char* fn, GridParams& p, int L, int log2T, const float* scales, float radius,
@@ -286,14 +264,14 @@ MMS_EXPORT int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group,
   if (rc) return rc;
   if (Mg == 0 || (dtable == nullptr && dpos == nullptr)) return 0;
   MMS_REQUIRE(pos && table && dout, fn, "null pointer");
-  const int64_t threads = Mg * 16;
+  const int64_t threads = Mg * 32;
   const dim3 grid(mms::grid_for(threads, 256, INT32_MAX));
   if (group == 5)
     hipLaunchKernelGGL(hashgrid_bwd_kernel<5>, grid, dim3(256), 0, mms::as_stream(stream), pos, Mg, gstride, ldx,
-                       reinterpret_cast<const float2*>(table), p, dout, ldd, dtable, dpos, lddx);
+                       table, p, dout, ldd, dtable, dpos, lddx);
   else
     hipLaunchKernelGGL(hashgrid_bwd_kernel<1>, grid, dim3(256), 0, mms::as_stream(stream), pos, Mg, Mg, ldx,
-                       reinterpret_cast<const float2*>(table), p, dout, ldd, dtable, dpos, lddx);
+                       table, p, dout, ldd, dtable, dpos, lddx);
   return mms::check_launch(fn);
 }
 

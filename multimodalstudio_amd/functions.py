@@ -53,6 +53,20 @@ def _alloc(rows: int, cols: int, dev, zero: bool = False) -> torch.Tensor:
     return buf[:, :cols]
 
 
+def grad_target(p: torch.Tensor) -> Optional[torch.Tensor]:
+    """The buffer a parameter's gradient is accumulated into directly by the backward kernels.
+
+    Parameter gradients are written in place into ``p.grad`` (for the trainer: views into the flat
+    gradient buffer of pipeline.FlatGroup) and the autograd Functions return ``None`` for them: no
+    per-parameter zero-fill, temporary and AccumulateGrad add per step (AccumulateGrad's semantics --
+    sum into .grad -- are kept: every kernel here accumulates)."""
+    if not p.requires_grad:
+        return None
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    return p.grad
+
+
 def _s() -> int:
     return torch.cuda.current_stream().cuda_stream
 
@@ -129,6 +143,8 @@ class MLPRun:
             act, beta, thr = self.acts[l]
             if l == self.L - 1 and last_out is not None:
                 Y = last_out
+            elif l == self.L - 1:
+                Y = torch.empty(M, N, device=dev)   # leaves the MLP: consumers expect a contiguous tensor
             else:
                 Y = _alloc(M, N, dev)
             Z = _alloc(M, N, dev) if (keep and act != 0) else None
@@ -142,13 +158,15 @@ class MLPRun:
             h = Y
         return h
 
-    def backward(self, dy: torch.Tensor, need_dx: bool) -> Tuple[Optional[torch.Tensor], List[torch.Tensor]]:
+    def backward(self, dy: torch.Tensor, need_dx: bool,
+                 pre_activated: bool = False) -> Tuple[Optional[torch.Tensor], List[torch.Tensor]]:
+        """dy = gradient of the last layer's output, or (pre_activated) already of its pre-activation."""
         x = self.x
         M = x.shape[0]
         dev = x.device
-        grads: List[Optional[torch.Tensor]] = [None] * len(self.params)
+        grads: List[Optional[torch.Tensor]] = [None] * len(self.params)   # accumulated in place (grad_target)
         act, beta, thr = self.acts[self.L - 1]
-        if act != 0:
+        if act != 0 and not pre_activated:
             dZ = _alloc(M, dy.shape[1], dev)
             act_bwd(dy, self.Zs[-1], act, beta, thr, dZ)
         else:
@@ -158,15 +176,16 @@ class MLPRun:
             g, v, b = self.params[3 * l: 3 * l + 3]
             N, K = v.shape
             Xin = x if l == 0 else self.Ys[l - 1]
-            dW = torch.zeros(N, K, device=dev)
-            db = torch.zeros(N, device=dev)
-            tiles = ((N + 127) // 128) * ((K + 127) // 128)
-            gemm(TN, N, K, M, dZ, dZ.stride(0), Xin, Xin.stride(0), dW, K, accumulate=True,
-                 splits=_splits_for(M, tiles), prec=self.prec, colsum=db)
-            dg = torch.zeros(N, device=dev)
-            dv = torch.zeros(N, K, device=dev)
-            weight_norm_bwd(g.reshape(-1), v, self.norms[l], dW, dg, dv)
-            grads[3 * l], grads[3 * l + 1], grads[3 * l + 2] = dg.view_as(g), dv, db
+            gt, vt, bt = grad_target(g), grad_target(v), grad_target(b)
+            if gt is not None or vt is not None or bt is not None:
+                dW = torch.zeros(N, K, device=dev)
+                db = bt if bt is not None else torch.zeros(N, device=dev)
+                tiles = ((N + 127) // 128) * ((K + 127) // 128)
+                gemm(TN, N, K, M, dZ, dZ.stride(0), Xin, Xin.stride(0), dW, K, accumulate=True,
+                     splits=_splits_for(M, tiles), prec=self.prec, colsum=db)
+                dg = gt.reshape(-1) if gt is not None else torch.zeros(N, device=dev)
+                dv = vt if vt is not None else torch.zeros(N, K, device=dev)
+                weight_norm_bwd(g.reshape(-1), v, self.norms[l], dW, dg, dv)
             if l > 0:
                 pa, pbeta, pthr = self.acts[l - 1]
                 dprev = _alloc(M, K, dev)
@@ -205,9 +224,20 @@ class SurfaceFunction(torch.autograd.Function):
         d32 = float(torch.tensor(delta, dtype=torch.float32))
         _lib.call("mms_geo_input_fwd", pos.data_ptr(), 3, M, 4, d32, 6, X.data_ptr(), X.stride(0), _s())
         grid_fwd(grid, X, X.stride(0), 5 * M, table, active, X, 39)
-        run = MLPRun(params, SDF_ACTS, PRECISION["sdf"])
-        out = run.forward(X, keep=True)
-        G = out.shape[1] - 1
+        # hidden layers over all 5M rows; the output layer (257 wide: sdf + geo feature) only needs the sdf
+        # column on the 4M tap rows (surface_model.py:137-153 uses the taps' sdf alone)
+        run = MLPRun(params[:-3], SDF_ACTS[:-1], PRECISION["sdf"])
+        H = run.forward(X, keep=True)
+        g3, v3, b3 = params[-3:]
+        N3, K3 = v3.shape
+        W3 = _alloc(N3, K3, dev)
+        n3 = torch.empty(N3, device=dev)
+        weight_norm_fwd(g3.reshape(-1), v3, W3, n3)
+        out = _alloc(5 * M, N3, dev)
+        prec = PRECISION["sdf"]
+        gemm(NT, M, N3, K3, H, H.stride(0), W3, W3.stride(0), out, out.stride(0), bias=b3, prec=prec)
+        gemm(NT, 4 * M, 1, K3, H[M:], H.stride(0), W3, W3.stride(0), out[M:], out.stride(0), bias=b3, prec=prec)
+        G = N3 - 1
         four_delta = float(torch.tensor(4.0 * delta, dtype=torch.float32))
         delta_sq = float(torch.tensor(delta ** 2, dtype=torch.float32))
         grads = torch.empty(M, 3, device=dev)
@@ -218,8 +248,9 @@ class SurfaceFunction(torch.autograd.Function):
         sdf = out[:M, 0:1].contiguous()
         geo = out[:M, 1:].contiguous()
         ctx.grid, ctx.active, ctx.M, ctx.G = grid, active, M, G
+        ctx.table = table          # the Parameter itself: its .grad is accumulated in place
         ctx.four_delta, ctx.delta_sq = four_delta, delta_sq
-        ctx.run = run
+        ctx.run, ctx.H, ctx.W3, ctx.n3, ctx.prec = run, H, W3, n3, prec
         ctx.X = X
         ctx.save_for_backward(pos, table, grads, *params)
         return sdf, geo, grads, hess, normals
@@ -229,19 +260,46 @@ class SurfaceFunction(torch.autograd.Function):
         pos, table, grads, *params = ctx.saved_tensors
         M, G = ctx.M, ctx.G
         dev = pos.device
-        dout = _alloc(5 * M, G + 1, dev, zero=True)
+        # dout: centre rows all 257 columns, tap rows only the sdf column (everything read is written here)
+        dout = _alloc(5 * M, G + 1, dev)
         _lib.call("mms_taps_combine_bwd", grads.data_ptr(), _p(dgrads if dgrads is not None else None),
                   _p(dhess), _p(dnormals), M, ctx.four_delta, ctx.delta_sq, dout.data_ptr(), dout.stride(0), _s())
         if dsdf is not None:
             dout[:M, 0:1] += dsdf
         if dgeo is not None:
             dout[:M, 1:] = dgeo
+        else:
+            dout[:M, 1:] = 0.0
         need_table = ctx.needs_input_grad[1]
         need_pos = ctx.needs_input_grad[0]
-        dX, pgrads = ctx.run.backward(dout, need_dx=True)
+        # output layer: centre rows (257 columns) and tap rows (sdf column) as two GEMM pairs
+        H, W3, prec = ctx.H, ctx.W3, ctx.prec
+        g3, v3, b3 = params[-3:]
+        N3, K3 = v3.shape
+        gt, vt, bt = grad_target(g3), grad_target(v3), grad_target(b3)
+        if gt is not None or vt is not None or bt is not None:
+            dW3 = torch.zeros(N3, K3, device=dev)
+            db3 = bt if bt is not None else torch.zeros(N3, device=dev)
+            gemm(TN, N3, K3, M, dout, dout.stride(0), H, H.stride(0), dW3, K3, accumulate=True,
+                 splits=_splits_for(M, 6), prec=prec, colsum=db3)
+            gemm(TN, 1, K3, 4 * M, dout[M:], dout.stride(0), H[M:], H.stride(0), dW3, K3, accumulate=True,
+                 splits=_splits_for(4 * M, 2), prec=prec, colsum=db3)
+            weight_norm_bwd(g3.reshape(-1), v3, ctx.n3, dW3, gt.reshape(-1) if gt is not None else
+                            torch.zeros(N3, device=dev), vt if vt is not None else torch.zeros(N3, K3, device=dev))
+        # dZ of the last hidden layer = (dout W3) * softplus'(Z) -- the activation gradient fused as aux
+        run = ctx.run
+        pa, pbeta, pthr = SDF_ACTS[-2]
+        Zl = run.Zs[-1]
+        dZ = _alloc(5 * M, K3, dev)
+        gemm(NN, M, K3, N3, dout, dout.stride(0), W3, W3.stride(0), dZ, dZ.stride(0), aux=Zl, ldaux=Zl.stride(0),
+             dact=pa, beta=pbeta, thr=pthr, prec=prec)
+        gemm(NN, 4 * M, K3, 1, dout[M:], dout.stride(0), W3, W3.stride(0), dZ[M:], dZ.stride(0), aux=Zl[M:],
+             ldaux=Zl.stride(0), dact=pa, beta=pbeta, thr=pthr, prec=prec)
+        dX, pgrads = run.backward(dZ, need_dx=True, pre_activated=True)
+        pgrads = list(pgrads) + [None, None, None]
         X = ctx.X
         K0 = X.stride(0)
-        dtable = torch.zeros_like(table) if need_table else None
+        dtable = grad_target(ctx.table) if need_table else None
         dP = torch.zeros(5 * M, 3, device=dev) if need_pos else None
         grid_bwd(ctx.grid, X, K0, 5 * M, table, ctx.active, dX, 39, dtable, dP, group=5)
         dpos = None
@@ -249,9 +307,8 @@ class SurfaceFunction(torch.autograd.Function):
             dpos = torch.zeros(M, 3, device=dev)
             _lib.call("mms_geo_input_bwd", X.data_ptr(), K0, dX.data_ptr(), dX.stride(0), dP.data_ptr(), 3, M, 4, 6,
                       dpos.data_ptr(), 3, _s())
-        ctx.run = None
-        ctx.X = None
-        return (dpos, dtable, None, None, None, *pgrads)
+        ctx.run = ctx.H = ctx.W3 = ctx.X = ctx.table = None
+        return (dpos, None, None, None, None, *pgrads)
 
 
 def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> torch.Tensor:
@@ -297,6 +354,7 @@ class RadianceFunction(torch.autograd.Function):
         run = MLPRun(params, RAD_ACTS, PRECISION["radiance"])
         feat = run.forward(X, keep=True)
         ctx.run, ctx.X, ctx.grid, ctx.active, ctx.S, ctx.G = run, X, grid, active, S, G
+        ctx.table = table
         ctx.save_for_backward(pos, dirs, normals, table, *params)
         return feat
 
@@ -309,7 +367,7 @@ class RadianceFunction(torch.autograd.Function):
         dX, pgrads = ctx.run.backward(dfeat.contiguous(), need_dx=True)
         X = ctx.X
         K0 = X.stride(0)
-        dtable = torch.zeros_like(table) if ctx.needs_input_grad[4] else None
+        dtable = grad_target(ctx.table) if ctx.needs_input_grad[4] else None
         need_pos = ctx.needs_input_grad[0]
         dP = torch.zeros(M, 3, device=dev) if need_pos else None
         grid_bwd(ctx.grid, X, K0, M, table, ctx.active, dX, 29 + G, dtable, dP)
@@ -320,7 +378,8 @@ class RadianceFunction(torch.autograd.Function):
                   S, G, _p(dpos), 3, _p(dgeo), G, _p(ddirs), _s())
         ctx.run = None
         ctx.X = None
-        return (dpos, ddirs, None, dgeo, dtable, None, None, None, *pgrads)
+        ctx.table = None
+        return (dpos, ddirs, None, dgeo, None, None, None, None, *pgrads)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -407,7 +466,7 @@ def _mlp_strided(run: MLPRun, H: torch.Tensor, Fb: int) -> torch.Tensor:
     nrm = torch.empty(N, device=dev)
     weight_norm_fwd(g.reshape(-1), v, W, nrm)
     act, beta, thr = run.acts[0]
-    Y = _alloc(M, N, dev)
+    Y = torch.empty(M, N, device=dev)
     Z = _alloc(M, N, dev)
     gemm(NT, M, N, K, H, H.stride(0), W, W.stride(0), Y, Y.stride(0), bias=b, Z=Z, ldz=Z.stride(0), act=act,
          beta=beta, thr=thr, prec=run.prec)
@@ -423,16 +482,18 @@ def _mlp_strided_bwd(run: MLPRun, dy: torch.Tensor, H: torch.Tensor, Fb: int):
     act, beta, thr = run.acts[0]
     dZ = _alloc(M, N, dev)
     act_bwd(dy, run.Zs[0], act, beta, thr, dZ)
-    dW = torch.zeros(N, K, device=dev)
-    db = torch.zeros(N, device=dev)
-    gemm(TN, N, K, M, dZ, dZ.stride(0), H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1),
-         prec=run.prec, colsum=db)
-    dg = torch.zeros(N, device=dev)
-    dv = torch.zeros(N, K, device=dev)
-    weight_norm_bwd(g.reshape(-1), v, run.norms[0], dW, dg, dv)
+    gt, vt, bt = grad_target(g), grad_target(v), grad_target(b)
+    if gt is not None or vt is not None or bt is not None:
+        dW = torch.zeros(N, K, device=dev)
+        db = bt if bt is not None else torch.zeros(N, device=dev)
+        gemm(TN, N, K, M, dZ, dZ.stride(0), H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1),
+             prec=run.prec, colsum=db)
+        dg = gt.reshape(-1) if gt is not None else torch.zeros(N, device=dev)
+        dv = vt if vt is not None else torch.zeros(N, K, device=dev)
+        weight_norm_bwd(g.reshape(-1), v, run.norms[0], dW, dg, dv)
     dxin = _alloc(M, K, dev)
     gemm(NN, M, K, N, dZ, dZ.stride(0), run.Ws[0], run.Ws[0].stride(0), dxin, dxin.stride(0), prec=run.prec)
-    return dxin, [dg.view_as(g), dv, db]
+    return dxin, [None, None, None]
 
 
 # ------------------------------------------------------------------------------------------------

@@ -129,3 +129,49 @@ def test_gemm_precisions(dev, prec, tol, M, N, K):
     ref_db = dZ.double().sum(0) + 0.5
     err = (db.cpu().double() - ref_db).abs().max() / dZ.double().abs().sum(0).max()
     assert err < 1e-6, f"fused colsum rel err {err:.2e}"
+
+
+@pytest.mark.parametrize("prec", [0, 1, 2])
+def test_gemm_degenerate_shapes_and_views(dev, prec):
+    """The output-layer split of the SDF MLP: N = 1 (tap-row sdf column), K = 1 (its data gradient), M = 1
+    (its weight gradient), on row-offset views of padded panels."""
+    from multimodalstudio_amd import hip_ops
+    from multimodalstudio_amd.functions import _alloc
+    tol = {0: 2e-6, 1: 2e-2, 2: 2e-5}[prec]
+    g = torch.Generator().manual_seed(3)
+    Mc, R, K, N = 300, 1500, 256, 257
+    H = _alloc(Mc + R, K, dev)
+    H.copy_(torch.randn(Mc + R, K, generator=g))
+    W = _alloc(N, K, dev)
+    W.copy_(torch.randn(N, K, generator=g) * 0.1)
+    b = torch.randn(N, generator=g).to(dev)
+    out = _alloc(Mc + R, N, dev)
+    out.fill_(float("nan"))
+    hip_ops.gemm(hip_ops.NT, R, 1, K, H[Mc:], H.stride(0), W, W.stride(0), out[Mc:], out.stride(0), bias=b, prec=prec)
+    ref = H[Mc:].double() @ W[0:1].double().T + b[0].double()
+    err = (out[Mc:, 0:1].double() - ref).abs().max() / ref.abs().max()
+    assert err < tol, f"NT N=1: {err:.2e}"
+    assert torch.isnan(out[Mc:, 1:]).all(), "NT N=1 wrote outside its column"
+    # K = 1: dZ[tap] = dout[:, 0:1] W[0:1, :] * act'(aux)
+    dout = _alloc(Mc + R, N, dev)
+    dout.copy_(torch.randn(Mc + R, N, generator=g))
+    aux = _alloc(Mc + R, K, dev)
+    aux.copy_(torch.randn(Mc + R, K, generator=g) * 0.01)
+    dZ = _alloc(Mc + R, K, dev)
+    hip_ops.gemm(hip_ops.NN, R, K, 1, dout[Mc:], dout.stride(0), W, W.stride(0), dZ[Mc:], dZ.stride(0),
+                 aux=aux[Mc:], ldaux=aux.stride(0), dact=2, beta=100.0, thr=20.0, prec=prec)
+    sp = torch.sigmoid(100.0 * aux[Mc:].double())
+    sp = torch.where(100.0 * aux[Mc:].double() > 20.0, torch.ones_like(sp), sp)
+    ref = (dout[Mc:, 0:1].double() @ W[0:1].double()) * sp
+    err = (dZ[Mc:].double() - ref).abs().max() / ref.abs().max()
+    assert err < tol, f"NN K=1: {err:.2e}"
+    # M = 1: dW[0] += dout[tap, 0]^T H[tap], db[0] += sum dout[tap, 0]
+    dW = torch.zeros(N, K, device=dev)
+    db = torch.zeros(N, device=dev)
+    hip_ops.gemm(hip_ops.TN, 1, K, R, dout[Mc:], dout.stride(0), H[Mc:], H.stride(0), dW, K, accumulate=True,
+                 splits=4, prec=prec, colsum=db)
+    ref = dout[Mc:, 0:1].double().T @ H[Mc:].double()
+    err = (dW[0:1].double() - ref).abs().max() / ref.abs().max()
+    assert err < tol, f"TN M=1: {err:.2e}"
+    assert (dW[1:] == 0).all() and (db[1:] == 0).all()
+    assert abs(float(db[0]) - float(dout[Mc:, 0].double().sum())) < 1e-3 * float(dout[Mc:, 0].abs().sum())

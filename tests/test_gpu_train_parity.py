@@ -75,6 +75,9 @@ def test_train_parity_fp32(dev):
     f, cfg, losses, psnr, preds = run_parity(dev, "fp32")
     ref = np.array([float(f[f"s{k}:loss"]) for k in range(cfg["steps"])])
     rel = np.abs(losses - ref) / np.abs(ref)
+    k = int(rel.argmax())
+    print("fp32 per-step loss (hip, oracle):", [(i, round(float(losses[i]), 6), round(float(ref[i]), 6))
+                                                 for i in range(min(6, len(ref)))], "worst", k, losses[k], ref[k])
     print(f"fp32: max loss rel err {rel.max():.2e}; PSNR {psnr} vs oracle "
           f"{ {m: float(f[f'eval:{m}:psnr']) for m in cfg['modalities']} }")
     assert rel.max() < 1e-3
