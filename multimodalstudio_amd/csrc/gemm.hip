@@ -73,24 +73,6 @@ struct Epi {
   float* colsum; // TA only: colsum[m] += sum_k A[k][m] (bias gradient of the weight-gradient GEMM), or null
 };
 
-__device__ __forceinline__ float act_fwd(int act, float v, float beta, float thr) {
-  switch (act) {
-    case ACT_RELU: return v > 0.f ? v : 0.f;
-    case ACT_SOFTPLUS: { const float bx = v * beta; return bx > thr ? v : log1pf(expf(bx)) / beta; }
-    case ACT_SIGMOID: return 1.0f / (1.0f + expf(-v));
-    default: return v;
-  }
-}
-
-__device__ __forceinline__ float act_grad(int act, float z, float beta, float thr) {
-  switch (act) {
-    case ACT_RELU: return z > 0.f ? 1.f : 0.f;
-    case ACT_SOFTPLUS: { const float bx = z * beta; if (bx > thr) return 1.f; const float e = expf(bx); return e / (e + 1.0f); }
-    case ACT_SIGMOID: { const float s = 1.0f / (1.0f + expf(-z)); return s * (1.0f - s); }
-    default: return 1.f;
-  }
-}
-
 // ---------------------------------------------------------------------------- global -> registers
 // NV = float4 per thread per operand tile = 128 * BK / 4 / 256 = BK / 8.
 // N source ([rows][K]): idx = t + 256 i -> row = idx / (BK/4), kc = idx % (BK/4)  (a row's BK floats by BK/4 lanes)
@@ -211,6 +193,9 @@ __device__ __forceinline__ float frag_f32(const float* img, int row0, int kk) {
 // ---------------------------------------------------------------------------- epilogue
 // one 32x32 accumulator tile -> C (bias, Z = pre-activation, activation, aux act-grad, store/accumulate/atomic).
 // C/D map (all dtypes): col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5).
+// Activations: the fp32 parity mode keeps the accurate libm forms; the bf16 modes use the hardware
+// transcendentals (common.h act_fwd_fast: the accurate forms made a 270k x 256 epilogue compute-bound).
+template <int PREC>
 __device__ __forceinline__ void epi_tile(const floatx16& a, int64_t rbase, int64_t col, int64_t M, int64_t N,
                                          float* __restrict__ C, int64_t ldc, const Epi& ep) {
   if (col >= N) return;
@@ -235,8 +220,11 @@ __device__ __forceinline__ void epi_tile(const floatx16& a, int64_t rbase, int64
     if (row < M) {
       float v = a[e] + bval;
       if (ep.Z != nullptr && ((MMS_GEMM_ABLATE & 1) == 0 || v == 1234.5f)) ep.Z[row * ep.ldz + col] = v;
-      if (ep.act != ACT_NONE) v = act_fwd(ep.act, v, ep.beta, ep.thr);
-      if (ep.aux != nullptr) v *= act_grad(ep.dact, rd[e], ep.beta, ep.thr);
+      if (ep.act != ACT_NONE)
+        v = PREC == P_F32 ? mms::act_fwd_exact(ep.act, v, ep.beta, ep.thr) : mms::act_fwd_fast(ep.act, v, ep.beta, ep.thr);
+      if (ep.aux != nullptr)
+        v *= PREC == P_F32 ? mms::act_grad_exact(ep.dact, rd[e], ep.beta, ep.thr)
+                           : mms::act_grad_fast(ep.dact, rd[e], ep.beta, ep.thr);
       float* dst = C + row * ldc + col;
       if ((MMS_GEMM_ABLATE & 1) && v != 1234.5f) continue;
       if (split) atomicAdd(dst, v);
@@ -373,10 +361,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t
 
   const int64_t rbase = m0 + wm * 64 + 4 * (lane >> 5);
   const int64_t cbase = n0 + wn * 64 + (lane & 31);
-  epi_tile(acc00, rbase, cbase, M, N, C, ldc, ep);
-  epi_tile(acc01, rbase, cbase + 32, M, N, C, ldc, ep);
-  epi_tile(acc10, rbase + 32, cbase, M, N, C, ldc, ep);
-  epi_tile(acc11, rbase + 32, cbase + 32, M, N, C, ldc, ep);
+  epi_tile<PREC>(acc00, rbase, cbase, M, N, C, ldc, ep);
+  epi_tile<PREC>(acc01, rbase, cbase + 32, M, N, C, ldc, ep);
+  epi_tile<PREC>(acc10, rbase + 32, cbase, M, N, C, ldc, ep);
+  epi_tile<PREC>(acc11, rbase + 32, cbase + 32, M, N, C, ldc, ep);
 }
 
 template <int PREC, bool TA, bool TB>

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ A
   atomicAdd(out + n, s);
 }
 
-// act ids match gemm_f32.hip: 0 none, 1 relu, 2 softplus(beta, thr), 3 sigmoid
+// act ids as common.h act_grad_fast: 0 none, 1 relu, 2 softplus(beta, thr), 3 sigmoid
 __global__ void act_bwd_kernel(const float* __restrict__ dY, int64_t ldy, const float* __restrict__ Z, int64_t ldz,
                                int64_t M, int64_t N, int act, float beta, float thr, float* __restrict__ dZ,
                                int64_t lddz) {
@@ -78,14 +78,7 @@ __global__ void act_bwd_kernel(const float* __restrict__ dY, int64_t ldy, const 
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t m = i / N, n = i - m * N;
     const float z = Z[m * ldz + n];
-    float d = 1.f;
-    switch (act) {
-      case 1: d = z > 0.f ? 1.f : 0.f; break;
-      case 2: { const float bx = z * beta; d = bx > thr ? 1.f : expf(bx) / (expf(bx) + 1.0f); } break;
-      case 3: { const float s = 1.0f / (1.0f + expf(-z)); d = s * (1.0f - s); } break;
-      default: break;
-    }
-    dZ[m * lddz + n] = dY[m * ldy + n] * d;
+    dZ[m * lddz + n] = dY[m * ldy + n] * mms::act_grad_exact(act, z, beta, thr);
   }
 }
 

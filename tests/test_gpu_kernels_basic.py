@@ -175,3 +175,41 @@ def test_gemm_degenerate_shapes_and_views(dev, prec):
     assert err < tol, f"TN M=1: {err:.2e}"
     assert (dW[1:] == 0).all() and (db[1:] == 0).all()
     assert abs(float(db[0]) - float(dout[Mc:, 0].double().sum())) < 1e-3 * float(dout[Mc:, 0].abs().sum())
+
+
+@pytest.mark.parametrize("prec,tol", [(1, 2e-2), (2, 3e-5)])
+@pytest.mark.parametrize("M,N,K", [(20000, 256, 256), (30011, 256, 72), (17000, 71, 256), (9000, 130, 200),
+                                   (25000, 1, 256)])
+def test_gemm_tall_skinny_epilogues(dev, prec, tol, M, N, K):
+    """Tall-skinny bf16 / bf16x3 layers at training sizes with the fast-math epilogues: forward NT with
+    bias + softplus + Z, data-gradient NN with the softplus-gradient aux, vs fp64."""
+    from multimodalstudio_amd import hip_ops
+    from multimodalstudio_amd.functions import _alloc
+    g = torch.Generator().manual_seed(M + N + K)
+    X = _alloc(M, K, dev)
+    X.copy_(torch.randn(M, K, generator=g))
+    W = _alloc(N, K, dev)
+    W.copy_(torch.randn(N, K, generator=g) * 0.1)
+    b = torch.randn(N, generator=g).to(dev) * 0.1
+    Y = _alloc(M, N, dev)
+    Z = _alloc(M, N, dev)
+    hip_ops.gemm(hip_ops.NT, M, N, K, X, X.stride(0), W, W.stride(0), Y, Y.stride(0), bias=b, Z=Z, ldz=Z.stride(0),
+                 act=2, beta=100.0, thr=20.0, prec=prec)
+    z_ref = X.double() @ W.double().T + b.double()
+    y_ref = torch.nn.functional.softplus(z_ref, beta=100, threshold=20)
+    ez = ((Z.double() - z_ref).abs().max() / z_ref.abs().max()).item()
+    ey = ((Y.double() - y_ref).abs().max() / y_ref.abs().max()).item()
+    assert ez < tol and ey < tol, (ez, ey)
+    # NN: dX = (dZ W) * softplus'(aux), dZ [M, N], W [N, K] seen as [K=N][N=K]
+    dZ = _alloc(M, N, dev)
+    dZ.copy_(torch.randn(M, N, generator=g))
+    aux = _alloc(M, K, dev)
+    aux.copy_(torch.randn(M, K, generator=g) * 0.02)
+    dX = _alloc(M, K, dev)
+    hip_ops.gemm(hip_ops.NN, M, K, N, dZ, dZ.stride(0), W, W.stride(0), dX, dX.stride(0), aux=aux,
+                 ldaux=aux.stride(0), dact=2, beta=100.0, thr=20.0, prec=prec)
+    bx = 100.0 * aux.double()
+    sg = torch.where(bx > 20.0, torch.ones_like(bx), torch.sigmoid(bx))
+    ref = (dZ.double() @ W.double()) * sg
+    e = ((dX.double() - ref).abs().max() / ref.abs().max()).item()
+    assert e < tol, e
