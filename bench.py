@@ -53,7 +53,8 @@ def gemm_work(a):
     mn = float(M) * N
     nbytes = 4.0 * (float(M) * K + float(N) * K + mn * (1 + (Z is not None) + (aux is not None) +
                                                          (bool(accumulate) and splits <= 1)))
-    return PREC_NAMES[prec], (2.0 * M * N * K, nbytes)
+    mode = {(0, 0): "NT", (0, 1): "NN", (1, 1): "TN"}.get((a[1], a[2]), "??")
+    return f"{PREC_NAMES[prec]}:{mode}", (2.0 * M * N * K, nbytes)
 
 
 def work_fns():
@@ -173,7 +174,7 @@ def main():
             if name.startswith("mms_gemm"):
                 # roofline = the slower of the MFMA and the HBM bound for this launch mix
                 flops, nbytes = work
-                peak = MFMA_PEAK_TF[name.split(":")[1]]
+                peak = MFMA_PEAK_TF[name.split(":")[1]]       # "mms_gemm:<precision>:<NT|NN|TN>"
                 t_mfma = flops / (peak * 1e12)
                 t_hbm = nbytes / (HBM_PEAK_GBS * 1e9)
                 if t_mfma >= t_hbm:
@@ -195,10 +196,20 @@ def main():
                                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "avg_ms": round(ms, 5),
                                 "launches_per_step": launches_per_step,
                                 "ms_per_step": round(ms * launches_per_step, 4), "traffic": None})
+        # HBM traffic per launch from the committed rocprofv3 PMC passes of this workload (scripts/gpu_pmc.sh ->
+        # scripts/pmc_traffic.py -> profiles/pmc_traffic_<precision>.json); null when not collected
+        pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.precision}.json")
+        pmc = json.load(open(pmc_path))["kernels"] if os.path.exists(pmc_path) else {}
+        for rec in kernels:
+            if rec["kernel"] in pmc:
+                rec["traffic"] = pmc[rec["kernel"]]["hbm_bytes_per_launch"]
+                rec["traffic_unit"] = "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
         kernels.sort(key=lambda k: -k["ms_per_step"])
         if kernels:
             top = kernels[0]
             roof = {k: top[k] for k in ["bound", "achieved", "peak", "unit", "frac", "traffic"]}
+            if "traffic_unit" in top:
+                roof["traffic_unit"] = top["traffic_unit"]
             roof["kernel"] = top["kernel"]
             roof["avg_ms"] = top["avg_ms"]
 

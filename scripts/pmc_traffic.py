@@ -1,0 +1,66 @@
+#!/usr/bin/env python
+"""Per-launch HBM traffic of the bench's watched kernels from rocprofv3 --pmc passes (scripts/gpu_pmc.sh).
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE
+tallies 128-B read requests at 64 B, i.e. reports half of the bytes of wide reads -> x2.  The result is keyed
+by the labels bench.py uses for its roofline entries and written to profiles/pmc_traffic_<precision>.json,
+which bench.py reads to fill `roofline.traffic`.
+
+    python scripts/pmc_traffic.py fast
+"""
+import collections
+import csv
+import json
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PREC = {"0": "fp32", "1": "bf16", "2": "bf16x3"}
+MODE = {("false", "false"): "NT", ("false", "true"): "NN", ("true", "true"): "TN"}
+
+
+def label(name):
+    m = re.search(r"gemm_kernel<(\d), (true|false), (true|false), (true|false)>", name)
+    if m:
+        return f"mms_gemm:{PREC[m.group(1)]}:{MODE.get((m.group(2), m.group(3)), '??')}"
+    if "hashgrid_bwd_kernel" in name:
+        return "mms_hashgrid_bwd_grouped"
+    if "hashgrid_fwd_kernel" in name:
+        return "mms_hashgrid_fwd"
+    return None
+
+
+def per_kernel(path, counter):
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        lab = label(r["Kernel_Name"])
+        if lab:
+            acc[lab].append(float(r["Counter_Value"]) * 1024.0)
+    return acc
+
+
+def main():
+    prec = sys.argv[1] if len(sys.argv) > 1 else "fast"
+    base = os.path.join(ROOT, "gpurun_out")
+    fetch = per_kernel(os.path.join(base, f"pmc_{prec}_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(base, f"pmc_{prec}_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
+    out = {"precision": prec, "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+           "bench.py --steps 5 --warmup 2; FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B)", "kernels": {}}
+    for lab in sorted(set(fetch) | set(write)):
+        f = fetch.get(lab, [])
+        w = write.get(lab, [])
+        fb = 2.0 * sum(f) / max(1, len(f))
+        wb = sum(w) / max(1, len(w))
+        out["kernels"][lab] = {"launches": len(f), "fetch_bytes_per_launch": round(fb), "write_bytes_per_launch":
+                               round(wb), "hbm_bytes_per_launch": round(fb + wb)}
+    dst = os.path.join(ROOT, "profiles", f"pmc_traffic_{prec}.json")
+    with open(dst, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
