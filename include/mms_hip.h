@@ -167,6 +167,11 @@ int mms_collider_bwd(const float* origins, const float* dirs, int64_t N, float r
                      void* stream);
 /* order-preserving mask compaction (TensorDataclass.__getitem__ with a bool mask, base_model.py:88-93) */
 int mms_compact(const unsigned char* mask, int64_t N, int64_t* idx, int64_t* count, void* stream);
+/* fixed-capacity form for static-shape (graph-captured) steps: idx [N] buffer, its first cap entries are used;
+ * rows [count, cap) are padding (gather index = first hit, scatter index sidx = N, a dummy row); count is
+ * clamped to cap on the device.  sidx may be NULL. */
+int mms_compact_padded(const unsigned char* mask, int64_t N, int64_t cap, int64_t* idx, int64_t* sidx,
+                       int64_t* count, void* stream);
 
 /* ---- losses (model_components/losses.py): L1 (+ SkipSaturation fill), eikonal, curvature; scalars on device */
 int mms_l1_loss_fwd(const float* out, int64_t ldo, const float* tgt, int64_t N, int C, float sat_thr,

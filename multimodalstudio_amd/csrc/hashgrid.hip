@@ -105,114 +105,115 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(const float* __restri
   *reinterpret_cast<float2*>(out + pt * ldo + 2 * level) = r;
 }
 
-// Backward: dtable (atomic accumulate) and optional dx (accumulate into dpos[:, 0:3]).
-//
-// Points come in groups of G rows (row = g + j * gstride, j < G): the SDF batch is [centre | 4 taps]
-// with the taps a few 1e-3 apart (surface_model.py:138-160), so at all but the finest levels the G points
-// of a group fall into one grid cell.  Each lane walks the G points of its group and merges the corner
-// gradients of consecutive points that share the cell before issuing the atomics: the table gradient is
-// bound by scattered f32 atomics, and this removes up to (G-1)/G of them.
-// One lane per (group, level, feature): the two features of a table entry are added by lanes 2j, 2j+1 of the
-// same atomic instruction, i.e. in one 64-B memory-side atomic request instead of two (scattered f32 atomics
-// cost per request, MI355X_MICROARCH.md §Global float atomics).
-__device__ __forceinline__ void flush_corners(float* __restrict__ dtable, int feat, const uint32_t (&idx)[8],
-                                              const float (&acc)[8]) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    // merge duplicate corners inside the cell (integer coordinates => ceil == floor)
-    bool dup = false;
-    float a = acc[i];
-#pragma unroll
-    for (int j = 0; j < i; ++j) dup |= (idx[j] == idx[i]);
-    if (dup) continue;
-#pragma unroll
-    for (int j = i + 1; j < 8; ++j)
-      if (idx[j] == idx[i]) a += acc[j];
-    atomicAdd(dtable + 2 * (int64_t)idx[i] + feat, a);
+// Backward ("walk"): one workgroup = 16 level groups x 16 lanes and owns CH consecutive point groups (rows
+// g0 .. g0+CH-1 and, for G = 5, their tap rows g + j * gstride).  A level group walks the CH * G points in order
+// (centre, then its 4 taps, then the next sample); lane q holds one (corner, feature) slot -- (y, z) corner pair
+// q >> 2, x side (q >> 1) & 1, feature q & 1 -- and keeps ONE pending (table entry, gradient) accumulator,
+// issuing its atomic only when its entry changes.  Consecutive samples of a ray and the 4 taps around a sample
+// share cells at all coarse levels, so most adds merge in registers.  The two x corners of a pair differ only in
+// the low hash bits (the x prime is 1): they usually share a 64-B line and sit in adjacent lanes, so an atomic
+// wave-instruction touches ~16 lines instead of 32 (scattered float atomics cost per 64-B request,
+// MI355X_MICROARCH.md §Global float atomics).  Position gradients are summed over the 16 lanes by shuffles and
+// over levels through LDS, then added to dpos once per point.
+template <int G, int CH>
+__global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __restrict__ pos, int64_t Mg,
+                                                                int64_t gstride, int64_t ldx,
+                                                                const float* __restrict__ table, GridParams p,
+                                                                const float* __restrict__ dout, int64_t ldd,
+                                                                float* __restrict__ dtable, float* __restrict__ dpos,
+                                                                int64_t lddx) {
+  __shared__ float sdp[CH * G * 3];
+  const int t = threadIdx.x;
+  const int level = t >> 4;
+  const int q = t & 15;
+  const int pr = q >> 2;                // 0: (y c, z c)  1: (y f, z c)  2: (y c, z f)  3: (y f, z f)
+  const bool xc = ((q >> 1) & 1) == 0;  // x = ceil corner
+  const bool yc = (pr & 1) == 0, zc = pr < 2;
+  const int feat = q & 1;
+  const int64_t g0 = (int64_t)blockIdx.x * CH;
+  const int nck = (int)((Mg - g0) < CH ? (Mg - g0) : CH);
+  if (dpos != nullptr) {
+    for (int i = t; i < CH * G * 3; i += 256) sdp[i] = 0.f;
+    __syncthreads();
   }
-}
-
-template <int G>
-__global__ __launch_bounds__(256) void hashgrid_bwd_kernel(const float* __restrict__ pos, int64_t Mg,
-                                                           int64_t gstride, int64_t ldx,
-                                                           const float* __restrict__ table, GridParams p,
-                                                           const float* __restrict__ dout, int64_t ldd,
-                                                           float* __restrict__ dtable, float* __restrict__ dpos,
-                                                           int64_t lddx) {
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t grp = tid >> 5;
-  const int level = (int)((tid >> 1) & 15);
-  const int feat = (int)(tid & 1);
-  const bool live = grp < Mg && level < p.levels && level < p.active_levels;
-  const float s = p.scale[level];
-  uint32_t pidx[8];
-  float pacc[8];
-  bool pending = false;
+  if (level < p.levels && level < p.active_levels) {
+    const float s = p.scale[level];
+    const uint32_t hmask = (1u << p.log2T) - 1u;
+    const uint32_t base = (uint32_t)level << p.log2T;
+    const float two_r = 2.0f * p.radius;
+    uint32_t pidx = 0u;
+    float pacc = 0.f;
+    for (int k = 0; k < nck; ++k) {
+      // the G points' inputs first: independent loads in flight together
+      float px[G], py[G], pz[G], pe[G];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { pidx[i] = 0; pacc[i] = 0.f; }
+      for (int j = 0; j < G; ++j) {
+        const int64_t pt = g0 + k + (int64_t)j * gstride;
+        const float* xp = pos + pt * ldx;
+        px[j] = xp[0];
+        py[j] = xp[1];
+        pz[j] = xp[2];
+        pe[j] = dout[pt * ldd + 2 * level + feat];
+      }
 #pragma unroll
-  for (int j = 0; j < G; ++j) {
-    const int64_t pt = grp + (int64_t)j * gstride;
-    float gx = 0.f, gy = 0.f, gz = 0.f;
-    if (live) {
-      const float* xp = pos + pt * ldx;
-      const Corners c = make_corners(xp[0], xp[1], xp[2], p.radius, p.inv_2r, s, level, p.log2T);
-      const float dE = dout[pt * ldd + 2 * level + feat];
-      const float ox = c.ox, oy = c.oy, oz = c.oz;
-      const float nx = 1.0f - ox, ny = 1.0f - oy, nz = 1.0f - oz;
-      // autograd order of encodings.py:292-302 reversed (per feature)
-      const float d0312 = dE * oz, d4756 = dE * nz;
-      const float d03 = d0312 * oy, d12 = d0312 * ny, d47 = d4756 * oy, d56 = d4756 * ny;
-      float df[8];
-      df[0] = d03 * ox; df[3] = d03 * nx;
-      df[1] = d12 * ox; df[2] = d12 * nx;
-      df[5] = d56 * ox; df[6] = d56 * nx;
-      df[4] = d47 * ox; df[7] = d47 * nx;
-      if (dtable != nullptr) {
-        // same 8 table entries as the pending point (same cell) -> merge, else flush the pending set
-        bool same = pending;
+      for (int j = 0; j < G; ++j) {
+        // same rounded values as make_corners (bit-exact corners)
+        const float sx = ((px[j] + p.radius) / two_r) * s;
+        const float sy = ((py[j] + p.radius) / two_r) * s;
+        const float sz = ((pz[j] + p.radius) / two_r) * s;
+        const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+        const float ox = sx - fx, oy = sy - fy, oz = sz - fz;
+        const int cx = xc ? (int)ceilf(sx) : (int)fx;
+        const int cy = yc ? (int)ceilf(sy) : (int)fy;
+        const int cz = zc ? (int)ceilf(sz) : (int)fz;
+        const uint32_t idx = base + hash3(cx, cy, cz, hmask);
+        const float wx = xc ? ox : 1.0f - ox, wy = yc ? oy : 1.0f - oy, wz = zc ? oz : 1.0f - oz;
+        const float dE = pe[j];
+        if (dtable != nullptr) {
+          // autograd order of encodings.py:292-302 reversed: ((dE * w_z) * w_y) * w_x
+          const float df = ((dE * wz) * wy) * wx;
+          if (idx == pidx) {
+            pacc += df;
+          } else {
+            if (pacc != 0.f) atomicAdd(dtable + 2 * (int64_t)pidx + feat, pacc);
+            pidx = idx;
+            pacc = df;
+          }
+        }
+        if (dpos != nullptr) {
+          const float e = dE * table[2 * (int64_t)idx + feat];
+          float gx = (xc ? e : -e) * (wz * wy);
+          float gy = (yc ? e : -e) * (wz * wx);
+          float gz = (zc ? e : -e) * (wy * wx);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) same &= (pidx[i] == c.idx[i]);
-        if (same) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) pacc[i] += df[i];
-        } else {
-          if (pending) flush_corners(dtable, feat, pidx, pacc);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) { pidx[i] = c.idx[i]; pacc[i] = df[i]; }
-          pending = true;
+          for (int off = 8; off >= 1; off >>= 1) {
+            gx += __shfl_xor(gx, off, 16);
+            gy += __shfl_xor(gy, off, 16);
+            gz += __shfl_xor(gz, off, 16);
+          }
+          if (q == 0) {
+            float* d = sdp + (k * G + j) * 3;
+            atomicAdd(d, gx * s);
+            atomicAdd(d + 1, gy * s);
+            atomicAdd(d + 2, gz * s);
+          }
         }
       }
-      if (dpos != nullptr) {
-        float f[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) f[i] = table[2 * (int64_t)c.idx[i] + feat];
-        const float f03 = f[0] * ox + f[3] * nx, f12 = f[1] * ox + f[2] * nx;
-        const float f56 = f[5] * ox + f[6] * nx, f47 = f[4] * ox + f[7] * nx;
-        const float f0312 = f03 * oy + f12 * ny, f4756 = f47 * oy + f56 * ny;
-        gz = dE * (f0312 - f4756) * s;
-        gy = (d0312 * (f03 - f12) + d4756 * (f47 - f56)) * s;
-        gx = (d03 * (f[0] - f[3]) + d12 * (f[1] - f[2]) + d56 * (f[5] - f[6]) + d47 * (f[4] - f[7])) * s;
-      }
     }
-    if (dpos != nullptr) {
-      // reduce over the 16 levels x 2 features of a point (32 consecutive lanes)
-#pragma unroll
-      for (int off = 16; off >= 1; off >>= 1) {
-        gx += __shfl_xor(gx, off, 32);
-        gy += __shfl_xor(gy, off, 32);
-        gz += __shfl_xor(gz, off, 32);
-      }
-      if ((tid & 31) == 0 && grp < Mg) {
-        float* dp = dpos + pt * lddx;
-        const float two_r = 2.0f * p.radius;
-        dp[0] += gx / two_r;
-        dp[1] += gy / two_r;
-        dp[2] += gz / two_r;
-      }
+    if (dtable != nullptr && pacc != 0.f) atomicAdd(dtable + 2 * (int64_t)pidx + feat, pacc);
+  }
+  if (dpos != nullptr) {
+    __syncthreads();
+    const float two_r = 2.0f * p.radius;
+    for (int i = t; i < nck * G; i += 256) {
+      const int k = i / G, j = i - k * G;
+      const int64_t pt = g0 + k + (int64_t)j * gstride;
+      float* dp = dpos + pt * lddx;
+      dp[0] += sdp[3 * i] / two_r;
+      dp[1] += sdp[3 * i + 1] / two_r;
+      dp[2] += sdp[3 * i + 2] / two_r;
     }
   }
-  if (pending) flush_corners(dtable, feat, pidx, pacc);
 }
 
 int fill_params(const char* fn, GridParams& p, int L, int log2T, const float* scales, float radius,
@@ -264,14 +265,15 @@ MMS_EXPORT int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group,
   if (rc) return rc;
   if (Mg == 0 || (dtable == nullptr && dpos == nullptr)) return 0;
   MMS_REQUIRE(pos && table && dout, fn, "null pointer");
-  const int64_t threads = Mg * 32;
-  const dim3 grid(mms::grid_for(threads, 256, INT32_MAX));
-  if (group == 5)
-    hipLaunchKernelGGL(hashgrid_bwd_kernel<5>, grid, dim3(256), 0, mms::as_stream(stream), pos, Mg, gstride, ldx,
-                       table, p, dout, ldd, dtable, dpos, lddx);
-  else
-    hipLaunchKernelGGL(hashgrid_bwd_kernel<1>, grid, dim3(256), 0, mms::as_stream(stream), pos, Mg, Mg, ldx,
-                       table, p, dout, ldd, dtable, dpos, lddx);
+  if (group == 5) {
+    constexpr int CH = 16;
+    hipLaunchKernelGGL((hashgrid_bwd_walk_kernel<5, CH>), dim3(mms::grid_for(Mg, CH, INT32_MAX)), dim3(256), 0,
+                       mms::as_stream(stream), pos, Mg, gstride, ldx, table, p, dout, ldd, dtable, dpos, lddx);
+  } else {
+    constexpr int CH = 32;
+    hipLaunchKernelGGL((hashgrid_bwd_walk_kernel<1, CH>), dim3(mms::grid_for(Mg, CH, INT32_MAX)), dim3(256), 0,
+                       mms::as_stream(stream), pos, Mg, Mg, ldx, table, p, dout, ldd, dtable, dpos, lddx);
+  }
   return mms::check_launch(fn);
 }
 

@@ -283,6 +283,22 @@ __global__ __launch_bounds__(1024) void compact_kernel(const unsigned char* __re
   if (threadIdx.x == 0) count[0] = base;
 }
 
+// fixed-capacity variant for static-shape (graph-captured) steps: after the compaction above, rows
+// [count, cap) are padding -- gather index = first hit (or 0: always a valid row), scatter index = N
+// (a dummy row one past the real ones).  Work on padding rows is discarded (their loss weight is zero).
+__global__ __launch_bounds__(1024) void compact_pad_kernel(int64_t N, int64_t cap, int64_t* __restrict__ idx,
+                                                           int64_t* __restrict__ sidx,
+                                                           int64_t* __restrict__ count) {
+  const int64_t c = count[0] < cap ? count[0] : cap;
+  const int64_t pad = c > 0 ? idx[0] : 0;
+  __syncthreads();
+  if (threadIdx.x == 0) count[0] = c;  // consumers read the clamped count
+  for (int64_t i = threadIdx.x; i < cap; i += blockDim.x) {
+    if (sidx) sidx[i] = i < c ? idx[i] : N;
+    if (i >= c) idx[i] = pad;
+  }
+}
+
 }  // namespace
 
 MMS_EXPORT int mms_raygen_fwd(const int* coords, int64_t N, const float* fx, const float* fy, const float* cx,
@@ -331,5 +347,18 @@ MMS_EXPORT int mms_collider_bwd(const float* origins, const float* dirs, int64_t
 MMS_EXPORT int mms_compact(const unsigned char* mask, int64_t N, int64_t* idx, int64_t* count, void* stream) {
   const char* fn = "mms_compact";
   hipLaunchKernelGGL(compact_kernel, dim3(1), dim3(1024), 0, mms::as_stream(stream), mask, N, idx, count);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_compact_padded(const unsigned char* mask, int64_t N, int64_t cap, int64_t* idx, int64_t* sidx,
+                                  int64_t* count, void* stream) {
+  const char* fn = "mms_compact_padded";
+  MMS_REQUIRE(cap >= 1 && cap <= N, fn, "capacity must be in [1, N]");
+  MMS_REQUIRE(idx && count, fn, "null pointer");
+  hipStream_t s = mms::as_stream(stream);
+  // the scan writes hit indices below the true count: idx needs N entries when more than cap rays hit,
+  // so the caller passes an [N] buffer and uses its first cap entries
+  hipLaunchKernelGGL(compact_kernel, dim3(1), dim3(1024), 0, s, mask, N, idx, count);
+  hipLaunchKernelGGL(compact_pad_kernel, dim3(1), dim3(1024), 0, s, N, cap, idx, sidx, count);
   return mms::check_launch(fn);
 }
