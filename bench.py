@@ -57,9 +57,31 @@ def gemm_work(a):
     return f"{PREC_NAMES[prec]}:{mode}", (2.0 * M * N * K, nbytes)
 
 
+def chain_work(a):
+    """(precision label, (algorithmic flops, algorithmic HBM bytes)) of one mms_mlp_chain launch (include/mms_hip.h
+    argument order): the three layers' 2MNK, narrowed on the SDF tap rows (rows >= rows_full: one output column of
+    the last forward layer, one input column of the first backward layer); bytes = input rows + the stores each
+    layer makes (+ the forward outputs the backward reads for its activation derivatives)."""
+    import ctypes
+    prec, bwd, K0, M, rf = a[0], a[1], a[4], a[5], a[6]
+    rf = M if rf < 0 else min(rf, M)
+    N = ctypes.cast(a[19], ctypes.POINTER(ctypes.c_int))
+    outs = ctypes.cast(a[17], ctypes.POINTER(ctypes.c_void_p))
+    n0, n1, n2 = N[0], N[1], N[2]
+    st = [outs[i] is not None for i in range(3)]
+    if bwd:
+        flops = 2.0 * (rf * K0 + (M - rf)) * n0 + 2.0 * M * (n0 * n1 + n1 * n2)
+        nbytes = 4.0 * ((rf * K0 + (M - rf)) + M * (n0 * st[0] + n1 * st[1] + n2 * st[2]) + M * (n0 + n1))
+    else:
+        flops = 2.0 * M * (K0 * n0 + n0 * n1) + 2.0 * (rf * n2 + (M - rf)) * n1
+        nbytes = 4.0 * (M * K0 + M * (n0 * st[0] + n1 * st[1]) + (rf * n2 + (M - rf)) * st[2])
+    return f"{PREC_NAMES[prec]}:chain{'_bwd' if bwd else '_fwd'}", (flops, nbytes)
+
+
 def work_fns():
     return {
         "mms_gemm": gemm_work,
+        "mms_mlp_chain": chain_work,
         "mms_hashgrid_fwd": lambda a: float(a[1]) * HASH_FWD_B,
         "mms_hashgrid_bwd_grouped": lambda a: float(a[1]) * a[2] * HASH_BWD_B,
     }
@@ -119,8 +141,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--precision", default="fp32", choices=list(DTYPES),
+    ap.add_argument("--precision", default="fast", choices=list(DTYPES),
                     help="MLP GEMM precision preset (functions.PRESETS); fp32 = reference-parity mode")
+    ap.add_argument("--mode", default="graph", choices=["graph", "eager"],
+                    help="graph: hipGraph-captured steps (multimodalstudio_amd/graphs.py); eager: Python-launched")
+    ap.add_argument("--timing-steps", type=int, default=5,
+                    help="eager steps after the timed region whose watched launches are timed with HIP events")
     args = ap.parse_args()
 
     from multimodalstudio_amd import _lib
@@ -140,26 +166,42 @@ def main():
     cfg = TrainConfig(method=method, modalities=mods, num_rays_per_modality=args.rays, log2T=args.log2T)
     trainer = Trainer(cfg, dev, rank=rank)
     trainer.set_step(args.start_step)
+    runner = None
+    if args.mode == "graph":
+        from multimodalstudio_amd.graphs import GraphTrainer
+        runner = GraphTrainer(trainer, ddp=ddp)
+        step = runner.step
+    else:
+        step = lambda: trainer.train_step(ddp=ddp)  # noqa: E731
 
     for _ in range(args.warmup):
-        trainer.train_step(ddp=ddp)
+        step()
     torch.cuda.synchronize()
     if ddp:
         ddp.barrier()
     torch.cuda.synchronize()
-    if not args.no_kernel_timing:
-        _lib.TIMER.start(work_fns())
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        trainer.train_step(ddp=ddp)
+        step()
     torch.cuda.synchronize()
     if ddp:
         ddp.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    _lib.TIMER.stop()
     if ddp:
         elapsed = ddp.max_over_ranks(elapsed, dev)
+    if runner is not None:
+        print(f"[bench] graph steps: {runner.stats}, {len(runner.graphs)} graphs"
+              + (f", capture disabled: {runner.disabled}" if runner.disabled else ""), file=sys.stderr)
+    # per-kernel durations: eager steps of the same workload right after the timed region, every watched launch
+    # bracketed by HIP events on the stream it is launched on (a graph replay cannot bracket single kernels)
+    timing_steps = max(1, args.timing_steps)
+    if not args.no_kernel_timing:
+        _lib.TIMER.start(work_fns())
+        for _ in range(timing_steps):
+            trainer.train_step(ddp=ddp)
+        torch.cuda.synchronize()
+        _lib.TIMER.stop()
 
     rays_per_step = args.rays * len(mods) * world
     value = rays_per_step * args.steps / elapsed
@@ -170,11 +212,11 @@ def main():
     if not args.no_kernel_timing:
         summ = _lib.TIMER.summary()
         for name, (n, ms, work) in summ.items():
-            launches_per_step = n / args.steps
-            if name.startswith("mms_gemm"):
+            launches_per_step = n / timing_steps
+            if name.startswith("mms_gemm") or name.startswith("mms_mlp_chain"):
                 # roofline = the slower of the MFMA and the HBM bound for this launch mix
                 flops, nbytes = work
-                peak = MFMA_PEAK_TF[name.split(":")[1]]       # "mms_gemm:<precision>:<NT|NN|TN>"
+                peak = MFMA_PEAK_TF[name.split(":")[1]]       # "mms_gemm:<precision>:<NT|NN|TN>", "mms_mlp_chain:..."
                 t_mfma = flops / (peak * 1e12)
                 t_hbm = nbytes / (HBM_PEAK_GBS * 1e9)
                 if t_mfma >= t_hbm:
@@ -233,7 +275,11 @@ def main():
             "data": "synthetic (analytic MMS-DATA-shaped scene, 45 train views 640x512, random-init weights)",
             "config": {"workload": desc, "num_rays_per_modality": args.rays, "modalities": list(mods),
                        "rays_per_step": rays_per_step, "log2_hashmap_size": args.log2T,
-                       "model_step": args.start_step, "precision": args.precision, "parallelism": f"dp{world}"},
+                       "model_step": args.start_step, "precision": args.precision, "parallelism": f"dp{world}",
+                       "step_mode": ("hipgraph replay (fixed-capacity foreground batches)" if runner is not None and
+                                     runner.disabled is None else "eager")},
+            "kernel_timing": (f"{timing_steps} eager steps of the same workload after the timed region, HIP events "
+                              "around every watched launch on its stream" if not args.no_kernel_timing else None),
             "roofline": roof,
             "roofline_kernels": kernels,
             "cpu_baseline": cpu,

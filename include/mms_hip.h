@@ -61,6 +61,28 @@ int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K
              const float* aux, int64_t ldaux, int act, int dact, float beta, float thr, int accumulate, int splits,
              int ones_col, float* colsum, void* stream);
 
+/* ---- fused MLP chains (MLP.forward mlp.py:152-171 under weight norm :206-209, three layers per launch) for the
+ * SDF field (71-256-256-257, Softplus(100), surface_field.py:99-116) and the radiance field (317-256-256-256,
+ * ReLU, radiance_field.py:72-77).  Layers are computed transposed so each layer's MFMA accumulator feeds the
+ * next layer from registers.  prec 1 = bf16, 2 = split bf16x3 operands (fp32 accumulate).
+ * Forward (backward = 0): out[l] = act_l(X_l W_l^T + b_l) for the 3 layers (out[0], out[1] may be NULL);
+ *   rows >= rows_full compute / store only output column 0 of the last layer (the SDF taps).
+ * Backward-data (backward = 1): X = dY of the last forward layer (rows >= rows_full: column 0 only), optionally
+ *   scaled by act'(xaux) (stored to xout); out[l] = (prev . W^T) * act_l'(aux[l]) with act' evaluated from the
+ *   forward output aux[l] (NULL: no scaling); out[2] = dX.
+ * a_hi / a_lo: per-layer packed weights from mms_mlp_pack (bf16 [32 ceil(N/32)][16 ceil(K/16)]); layers 1, 2 are
+ * register-fed and must be packed with permute = 1.  All row pitches multiples of 4 floats, 16-B aligned. */
+int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx, int K0, int64_t M, int64_t rows_full,
+                  const float* xaux, int64_t ldxaux, int xact, float* xout, int64_t ldxout, const void* const* a_hi,
+                  const void* const* a_lo, const float* const* bias, const float* const* aux, const int64_t* ldaux,
+                  float* const* out, const int64_t* ldo, const int* N, const int* act, float beta, float thr,
+                  void* stream);
+/* bf16 (hi, and lo = residual if non-NULL) image of W [N, K] (ldw) as an MFMA A operand [rows][cols]:
+ * transpose = 0 -> A = W, 1 -> A = W^T; permute = 1 stores each 16-column step in register-fed order
+ * (columns 0-3, 8-11, 4-7, 12-15).  Zero padded; rows % 32 == 0, cols % 16 == 0. */
+int mms_mlp_pack(const float* W, int64_t N, int64_t K, int64_t ldw, int transpose, int permute, int64_t rows,
+                 int64_t cols, void* hi, void* lo, void* stream);
+
 /* ---- weight norm (mlp.py:206-209; torch weight_norm dim=0): W = v * (g / ||v||_row); bwd dg += , dv += */
 int mms_weight_norm_fwd(const float* g, const float* v, int64_t N, int64_t K, float* W, int64_t ldw, float* norms,
                         void* stream);
@@ -184,12 +206,23 @@ int mms_geo_loss_fwd(const float* grads, const float* hess, int64_t M, float inv
 int mms_geo_loss_bwd(const float* grads, const float* hess, int64_t M, float inv_total, const float* deik,
                      float eik_scale, const float* dcurv, float curv_scale, float* dgrads, float* dhess,
                      void* stream);
+/* fixed-capacity batches (graph-captured steps): rows >= count[0] * S are padding and skipped, and 1 / total is
+ * read on the device (inv_total[0]), so the hit count never reaches the host */
+int mms_geo_loss_fwd_masked(const float* grads, const float* hess, int64_t M, int S, const int64_t* count,
+                            const float* inv_total, float* eik, float* curv, void* stream);
+int mms_geo_loss_bwd_masked(const float* grads, const float* hess, int64_t M, int S, const int64_t* count,
+                            const float* inv_total, const float* deik, float eik_scale, const float* dcurv,
+                            float curv_scale, float* dgrads, float* dhess, void* stream);
 
 /* ---- optimizer (pipelines/base_pipeline.py:232-248 clip_gradients, torch.optim.AdamW): acc += sum x^2 ;
  * AdamW with clip coefficient min(1, max_norm / (sqrt(*sumsq) + 1e-6)) read on device */
 int mms_sumsq(const float* x, int64_t n, float* acc, void* stream);
 int mms_adamw(float* p, const float* g, float* m, float* v, int64_t n, const float* sumsq, float max_norm, float lr,
               float wd, float beta1, float beta2, float eps, float step_size, float bc2_sqrt, void* stream);
+/* the same step with its per-step scalars read on the device: hyper = [lr, wd, beta1, beta2, eps, step_size,
+ * bc2_sqrt] (graph replays: the host rewrites the 7 floats before each launch) */
+int mms_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* sumsq, float max_norm,
+                  const float* hyper, void* stream);
 
 #ifdef __cplusplus
 }

@@ -115,6 +115,9 @@ TIMER = KernelTimer()
 def call(name: str, *args) -> None:
     """Invoke ``name`` and raise RuntimeError with mms_last_error() on a non-zero status."""
     L = lib()
+    if name not in SIGNATURES:
+        # an undeclared entry point would be called with ctypes' default (32-bit int) argument conversion
+        raise HipLibraryError(f"{name} is not declared in {HEADER.name}: refusing an untyped call")
     timed = TIMER.active and name in TIMER.watch
     if timed:
         import torch

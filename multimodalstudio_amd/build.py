@@ -14,6 +14,7 @@ from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
+INCLUDE = PKG.parent / "include"
 BUILD = PKG.parent / "build" / "mms_hip"
 LIB = PKG / "libmms_hip.so"
 ARCH = os.environ.get("MMS_OFFLOAD_ARCH", "gfx950")
@@ -28,12 +29,13 @@ CFLAGS = [
     "-Wall",
     "-Wno-unused-function",
     "-munsafe-fp-atomics",  # hardware global_atomic_add_f32 (no CAS loop)
+    f"-I{INCLUDE}",         # common.h includes the C-ABI header: definitions are checked against it
 ]
 
 
 def _compile(src: Path) -> Path:
     obj = BUILD / (src.stem + ".o")
-    deps = [src] + sorted(CSRC.glob("*.h"))
+    deps = [src] + sorted(CSRC.glob("*.h")) + sorted(INCLUDE.glob("*.h"))
     if obj.exists() and all(obj.stat().st_mtime >= d.stat().st_mtime for d in deps):
         return obj
     cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]

@@ -11,6 +11,11 @@
 #include <stdio.h>
 #include <string.h>
 
+// The public declarations: every entry point's definition is checked against its header prototype by the
+// compiler (a parameter-list drift between header and definition is a "conflicting declaration" error, so the
+// ctypes argtypes _lib.py derives from the header always match the code).
+#include "mms_hip.h"
+
 #define MMS_EXPORT extern "C" __attribute__((visibility("default")))
 
 namespace mms {

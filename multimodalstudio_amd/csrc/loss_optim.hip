@@ -71,12 +71,18 @@ __global__ void l1_bwd_kernel(const float* __restrict__ out, int64_t ldo, const 
   }
 }
 
-// eikonal: sum over rows of (||g|| - 1)^2 / M_total ; curvature: sum |h0 + h1 + h2| / M_total
+// eikonal: sum over rows of (||g|| - 1)^2 / M_total ; curvature: sum |h0 + h1 + h2| / M_total.
+// Fixed-capacity batches (graph-captured steps, graphs.py): with `count`, only rows [0, count[0] * S) are real, and
+// 1 / M_total is read from the device (inv_dev[0]) -- the hit count never reaches the host.
 __global__ __launch_bounds__(256) void geo_loss_fwd_kernel(const float* __restrict__ grads,
-                                                           const float* __restrict__ hess, int64_t M, float inv_total,
-                                                           float* __restrict__ eik, float* __restrict__ curv) {
+                                                           const float* __restrict__ hess, int64_t M,
+                                                           const int64_t* __restrict__ count, int S, float inv_total,
+                                                           const float* __restrict__ inv_dev, float* __restrict__ eik,
+                                                           float* __restrict__ curv) {
+  const int64_t lim = count ? (count[0] * S < M ? count[0] * S : M) : M;
+  const float inv = inv_dev ? inv_dev[0] : inv_total;
   float se = 0.f, sc = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += (int64_t)gridDim.x * blockDim.x) {
     if (grads) {
       const float g0 = grads[i * 3], g1 = grads[i * 3 + 1], g2 = grads[i * 3 + 2];
       const float n = sqrtf(g0 * g0 + g1 * g1 + g2 * g2);
@@ -88,18 +94,21 @@ __global__ __launch_bounds__(256) void geo_loss_fwd_kernel(const float* __restri
   __syncthreads();
   sc = block_reduce_sum(sc);
   if (threadIdx.x == 0) {
-    if (eik) atomicAdd(eik, se * inv_total);
-    if (curv) atomicAdd(curv, sc * inv_total);
+    if (eik) atomicAdd(eik, se * inv);
+    if (curv) atomicAdd(curv, sc * inv);
   }
 }
 
 __global__ void geo_loss_bwd_kernel(const float* __restrict__ grads, const float* __restrict__ hess, int64_t M,
-                                    float inv_total, const float* __restrict__ deik, float eik_scale,
+                                    const int64_t* __restrict__ count, int S, float inv_total,
+                                    const float* __restrict__ inv_dev, const float* __restrict__ deik, float eik_scale,
                                     const float* __restrict__ dcurv, float curv_scale, float* __restrict__ dgrads,
                                     float* __restrict__ dhess) {
-  const float ge = deik ? deik[0] * eik_scale * inv_total : 0.f;
-  const float gc = dcurv ? dcurv[0] * curv_scale * inv_total : 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t lim = count ? (count[0] * S < M ? count[0] * S : M) : M;
+  const float inv = inv_dev ? inv_dev[0] : inv_total;
+  const float ge = deik ? deik[0] * eik_scale * inv : 0.f;
+  const float gc = dcurv ? dcurv[0] * curv_scale * inv : 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += (int64_t)gridDim.x * blockDim.x) {
     if (grads && dgrads && deik) {
       const float g0 = grads[i * 3], g1 = grads[i * 3 + 1], g2 = grads[i * 3 + 2];
       const float n = sqrtf(g0 * g0 + g1 * g1 + g2 * g2);
@@ -134,11 +143,10 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
 }
 
 // AdamW with the clip coefficient coef = min(1, max_norm / (sqrt(sumsq) + 1e-6)) applied to g.
-__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
-                                                    const float* __restrict__ sumsq, float max_norm, float lr, float wd,
-                                                    float beta1, float beta2, float eps, float step_size,
-                                                    float bc2_sqrt) {
+__device__ __forceinline__ void adamw_apply(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                            float* __restrict__ v, int64_t n, const float* __restrict__ sumsq,
+                                            float max_norm, float lr, float wd, float beta1, float beta2, float eps,
+                                            float step_size, float bc2_sqrt) {
   float coef = 1.0f;
   if (sumsq != nullptr && max_norm > 0.f) {
     const float total = sqrtf(sumsq[0]);
@@ -157,6 +165,22 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
     m[i] = mi;
     v[i] = vi;
   }
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                    const float* __restrict__ sumsq, float max_norm, float lr, float wd,
+                                                    float beta1, float beta2, float eps, float step_size,
+                                                    float bc2_sqrt) {
+  adamw_apply(p, g, m, v, n, sumsq, max_norm, lr, wd, beta1, beta2, eps, step_size, bc2_sqrt);
+}
+
+// the per-step scalars read on the device: hyper = [lr, wd, beta1, beta2, eps, step_size, bc2_sqrt]
+__global__ __launch_bounds__(256) void adamw_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                        const float* __restrict__ sumsq, float max_norm,
+                                                        const float* __restrict__ hyper) {
+  adamw_apply(p, g, m, v, n, sumsq, max_norm, hyper[0], hyper[1], hyper[2], hyper[3], hyper[4], hyper[5], hyper[6]);
 }
 
 }  // namespace
@@ -192,7 +216,18 @@ MMS_EXPORT int mms_geo_loss_fwd(const float* grads, const float* hess, int64_t M
   const char* fn = "mms_geo_loss_fwd";
   if (M == 0) return 0;
   hipLaunchKernelGGL(geo_loss_fwd_kernel, dim3(mms::grid_for(M, 256, 1024)), dim3(256), 0, mms::as_stream(stream),
-                     grads, hess, M, inv_total, eik, curv);
+                     grads, hess, M, nullptr, 1, inv_total, nullptr, eik, curv);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_geo_loss_fwd_masked(const float* grads, const float* hess, int64_t M, int S, const int64_t* count,
+                                       const float* inv_total, float* eik, float* curv, void* stream) {
+  const char* fn = "mms_geo_loss_fwd_masked";
+  MMS_REQUIRE(S >= 1 && count != nullptr && inv_total != nullptr, fn,
+              "needs S >= 1, a device hit count and a device 1/total");
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(geo_loss_fwd_kernel, dim3(mms::grid_for(M, 256, 1024)), dim3(256), 0, mms::as_stream(stream),
+                     grads, hess, M, count, S, 0.f, inv_total, eik, curv);
   return mms::check_launch(fn);
 }
 
@@ -202,7 +237,19 @@ MMS_EXPORT int mms_geo_loss_bwd(const float* grads, const float* hess, int64_t M
   const char* fn = "mms_geo_loss_bwd";
   if (M == 0) return 0;
   hipLaunchKernelGGL(geo_loss_bwd_kernel, dim3(mms::grid_for(M, 256, 8192)), dim3(256), 0, mms::as_stream(stream),
-                     grads, hess, M, inv_total, deik, eik_scale, dcurv, curv_scale, dgrads, dhess);
+                     grads, hess, M, nullptr, 1, inv_total, nullptr, deik, eik_scale, dcurv, curv_scale, dgrads, dhess);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_geo_loss_bwd_masked(const float* grads, const float* hess, int64_t M, int S, const int64_t* count,
+                                       const float* inv_total, const float* deik, float eik_scale, const float* dcurv,
+                                       float curv_scale, float* dgrads, float* dhess, void* stream) {
+  const char* fn = "mms_geo_loss_bwd_masked";
+  MMS_REQUIRE(S >= 1 && count != nullptr && inv_total != nullptr, fn,
+              "needs S >= 1, a device hit count and a device 1/total");
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(geo_loss_bwd_kernel, dim3(mms::grid_for(M, 256, 8192)), dim3(256), 0, mms::as_stream(stream),
+                     grads, hess, M, count, S, 0.f, inv_total, deik, eik_scale, dcurv, curv_scale, dgrads, dhess);
   return mms::check_launch(fn);
 }
 
@@ -222,5 +269,15 @@ MMS_EXPORT int mms_adamw(float* p, const float* g, float* m, float* v, int64_t n
   if (n == 0) return 0;
   hipLaunchKernelGGL(adamw_kernel, dim3(mms::grid_for(n, 256, 8192)), dim3(256), 0, mms::as_stream(stream), p, g, m, v,
                      n, sumsq, max_norm, lr, wd, beta1, beta2, eps, step_size, bc2_sqrt);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* sumsq, float max_norm,
+                             const float* hyper, void* stream) {
+  const char* fn = "mms_adamw_dev";
+  MMS_REQUIRE(hyper != nullptr, fn, "null hyper-parameter buffer");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(adamw_dev_kernel, dim3(mms::grid_for(n, 256, 8192)), dim3(256), 0, mms::as_stream(stream), p, g, m,
+                     v, n, sumsq, max_norm, hyper);
   return mms::check_launch(fn);
 }

@@ -1,0 +1,363 @@
+// Fused weight-normed MLP chains on gfx950: the SDF field's 71 -> 256 -> 256 -> 257 Softplus(100) MLP and the
+// radiance field's 317 -> 256 -> 256 -> 256 ReLU MLP, forward and backward-data, one kernel launch each.
+//
+// Reference layers: nn.Linear + activation under weight norm (/root/reference/src/field_components/mlp.py:152-209)
+// inside FeatureGridAndMLP (field_components/feature_structures.py:153-169) for SDFField
+// (fields/surface_field.py:99-116) and RadianceField (fields/radiance_field.py:72-77).
+//
+// Orientation: every layer is computed transposed, H^T[n][m] = sum_k W[n][k] X[m][k], with the data rows m on
+// the MFMA column (lane) axis and the output units n on its row (register) axis.  The 32x32 accumulator of
+// v_mfma_f32_32x32x16_bf16 keeps its column on the lane and its rows in 16 registers, so the next layer --
+// which sums over n, the tile's ROW index -- takes it as its B operand straight from registers (registers
+// 8s..8s+7 = k-step s; cdna_hip_programming.md §3 "accumulator tile as the next MFMA's operand"): no LDS
+// image, no barrier and no HBM round trip between layers.  Inside a register-fed k-step the operand holds
+// units 0-3, 8-11, 4-7, 12-15 of the step, so mms_mlp_pack stores those layers' weight columns in that order
+// and every A fragment stays one 16-byte load.  One wave carries 32 data rows through the whole chain; the
+// weights stream from L2 as A fragments.
+//
+// Forward epilogue: + bias, activation, fp32 store of each layer's output (the backward reads it).
+// Backward-data: dZ_l = (W_{l+1}^T dZ_{l+1}) * act'(Y_l), with act' taken from the stored forward OUTPUT
+// (ReLU: Y > 0; Softplus(b): 1 - exp(-b Y) = sigmoid(b Z); Sigmoid: Y (1 - Y)) -- no pre-activation is ever
+// stored -- and an fp32 store of every dZ for the weight-gradient GEMMs.
+// PREC 1: bf16 operands; PREC 2: split bf16x3 (x = hi + lo, acc += lo.hi + hi.lo + hi.hi); fp32 accumulation.
+#include "common.h"
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+struct ChainLayer {
+  const __bf16* a_hi;  // packed A operand [32 nt][16 ks] (mms_mlp_pack)
+  const __bf16* a_lo;  // split-bf16x3 residual image, or null
+  const float* bias;   // forward: [N], or null
+  const float* aux;    // backward: forward output Y [rows][ldaux] whose act' scales the product, or null
+  int64_t ldaux;
+  float* out;          // fp32 store [rows][ldo] of the layer result, or null
+  int64_t ldo;
+  int N;               // valid output columns
+  int act;             // forward: activation; backward: derivative taken at aux
+};
+
+struct ChainArgs {
+  const float* X;      // layer-0 input [rows][ldx], K0 valid columns (16-B aligned rows)
+  int64_t ldx;
+  int K0;
+  int64_t M;
+  int64_t rows_full;   // SDF tap rows (>= rows_full): forward keeps only column 0 of the last layer,
+                       // backward reads only column 0 of the input
+  const float* xaux;   // backward: input first scaled by act'(xaux) (the last forward activation), or null
+  int64_t ldxaux;
+  int xact;
+  float* xout;         // backward: store of the scaled input (dZ of the last forward layer), or null
+  int64_t ldxout;
+  float beta, thr;     // Softplus(beta, threshold)
+  ChainLayer L[3];
+};
+
+__device__ __forceinline__ float act_grad_out(int act, float y, float beta, float thr) {
+  switch (act) {
+    case 1: return y > 0.f ? 1.f : 0.f;
+    case 2: {
+      const float by = y * beta;
+      if (by > thr) return 1.f;
+      return 1.0f - __builtin_amdgcn_exp2f(-by * 1.4426950408889634f);
+    }
+    case 3: return y * (1.0f - y);
+    default: return 1.f;
+  }
+}
+
+template <int PREC>
+__device__ __forceinline__ void split8(const float* v, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 b = (__bf16)v[j];
+    hi[j] = b;
+    if constexpr (PREC == 2) lo[j] = (__bf16)(v[j] - (float)b);
+  }
+}
+
+template <int PREC>
+__device__ __forceinline__ void mma(floatx16& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
+                                    const bf16x8& bl) {
+  if constexpr (PREC == 2) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  }
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+// 8 consecutive floats of a 16-B aligned row from column k0 (zero past K)
+__device__ __forceinline__ void load8(const float* __restrict__ row, int k0, int K, float* v) {
+  if (k0 + 8 <= K) {
+    const float4 a = *reinterpret_cast<const float4*>(row + k0);
+    const float4 b = *reinterpret_cast<const float4*>(row + k0 + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (k0 + j < K) ? row[k0 + j] : 0.f;
+  }
+}
+
+// acc[t] += A(tile t, k-step s) . B for the first nt tiles; A fragment: lane (r, h) = row 32 t + r, k 16 s + 8 h + j
+template <int PREC, int NT>
+__device__ __forceinline__ void mma_step(const ChainLayer& Ly, int kp, int s, int r, int h, int nt,
+                                         floatx16 (&acc)[NT], const bf16x8& bh, const bf16x8& bl) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (t < nt) {
+      const int64_t off = (int64_t)(32 * t + r) * kp + 16 * s + 8 * h;
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Ly.a_hi + off);
+      bf16x8 al = ah;
+      if constexpr (PREC == 2) al = *reinterpret_cast<const bf16x8*>(Ly.a_lo + off);
+      mma<PREC>(acc[t], ah, al, bh, bl);
+    }
+  }
+}
+
+// Epilogue in place.  Lane (m, h): tile t, register 4 g + i holds unit n = 32 t + 8 g + 4 h + i of data row m.
+template <int NT, bool BWD>
+__device__ __forceinline__ void epilogue(floatx16 (&acc)[NT], const ChainLayer& Ly, int nt, int64_t m, int64_t mc,
+                                         bool mval, bool only_col0, int h, float beta, float thr) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (t >= nt) continue;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int n0 = 32 * t + 8 * g + 4 * h;
+      float ax[4] = {0.f, 0.f, 0.f, 0.f};
+      if (BWD && Ly.aux != nullptr) {
+        const float* ar = Ly.aux + mc * Ly.ldaux;
+        if (n0 + 4 <= Ly.N) {
+          const float4 q = *reinterpret_cast<const float4*>(ar + n0);
+          ax[0] = q.x; ax[1] = q.y; ax[2] = q.z; ax[3] = q.w;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ax[i] = (n0 + i < Ly.N) ? ar[n0 + i] : 0.f;
+        }
+      }
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + i;
+        float x = acc[t][4 * g + i];
+        if constexpr (!BWD) {
+          if (Ly.bias != nullptr && n < Ly.N) x += Ly.bias[n];
+          x = mms::act_fwd_fast(Ly.act, x, beta, thr);
+        } else {
+          if (Ly.aux != nullptr) x *= act_grad_out(Ly.act, ax[i], beta, thr);
+        }
+        acc[t][4 * g + i] = x;
+        v[i] = x;
+      }
+      if (Ly.out != nullptr && mval) {
+        float* orow = Ly.out + m * Ly.ldo;
+        if (only_col0) {
+          if (n0 == 0) orow[0] = v[0];
+        } else if (n0 + 4 <= Ly.N) {
+          *reinterpret_cast<float4*>(orow + n0) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (n0 + i < Ly.N) orow[n0 + i] = v[i];
+        }
+      }
+    }
+  }
+}
+
+// accumulator tiles -> next layer's B fragments (k-step 2 t + s = registers 8 s .. 8 s + 7 of tile t)
+template <int PREC, int NT>
+__device__ __forceinline__ void to_b(const floatx16 (&acc)[NT], bf16x8 (&bh)[2 * NT], bf16x8 (&bl)[2 * NT]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = acc[t][8 * s + j];
+      split8<PREC>(v, bh[2 * t + s], bl[2 * t + s]);
+    }
+  }
+}
+
+template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD>
+__global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t m0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 32;
+  if (m0 >= a.M) return;
+  const int64_t m = m0 + r;
+  const bool mval = m < a.M;
+  const int64_t mc = mval ? m : a.M - 1;
+  const bool rowfull = m < a.rows_full;
+  const bool anyfull = m0 < a.rows_full;  // wave-uniform
+  const floatx16 zero = {};
+
+  // ---- layer 0: B operand from memory, natural k order
+  floatx16 acc0[NT0];
+#pragma unroll
+  for (int t = 0; t < NT0; ++t) acc0[t] = zero;
+  {
+    const float* xr = a.X + mc * a.ldx;
+    const float* xa = (BWD && a.xaux != nullptr) ? a.xaux + mc * a.ldxaux : nullptr;
+    float* xo = (BWD && a.xout != nullptr && mval) ? a.xout + m * a.ldxout : nullptr;
+    const int ksn = (BWD && !anyfull) ? 1 : KS0;
+#pragma unroll
+    for (int s = 0; s < KS0; ++s) {
+      if (s < ksn) {
+        const int k0 = 16 * s + 8 * h;
+        float v[8];
+        load8(xr, k0, a.K0, v);
+        if constexpr (BWD) {
+          if (!rowfull) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (k0 + j > 0) v[j] = 0.f;
+          }
+          if (xa != nullptr) {
+            float w[8];
+            load8(xa, k0, a.K0, w);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] *= act_grad_out(a.xact, w[j], a.beta, a.thr);
+          }
+          if (xo != nullptr) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (k0 + j < a.K0) xo[k0 + j] = v[j];
+          }
+        }
+        bf16x8 bh, bl;
+        split8<PREC>(v, bh, bl);
+        mma_step<PREC, NT0>(a.L[0], 16 * KS0, s, r, h, NT0, acc0, bh, bl);
+      }
+    }
+  }
+  epilogue<NT0, BWD>(acc0, a.L[0], NT0, m, mc, mval, false, h, a.beta, a.thr);
+  bf16x8 b1h[2 * NT0], b1l[2 * NT0];
+  to_b<PREC, NT0>(acc0, b1h, b1l);
+
+  // ---- layer 1: B operand from layer 0's registers
+  floatx16 acc1[NT1];
+#pragma unroll
+  for (int t = 0; t < NT1; ++t) acc1[t] = zero;
+#pragma unroll
+  for (int s = 0; s < 2 * NT0; ++s) mma_step<PREC, NT1>(a.L[1], 32 * NT0, s, r, h, NT1, acc1, b1h[s], b1l[s]);
+  epilogue<NT1, BWD>(acc1, a.L[1], NT1, m, mc, mval, false, h, a.beta, a.thr);
+  bf16x8 b2h[2 * NT1], b2l[2 * NT1];
+  to_b<PREC, NT1>(acc1, b2h, b2l);
+
+  // ---- layer 2 (forward: SDF tap-only waves need only the sdf column tile)
+  floatx16 acc2[NT2];
+#pragma unroll
+  for (int t = 0; t < NT2; ++t) acc2[t] = zero;
+  const int nt2 = (!BWD && !anyfull) ? 1 : NT2;
+#pragma unroll
+  for (int s = 0; s < 2 * NT1; ++s) mma_step<PREC, NT2>(a.L[2], 32 * NT1, s, r, h, nt2, acc2, b2h[s], b2l[s]);
+  epilogue<NT2, BWD>(acc2, a.L[2], nt2, m, mc, mval, !BWD && !rowfull, h, a.beta, a.thr);
+}
+
+template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD>
+void launch_chain(const ChainArgs& a, hipStream_t s) {
+  const int64_t waves = (a.M + 31) / 32;
+  const unsigned blocks = (unsigned)((waves + 3) / 4);
+  hipLaunchKernelGGL((chain_kernel<PREC, KS0, NT0, NT1, NT2, BWD>), dim3(blocks), dim3(256), 0, s, a);
+}
+
+// the chains of the SDF and radiance fields (ks0 = ceil(K0 / 16), nt_l = ceil(N_l / 32))
+template <int PREC>
+bool dispatch_chain(int ks0, int nt0, int nt1, int nt2, bool bwd, const ChainArgs& a, hipStream_t s) {
+  if (!bwd && ks0 == 5 && nt0 == 8 && nt1 == 8 && nt2 == 9) launch_chain<PREC, 5, 8, 8, 9, false>(a, s);
+  else if (!bwd && ks0 == 20 && nt0 == 8 && nt1 == 8 && nt2 == 8) launch_chain<PREC, 20, 8, 8, 8, false>(a, s);
+  else if (bwd && ks0 == 17 && nt0 == 8 && nt1 == 8 && nt2 == 3) launch_chain<PREC, 17, 8, 8, 3, true>(a, s);
+  else if (bwd && ks0 == 16 && nt0 == 8 && nt1 == 8 && nt2 == 10) launch_chain<PREC, 16, 8, 8, 10, true>(a, s);
+  else return false;
+  return true;
+}
+
+// perm(q): swap bits 2 and 3 of the in-step column (units 0-3, 8-11, 4-7, 12-15 of a register-fed k-step)
+__device__ __forceinline__ int64_t perm_col(int64_t c) {
+  const int64_t q = c & 15;
+  return (c & ~(int64_t)15) | (q & 3) | ((q & 4) << 1) | ((q & 8) >> 1);
+}
+
+__global__ void pack_kernel(const float* __restrict__ W, int64_t N, int64_t K, int64_t ldw, int transpose,
+                            int permute, int64_t rows, int64_t cols, __bf16* __restrict__ hi, __bf16* __restrict__ lo) {
+  const int64_t total = rows * cols;
+  const int64_t R = transpose ? K : N, C = transpose ? N : K;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / cols, c = i - row * cols;
+    const int64_t src = permute ? perm_col(c) : c;
+    float v = 0.f;
+    if (row < R && src < C) v = transpose ? W[src * ldw + row] : W[row * ldw + src];
+    const __bf16 b = (__bf16)v;
+    hi[i] = b;
+    if (lo != nullptr) lo[i] = (__bf16)(v - (float)b);
+  }
+}
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+MMS_EXPORT int mms_mlp_pack(const float* W, int64_t N, int64_t K, int64_t ldw, int transpose, int permute,
+                            int64_t rows, int64_t cols, void* hi, void* lo, void* stream) {
+  const char* fn = "mms_mlp_pack";
+  MMS_REQUIRE(N > 0 && K > 0 && ldw >= K, fn, "bad weight shape");
+  MMS_REQUIRE(rows >= (transpose ? K : N) && cols >= (transpose ? N : K), fn, "packed image smaller than the weight");
+  MMS_REQUIRE(rows % 32 == 0 && cols % 16 == 0, fn, "packed image must be [32 x tiles][16 x k-steps]");
+  MMS_REQUIRE(W && hi, fn, "null pointer");
+  hipLaunchKernelGGL(pack_kernel, dim3(mms::grid_for(rows * cols, 256, 4096)), dim3(256), 0, mms::as_stream(stream), W,
+                     N, K, ldw, transpose, permute, rows, cols, reinterpret_cast<__bf16*>(hi),
+                     reinterpret_cast<__bf16*>(lo));
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx, int K0, int64_t M,
+                             int64_t rows_full, const float* xaux, int64_t ldxaux, int xact, float* xout,
+                             int64_t ldxout, const void* const* a_hi, const void* const* a_lo,
+                             const float* const* bias, const float* const* aux, const int64_t* ldaux,
+                             float* const* out, const int64_t* ldo, const int* N, const int* act, float beta,
+                             float thr, void* stream) {
+  const char* fn = "mms_mlp_chain";
+  MMS_REQUIRE(prec == 1 || prec == 2, fn, "prec must be 1 (bf16) or 2 (split bf16x3)");
+  MMS_REQUIRE(M >= 0 && K0 > 0, fn, "bad shape");
+  if (M == 0) return 0;
+  MMS_REQUIRE(X && a_hi && N && act && out && ldo, fn, "null pointer");
+  MMS_REQUIRE(aligned16(X) && ldx % 4 == 0 && ldx >= K0, fn, "input rows must be 16-B aligned");
+  MMS_REQUIRE(!backward || xaux == nullptr || (aligned16(xaux) && ldxaux % 4 == 0), fn, "xaux rows must be 16-B aligned");
+  ChainArgs a;
+  a.X = X; a.ldx = ldx; a.K0 = K0; a.M = M; a.rows_full = rows_full < 0 ? M : rows_full;
+  a.xaux = backward ? xaux : nullptr; a.ldxaux = ldxaux; a.xact = xact;
+  a.xout = backward ? xout : nullptr; a.ldxout = ldxout;
+  a.beta = beta; a.thr = thr;
+  int nt[3];
+  for (int l = 0; l < 3; ++l) {
+    MMS_REQUIRE(a_hi[l] != nullptr && N[l] > 0, fn, "missing layer weights");
+    MMS_REQUIRE(prec == 1 || (a_lo && a_lo[l] != nullptr), fn, "split bf16x3 needs the residual images");
+    MMS_REQUIRE(act[l] >= 0 && act[l] <= 3, fn, "bad activation id");
+    ChainLayer& L = a.L[l];
+    L.a_hi = reinterpret_cast<const __bf16*>(a_hi[l]);
+    L.a_lo = prec == 2 ? reinterpret_cast<const __bf16*>(a_lo[l]) : nullptr;
+    L.bias = (!backward && bias) ? bias[l] : nullptr;
+    L.aux = (backward && aux) ? aux[l] : nullptr;
+    L.ldaux = (backward && ldaux) ? ldaux[l] : 0;
+    MMS_REQUIRE(L.aux == nullptr || (aligned16(L.aux) && L.ldaux % 4 == 0), fn, "aux rows must be 16-B aligned");
+    L.out = out[l];
+    L.ldo = ldo[l];
+    MMS_REQUIRE(L.out == nullptr || (aligned16(L.out) && L.ldo % 4 == 0 && L.ldo >= N[l]), fn,
+                "output rows must be 16-B aligned");
+    L.N = N[l];
+    L.act = act[l];
+    nt[l] = (N[l] + 31) / 32;
+  }
+  const int ks0 = (K0 + 15) / 16;
+  // register-fed layers consume exactly the previous layer's padded unit count
+  hipStream_t s = mms::as_stream(stream);
+  const bool ok = prec == 1 ? dispatch_chain<1>(ks0, nt[0], nt[1], nt[2], backward != 0, a, s)
+                            : dispatch_chain<2>(ks0, nt[0], nt[1], nt[2], backward != 0, a, s);
+  MMS_REQUIRE(ok, fn, "unsupported chain shape (SDF 71-256-256-257 and radiance 317-256-256-256 chains only)");
+  return mms::check_launch(fn);
+}

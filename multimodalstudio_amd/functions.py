@@ -201,6 +201,124 @@ class MLPRun:
         return dx, grads
 
 
+class ChainRun:
+    """A weight-normed 3-layer MLP on the fused chain kernel (mms_mlp_chain: all three layers in one launch, bf16 or
+    split-bf16x3 operands) plus the weight-gradient GEMMs.  Serves the SDF (71-256-256-257) and radiance
+    (317-256-256-256) MLPs in the bf16 precision modes; the fp32 parity mode keeps MLPRun.
+
+    ``rows_full``: rows >= rows_full only need output column 0 (the SDF's tap rows, surface_model.py:137-153)."""
+
+    def __init__(self, params: Sequence[torch.Tensor], acts: Sequence[Tuple[int, float, float]], prec: int):
+        if prec not in (1, 2):
+            raise ValueError("the fused chain runs the bf16 (1) and split-bf16x3 (2) modes")
+        self.params, self.acts, self.prec = list(params), list(acts), int(prec)
+        self.beta, self.thr = float(acts[0][1]), float(acts[0][2])
+
+    def _pack(self, W, rows: int, cols: int, transpose: bool, permute: bool):
+        hi = torch.empty(rows, cols, dtype=torch.bfloat16, device=W.device)
+        lo = torch.empty_like(hi) if self.prec == 2 else None
+        N, K = W.shape
+        _lib.call("mms_mlp_pack", W.data_ptr(), N, K, W.stride(0), int(transpose), int(permute), rows, cols,
+                  hi.data_ptr(), _p(lo), _s())
+        return hi, lo
+
+    def _chain(self, backward: bool, X, K0: int, rows_full: int, packs, bias, aux, outs, Ns, acts,
+               xaux=None, xact: int = 0, xout=None):
+        VP = ctypes.c_void_p * 3
+        his = VP(*[p[0].data_ptr() for p in packs])
+        los = VP(*[(p[1].data_ptr() if p[1] is not None else None) for p in packs])
+        bs = VP(*[(b.data_ptr() if b is not None else None) for b in bias])
+        auxs = VP(*[(a.data_ptr() if a is not None else None) for a in aux])
+        ldaux = (ctypes.c_int64 * 3)(*[(a.stride(0) if a is not None else 0) for a in aux])
+        os_ = VP(*[(o.data_ptr() if o is not None else None) for o in outs])
+        ldo = (ctypes.c_int64 * 3)(*[(o.stride(0) if o is not None else 0) for o in outs])
+        ns = (ctypes.c_int * 3)(*Ns)
+        ac = (ctypes.c_int * 3)(*acts)
+        cast = lambda a: ctypes.cast(a, ctypes.c_void_p)
+        _lib.call("mms_mlp_chain", self.prec, int(backward), X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
+                  _p(xaux), 0 if xaux is None else xaux.stride(0), int(xact), _p(xout),
+                  0 if xout is None else xout.stride(0), cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux),
+                  cast(os_), cast(ldo), cast(ns), cast(ac), self.beta, self.thr, _s())
+
+    def forward(self, x: torch.Tensor, keep: bool, rows_full: Optional[int] = None) -> torch.Tensor:
+        """x [M, K0] (16-B aligned rows); returns the last layer's output [M, N2] (row stride rounded to 4)."""
+        M, K0 = x.shape
+        dev = x.device
+        self.x = x
+        self.Ws, self.norms = [], []
+        for l in range(3):
+            g, v, _ = self.params[3 * l: 3 * l + 3]
+            N, K = v.shape
+            W = _alloc(N, K, dev)
+            nrm = torch.empty(N, device=dev)
+            weight_norm_fwd(g.reshape(-1), v, W, nrm)
+            self.Ws.append(W)
+            self.norms.append(nrm)
+        Ns = [W.shape[0] for W in self.Ws]
+        nt = [(n + 31) // 32 for n in Ns]
+        packs = [self._pack(self.Ws[0], 32 * nt[0], 16 * ((K0 + 15) // 16), False, False),
+                 self._pack(self.Ws[1], 32 * nt[1], 32 * nt[0], False, True),
+                 self._pack(self.Ws[2], 32 * nt[2], 32 * nt[1], False, True)]
+        Y = [_alloc(M, Ns[0], dev) if keep else None, _alloc(M, Ns[1], dev) if keep else None, _alloc(M, Ns[2], dev)]
+        self.rows_full = M if rows_full is None else int(rows_full)
+        self._chain(False, x, K0, self.rows_full, packs, [self.params[3 * l + 2] for l in range(3)], [None] * 3, Y,
+                    Ns, [a[0] for a in self.acts])
+        self.Y = Y
+        return Y[2]
+
+    def backward(self, dy: torch.Tensor) -> torch.Tensor:
+        """dy [M, N2] (rows >= rows_full: column 0 only); accumulates the parameter gradients (grad_target) and
+        returns dx [M, K0]."""
+        x, Y = self.x, self.Y
+        M, K0 = x.shape
+        dev = x.device
+        Ns = [W.shape[0] for W in self.Ws]
+        N0, N1, N2 = Ns
+        acts = [a[0] for a in self.acts]
+        # backward chain: f2^T (natural: B = dy from memory), f1^T, f0^T (register-fed, permuted)
+        packs = [self._pack(self.Ws[2], 32 * ((N1 + 31) // 32), 16 * ((N2 + 15) // 16), True, False),
+                 self._pack(self.Ws[1], 32 * ((N0 + 31) // 32), 32 * ((N1 + 31) // 32), True, True),
+                 self._pack(self.Ws[0], 32 * ((K0 + 31) // 32), 32 * ((N0 + 31) // 32), True, True)]
+        dZ2 = _alloc(M, N2, dev) if acts[2] != 0 else None
+        dZ1, dZ0, dx = _alloc(M, N1, dev), _alloc(M, N0, dev), _alloc(M, K0, dev)
+        dy = dy if dy.stride(1) == 1 and dy.stride(0) % 4 == 0 else _copy_aligned(dy)
+        self._chain(True, dy, N2, self.rows_full, packs, [None] * 3, [Y[1], Y[0], None], [dZ1, dZ0, dx],
+                    [N1, N0, K0], [acts[1], acts[0], 0], xaux=Y[2] if acts[2] != 0 else None, xact=acts[2],
+                    xout=dZ2)
+        dZ = [dZ0, dZ1, dZ2 if dZ2 is not None else dy]
+        Xin = [x, Y[0], Y[1]]
+        rf = self.rows_full
+        for l in range(3):
+            g, v, b = self.params[3 * l: 3 * l + 3]
+            N, K = v.shape
+            gt, vt, bt = grad_target(g), grad_target(v), grad_target(b)
+            if gt is None and vt is None and bt is None:
+                continue
+            dW = torch.zeros(N, K, device=dev)
+            db = bt if bt is not None else torch.zeros(N, device=dev)
+            A, B = dZ[l], Xin[l]
+            tiles = ((N + 127) // 128) * ((K + 127) // 128)
+            if l == 2 and rf < M:
+                # rows past rows_full carry only the output column 0
+                gemm(TN, N, K, rf, A, A.stride(0), B, B.stride(0), dW, K, accumulate=True,
+                     splits=_splits_for(rf, tiles), prec=self.prec, colsum=db)
+                gemm(TN, 1, K, M - rf, A[rf:], A.stride(0), B[rf:], B.stride(0), dW, K, accumulate=True,
+                     splits=_splits_for(M - rf, 2), prec=self.prec, colsum=db)
+            else:
+                gemm(TN, N, K, M, A, A.stride(0), B, B.stride(0), dW, K, accumulate=True,
+                     splits=_splits_for(M, tiles), prec=self.prec, colsum=db)
+            weight_norm_bwd(g.reshape(-1), v, self.norms[l], dW, gt.reshape(-1) if gt is not None else
+                            torch.zeros(N, device=dev), vt if vt is not None else torch.zeros(N, K, device=dev))
+        self.Y = self.x = None
+        return dx
+
+
+def _copy_aligned(t: torch.Tensor) -> torch.Tensor:
+    out = _alloc(t.shape[0], t.shape[1], t.device)
+    out.copy_(t)
+    return out
+
+
 # ------------------------------------------------------------------------------------------------
 # surface field (SDF + taps)
 # ------------------------------------------------------------------------------------------------
@@ -224,20 +342,16 @@ class SurfaceFunction(torch.autograd.Function):
         d32 = float(torch.tensor(delta, dtype=torch.float32))
         _lib.call("mms_geo_input_fwd", pos.data_ptr(), 3, M, 4, d32, 6, X.data_ptr(), X.stride(0), _s())
         grid_fwd(grid, X, X.stride(0), 5 * M, table, active, X, 39)
-        # hidden layers over all 5M rows; the output layer (257 wide: sdf + geo feature) only needs the sdf
-        # column on the 4M tap rows (surface_model.py:137-153 uses the taps' sdf alone)
-        run = MLPRun(params[:-3], SDF_ACTS[:-1], PRECISION["sdf"])
-        H = run.forward(X, keep=True)
-        g3, v3, b3 = params[-3:]
-        N3, K3 = v3.shape
-        W3 = _alloc(N3, K3, dev)
-        n3 = torch.empty(N3, device=dev)
-        weight_norm_fwd(g3.reshape(-1), v3, W3, n3)
-        out = _alloc(5 * M, N3, dev)
         prec = PRECISION["sdf"]
-        gemm(NT, M, N3, K3, H, H.stride(0), W3, W3.stride(0), out, out.stride(0), bias=b3, prec=prec)
-        gemm(NT, 4 * M, 1, K3, H[M:], H.stride(0), W3, W3.stride(0), out[M:], out.stride(0), bias=b3, prec=prec)
-        G = N3 - 1
+        ctx.chain = None
+        if prec != 0:
+            # bf16 modes: the whole 3-layer chain in one kernel; tap rows keep only the sdf column
+            chain = ChainRun(params, SDF_ACTS, prec)
+            out = chain.forward(X, keep=True, rows_full=M)
+            ctx.chain = chain
+        else:
+            out = _sdf_mlp_unfused(ctx, X, M, params, dev)
+        G = out.shape[1] - 1
         four_delta = float(torch.tensor(4.0 * delta, dtype=torch.float32))
         delta_sq = float(torch.tensor(delta ** 2, dtype=torch.float32))
         grads = torch.empty(M, 3, device=dev)
@@ -250,7 +364,6 @@ class SurfaceFunction(torch.autograd.Function):
         ctx.grid, ctx.active, ctx.M, ctx.G = grid, active, M, G
         ctx.table = table          # the Parameter itself: its .grad is accumulated in place
         ctx.four_delta, ctx.delta_sq = four_delta, delta_sq
-        ctx.run, ctx.H, ctx.W3, ctx.n3, ctx.prec = run, H, W3, n3, prec
         ctx.X = X
         ctx.save_for_backward(pos, table, grads, *params)
         return sdf, geo, grads, hess, normals
@@ -272,31 +385,11 @@ class SurfaceFunction(torch.autograd.Function):
             dout[:M, 1:] = 0.0
         need_table = ctx.needs_input_grad[1]
         need_pos = ctx.needs_input_grad[0]
-        # output layer: centre rows (257 columns) and tap rows (sdf column) as two GEMM pairs
-        H, W3, prec = ctx.H, ctx.W3, ctx.prec
-        g3, v3, b3 = params[-3:]
-        N3, K3 = v3.shape
-        gt, vt, bt = grad_target(g3), grad_target(v3), grad_target(b3)
-        if gt is not None or vt is not None or bt is not None:
-            dW3 = torch.zeros(N3, K3, device=dev)
-            db3 = bt if bt is not None else torch.zeros(N3, device=dev)
-            gemm(TN, N3, K3, M, dout, dout.stride(0), H, H.stride(0), dW3, K3, accumulate=True,
-                 splits=_splits_for(M, 6), prec=prec, colsum=db3)
-            gemm(TN, 1, K3, 4 * M, dout[M:], dout.stride(0), H[M:], H.stride(0), dW3, K3, accumulate=True,
-                 splits=_splits_for(4 * M, 2), prec=prec, colsum=db3)
-            weight_norm_bwd(g3.reshape(-1), v3, ctx.n3, dW3, gt.reshape(-1) if gt is not None else
-                            torch.zeros(N3, device=dev), vt if vt is not None else torch.zeros(N3, K3, device=dev))
-        # dZ of the last hidden layer = (dout W3) * softplus'(Z) -- the activation gradient fused as aux
-        run = ctx.run
-        pa, pbeta, pthr = SDF_ACTS[-2]
-        Zl = run.Zs[-1]
-        dZ = _alloc(5 * M, K3, dev)
-        gemm(NN, M, K3, N3, dout, dout.stride(0), W3, W3.stride(0), dZ, dZ.stride(0), aux=Zl, ldaux=Zl.stride(0),
-             dact=pa, beta=pbeta, thr=pthr, prec=prec)
-        gemm(NN, 4 * M, K3, 1, dout[M:], dout.stride(0), W3, W3.stride(0), dZ[M:], dZ.stride(0), aux=Zl[M:],
-             ldaux=Zl.stride(0), dact=pa, beta=pbeta, thr=pthr, prec=prec)
-        dX, pgrads = run.backward(dZ, need_dx=True, pre_activated=True)
-        pgrads = list(pgrads) + [None, None, None]
+        if ctx.chain is not None:
+            dX = ctx.chain.backward(dout)
+            pgrads = [None] * len(params)
+        else:
+            dX, pgrads = _sdf_mlp_unfused_bwd(ctx, dout, params, dev)
         X = ctx.X
         K0 = X.stride(0)
         dtable = grad_target(ctx.table) if need_table else None
@@ -307,8 +400,55 @@ class SurfaceFunction(torch.autograd.Function):
             dpos = torch.zeros(M, 3, device=dev)
             _lib.call("mms_geo_input_bwd", X.data_ptr(), K0, dX.data_ptr(), dX.stride(0), dP.data_ptr(), 3, M, 4, 6,
                       dpos.data_ptr(), 3, _s())
-        ctx.run = ctx.H = ctx.W3 = ctx.X = ctx.table = None
+        ctx.run = ctx.H = ctx.W3 = ctx.X = ctx.table = ctx.chain = None
         return (dpos, None, None, None, None, *pgrads)
+
+
+def _sdf_mlp_unfused(ctx, X, M, params, dev):
+    """fp32 parity mode: hidden layers over all 5M rows; the output layer (257 wide: sdf + geo feature) only
+    needs the sdf column on the 4M tap rows (surface_model.py:137-153 uses the taps' sdf alone)."""
+    run = MLPRun(params[:-3], SDF_ACTS[:-1], PRECISION["sdf"])
+    H = run.forward(X, keep=True)
+    g3, v3, b3 = params[-3:]
+    N3, K3 = v3.shape
+    W3 = _alloc(N3, K3, dev)
+    n3 = torch.empty(N3, device=dev)
+    weight_norm_fwd(g3.reshape(-1), v3, W3, n3)
+    out = _alloc(5 * M, N3, dev)
+    prec = PRECISION["sdf"]
+    gemm(NT, M, N3, K3, H, H.stride(0), W3, W3.stride(0), out, out.stride(0), bias=b3, prec=prec)
+    gemm(NT, 4 * M, 1, K3, H[M:], H.stride(0), W3, W3.stride(0), out[M:], out.stride(0), bias=b3, prec=prec)
+    ctx.run, ctx.H, ctx.W3, ctx.n3, ctx.prec = run, H, W3, n3, prec
+    return out
+
+
+def _sdf_mlp_unfused_bwd(ctx, dout, params, dev):
+    M = ctx.M
+    # output layer: centre rows (257 columns) and tap rows (sdf column) as two GEMM pairs
+    H, W3, prec = ctx.H, ctx.W3, ctx.prec
+    g3, v3, b3 = params[-3:]
+    N3, K3 = v3.shape
+    gt, vt, bt = grad_target(g3), grad_target(v3), grad_target(b3)
+    if gt is not None or vt is not None or bt is not None:
+        dW3 = torch.zeros(N3, K3, device=dev)
+        db3 = bt if bt is not None else torch.zeros(N3, device=dev)
+        gemm(TN, N3, K3, M, dout, dout.stride(0), H, H.stride(0), dW3, K3, accumulate=True,
+             splits=_splits_for(M, 6), prec=prec, colsum=db3)
+        gemm(TN, 1, K3, 4 * M, dout[M:], dout.stride(0), H[M:], H.stride(0), dW3, K3, accumulate=True,
+             splits=_splits_for(4 * M, 2), prec=prec, colsum=db3)
+        weight_norm_bwd(g3.reshape(-1), v3, ctx.n3, dW3, gt.reshape(-1) if gt is not None else
+                        torch.zeros(N3, device=dev), vt if vt is not None else torch.zeros(N3, K3, device=dev))
+    # dZ of the last hidden layer = (dout W3) * softplus'(Z) -- the activation gradient fused as aux
+    run = ctx.run
+    pa, pbeta, pthr = SDF_ACTS[-2]
+    Zl = run.Zs[-1]
+    dZ = _alloc(5 * M, K3, dev)
+    gemm(NN, M, K3, N3, dout, dout.stride(0), W3, W3.stride(0), dZ, dZ.stride(0), aux=Zl, ldaux=Zl.stride(0),
+         dact=pa, beta=pbeta, thr=pthr, prec=prec)
+    gemm(NN, 4 * M, K3, 1, dout[M:], dout.stride(0), W3, W3.stride(0), dZ[M:], dZ.stride(0), aux=Zl[M:],
+         ldaux=Zl.stride(0), dact=pa, beta=pbeta, thr=pthr, prec=prec)
+    dX, pgrads = run.backward(dZ, need_dx=True, pre_activated=True)
+    return dX, list(pgrads) + [None, None, None]
 
 
 def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> torch.Tensor:
@@ -319,6 +459,10 @@ def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> to
     X = _alloc(M, K0, dev)
     _lib.call("mms_geo_input_fwd", pos.data_ptr(), pos.stride(0), M, 0, 0.0, 6, X.data_ptr(), X.stride(0), _s())
     grid_fwd(grid, X, X.stride(0), M, table, active, X, 39)
+    if PRECISION["sdf"] != 0:
+        # fused chain, no hidden-layer stores, only the sdf column tile of the output layer (rows_full = 0)
+        out = ChainRun(params, SDF_ACTS, PRECISION["sdf"]).forward(X, keep=False, rows_full=0)
+        return out[:, 0].contiguous()      # the sampler kernel reads the sdf rows densely
     # only the sdf column of the last layer is needed
     last = list(params[-3:])
     g, v, b = last
@@ -351,7 +495,8 @@ class RadianceFunction(torch.autograd.Function):
         _lib.call("mms_rad_input_fwd", pos.data_ptr(), 3, dirs.data_ptr(), normals.data_ptr(), geo.data_ptr(),
                   geo.stride(0), M, S, G, X.data_ptr(), X.stride(0), _s())
         grid_fwd(grid, X, X.stride(0), M, table, active, X, 29 + G)
-        run = MLPRun(params, RAD_ACTS, PRECISION["radiance"])
+        prec = PRECISION["radiance"]
+        run = ChainRun(params, RAD_ACTS, prec) if prec != 0 else MLPRun(params, RAD_ACTS, prec)
         feat = run.forward(X, keep=True)
         ctx.run, ctx.X, ctx.grid, ctx.active, ctx.S, ctx.G = run, X, grid, active, S, G
         ctx.table = table
@@ -364,7 +509,11 @@ class RadianceFunction(torch.autograd.Function):
         M, S, G = pos.shape[0], ctx.S, ctx.G
         R = M // S
         dev = pos.device
-        dX, pgrads = ctx.run.backward(dfeat.contiguous(), need_dx=True)
+        if isinstance(ctx.run, ChainRun):
+            dX = ctx.run.backward(dfeat.contiguous())
+            pgrads = [None] * len(params)
+        else:
+            dX, pgrads = ctx.run.backward(dfeat.contiguous(), need_dx=True)
         X = ctx.X
         K0 = X.stride(0)
         dtable = grad_target(ctx.table) if ctx.needs_input_grad[4] else None
@@ -706,6 +855,18 @@ class ColliderFunction(torch.autograd.Function):
         return do, dd, None
 
 
+def compact_padded(mask: torch.Tensor, cap: int):
+    """Fixed-capacity compaction for static-shape (graph-captured) steps, no host read: (gather index [cap] -- rows
+    past the hit count repeat the first hit ray --, scatter index [cap] -- N for those padding rows --, device hit
+    count [1])."""
+    N = mask.shape[0]
+    idx = torch.empty(N, dtype=torch.int64, device=mask.device)
+    sidx = torch.empty(cap, dtype=torch.int64, device=mask.device)
+    cnt = torch.empty(1, dtype=torch.int64, device=mask.device)
+    _lib.call("mms_compact_padded", mask.data_ptr(), N, cap, idx.data_ptr(), sidx.data_ptr(), cnt.data_ptr(), _s())
+    return idx[:cap], sidx, cnt
+
+
 def compact(mask: torch.Tensor) -> torch.Tensor:
     """Order-preserving indices of mask != 0 (int64); one device->host read of the count."""
     N = mask.shape[0]
@@ -778,6 +939,43 @@ class GeoLossFunction(torch.autograd.Function):
             dg_list.append(dg)
             dh_list.append(dh)
         return (*dg_list, *dh_list)
+
+
+class GeoLossMaskedFunction(torch.autograd.Function):
+    """GeoLossFunction over fixed-capacity batches: modality m's rows >= counts[m] * S are padding and carry no loss,
+    and the mean runs over the true rows (1 / total computed on the device from the hit counts)."""
+
+    @staticmethod
+    def forward(ctx, S: int, counts, *tensors):
+        n = len(tensors) // 2
+        grads, hess = tensors[:n], tensors[n:]
+        dev = grads[0].device
+        tot = torch.stack([c.reshape(()) for c in counts]).sum() * S
+        inv = (1.0 / tot.clamp_min(1).to(torch.float32)).reshape(1)
+        eik = torch.zeros((), device=dev)
+        curv = torch.zeros((), device=dev)
+        ts = [t.contiguous() for t in tensors]
+        for g, h, c in zip(ts[:n], ts[n:], counts):
+            _lib.call("mms_geo_loss_fwd_masked", g.data_ptr(), h.data_ptr(), g.shape[0], S, c.data_ptr(),
+                      inv.data_ptr(), eik.data_ptr(), curv.data_ptr(), _s())
+        ctx.save_for_backward(inv, *ts)
+        ctx.counts, ctx.S, ctx.n = list(counts), S, n
+        return eik, curv
+
+    @staticmethod
+    def backward(ctx, deik, dcurv):
+        inv, *ts = ctx.saved_tensors
+        n, S = ctx.n, ctx.S
+        dg_list, dh_list = [], []
+        for g, h, c in zip(ts[:n], ts[n:], ctx.counts):
+            dg = torch.zeros_like(g)
+            dh = torch.zeros_like(h)
+            _lib.call("mms_geo_loss_bwd_masked", g.data_ptr(), h.data_ptr(), g.shape[0], S, c.data_ptr(),
+                      inv.data_ptr(), _p(None if deik is None else deik.contiguous()), 1.0,
+                      _p(None if dcurv is None else dcurv.contiguous()), 1.0, dg.data_ptr(), dh.data_ptr(), _s())
+            dg_list.append(dg)
+            dh_list.append(dh)
+        return (None, None, *dg_list, *dh_list)
 
 
 class PolarizerFunction(torch.autograd.Function):

@@ -1,0 +1,216 @@
+"""Graph-captured training step: the whole of ``Trainer.train_step`` replayed as hipGraphs.
+
+The eager step issues ~470 kernel launches from Python (autograd nodes, ctypes calls, allocator work); on
+MI355X the GPU sat idle for about half of every step waiting for them (profiles/round1_fast_trace_summary.txt:
+busy 9.7 of 20.6 ms per step).  Here the step body -- pixel-value gather, ray generation with pose refinement,
+the model, losses, backward, grad-norm clip and AdamW -- is captured once with ``torch.cuda.graph``
+(hipStreamBeginCapture under ROCm) and replayed; per step the host only samples pixels (the reference's CPU
+generator, pixel_samplers.py:71-89), uploads them into static buffers and launches the graph.
+
+Static shapes.  The foreground batch is the set of rays that hit the unit sphere (scene_colliders.py:60-80,
+base_model.py:88-93); its size N_hit changes every step.  A replayable graph needs fixed sizes, so each
+modality's hit rays are compacted into a fixed-capacity batch of ``cap`` rows (BaseModel.forward(cap=...),
+``mms_compact_padded``): rows past the true count repeat the first hit ray (valid, finite inputs), scatter
+their composite into a dummy output row N that the loss never reads, and are skipped by the eikonal /
+curvature terms (``GeoLossMaskedFunction``), so every gradient they produce is exactly zero.  ``cap`` is the
+largest N_hit over the modalities rounded up to a granule (64 rays); one graph is kept per capacity, and the
+neighbouring capacities are captured together with the first one.  Choosing ``cap`` needs N_hit on the host:
+a collider pass on the step's rays (raygen + collider + compaction count, no autograd) and one small
+device->host read per step -- the step's only synchronisation.
+
+Scalars.  Values the kernels take by value are baked into a graph: the coarse-to-fine level, the tap delta,
+the cos-anneal ratio and the curvature-loss factor (feature_structures.py:97-108, surface_model.py:254-271,
+volume_rendering.py:227-230, schedulers.py:320-343).  They are part of the graph key; a step whose values
+differ from the previous step's runs eagerly (early in a 100k-step run some of them change every step), and a
+graph is captured once they hold still.  The AdamW scalars (learning-rate schedule, bias corrections) change
+every step and are read from a device buffer instead (``mms_adamw_dev``).
+
+Multi-GPU: the RCCL gradient all-reduce stays outside the graphs (forward/backward graph, all-reduce,
+optimizer graph), so each rank may replay a different capacity and no collective is ever captured.
+"""
+from __future__ import annotations
+
+import sys
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _lib
+from . import functions as fx
+from .pipeline import Trainer, compute_loss, curvature_factor, lr_factor, select_right_channel
+
+
+def bucket_capacity(counts, granule: int, n: int) -> int:
+    """Fixed foreground capacity for hit counts ``counts``: the largest, rounded up to ``granule``, at most n."""
+    c = max(counts)
+    return min(n, -(-c // granule) * granule)
+
+
+class GraphTrainer:
+    """Drive a ``pipeline.Trainer`` with graph-captured steps (see the module docstring)."""
+
+    def __init__(self, trainer: Trainer, granule: int = 64, neighbours: int = 2, ddp=None):
+        self.t = trainer
+        self.ddp = ddp
+        self.granule = int(granule)
+        self.neighbours = int(neighbours)
+        dev = trainer.device
+        n = trainer.cfg.num_rays_per_modality
+        self.n = n
+        mods = trainer.modalities
+        self.coords = {m: torch.zeros(n, 3, dtype=torch.int32, device=dev) for m in mods}
+        self.sel = {m: torch.zeros(n, dtype=torch.int64, device=dev) for m in mods}
+        self.h_coords = {m: torch.zeros(n, 3, dtype=torch.int32).pin_memory() for m in mods}
+        self.h_sel = {m: torch.zeros(n, dtype=torch.int64).pin_memory() for m in mods}
+        self.count_dev = torch.zeros(len(mods), dtype=torch.int64, device=dev)
+        self.count_host = torch.zeros(len(mods), dtype=torch.int64).pin_memory()
+        self.idx_scratch = torch.empty(n, dtype=torch.int64, device=dev)
+        self.side = torch.cuda.Stream(device=dev)
+        self.graphs: Dict[tuple, Tuple[torch.cuda.CUDAGraph, Optional[torch.cuda.CUDAGraph], tuple]] = {}
+        self.pool = None
+        self.last_sig = None
+        self.ran_eager = False
+        self.disabled: Optional[str] = None
+        self.stats = {"replays": 0, "eager": 0, "captures": 0}
+
+    # -- host side ---------------------------------------------------------------------------------
+    def scalar_signature(self) -> tuple:
+        """The by-value kernel scalars of the current step (the callbacks applied for t.step)."""
+        t = self.t
+        t.model.set_step(t.step, t.cfg.max_iters)
+        sm = t.model.surface_model
+        rg = t.model.radiance_model.radiance_field.base_field.feature_grid
+        return (sm.surface_field.field.feature_grid.active_levels, rg.active_levels,
+                float(sm.numerical_gradients_delta), float(sm.volume_rendering._cos_anneal_ratio),
+                float(curvature_factor(t.step, t.cfg.max_iters)))
+
+    def _stage_inputs(self):
+        """Host pixel sampling (reference RNG order) into pinned buffers, then async upload to the static ones."""
+        t = self.t
+        coords, sel = t.sampler.sample(t.frames)
+        for m in t.modalities:
+            self.h_coords[m].copy_(coords[m])
+            self.h_sel[m].copy_(sel[m].to(torch.int64))
+            self.coords[m].copy_(self.h_coords[m], non_blocking=True)
+            self.sel[m].copy_(self.h_sel[m], non_blocking=True)
+        return coords
+
+    @torch.no_grad()
+    def hit_counts(self):
+        """N_hit per modality for the staged rays: ray generation (current pose deltas) + collider + compaction
+        count, then one small device->host read (the step's only synchronisation)."""
+        t = self.t
+        dev = t.device
+        for i, m in enumerate(t.modalities):
+            mats = t.pose.matrices(m, dev)
+            o, d, _, _, _ = fx.RaysFunction.apply(mats, self.coords[m], t.cams[m], t.raygen.pixel_offset)
+            mask = fx.ColliderFunction.apply(o, d, 1.0)[4]
+            _lib.call("mms_compact", mask.data_ptr(), self.n, self.idx_scratch.data_ptr(),
+                      self.count_dev[i:i + 1].data_ptr(), fx._s())
+        self.count_host.copy_(self.count_dev, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        return [int(c) for c in self.count_host.tolist()]
+
+    # -- the captured work ---------------------------------------------------------------------------
+    def _targets(self):
+        t = self.t
+        return {m: t.images[m][self.sel[m], self.coords[m][:, 1].long(), self.coords[m][:, 2].long()]
+                for m in t.modalities}
+
+    def _forward_backward(self, cap: int):
+        t = self.t
+        targets = self._targets()
+        t.fields.zero_grad()
+        if t.poses is not None:
+            t.poses.zero_grad()
+        rays = t.raygen(self.coords)
+        outputs = t.model(rays, None, cap=cap)
+        if t.raw:
+            for m in t.modalities:
+                c = self.coords[m]
+                band = t.masks[m][c[:, 1].long(), c[:, 2].long()].long()[:, None]
+                outputs[m][m] = select_right_channel(outputs[m][m], band)
+        losses, total = compute_loss(outputs, targets, t.modalities, t.step)
+        total.backward()
+        return losses, total
+
+    def _optimizer(self):
+        t = self.t
+        t.fields.step_captured()
+        if t.poses is not None:
+            t.poses.step_captured()
+
+    def capture(self, key: tuple) -> None:
+        cap = key[0]
+        # thread-local capture mode when a process group is up: RCCL's watchdog thread queries events meanwhile
+        mode = "thread_local" if self.ddp is not None else "global"
+        torch.cuda.synchronize()
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1, pool=self.pool, capture_error_mode=mode):
+            out = self._forward_backward(cap)
+            if self.ddp is None:
+                self._optimizer()
+        if self.pool is None:
+            self.pool = g1.pool()
+        g2 = None
+        if self.ddp is not None:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2, pool=self.pool, capture_error_mode=mode):
+                self._optimizer()
+        self.graphs[key] = (g1, g2, out)
+        self.stats["captures"] += 1
+
+    # -- one training iteration ------------------------------------------------------------------
+    def eager_step(self, coords):
+        """Trainer.train_step on the already-staged inputs (dynamic shapes, no graph), on the side stream the
+        captures run on (lazy per-stream state is initialised before the first capture)."""
+        self.stats["eager"] += 1
+        self.ran_eager = True
+        cur = torch.cuda.current_stream()
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            losses, total, _ = self.t.train_step(coords, self._targets(), ddp=self.ddp)
+        cur.wait_stream(self.side)
+        return losses, total
+
+    def step(self):
+        """One training iteration; returns (losses, total) -- when replayed, the graph's output tensors (valid until
+        the next replay)."""
+        t = self.t
+        sig = self.scalar_signature()
+        coords = self._stage_inputs()
+        if self.disabled is not None:
+            return self.eager_step(coords)
+        counts = self.hit_counts()
+        stable = sig == self.last_sig
+        self.last_sig = sig
+        if min(counts) == 0 or not (stable and self.ran_eager):
+            # a modality without hits, scalars that changed this step, or nothing run yet: one eager step
+            return self.eager_step(coords)
+        cap = bucket_capacity(counts, self.granule, self.n)
+        key = (cap,) + sig
+        if key not in self.graphs:
+            try:
+                for k in [0] + [d for j in range(1, self.neighbours + 1) for d in (j, -j)]:
+                    c = min(cap + k * self.granule, self.n)
+                    if c >= self.granule or c == cap:
+                        kk = (c,) + sig
+                        if kk not in self.graphs:
+                            self.capture(kk)
+            except Exception as e:  # capture unsupported here: keep training eagerly
+                self.disabled = f"{type(e).__name__}: {e}"
+                print(f"[graphs] capture failed, eager steps from now on: {self.disabled}", file=sys.stderr)
+                torch.cuda.synchronize()
+                return self.eager_step(coords)
+        f = lr_factor(t.step, t.cfg.max_iters)
+        t.fields.load_hyper(f)
+        if t.poses is not None:
+            t.poses.load_hyper(f)
+        g1, g2, out = self.graphs[key]
+        g1.replay()
+        if self.ddp is not None:
+            self.ddp.allreduce_grads([t.fields] + ([t.poses] if t.poses is not None else []))
+            g2.replay()
+        t.step += 1
+        self.stats["replays"] += 1
+        return out

@@ -322,6 +322,14 @@ class RNG:
     background: Dict[str, torch.Tensor] = field(default_factory=dict)
 
 
+def _pad_rows(t: Optional[torch.Tensor], R: int) -> Optional[torch.Tensor]:
+    """Injected per-hit-ray uniforms padded with zeros to a fixed-capacity batch of R rows (padding rows' samples are
+    discarded)."""
+    if t is None or t.shape[0] >= R:
+        return t
+    return torch.cat([t, t.new_zeros(R - t.shape[0], *t.shape[1:])])
+
+
 def _linspace(n: int, lo: float = 0.0, hi: float = 1.0) -> torch.Tensor:
     """torch.linspace on the host (the reference's CPU values), for upload."""
     return torch.linspace(lo, hi, n)
@@ -421,8 +429,14 @@ class BaseModel(nn.Module):
         return pos
 
     # -- forward ----------------------------------------------------------------------------------------
-    def forward(self, rays: Dict[str, Dict[str, torch.Tensor]], rng: Optional[RNG] = None):
-        """rays[mod] = {"origins", "directions", "up_directions"} ([N,3] device); returns per-modality outputs."""
+    def forward(self, rays: Dict[str, Dict[str, torch.Tensor]], rng: Optional[RNG] = None, cap: Optional[int] = None):
+        """rays[mod] = {"origins", "directions", "up_directions"} ([N,3] device); returns per-modality outputs.
+
+        ``cap``: fixed-capacity foreground batch for graph capture (graphs.py).  Each modality's hit rays are
+        compacted into ``cap`` rows without reading the hit count on the host; rows past the count repeat the first
+        hit ray, composite into a dummy output row N that is cut off, and are skipped by the geometric losses
+        (outputs[mod]["count"] is the device hit count), so every gradient they produce is exactly zero and the
+        results equal the dynamic path's.  Per-ray outputs ("gradients", "weights", ...) then have ``cap`` rows."""
         rng = rng or RNG()
         sp = self.spec
         outputs = {}
@@ -433,15 +447,21 @@ class BaseModel(nn.Module):
             N = o.shape[0]
             dev = o.device
             nears, fars, bnears, bfars, mask = fx.ColliderFunction.apply(o, d, 1.0)
-            idx = fx.compact(mask)
+            if cap is None:
+                idx = fx.compact(mask)
+                sidx, count = idx, None
+            else:
+                idx, sidx, count = fx.compact_padded(mask, min(int(cap), N))
             R = idx.shape[0]
             o_h, d_h, up_h = o.index_select(0, idx), d.index_select(0, idx), up.index_select(0, idx)
             n_h, f_h = nears.index_select(0, idx), fars.index_select(0, idx)
-            t_rand = rng.uniform.get(mod)
+            t_rand = _pad_rows(rng.uniform.get(mod), R)
             if t_rand is None and self.training:
                 t_rand = torch.rand(R, 1, device=dev)
             pdf = rng.pdf.get(mod)
-            if pdf is None and self.training:
+            if pdf is not None:
+                pdf = [_pad_rows(p, R) for p in pdf]
+            elif self.training:
                 pdf = [torch.rand(R, 1, device=dev) for _ in range(sp.upsample_steps)]
             bins = self.neus_bins(n_h.detach(), f_h.detach(), o_h.detach(), d_h.detach(), t_rand, pdf)
             S = bins.shape[1] - 1
@@ -467,21 +487,26 @@ class BaseModel(nn.Module):
             w = fx.NeusWeightsFunction.apply(sdf, grads, d_h, deltas, s_param, vr._cos_anneal_ratio, S)
             feat = self.radiance_model.features(pos, d_h, normals.detach(), geo, S)
             out = {}
+            rows = N if cap is None else N + 1     # padded batches scatter into a dummy row N, cut off below
             for m, head in self.radiance_model.modality_heads.items():
                 vals = head(feat, d_h, up_h, S)
-                out[m] = fx.CompositeFunction.apply(w, vals, bg_out[m], idx, S)
+                bg = bg_out[m]
+                if cap is not None:
+                    bg = torch.cat([bg, bg.new_zeros(1, bg.shape[1])])
+                out[m] = fx.CompositeFunction.apply(w, vals, bg, sidx, S)[:N]
             with torch.no_grad():
-                acc = torch.zeros(N, 1, device=dev)
-                acc.index_copy_(0, idx, w.sum(-1, keepdim=True))
-                nrm = torch.zeros(N, 3, device=dev)
-                nrm.index_copy_(0, idx, (w[..., None] * normals.view(R, S, 3)).sum(1))
+                acc = torch.zeros(rows, 1, device=dev)
+                acc.index_copy_(0, sidx, w.sum(-1, keepdim=True))
+                nrm = torch.zeros(rows, 3, device=dev)
+                nrm.index_copy_(0, sidx, (w[..., None] * normals.view(R, S, 3)).sum(1))
                 steps = ((starts + ends) / 2).view(R, S)
-                dep = torch.zeros(N, 1, device=dev)
+                dep = torch.zeros(rows, 1, device=dev)
                 if R > 0:
-                    dep.index_copy_(0, idx, torch.clip((w * steps).sum(-1, keepdim=True), steps.min(), steps.max()))
-            out["normals"] = nrm
-            out["depth"] = dep
-            out["accumulation"] = acc
+                    dep.index_copy_(0, sidx, torch.clip((w * steps).sum(-1, keepdim=True), steps.min(), steps.max()))
+            out["normals"] = nrm[:N]
+            out["depth"] = dep[:N]
+            out["accumulation"] = acc[:N]
+            out["count"] = count
             out["gradients"] = grads.view(R, S, 3)
             out["hessians"] = hess.view(R, S, 3)
             out["inv_s"] = 1.0 / self.surface_model.volume_rendering.density_fn.variance_network.get_inv_variance()

@@ -139,6 +139,9 @@ class FlatGroup:
         self.m = torch.zeros(n + pad, device=dev)
         self.v = torch.zeros(n + pad, device=dev)
         self.sumsq = torch.zeros(1, device=dev)
+        # this step's AdamW scalars for graph replays (mms_adamw_dev): [lr, wd, beta1, beta2, eps, step_size, bc2_sqrt]
+        self.hyper = torch.zeros(8, device=dev)
+        self._hyper_host = torch.zeros(8).pin_memory() if dev.type == "cuda" else torch.zeros(8)
         off = 0
         for p in self.params:
             k = p.numel()
@@ -167,20 +170,36 @@ class FlatGroup:
                 p.grad = view
             off += k
 
-    def step(self, lr_factor: float, max_norm: float = 2.0):
-        """clip_grad_norm_(max_norm) then torch AdamW math (single launch each; scalars stay on device)."""
-        self.check_grads_attached()
+    def _advance(self, lr_factor: float):
+        """Advance the step counter; torch AdamW's scalars for this step."""
         self.step_count += 1
         t = self.step_count
         b1, b2 = self.betas
         lr = self.lr * lr_factor
-        bc1 = 1 - b1 ** t
-        bc2 = 1 - b2 ** t
+        return [lr, self.wd, b1, b2, self.eps, lr / (1 - b1 ** t), math.sqrt(1 - b2 ** t)]
+
+    def step(self, lr_factor: float, max_norm: float = 2.0):
+        """clip_grad_norm_(max_norm) then torch AdamW math (single launch each; scalars stay on device)."""
+        self.check_grads_attached()
+        h = self._advance(lr_factor)
         self.sumsq.zero_()
         _lib.call("mms_sumsq", self.grad.data_ptr(), self.n, self.sumsq.data_ptr(), _s())
         _lib.call("mms_adamw", self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.n,
-                  self.sumsq.data_ptr(), float(max_norm), float(lr), float(self.wd), float(b1), float(b2),
-                  float(self.eps), float(lr / bc1), float(math.sqrt(bc2)), _s())
+                  self.sumsq.data_ptr(), float(max_norm), *[float(x) for x in h], _s())
+
+    def load_hyper(self, lr_factor: float):
+        """Graph mode, before a replay: advance the step and upload its scalars (read by the captured launch)."""
+        h = self._advance(lr_factor)
+        self._hyper_host[:7] = torch.tensor(h, dtype=torch.float32)
+        self.hyper.copy_(self._hyper_host, non_blocking=True)
+
+    def step_captured(self, max_norm: float = 2.0):
+        """The clip + AdamW launches with device-resident scalars (captured into the step graph)."""
+        self.check_grads_attached()
+        self.sumsq.zero_()
+        _lib.call("mms_sumsq", self.grad.data_ptr(), self.n, self.sumsq.data_ptr(), _s())
+        _lib.call("mms_adamw_dev", self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                  self.n, self.sumsq.data_ptr(), float(max_norm), self.hyper.data_ptr(), _s())
 
 
 def lr_factor(step: int, max_iters: int = 100000, warm_up_ratio=0.1, milestones=(0.5, 0.75, 0.9), gamma=0.4):
@@ -218,7 +237,13 @@ def compute_loss(outputs, targets: Dict[str, torch.Tensor], modalities: List[str
         total = l if total is None else total + l
     grads = [outputs[m]["gradients"].reshape(-1, 3) for m in modalities]
     hess = [outputs[m]["hessians"].reshape(-1, 3) for m in modalities]
-    eik, curv = fx.GeoLossFunction.apply(*grads, *hess)
+    counts = [outputs[m].get("count") for m in modalities]
+    if any(c is not None for c in counts):
+        # fixed-capacity batches (graph-captured steps): padding rows carry no geometric loss
+        S = outputs[modalities[0]]["weights"].shape[1]
+        eik, curv = fx.GeoLossMaskedFunction.apply(S, counts, *grads, *hess)
+    else:
+        eik, curv = fx.GeoLossFunction.apply(*grads, *hess)
     cf = curvature_factor(step)
     losses["eikonal_loss"] = eik
     losses["curvature_loss"] = curv

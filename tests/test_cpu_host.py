@@ -118,3 +118,27 @@ def test_ddp_gradient_average_gloo_world2():
         p.join(timeout=60)
     assert all(ok for _, ok, _ in res), res
     assert all(mx == 1.5 for _, _, mx in res), res
+
+
+def test_every_called_entry_point_is_declared():
+    """Each _lib.call("mms_...") in the package names a header declaration (an undeclared one would be called with
+    ctypes' default 32-bit argument conversion; _lib.call refuses it at run time, this catches it statically)."""
+    import re
+    from multimodalstudio_amd import _lib
+    pkg = os.path.join(ROOT, "multimodalstudio_amd")
+    called = set()
+    for fn in os.listdir(pkg):
+        if fn.endswith(".py"):
+            called |= set(re.findall(r'call\(\s*"(mms_\w+)"', open(os.path.join(pkg, fn)).read()))
+    assert called, "no entry-point calls found"
+    missing = sorted(c for c in called if c not in _lib.SIGNATURES)
+    assert not missing, f"called but not declared in include/mms_hip.h: {missing}"
+
+
+def test_graph_capacity_buckets():
+    from multimodalstudio_amd.graphs import bucket_capacity
+    assert bucket_capacity([850], 64, 2048) == 896
+    assert bucket_capacity([850, 900, 12], 64, 2048) == 960
+    assert bucket_capacity([896], 64, 2048) == 896
+    assert bucket_capacity([2040], 64, 2048) == 2048
+    assert bucket_capacity([1], 64, 2048) == 64

@@ -1,0 +1,161 @@
+"""GPU parity of the fused MLP chain kernels (mms_mlp_chain: all three layers of the SDF / radiance MLP in one
+launch, bf16 or split-bf16x3 operands) against the reference's golden MLP vectors (tests/golden/mlp_*.npz) and,
+for the SDF's tap-row mode (rows_full), against an fp64 PyTorch restatement.
+
+Tolerances (scale-relative, written per mode): split-bf16x3 operands carry ~2^-16 relative precision, so outputs
+and gradients are held to 1e-4; plain bf16 operands (8 bits) to 3e-2.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TOL = {2: 1e-4, 1: 3e-2}
+CASES = {"geo": [(2, 100.0, 20.0), (2, 100.0, 20.0), (0, 1.0, 20.0)],
+         "rad": [(1, 1.0, 20.0), (1, 1.0, 20.0), (1, 1.0, 20.0)]}
+PKEYS = ["parametrizations.weight.original0", "parametrizations.weight.original1", "bias"]
+
+
+def rel(actual, ref):
+    a = np.asarray(actual, dtype=np.float64)
+    r = np.asarray(ref, dtype=np.float64)
+    return np.abs(a - r).max() / max(np.abs(r).max(), 1e-30)
+
+
+def _params(f, dev):
+    return [torch.from_numpy(f[f"p:layers.{l}.{k}"]).to(dev).requires_grad_(True) for l in range(3) for k in PKEYS]
+
+
+def _panel(x, dev):
+    from multimodalstudio_amd.functions import _alloc
+    X = _alloc(x.shape[0], x.shape[1], dev)
+    X.copy_(torch.as_tensor(x))
+    return X
+
+
+def _masked_ref(x, params, acts, Y, dy):
+    """fp64 backward of the weight-normed MLP with every activation derivative taken at the kernel's OWN forward
+    outputs Y[l] (act' from the output, as the kernel does).  With bf16 operands a pre-activation within rounding of
+    zero can land on the other side of a ReLU than in fp32; such sign flips are forward precision, not backward
+    errors, so the bf16 backward is checked against this reference.  Returns dx and the parameter gradients."""
+    ins = [torch.as_tensor(x).double(), Y[0].double().cpu(), Y[1].double().cpu()]
+    d = torch.as_tensor(dy).double()
+    out = [None] * 9
+    for l in (2, 1, 0):
+        act, beta, thr = acts[l]
+        y = (Y[l] if l < 2 else Y[2]).double().cpu()
+        if act == 1:
+            d = d * (y > 0)
+        elif act == 2:
+            d = d * torch.where(y * beta > thr, torch.ones_like(y), 1.0 - torch.exp(-beta * y))
+        g64 = params[3 * l].detach().double().cpu().requires_grad_(True)
+        v64 = params[3 * l + 1].detach().double().cpu().requires_grad_(True)
+        W = torch._weight_norm(v64, g64, 0)
+        W.backward(d.T @ ins[l])
+        out[3 * l], out[3 * l + 1], out[3 * l + 2] = g64.grad, v64.grad, d.sum(0)
+        d = d @ W.detach()
+    return d, out
+
+
+@pytest.mark.parametrize("prec", [2, 1])
+@pytest.mark.parametrize("name", list(CASES))
+def test_chain_vs_golden(dev, name, prec):
+    """Forward vs the reference's golden output; backward vs the golden gradients (split bf16x3) or, for plain bf16,
+    vs an fp64 backward taken at the kernel's own activations (see _masked_ref)."""
+    from multimodalstudio_amd import functions as fx
+    f = dict(np.load(os.path.join(GOLD, f"mlp_{name}.npz")))
+    params = _params(f, dev)
+    X = _panel(f["x"], dev)
+    run = fx.ChainRun(params, CASES[name], prec)
+    y = run.forward(X, keep=True)
+    Y = [t.detach().clone() for t in run.Y]
+    dy = _panel(f["dy"], dev)
+    dx = run.backward(dy)
+    torch.cuda.synchronize()
+    tol = TOL[prec]
+    errs = {"y": rel(y.cpu(), f["y"])}
+    if prec == 2:
+        ref_dx = f["dx"]
+        ref_g = [f[f"g:layers.{l}.{k}"] for l in range(3) for k in PKEYS]
+    else:
+        ref_dx, ref_g = _masked_ref(f["x"], params, CASES[name], Y, f["dy"])
+    errs["dx"] = rel(dx.cpu(), ref_dx)
+    for i, p in enumerate(params):
+        l, k = divmod(i, 3)
+        errs[f"g{l}.{PKEYS[k][-9:]}"] = rel(p.grad.cpu(), ref_g[i])
+    print(name, prec, {k: f"{v:.1e}" for k, v in errs.items()})
+    for k, v in errs.items():
+        assert v < tol, f"{name} prec={prec} {k}: {v:.2e}"
+
+
+def _ref_mlp(x, params, acts):
+    h = x
+    for l in range(3):
+        g, v, b = [p.detach().double().cpu() for p in params[3 * l: 3 * l + 3]]
+        w = torch._weight_norm(v, g, 0)
+        h = h @ w.T + b
+        act, beta, thr = acts[l]
+        if act == 1:
+            h = torch.relu(h)
+        elif act == 2:
+            h = torch.nn.functional.softplus(h, beta=beta, threshold=thr)
+    return h
+
+
+@pytest.mark.parametrize("M,rows_full", [(1000, 200), (777, 777), (640, 0)])
+def test_chain_sdf_tap_rows(dev, M, rows_full):
+    """SDF chain with tap rows (>= rows_full): column 0 for every row, all 257 columns for the rows below; the
+    backward reads only column 0 of the tap rows (the rest of those rows is garbage on purpose)."""
+    from multimodalstudio_amd import functions as fx
+    g = torch.Generator().manual_seed(M + rows_full)
+    f = dict(np.load(os.path.join(GOLD, "mlp_geo.npz")))
+    params = _params(f, dev)
+    x = torch.randn(M, 71, generator=g) * 0.5
+    X = _panel(x, dev)
+    run = fx.ChainRun(params, CASES["geo"], 2)
+    keep = rows_full > 0
+    y = run.forward(X, keep=keep, rows_full=rows_full)
+    xr = x.double().requires_grad_(True)
+    ref = _ref_mlp(xr, params, CASES["geo"])
+    yc = y.detach().cpu().double()
+    assert rel(yc[:, 0], ref[:, 0].detach()) < TOL[2]
+    if rows_full > 0:
+        assert rel(yc[:rows_full], ref[:rows_full].detach()) < TOL[2]
+    if not keep:
+        return
+    dy = torch.randn(M, 257, generator=g)
+    dy[rows_full:, 1:] = float("nan")            # never read
+    dyd = _panel(dy, dev)
+    for p in params:
+        p.grad = None
+    dx = run.backward(dyd)
+    torch.cuda.synchronize()
+    dyr = dy.double().clone()
+    dyr[rows_full:, 1:] = 0.0
+    ref.backward(dyr)
+    assert rel(dx.cpu(), xr.grad) < TOL[2]
+    assert torch.isfinite(dx).all()
+
+
+def test_sdf_only_fast_matches_fp32(dev):
+    """The sampler's inference SDF (functions.sdf_only) on the chain kernel (fast preset) vs the fp32 GEMM path:
+    same values, returned as a dense [M] vector (mms_neus_step reads it densely)."""
+    from multimodalstudio_amd import functions as fx
+    f = dict(np.load(os.path.join(GOLD, "mlp_geo.npz")))
+    params = _params(f, dev)
+    g = torch.Generator().manual_seed(3)
+    pos = (torch.rand(3000, 3, generator=g) * 2 - 1).to(dev)
+    grid = fx.GridCfg([float(int(16 * 1.3195079 ** l)) for l in range(16)], 12, 1.0)
+    table = ((torch.rand(16 << 12, 2, generator=g) * 2 - 1) * 1e-2).to(dev)
+    ref = fx.sdf_only(pos, table, grid, 16, params)
+    fx.set_precision("fast")
+    try:
+        out = fx.sdf_only(pos, table, grid, 16, params)
+    finally:
+        fx.set_precision("fp32")
+    torch.cuda.synchronize()
+    assert out.is_contiguous() and out.shape == ref.shape
+    assert rel(out.cpu(), ref.cpu()) < TOL[2]

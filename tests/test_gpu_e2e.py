@@ -33,7 +33,7 @@ def rel_err(actual, ref):
     return (np.abs(a - r).max() / scale) if scale > 0 else np.abs(a - r).max()
 
 
-def run_hip_e2e(f, dev):
+def run_hip_e2e(f, dev, cap=None):
     from multimodalstudio_amd import model as mm
     from multimodalstudio_amd import pipeline as pl
     from multimodalstudio_amd import scene as ms
@@ -63,7 +63,7 @@ def run_hip_e2e(f, dev):
                  pdf={m: draws[nm + 4 * i: nm + 4 * i + 4] for i, m in enumerate(mods)},
                  background={m: draws[5 * nm + i] for i, m in enumerate(mods)})
     rays = gen(coords)
-    outs = model(rays, rng)
+    outs = model(rays, rng, cap=cap)
     if raw:
         for m in mods:
             mask = ms.mosaick_mask(m, int(f["W"]), int(f["H"])).to(dev)

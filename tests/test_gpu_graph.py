@@ -1,0 +1,71 @@
+"""Graph-captured steps (multimodalstudio_amd/graphs.py) against the reference and against the eager path.
+
+* Fixed-capacity foreground batches (BaseModel.forward(cap=N): every ray slot kept, padding rows repeat the first
+  hit ray) on the reference's golden end-to-end vectors, with the tolerances of the dynamic path
+  (tests/test_gpu_e2e.py): the padding changes nothing.
+* GraphTrainer replays vs eager Trainer.train_step from the same initial state on the same pixel draws, with the
+  sampler jitter off (eval-mode sampler, so both paths see identical samples): per-step losses within 1e-3
+  relative over 6 steps (the first is eager, then captures and replays).  Not bit-exact: float-atomic gradient
+  sums differ between any two runs, and AdamW (eps 1e-15) turns last-bit differences of near-zero gradients into
+  full-size updates.
+"""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_e2e import load, rel_err, run_hip_e2e
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000"])
+def test_e2e_fixed_capacity(dev, name):
+    f = load(name)
+    N = f[f"{str(f['mods'][0])}:coords"].shape[0]
+    mods, model, pose, outs, losses, total = run_hip_e2e(f, dev, cap=N)
+    assert abs(total.item() - float(f["loss"])) / abs(float(f["loss"])) < 1e-4
+    for m in mods:
+        o = outs[m]
+        cnt = int(o["count"].item())
+        assert cnt == int(np.asarray(f[f"{m}:out:gradients"]).shape[0])
+        assert rel_err(o[m].detach().cpu(), f[f"{m}:out:{m}"]) < 1e-4, m
+        assert rel_err(o["accumulation"].cpu(), f[f"{m}:out:accumulation"]) < 1e-4, m
+        assert rel_err(o["normals"].cpu(), f[f"{m}:out:normals"]) < 2e-3, m
+        assert rel_err(o["gradients"][:cnt].detach().cpu(), f[f"{m}:out:gradients"]) < 2e-3, m
+        assert rel_err(pose.pose_adjustment[m].grad.cpu(), f[f"{m}:dpose"]) < 5e-2, m
+    worst = max(rel_err(p.grad.cpu(), f["g:" + k]) for k, p in model.named_parameters() if "g:" + k in f)
+    assert worst < 5e-2
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fast"])
+def test_graph_trainer_matches_eager(dev, precision):
+    from multimodalstudio_amd import functions as fx
+    from multimodalstudio_amd import graphs
+    from multimodalstudio_amd import pipeline as pl
+    cfg = pl.TrainConfig(method="grid", modalities=("rgb",), num_rays_per_modality=512, log2T=14, n_views=10,
+                         width=160, height=128)
+
+    def make():
+        tr = pl.Trainer(cfg, dev)
+        tr.set_step(95000)
+        tr.model.eval()       # no sampler jitter: both paths see identical samples
+        return tr
+
+    fx.set_precision(precision)
+    try:
+        eager, graphed = make(), make()
+        runner = graphs.GraphTrainer(graphed, granule=64)
+        le, lg = [], []
+        for _ in range(6):
+            le.append(float(eager.train_step()[1]))
+            lg.append(float(runner.step()[1]))
+        torch.cuda.synchronize()
+    finally:
+        fx.set_precision("fp32")
+    le, lg = np.array(le), np.array(lg)
+    rel = np.abs(le - lg) / np.abs(le)
+    print(precision, runner.stats, le, lg, rel)
+    assert runner.disabled is None, runner.disabled
+    assert runner.stats["replays"] >= 4 and runner.stats["captures"] >= 1, runner.stats
+    assert eager.step == graphed.step and eager.fields.step_count == graphed.fields.step_count
+    assert rel.max() < 1e-3
