@@ -70,16 +70,17 @@ int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K
  * Backward-data (backward = 1): X = dY of the last forward layer (rows >= rows_full: column 0 only), optionally
  *   scaled by act'(xaux) (stored to xout); out[l] = (prev . W^T) * act_l'(aux[l]) with act' evaluated from the
  *   forward output aux[l] (NULL: no scaling); out[2] = dX.
- * a_hi / a_lo: per-layer packed weights from mms_mlp_pack (bf16 [32 ceil(N/32)][16 ceil(K/16)]); layers 1, 2 are
+ * a_hi / a_lo: per-layer packed weights from mms_mlp_pack (bf16, 32 ceil(N/32) x 16 ceil(K/16)); layers 1, 2 are
  * register-fed and must be packed with permute = 1.  All row pitches multiples of 4 floats, 16-B aligned. */
 int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx, int K0, int64_t M, int64_t rows_full,
                   const float* xaux, int64_t ldxaux, int xact, float* xout, int64_t ldxout, const void* const* a_hi,
                   const void* const* a_lo, const float* const* bias, const float* const* aux, const int64_t* ldaux,
                   float* const* out, const int64_t* ldo, const int* N, const int* act, float beta, float thr,
                   void* stream);
-/* bf16 (hi, and lo = residual if non-NULL) image of W [N, K] (ldw) as an MFMA A operand [rows][cols]:
+/* bf16 (hi, and lo = residual if non-NULL) image of W [N, K] (ldw) as an MFMA A operand of rows x cols:
  * transpose = 0 -> A = W, 1 -> A = W^T; permute = 1 stores each 16-column step in register-fed order
- * (columns 0-3, 8-11, 4-7, 12-15).  Zero padded; rows % 32 == 0, cols % 16 == 0. */
+ * (columns 0-3, 8-11, 4-7, 12-15).  Zero padded; rows % 32 == 0, cols % 16 == 0.  Fragment-major: the 32x16
+ * fragment of (k-step s, row tile t) is one 1 KiB block at element ((s * rows/32 + t) * 64 + lane) * 8. */
 int mms_mlp_pack(const float* W, int64_t N, int64_t K, int64_t ldw, int transpose, int permute, int64_t rows,
                  int64_t cols, void* hi, void* lo, void* stream);
 

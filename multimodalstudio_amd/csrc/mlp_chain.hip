@@ -26,6 +26,12 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// streamed activations bypass the caches' retention (non-temporal), so the packed weights the waves re-read
+// from L2 at every k-step stay resident
+__device__ __forceinline__ f32x4 ld_nt4(const float* p) { return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p)); }
+__device__ __forceinline__ void st_nt4(float* p, f32x4 v) { __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p)); }
 
 struct ChainLayer {
   const __bf16* a_hi;  // packed A operand [32 nt][16 ks] (mms_mlp_pack)
@@ -91,28 +97,79 @@ __device__ __forceinline__ void mma(floatx16& acc, const bf16x8& ah, const bf16x
 // 8 consecutive floats of a 16-B aligned row from column k0 (zero past K)
 __device__ __forceinline__ void load8(const float* __restrict__ row, int k0, int K, float* v) {
   if (k0 + 8 <= K) {
-    const float4 a = *reinterpret_cast<const float4*>(row + k0);
-    const float4 b = *reinterpret_cast<const float4*>(row + k0 + 4);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    const f32x4 a = ld_nt4(row + k0);
+    const f32x4 b = ld_nt4(row + k0 + 4);
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (k0 + j < K) ? row[k0 + j] : 0.f;
   }
 }
 
-// acc[t] += A(tile t, k-step s) . B for the first nt tiles; A fragment: lane (r, h) = row 32 t + r, k 16 s + 8 h + j
-template <int PREC, int NT>
-__device__ __forceinline__ void mma_step(const ChainLayer& Ly, int kp, int s, int r, int h, int nt,
-                                         floatx16 (&acc)[NT], const bf16x8& bh, const bf16x8& bl) {
+// ---- weight fragments: block-shared, staged in LDS by LDS-DMA.  All four waves of a block multiply the SAME weight
+// fragments (the A operand) with their own rows, so each k-step's fragments are fetched once per block
+// (global_load_lds_dwordx4: no VGPRs, lane-linear 1 KiB per wave-instruction) into a 3-slot ring, two k-steps
+// ahead of the MFMAs, with one barrier per k-step.  Per-wave streaming of the fragments from L2 right before their
+// MFMAs (one wave per SIMD) left every k-step waiting on L2 latency: 6 % of the MFMA rate.
+// Packed images are fragment-major (mms_mlp_pack): fragment (k-step s, tile t) is one contiguous 1 KiB block at
+// element ((s * NT + t) * 64 + lane) * 8.
+constexpr int kRing = 3;
+constexpr int kSlot = 21;  // 1 KiB chunks per ring slot: hi + lo images of up to 10 tiles, + 1 spare (dummy loads)
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int PREC>
+constexpr int nimg() { return PREC == 2 ? 2 : 1; }
+
+// loads per wave per k-step when NTL tiles are staged (uniform over the 4 waves: padded with dummy loads)
+template <int PREC, int NTL>
+constexpr int stage_per() { return (nimg<PREC>() * NTL + 3) / 4; }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// issue k-step s's fragments of tiles [0, NTL) (hi, then lo) into ring slot s % kRing
+template <int PREC, int NT, int NTL>
+__device__ __forceinline__ void stage(const ChainLayer& Ly, int s, int wave, int lane, bf16x8 (*ring)[kSlot][64]) {
+  constexpr int TOTAL = nimg<PREC>() * NTL;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    if (t < nt) {
-      const int64_t off = (int64_t)(32 * t + r) * kp + 16 * s + 8 * h;
-      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Ly.a_hi + off);
-      bf16x8 al = ah;
-      if constexpr (PREC == 2) al = *reinterpret_cast<const bf16x8*>(Ly.a_lo + off);
-      mma<PREC>(acc[t], ah, al, bh, bl);
+  for (int i = 0; i < stage_per<PREC, NTL>(); ++i) {
+    const int c = wave + 4 * i;
+    const bool real = c < TOTAL;
+    const int cc = real ? c : 0;
+    const int img = cc / NTL, t = cc - img * NTL;
+    const __bf16* src = (img ? Ly.a_lo : Ly.a_hi) + ((int64_t)(s * NT + t) * 64 + lane) * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)&ring[s % kRing][real ? c : kSlot - 1][0], 16, 0,
+                                     0);
+  }
+}
+
+// one layer: acc[t] (t < nt) += sum_{s < ks} A(s, t) . B(s); B(s) = get_b(s) (compile-time s: register arrays).
+// ks and NTL are block-uniform (every wave takes part in every barrier); nt may be smaller per wave (nt <= NTL).
+template <int PREC, int NT, int NTL, int KS, typename GetB>
+__device__ __forceinline__ void run_layer(const ChainLayer& Ly, int ks, int nt, floatx16 (&acc)[NT], int wave,
+                                          int lane, bf16x8 (*ring)[kSlot][64], GetB&& get_b) {
+  constexpr int PER = stage_per<PREC, NTL>();
+  __builtin_amdgcn_s_barrier();  // every wave is done with the ring (previous layer / launch prologue)
+  stage<PREC, NT, NTL>(Ly, 0, wave, lane, ring);
+  if (ks > 1) stage<PREC, NT, NTL>(Ly, 1, wave, lane, ring);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (s < ks) {
+      if (s + 1 < ks) wait_vm<PER>(); else wait_vm<0>();  // this wave's loads of step s have landed
+      __builtin_amdgcn_s_barrier();                        // ... and every wave's; slot (s + 2) % 3 is free
+      if (s + 2 < ks) stage<PREC, NT, NTL>(Ly, s + 2, wave, lane, ring);
+      bf16x8 bh, bl;
+      get_b(s, bh, bl);
+      const bf16x8* slot = &ring[s % kRing][0][0];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        if (t < nt) {
+          const bf16x8 ah = slot[t * 64 + lane];
+          const bf16x8 al = PREC == 2 ? slot[(NTL + t) * 64 + lane] : ah;
+          mma<PREC>(acc[t], ah, al, bh, bl);
+        }
+      }
     }
   }
 }
@@ -131,8 +188,8 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[NT], const ChainLayer& 
       if (BWD && Ly.aux != nullptr) {
         const float* ar = Ly.aux + mc * Ly.ldaux;
         if (n0 + 4 <= Ly.N) {
-          const float4 q = *reinterpret_cast<const float4*>(ar + n0);
-          ax[0] = q.x; ax[1] = q.y; ax[2] = q.z; ax[3] = q.w;
+          const f32x4 q = ld_nt4(ar + n0);
+          ax[0] = q[0]; ax[1] = q[1]; ax[2] = q[2]; ax[3] = q[3];
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i) ax[i] = (n0 + i < Ly.N) ? ar[n0 + i] : 0.f;
@@ -155,13 +212,13 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[NT], const ChainLayer& 
       if (Ly.out != nullptr && mval) {
         float* orow = Ly.out + m * Ly.ldo;
         if (only_col0) {
-          if (n0 == 0) orow[0] = v[0];
+          if (n0 == 0) __builtin_nontemporal_store(v[0], orow);
         } else if (n0 + 4 <= Ly.N) {
-          *reinterpret_cast<float4*>(orow + n0) = make_float4(v[0], v[1], v[2], v[3]);
+          st_nt4(orow + n0, f32x4{v[0], v[1], v[2], v[3]});
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            if (n0 + i < Ly.N) orow[n0 + i] = v[i];
+            if (n0 + i < Ly.N) __builtin_nontemporal_store(v[i], orow + n0 + i);
         }
       }
     }
@@ -185,15 +242,20 @@ __device__ __forceinline__ void to_b(const floatx16 (&acc)[NT], bf16x8 (&bh)[2 *
 
 template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD>
 __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
+  __shared__ __attribute__((aligned(1024))) bf16x8 ring[kRing][kSlot][64];
   const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int64_t m0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 32;
-  if (m0 >= a.M) return;
+  // 128 rows per block, 32 per wave.  Waves past M keep running on clamped rows (no stores): every wave takes part
+  // in the block's barriers.
+  const int64_t mb = (int64_t)blockIdx.x * 128;
+  const int64_t m0 = mb + 32 * wave;
   const int64_t m = m0 + r;
   const bool mval = m < a.M;
   const int64_t mc = mval ? m : a.M - 1;
   const bool rowfull = m < a.rows_full;
-  const bool anyfull = m0 < a.rows_full;  // wave-uniform
+  const bool anyfull = m0 < a.rows_full;   // wave-uniform
+  const bool blockfull = mb < a.rows_full;  // block-uniform
   const floatx16 zero = {};
 
   // ---- layer 0: B operand from memory, natural k order
@@ -204,36 +266,33 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     const float* xr = a.X + mc * a.ldx;
     const float* xa = (BWD && a.xaux != nullptr) ? a.xaux + mc * a.ldxaux : nullptr;
     float* xo = (BWD && a.xout != nullptr && mval) ? a.xout + m * a.ldxout : nullptr;
-    const int ksn = (BWD && !anyfull) ? 1 : KS0;
+    // backward on SDF tap rows: only input column 0 is live (a block of tap rows needs k-step 0 alone)
+    const int ks0 = (BWD && !blockfull) ? 1 : KS0;
+    auto get_b = [&](int s, bf16x8& bh, bf16x8& bl) {
+      const int k0 = 16 * s + 8 * h;
+      float v[8];
+      load8(xr, k0, a.K0, v);
+      if constexpr (BWD) {
+        if (!rowfull) {
 #pragma unroll
-    for (int s = 0; s < KS0; ++s) {
-      if (s < ksn) {
-        const int k0 = 16 * s + 8 * h;
-        float v[8];
-        load8(xr, k0, a.K0, v);
-        if constexpr (BWD) {
-          if (!rowfull) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (k0 + j > 0) v[j] = 0.f;
-          }
-          if (xa != nullptr) {
-            float w[8];
-            load8(xa, k0, a.K0, w);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] *= act_grad_out(a.xact, w[j], a.beta, a.thr);
-          }
-          if (xo != nullptr) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (k0 + j < a.K0) xo[k0 + j] = v[j];
-          }
+          for (int j = 0; j < 8; ++j)
+            if (k0 + j > 0) v[j] = 0.f;
         }
-        bf16x8 bh, bl;
-        split8<PREC>(v, bh, bl);
-        mma_step<PREC, NT0>(a.L[0], 16 * KS0, s, r, h, NT0, acc0, bh, bl);
+        if (xa != nullptr) {
+          float w[8];
+          load8(xa, k0, a.K0, w);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] *= act_grad_out(a.xact, w[j], a.beta, a.thr);
+        }
+        if (xo != nullptr && (rowfull || s == 0)) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (k0 + j < a.K0 && (rowfull || k0 + j == 0)) __builtin_nontemporal_store(v[j], xo + k0 + j);
+        }
       }
-    }
+      split8<PREC>(v, bh, bl);
+    };
+    run_layer<PREC, NT0, NT0, KS0>(a.L[0], ks0, NT0, acc0, wave, lane, ring, get_b);
   }
   epilogue<NT0, BWD>(acc0, a.L[0], NT0, m, mc, mval, false, h, a.beta, a.thr);
   bf16x8 b1h[2 * NT0], b1l[2 * NT0];
@@ -243,26 +302,28 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   floatx16 acc1[NT1];
 #pragma unroll
   for (int t = 0; t < NT1; ++t) acc1[t] = zero;
-#pragma unroll
-  for (int s = 0; s < 2 * NT0; ++s) mma_step<PREC, NT1>(a.L[1], 32 * NT0, s, r, h, NT1, acc1, b1h[s], b1l[s]);
+  run_layer<PREC, NT1, NT1, 2 * NT0>(a.L[1], 2 * NT0, NT1, acc1, wave, lane, ring,
+                                     [&](int s, bf16x8& bh, bf16x8& bl) { bh = b1h[s]; bl = b1l[s]; });
   epilogue<NT1, BWD>(acc1, a.L[1], NT1, m, mc, mval, false, h, a.beta, a.thr);
   bf16x8 b2h[2 * NT1], b2l[2 * NT1];
   to_b<PREC, NT1>(acc1, b2h, b2l);
 
-  // ---- layer 2 (forward: SDF tap-only waves need only the sdf column tile)
+  // ---- layer 2 (forward: SDF tap rows need only the sdf column tile; a block of tap rows stages only that tile)
   floatx16 acc2[NT2];
 #pragma unroll
   for (int t = 0; t < NT2; ++t) acc2[t] = zero;
   const int nt2 = (!BWD && !anyfull) ? 1 : NT2;
-#pragma unroll
-  for (int s = 0; s < 2 * NT1; ++s) mma_step<PREC, NT2>(a.L[2], 32 * NT1, s, r, h, nt2, acc2, b2h[s], b2l[s]);
+  auto get_b2 = [&](int s, bf16x8& bh, bf16x8& bl) { bh = b2h[s]; bl = b2l[s]; };
+  if (BWD || blockfull)
+    run_layer<PREC, NT2, NT2, 2 * NT1>(a.L[2], 2 * NT1, nt2, acc2, wave, lane, ring, get_b2);
+  else
+    run_layer<PREC, NT2, 1, 2 * NT1>(a.L[2], 2 * NT1, 1, acc2, wave, lane, ring, get_b2);
   epilogue<NT2, BWD>(acc2, a.L[2], nt2, m, mc, mval, !BWD && !rowfull, h, a.beta, a.thr);
 }
 
 template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD>
 void launch_chain(const ChainArgs& a, hipStream_t s) {
-  const int64_t waves = (a.M + 31) / 32;
-  const unsigned blocks = (unsigned)((waves + 3) / 4);
+  const unsigned blocks = (unsigned)((a.M + 127) / 128);
   hipLaunchKernelGGL((chain_kernel<PREC, KS0, NT0, NT1, NT2, BWD>), dim3(blocks), dim3(256), 0, s, a);
 }
 
@@ -287,14 +348,18 @@ __global__ void pack_kernel(const float* __restrict__ W, int64_t N, int64_t K, i
                             int permute, int64_t rows, int64_t cols, __bf16* __restrict__ hi, __bf16* __restrict__ lo) {
   const int64_t total = rows * cols;
   const int64_t R = transpose ? K : N, C = transpose ? N : K;
+  const int64_t nt = rows / 32;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t row = i / cols, c = i - row * cols;
     const int64_t src = permute ? perm_col(c) : c;
     float v = 0.f;
     if (row < R && src < C) v = transpose ? W[src * ldw + row] : W[row * ldw + src];
+    // fragment-major destination: (k-step s, tile t) block, lane r + 32 h, element j
+    const int64_t s = c >> 4, q = c & 15, t = row >> 5, r = row & 31;
+    const int64_t o = ((s * nt + t) * 64 + r + 32 * (q >> 3)) * 8 + (q & 7);
     const __bf16 b = (__bf16)v;
-    hi[i] = b;
-    if (lo != nullptr) lo[i] = (__bf16)(v - (float)b);
+    hi[o] = b;
+    if (lo != nullptr) lo[o] = (__bf16)(v - (float)b);
   }
 }
 
