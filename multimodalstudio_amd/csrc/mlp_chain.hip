@@ -22,6 +22,8 @@
 // PREC 1: bf16 operands; PREC 2: split bf16x3 (x = hi + lo, acc += lo.hi + hi.lo + hi.hi); fp32 accumulation.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -61,16 +63,40 @@ struct ChainArgs {
   ChainLayer L[3];
 };
 
-__device__ __forceinline__ float act_grad_out(int act, float y, float beta, float thr) {
+// activation derivative from the forward OUTPUT y (compile-time activation: branch-free epilogues)
+template <int ACT>
+__device__ __forceinline__ float act_grad_out(float y, float beta, float thr) {
+  if constexpr (ACT == 1) return y > 0.f ? 1.f : 0.f;
+  if constexpr (ACT == 2) {
+    const float by = y * beta;
+    return by > thr ? 1.f : 1.0f - __builtin_amdgcn_exp2f(-by * 1.4426950408889634f);
+  }
+  if constexpr (ACT == 3) return y * (1.0f - y);
+  return 1.f;
+}
+
+// forward activation (the bf16 modes' hardware-transcendental forms of mms::act_fwd_fast, without branches)
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float v, float beta, float thr) {
+  if constexpr (ACT == 1) return v > 0.f ? v : 0.f;
+  if constexpr (ACT == 2) {
+    const float bx = v * beta;
+    const float e = __builtin_amdgcn_exp2f(bx * 1.4426950408889634f);
+    const float sp = __builtin_amdgcn_logf(1.0f + e) * (0.6931471805599453f * __builtin_amdgcn_rcpf(beta));
+    return bx > thr ? v : sp;
+  }
+  if constexpr (ACT == 3) return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f));
+  return v;
+}
+
+// run f with the activation id as a compile-time constant (the id is launch-uniform: one scalar branch)
+template <typename F>
+__device__ __forceinline__ void with_act(int act, F&& f) {
   switch (act) {
-    case 1: return y > 0.f ? 1.f : 0.f;
-    case 2: {
-      const float by = y * beta;
-      if (by > thr) return 1.f;
-      return 1.0f - __builtin_amdgcn_exp2f(-by * 1.4426950408889634f);
-    }
-    case 3: return y * (1.0f - y);
-    default: return 1.f;
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    default: f(std::integral_constant<int, 0>{}); break;
   }
 }
 
@@ -94,16 +120,16 @@ __device__ __forceinline__ void mma(floatx16& acc, const bf16x8& ah, const bf16x
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
 }
 
-// 8 consecutive floats of a 16-B aligned row from column k0 (zero past K)
+// 8 consecutive floats of a 16-B aligned row (pitch a multiple of 4 floats, >= K) from column k0 (a multiple of 8),
+// zero past K.  Both 16-B loads are unconditional (a column past K reads column 0 instead, then is zeroed), so a
+// k-step's loads issue back to back without exec-masked branches.
 __device__ __forceinline__ void load8(const float* __restrict__ row, int k0, int K, float* v) {
-  if (k0 + 8 <= K) {
-    const f32x4 a = ld_nt4(row + k0);
-    const f32x4 b = ld_nt4(row + k0 + 4);
-    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
-    v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
-  } else {
+  const f32x4 a = ld_nt4(row + (k0 < K ? k0 : 0));
+  const f32x4 b = ld_nt4(row + (k0 + 4 < K ? k0 + 4 : 0));
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (k0 + j < K) ? row[k0 + j] : 0.f;
+  for (int j = 0; j < 4; ++j) {
+    v[j] = k0 + j < K ? a[j] : 0.f;
+    v[4 + j] = k0 + 4 + j < K ? b[j] : 0.f;
   }
 }
 
@@ -115,6 +141,7 @@ __device__ __forceinline__ void load8(const float* __restrict__ row, int k0, int
 // Packed images are fragment-major (mms_mlp_pack): fragment (k-step s, tile t) is one contiguous 1 KiB block at
 // element ((s * NT + t) * 64 + lane) * 8.
 constexpr int kRing = 3;
+constexpr int kMaxTiles = 10;  // widest chain layer: 10 column tiles (320 units)
 constexpr int kSlot = 21;  // 1 KiB chunks per ring slot: hi + lo images of up to 10 tiles, + 1 spare (dummy loads)
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -125,8 +152,19 @@ constexpr int nimg() { return PREC == 2 ? 2 : 1; }
 template <int PREC, int NTL>
 constexpr int stage_per() { return (nimg<PREC>() * NTL + 3) / 4; }
 
+// wait until at most N vector-memory operations of this wave are outstanding, then the block barrier (one asm
+// statement with a memory clobber: no LDS read of the ring moves above either)
 template <int N>
-__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ void wait_vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// 16 B per lane, global -> LDS (lane-linear at lds_addr), issued as inline asm: the compiler does not see an LDS
+// DMA, so it does not guard every later LDS read of the ring with a full vmcnt(0) drain (which waited out the
+// prefetch of the next two k-steps); the ring's ordering is the explicit wait_vm_barrier above.
+__device__ __forceinline__ void lds_dma16(const void* src, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr) : "memory", "m0");
+}
 
 // issue k-step s's fragments of tiles [0, NTL) (hi, then lo) into ring slot s % kRing
 template <int PREC, int NT, int NTL>
@@ -139,25 +177,29 @@ __device__ __forceinline__ void stage(const ChainLayer& Ly, int s, int wave, int
     const int cc = real ? c : 0;
     const int img = cc / NTL, t = cc - img * NTL;
     const __bf16* src = (img ? Ly.a_lo : Ly.a_hi) + ((int64_t)(s * NT + t) * 64 + lane) * 8;
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)&ring[s % kRing][real ? c : kSlot - 1][0], 16, 0,
-                                     0);
+    const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&ring[s % kRing][real ? c : kSlot - 1][0]);
+    lds_dma16(src, __builtin_amdgcn_readfirstlane(dst));
   }
 }
 
 // one layer: acc[t] (t < nt) += sum_{s < ks} A(s, t) . B(s); B(s) = get_b(s) (compile-time s: register arrays).
 // ks and NTL are block-uniform (every wave takes part in every barrier); nt may be smaller per wave (nt <= NTL).
-template <int PREC, int NT, int NTL, int KS, typename GetB>
+// pre(s) issues the global loads get_b(s) will consume, one k-step ahead (before the ring loads of step s + 1), so
+// the wait for the ring's step s also covers them.
+template <int PREC, int NT, int NTL, int KS, typename Pre, typename GetB>
 __device__ __forceinline__ void run_layer(const ChainLayer& Ly, int ks, int nt, floatx16 (&acc)[NT], int wave,
-                                          int lane, bf16x8 (*ring)[kSlot][64], GetB&& get_b) {
+                                          int lane, bf16x8 (*ring)[kSlot][64], Pre&& pre, GetB&& get_b) {
   constexpr int PER = stage_per<PREC, NTL>();
-  __builtin_amdgcn_s_barrier();  // every wave is done with the ring (previous layer / launch prologue)
+  wait_vm_barrier<63>();  // every wave is done with the ring (previous layer / launch prologue)
+  pre(0);
   stage<PREC, NT, NTL>(Ly, 0, wave, lane, ring);
   if (ks > 1) stage<PREC, NT, NTL>(Ly, 1, wave, lane, ring);
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     if (s < ks) {
-      if (s + 1 < ks) wait_vm<PER>(); else wait_vm<0>();  // this wave's loads of step s have landed
-      __builtin_amdgcn_s_barrier();                        // ... and every wave's; slot (s + 2) % 3 is free
+      // this wave's loads of step s have landed, and (barrier) every wave's; slot (s + 2) % 3 is free
+      if (s + 1 < ks) wait_vm_barrier<PER>(); else wait_vm_barrier<0>();
+      if (s + 1 < ks) pre(s + 1);
       if (s + 2 < ks) stage<PREC, NT, NTL>(Ly, s + 2, wave, lane, ring);
       bf16x8 bh, bl;
       get_b(s, bh, bl);
@@ -175,46 +217,47 @@ __device__ __forceinline__ void run_layer(const ChainLayer& Ly, int ks, int nt, 
 }
 
 // Epilogue in place.  Lane (m, h): tile t, register 4 g + i holds unit n = 32 t + 8 g + 4 h + i of data row m.
-template <int NT, bool BWD>
-__device__ __forceinline__ void epilogue(floatx16 (&acc)[NT], const ChainLayer& Ly, int nt, int64_t m, int64_t mc,
-                                         bool mval, bool only_col0, int h, float beta, float thr) {
+// Forward: + bias (zero-padded LDS copy), activation.  Backward: * act'(aux), the aux row's four 16-B loads of a
+// tile issued together (unconditional: a quad past N reads quad 0 and is zeroed; quads below N lie inside the
+// row since the pitch is a multiple of 4 >= N).
+template <int NT, bool BWD, int ACT>
+__device__ __forceinline__ void epilogue(floatx16 (&acc)[NT], const ChainLayer& Ly, const float* sb, int nt, int64_t m,
+                                         int64_t mc, bool mval, bool only_col0, int h, float beta, float thr) {
+  const float* ar = (BWD && Ly.aux != nullptr) ? Ly.aux + mc * Ly.ldaux : nullptr;
+  float* orow = (Ly.out != nullptr && mval) ? Ly.out + m * Ly.ldo : nullptr;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     if (t >= nt) continue;
+    f32x4 q[4];
+    if (BWD && ar != nullptr) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n0 = 32 * t + 8 * g + 4 * h;
+        q[g] = ld_nt4(ar + (n0 < Ly.N ? n0 : 0));
+      }
+    }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int n0 = 32 * t + 8 * g + 4 * h;
-      float ax[4] = {0.f, 0.f, 0.f, 0.f};
-      if (BWD && Ly.aux != nullptr) {
-        const float* ar = Ly.aux + mc * Ly.ldaux;
-        if (n0 + 4 <= Ly.N) {
-          const f32x4 q = ld_nt4(ar + n0);
-          ax[0] = q[0]; ax[1] = q[1]; ax[2] = q[2]; ax[3] = q[3];
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) ax[i] = (n0 + i < Ly.N) ? ar[n0 + i] : 0.f;
-        }
-      }
-      float v[4];
+      f32x4 bq = {};
+      if (!BWD) bq = *reinterpret_cast<const f32x4*>(sb + n0);
+      f32x4 v;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int n = n0 + i;
         float x = acc[t][4 * g + i];
         if constexpr (!BWD) {
-          if (Ly.bias != nullptr && n < Ly.N) x += Ly.bias[n];
-          x = mms::act_fwd_fast(Ly.act, x, beta, thr);
+          x = act_fwd<ACT>(x + bq[i], beta, thr);
         } else {
-          if (Ly.aux != nullptr) x *= act_grad_out(Ly.act, ax[i], beta, thr);
+          if (ar != nullptr) x *= act_grad_out<ACT>(n0 + i < Ly.N ? q[g][i] : 0.f, beta, thr);
         }
         acc[t][4 * g + i] = x;
         v[i] = x;
       }
-      if (Ly.out != nullptr && mval) {
-        float* orow = Ly.out + m * Ly.ldo;
+      if (orow != nullptr) {
         if (only_col0) {
           if (n0 == 0) __builtin_nontemporal_store(v[0], orow);
         } else if (n0 + 4 <= Ly.N) {
-          st_nt4(orow + n0, f32x4{v[0], v[1], v[2], v[3]});
+          st_nt4(orow + n0, v);
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
@@ -223,6 +266,13 @@ __device__ __forceinline__ void epilogue(floatx16 (&acc)[NT], const ChainLayer& 
       }
     }
   }
+}
+
+template <int NT, bool BWD>
+__device__ __forceinline__ void epilogue_any(floatx16 (&acc)[NT], const ChainLayer& Ly, const float* sb, int nt,
+                                             int64_t m, int64_t mc, bool mval, bool only_col0, int h, float beta,
+                                             float thr) {
+  with_act(Ly.act, [&](auto A) { epilogue<NT, BWD, decltype(A)::value>(acc, Ly, sb, nt, m, mc, mval, only_col0, h, beta, thr); });
 }
 
 // accumulator tiles -> next layer's B fragments (k-step 2 t + s = registers 8 s .. 8 s + 7 of tile t)
@@ -243,6 +293,7 @@ __device__ __forceinline__ void to_b(const floatx16 (&acc)[NT], bf16x8 (&bh)[2 *
 template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD>
 __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   __shared__ __attribute__((aligned(1024))) bf16x8 ring[kRing][kSlot][64];
+  __shared__ __attribute__((aligned(16))) float sbias[3][32 * kMaxTiles];  // forward biases, zero padded
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -257,6 +308,12 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   const bool anyfull = m0 < a.rows_full;   // wave-uniform
   const bool blockfull = mb < a.rows_full;  // block-uniform
   const floatx16 zero = {};
+  if constexpr (!BWD) {
+#pragma unroll
+    for (int l = 0; l < 3; ++l)
+      for (int i = threadIdx.x; i < 32 * kMaxTiles; i += 256)
+        sbias[l][i] = (a.L[l].bias != nullptr && i < a.L[l].N) ? a.L[l].bias[i] : 0.f;
+  }  // (visible after the first layer's opening barrier)
 
   // ---- layer 0: B operand from memory, natural k order
   floatx16 acc0[NT0];
@@ -268,10 +325,16 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     float* xo = (BWD && a.xout != nullptr && mval) ? a.xout + m * a.ldxout : nullptr;
     // backward on SDF tap rows: only input column 0 is live (a block of tap rows needs k-step 0 alone)
     const int ks0 = (BWD && !blockfull) ? 1 : KS0;
+    float xv[2][8], wv[2][8];  // k-step s's input (and xaux) row slice in buffer s & 1
+    auto pre = [&](int s) {
+      load8(xr, 16 * s + 8 * h, a.K0, xv[s & 1]);
+      if (BWD && xa != nullptr) load8(xa, 16 * s + 8 * h, a.K0, wv[s & 1]);
+    };
     auto get_b = [&](int s, bf16x8& bh, bf16x8& bl) {
       const int k0 = 16 * s + 8 * h;
       float v[8];
-      load8(xr, k0, a.K0, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = xv[s & 1][j];
       if constexpr (BWD) {
         if (!rowfull) {
 #pragma unroll
@@ -279,10 +342,10 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
             if (k0 + j > 0) v[j] = 0.f;
         }
         if (xa != nullptr) {
-          float w[8];
-          load8(xa, k0, a.K0, w);
+          with_act(a.xact, [&](auto A) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] *= act_grad_out(a.xact, w[j], a.beta, a.thr);
+            for (int j = 0; j < 8; ++j) v[j] *= act_grad_out<decltype(A)::value>(wv[s & 1][j], a.beta, a.thr);
+          });
         }
         if (xo != nullptr && (rowfull || s == 0)) {
 #pragma unroll
@@ -292,19 +355,20 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
       }
       split8<PREC>(v, bh, bl);
     };
-    run_layer<PREC, NT0, NT0, KS0>(a.L[0], ks0, NT0, acc0, wave, lane, ring, get_b);
+    run_layer<PREC, NT0, NT0, KS0>(a.L[0], ks0, NT0, acc0, wave, lane, ring, pre, get_b);
   }
-  epilogue<NT0, BWD>(acc0, a.L[0], NT0, m, mc, mval, false, h, a.beta, a.thr);
+  epilogue_any<NT0, BWD>(acc0, a.L[0], sbias[0], NT0, m, mc, mval, false, h, a.beta, a.thr);
   bf16x8 b1h[2 * NT0], b1l[2 * NT0];
   to_b<PREC, NT0>(acc0, b1h, b1l);
+  auto nopre = [](int) {};
 
   // ---- layer 1: B operand from layer 0's registers
   floatx16 acc1[NT1];
 #pragma unroll
   for (int t = 0; t < NT1; ++t) acc1[t] = zero;
-  run_layer<PREC, NT1, NT1, 2 * NT0>(a.L[1], 2 * NT0, NT1, acc1, wave, lane, ring,
+  run_layer<PREC, NT1, NT1, 2 * NT0>(a.L[1], 2 * NT0, NT1, acc1, wave, lane, ring, nopre,
                                      [&](int s, bf16x8& bh, bf16x8& bl) { bh = b1h[s]; bl = b1l[s]; });
-  epilogue<NT1, BWD>(acc1, a.L[1], NT1, m, mc, mval, false, h, a.beta, a.thr);
+  epilogue_any<NT1, BWD>(acc1, a.L[1], sbias[1], NT1, m, mc, mval, false, h, a.beta, a.thr);
   bf16x8 b2h[2 * NT1], b2l[2 * NT1];
   to_b<PREC, NT1>(acc1, b2h, b2l);
 
@@ -315,10 +379,10 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   const int nt2 = (!BWD && !anyfull) ? 1 : NT2;
   auto get_b2 = [&](int s, bf16x8& bh, bf16x8& bl) { bh = b2h[s]; bl = b2l[s]; };
   if (BWD || blockfull)
-    run_layer<PREC, NT2, NT2, 2 * NT1>(a.L[2], 2 * NT1, nt2, acc2, wave, lane, ring, get_b2);
+    run_layer<PREC, NT2, NT2, 2 * NT1>(a.L[2], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2);
   else
-    run_layer<PREC, NT2, 1, 2 * NT1>(a.L[2], 2 * NT1, 1, acc2, wave, lane, ring, get_b2);
-  epilogue<NT2, BWD>(acc2, a.L[2], nt2, m, mc, mval, !BWD && !rowfull, h, a.beta, a.thr);
+    run_layer<PREC, NT2, 1, 2 * NT1>(a.L[2], 2 * NT1, 1, acc2, wave, lane, ring, nopre, get_b2);
+  epilogue_any<NT2, BWD>(acc2, a.L[2], sbias[2], nt2, m, mc, mval, !BWD && !rowfull, h, a.beta, a.thr);
 }
 
 template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD>
