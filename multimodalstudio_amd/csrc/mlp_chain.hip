@@ -22,7 +22,6 @@
 // PREC 1: bf16 operands; PREC 2: split bf16x3 (x = hi + lo, acc += lo.hi + hi.lo + hi.hi); fp32 accumulation.
 #include "common.h"
 
-#include <type_traits>
 
 namespace {
 
@@ -87,17 +86,6 @@ __device__ __forceinline__ float act_fwd(float v, float beta, float thr) {
   }
   if constexpr (ACT == 3) return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f));
   return v;
-}
-
-// run f with the activation id as a compile-time constant (the id is launch-uniform: one scalar branch)
-template <typename F>
-__device__ __forceinline__ void with_act(int act, F&& f) {
-  switch (act) {
-    case 1: f(std::integral_constant<int, 1>{}); break;
-    case 2: f(std::integral_constant<int, 2>{}); break;
-    case 3: f(std::integral_constant<int, 3>{}); break;
-    default: f(std::integral_constant<int, 0>{}); break;
-  }
 }
 
 template <int PREC>
@@ -176,7 +164,9 @@ __device__ __forceinline__ void stage(const ChainLayer& Ly, int s, int wave, int
     const bool real = c < TOTAL;
     const int cc = real ? c : 0;
     const int img = cc / NTL, t = cc - img * NTL;
-    const __bf16* src = (img ? Ly.a_lo : Ly.a_hi) + ((int64_t)(s * NT + t) * 64 + lane) * 8;
+    const __bf16* base = Ly.a_hi;
+    if constexpr (PREC == 2) base = img ? Ly.a_lo : Ly.a_hi;  // a select of two values (no divergent address)
+    const __bf16* src = base + ((int64_t)(s * NT + t) * 64 + lane) * 8;
     const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&ring[s % kRing][real ? c : kSlot - 1][0]);
     lds_dma16(src, __builtin_amdgcn_readfirstlane(dst));
   }
@@ -216,86 +206,110 @@ __device__ __forceinline__ void run_layer(const ChainLayer& Ly, int ks, int nt, 
   }
 }
 
-// Epilogue in place.  Lane (m, h): tile t, register 4 g + i holds unit n = 32 t + 8 g + 4 h + i of data row m.
-// Forward: + bias (zero-padded LDS copy), activation.  Backward: * act'(aux), the aux row's four 16-B loads of a
-// tile issued together (unconditional: a quad past N reads quad 0 and is zeroed; quads below N lie inside the
-// row since the pitch is a multiple of 4 >= N).
+// Epilogue of one accumulator tile t, in place.  Lane (m, h): register 4 g + i holds unit n = 32 t + 8 g + 4 h + i
+// of data row m.  Forward: + bias (zero-padded LDS copy), activation.  Backward: * act'(aux), the aux row's four
+// 16-B loads of the tile issued together (unconditional: a quad past N reads quad 0 and is zeroed; quads below N
+// lie inside the row since the pitch is a multiple of 4 >= N).
+template <bool BWD, int ACT>
+__device__ __forceinline__ void epi_tile(floatx16& acc, int t, const ChainLayer& Ly, const float* sb, const float* ar,
+                                         float* orow, bool only_col0, int h, float beta, float thr) {
+  f32x4 q[4];
+  if (BWD && ar != nullptr) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int n0 = 32 * t + 8 * g + 4 * h;
+      q[g] = ld_nt4(ar + (n0 < Ly.N ? n0 : 0));
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int n0 = 32 * t + 8 * g + 4 * h;
+    f32x4 bq = {};
+    if (!BWD) bq = *reinterpret_cast<const f32x4*>(sb + n0);
+    f32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float x = acc[4 * g + i];
+      if constexpr (!BWD) {
+        x = act_fwd<ACT>(x + bq[i], beta, thr);
+      } else {
+        if (ar != nullptr) x *= act_grad_out<ACT>(n0 + i < Ly.N ? q[g][i] : 0.f, beta, thr);
+      }
+      acc[4 * g + i] = x;
+      v[i] = x;
+    }
+    if (orow != nullptr) {
+      if (only_col0) {
+        if (n0 == 0) __builtin_nontemporal_store(v[0], orow);
+      } else if (n0 + 4 <= Ly.N) {
+        st_nt4(orow + n0, v);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (n0 + i < Ly.N) __builtin_nontemporal_store(v[i], orow + n0 + i);
+      }
+    }
+  }
+}
+
+// The forward's lazy epilogue of a full 32-unit tile (hidden layers: N = 32 NT, checked at dispatch): bias,
+// activation, and (KEEP) the fp32 store, with no guards at all, so it schedules in one basic block with the
+// MFMAs around it.  Rows past M compute row M - 1's values and store them there again (identical bits).
+template <int ACT, bool KEEP>
+__device__ __forceinline__ void epi_tile_full(floatx16& acc, int t, const float* sb, float* orow, int h, float beta,
+                                              float thr) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int n0 = 32 * t + 8 * g + 4 * h;
+    const f32x4 bq = *reinterpret_cast<const f32x4*>(sb + n0);
+    f32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = act_fwd<ACT>(acc[4 * g + i] + bq[i], beta, thr);
+      acc[4 * g + i] = v[i];
+    }
+    if constexpr (KEEP) st_nt4(orow + n0, v);
+  }
+}
+
 template <int NT, bool BWD, int ACT>
 __device__ __forceinline__ void epilogue(floatx16 (&acc)[NT], const ChainLayer& Ly, const float* sb, int nt, int64_t m,
                                          int64_t mc, bool mval, bool only_col0, int h, float beta, float thr) {
   const float* ar = (BWD && Ly.aux != nullptr) ? Ly.aux + mc * Ly.ldaux : nullptr;
   float* orow = (Ly.out != nullptr && mval) ? Ly.out + m * Ly.ldo : nullptr;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    if (t >= nt) continue;
-    f32x4 q[4];
-    if (BWD && ar != nullptr) {
+  for (int t = 0; t < NT; ++t)
+    if (t < nt) epi_tile<BWD, ACT>(acc[t], t, Ly, sb, ar, orow, only_col0, h, beta, thr);
+}
+
+// accumulator tile -> the next layer's B fragments of k-steps 2 t, 2 t + 1 (registers 8 s .. 8 s + 7)
+template <int PREC>
+__device__ __forceinline__ void tile_to_b(const floatx16& acc, bf16x8* bh, bf16x8* bl) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int n0 = 32 * t + 8 * g + 4 * h;
-        q[g] = ld_nt4(ar + (n0 < Ly.N ? n0 : 0));
-      }
-    }
+  for (int s = 0; s < 2; ++s) {
+    float v[8];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int n0 = 32 * t + 8 * g + 4 * h;
-      f32x4 bq = {};
-      if (!BWD) bq = *reinterpret_cast<const f32x4*>(sb + n0);
-      f32x4 v;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float x = acc[t][4 * g + i];
-        if constexpr (!BWD) {
-          x = act_fwd<ACT>(x + bq[i], beta, thr);
-        } else {
-          if (ar != nullptr) x *= act_grad_out<ACT>(n0 + i < Ly.N ? q[g][i] : 0.f, beta, thr);
-        }
-        acc[t][4 * g + i] = x;
-        v[i] = x;
-      }
-      if (orow != nullptr) {
-        if (only_col0) {
-          if (n0 == 0) __builtin_nontemporal_store(v[0], orow);
-        } else if (n0 + 4 <= Ly.N) {
-          st_nt4(orow + n0, v);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (n0 + i < Ly.N) __builtin_nontemporal_store(v[i], orow + n0 + i);
-        }
-      }
-    }
+    for (int j = 0; j < 8; ++j) v[j] = acc[8 * s + j];
+    split8<PREC>(v, bh[s], bl[s]);
   }
 }
 
-template <int NT, bool BWD>
-__device__ __forceinline__ void epilogue_any(floatx16 (&acc)[NT], const ChainLayer& Ly, const float* sb, int nt,
-                                             int64_t m, int64_t mc, bool mval, bool only_col0, int h, float beta,
-                                             float thr) {
-  with_act(Ly.act, [&](auto A) { epilogue<NT, BWD, decltype(A)::value>(acc, Ly, sb, nt, m, mc, mval, only_col0, h, beta, thr); });
-}
-
-// accumulator tiles -> next layer's B fragments (k-step 2 t + s = registers 8 s .. 8 s + 7 of tile t)
 template <int PREC, int NT>
 __device__ __forceinline__ void to_b(const floatx16 (&acc)[NT], bf16x8 (&bh)[2 * NT], bf16x8 (&bl)[2 * NT]) {
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = acc[t][8 * s + j];
-      split8<PREC>(v, bh[2 * t + s], bl[2 * t + s]);
-    }
-  }
+  for (int t = 0; t < NT; ++t) tile_to_b<PREC>(acc[t], &bh[2 * t], &bl[2 * t]);
 }
 
-template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD>
+// Activations are template arguments (A0..A2: layer activations, forward ids or backward derivative ids; XA: the
+// backward's input scaling).  The forward's epilogue of layer l is LAZY: tile t is finished (bias, activation,
+// store, bf16 split) inside layer l + 1's k-step 2 t, right before the MFMAs that consume it, so its VALU and
+// transcendental work issues between the previous k-step's MFMAs (one wave per SIMD: nothing else hides it).
+template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, int XA, bool KEEP>
 __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   __shared__ __attribute__((aligned(1024))) bf16x8 ring[kRing][kSlot][64];
   __shared__ __attribute__((aligned(16))) float sbias[3][32 * kMaxTiles];  // forward biases, zero padded
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar staging addresses
   const int r = lane & 31, h = lane >> 5;
   // 128 rows per block, 32 per wave.  Waves past M keep running on clamped rows (no stores): every wave takes part
   // in the block's barriers.
@@ -314,6 +328,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
       for (int i = threadIdx.x; i < 32 * kMaxTiles; i += 256)
         sbias[l][i] = (a.L[l].bias != nullptr && i < a.L[l].N) ? a.L[l].bias[i] : 0.f;
   }  // (visible after the first layer's opening barrier)
+  // forward hidden-layer stores (KEEP): every lane stores its (clamped) row
+  auto orow_of = [&](const ChainLayer& Ly) -> float* { return KEEP ? Ly.out + mc * Ly.ldo : nullptr; };
 
   // ---- layer 0: B operand from memory, natural k order
   floatx16 acc0[NT0];
@@ -342,10 +358,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
             if (k0 + j > 0) v[j] = 0.f;
         }
         if (xa != nullptr) {
-          with_act(a.xact, [&](auto A) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] *= act_grad_out<decltype(A)::value>(wv[s & 1][j], a.beta, a.thr);
-          });
+          for (int j = 0; j < 8; ++j) v[j] *= act_grad_out<XA>(wv[s & 1][j], a.beta, a.thr);
         }
         if (xo != nullptr && (rowfull || s == 0)) {
 #pragma unroll
@@ -357,48 +371,94 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     };
     run_layer<PREC, NT0, NT0, KS0>(a.L[0], ks0, NT0, acc0, wave, lane, ring, pre, get_b);
   }
-  epilogue_any<NT0, BWD>(acc0, a.L[0], sbias[0], NT0, m, mc, mval, false, h, a.beta, a.thr);
-  bf16x8 b1h[2 * NT0], b1l[2 * NT0];
-  to_b<PREC, NT0>(acc0, b1h, b1l);
   auto nopre = [](int) {};
+  bf16x8 b1h[2 * NT0], b1l[2 * NT0];
+  if constexpr (BWD) {
+    epilogue<NT0, BWD, A0>(acc0, a.L[0], sbias[0], NT0, m, mc, mval, false, h, a.beta, a.thr);
+    to_b<PREC, NT0>(acc0, b1h, b1l);
+  }
 
   // ---- layer 1: B operand from layer 0's registers
   floatx16 acc1[NT1];
 #pragma unroll
   for (int t = 0; t < NT1; ++t) acc1[t] = zero;
-  run_layer<PREC, NT1, NT1, 2 * NT0>(a.L[1], 2 * NT0, NT1, acc1, wave, lane, ring, nopre,
-                                     [&](int s, bf16x8& bh, bf16x8& bl) { bh = b1h[s]; bl = b1l[s]; });
-  epilogue_any<NT1, BWD>(acc1, a.L[1], sbias[1], NT1, m, mc, mval, false, h, a.beta, a.thr);
+  {
+    float* orow0 = orow_of(a.L[0]);
+    run_layer<PREC, NT1, NT1, 2 * NT0>(a.L[1], 2 * NT0, NT1, acc1, wave, lane, ring, nopre,
+                                       [&](int s, bf16x8& bh, bf16x8& bl) {
+      if constexpr (!BWD) {
+        if ((s & 1) == 0) {
+          epi_tile_full<A0, KEEP>(acc0[s >> 1], s >> 1, sbias[0], orow0, h, a.beta, a.thr);
+          tile_to_b<PREC>(acc0[s >> 1], &b1h[s], &b1l[s]);
+        }
+      }
+      bh = b1h[s]; bl = b1l[s];
+    });
+  }
   bf16x8 b2h[2 * NT1], b2l[2 * NT1];
-  to_b<PREC, NT1>(acc1, b2h, b2l);
+  if constexpr (BWD) {
+    epilogue<NT1, BWD, A1>(acc1, a.L[1], sbias[1], NT1, m, mc, mval, false, h, a.beta, a.thr);
+    to_b<PREC, NT1>(acc1, b2h, b2l);
+  }
 
   // ---- layer 2 (forward: SDF tap rows need only the sdf column tile; a block of tap rows stages only that tile)
   floatx16 acc2[NT2];
 #pragma unroll
   for (int t = 0; t < NT2; ++t) acc2[t] = zero;
   const int nt2 = (!BWD && !anyfull) ? 1 : NT2;
-  auto get_b2 = [&](int s, bf16x8& bh, bf16x8& bl) { bh = b2h[s]; bl = b2l[s]; };
-  if (BWD || blockfull)
-    run_layer<PREC, NT2, NT2, 2 * NT1>(a.L[2], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2);
-  else
-    run_layer<PREC, NT2, 1, 2 * NT1>(a.L[2], 2 * NT1, 1, acc2, wave, lane, ring, nopre, get_b2);
-  epilogue_any<NT2, BWD>(acc2, a.L[2], sbias[2], nt2, m, mc, mval, !BWD && !rowfull, h, a.beta, a.thr);
+  {
+    float* orow1 = orow_of(a.L[1]);
+    auto get_b2 = [&](int s, bf16x8& bh, bf16x8& bl) {
+      if constexpr (!BWD) {
+        if ((s & 1) == 0) {
+          epi_tile_full<A1, KEEP>(acc1[s >> 1], s >> 1, sbias[1], orow1, h, a.beta, a.thr);
+          tile_to_b<PREC>(acc1[s >> 1], &b2h[s], &b2l[s]);
+        }
+      }
+      bh = b2h[s]; bl = b2l[s];
+    };
+    if (BWD || blockfull)
+      run_layer<PREC, NT2, NT2, 2 * NT1>(a.L[2], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2);
+    else
+      run_layer<PREC, NT2, 1, 2 * NT1>(a.L[2], 2 * NT1, 1, acc2, wave, lane, ring, nopre, get_b2);
+  }
+  epilogue<NT2, BWD, A2>(acc2, a.L[2], sbias[2], nt2, m, mc, mval, !BWD && !rowfull, h, a.beta, a.thr);
 }
 
-template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD>
+template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, int XA, bool KEEP = false>
 void launch_chain(const ChainArgs& a, hipStream_t s) {
   const unsigned blocks = (unsigned)((a.M + 127) / 128);
-  hipLaunchKernelGGL((chain_kernel<PREC, KS0, NT0, NT1, NT2, BWD>), dim3(blocks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((chain_kernel<PREC, KS0, NT0, NT1, NT2, BWD, A0, A1, A2, XA, KEEP>), dim3(blocks), dim3(256), 0, s,
+                     a);
 }
 
-// the chains of the SDF and radiance fields (ks0 = ceil(K0 / 16), nt_l = ceil(N_l / 32))
+// the chains of the SDF and radiance fields (ks0 = ceil(K0 / 16), nt_l = ceil(N_l / 32)) with their activations:
+// SDF Softplus(100), Softplus(100), identity; radiance ReLU x 3 (backward: derivative ids of layers 1, 0 and none,
+// the input scaled by the last ReLU's derivative).  Forward: both hidden layers full (256 units) and stored
+// together (keep) or neither.
 template <int PREC>
 bool dispatch_chain(int ks0, int nt0, int nt1, int nt2, bool bwd, const ChainArgs& a, hipStream_t s) {
-  if (!bwd && ks0 == 5 && nt0 == 8 && nt1 == 8 && nt2 == 9) launch_chain<PREC, 5, 8, 8, 9, false>(a, s);
-  else if (!bwd && ks0 == 20 && nt0 == 8 && nt1 == 8 && nt2 == 8) launch_chain<PREC, 20, 8, 8, 8, false>(a, s);
-  else if (bwd && ks0 == 17 && nt0 == 8 && nt1 == 8 && nt2 == 3) launch_chain<PREC, 17, 8, 8, 3, true>(a, s);
-  else if (bwd && ks0 == 16 && nt0 == 8 && nt1 == 8 && nt2 == 10) launch_chain<PREC, 16, 8, 8, 10, true>(a, s);
-  else return false;
+  const int a0 = a.L[0].act, a1 = a.L[1].act, a2 = a.L[2].act;
+  const bool noxa = a.xaux == nullptr;
+  const bool hidden_full = a.L[0].N == 256 && a.L[1].N == 256;
+  const bool keep = a.L[0].out != nullptr && a.L[1].out != nullptr;
+  const bool nokeep = a.L[0].out == nullptr && a.L[1].out == nullptr;
+  if (!bwd && ks0 == 5 && nt0 == 8 && nt1 == 8 && nt2 == 9 && a0 == 2 && a1 == 2 && a2 == 0 && hidden_full &&
+      (keep || nokeep)) {
+    if (keep) launch_chain<PREC, 5, 8, 8, 9, false, 2, 2, 0, 0, true>(a, s);
+    else launch_chain<PREC, 5, 8, 8, 9, false, 2, 2, 0, 0, false>(a, s);
+  } else if (!bwd && ks0 == 20 && nt0 == 8 && nt1 == 8 && nt2 == 8 && a0 == 1 && a1 == 1 && a2 == 1 &&
+             hidden_full && keep) {
+    launch_chain<PREC, 20, 8, 8, 8, false, 1, 1, 1, 0, true>(a, s);
+  } else if (bwd && ks0 == 17 && nt0 == 8 && nt1 == 8 && nt2 == 3 && a0 == 2 && a1 == 2 && a2 == 0 &&
+             (noxa || a.xact == 0)) {
+    launch_chain<PREC, 17, 8, 8, 3, true, 2, 2, 0, 0>(a, s);
+  } else if (bwd && ks0 == 16 && nt0 == 8 && nt1 == 8 && nt2 == 10 && a0 == 1 && a1 == 1 && a2 == 0 &&
+             (noxa || a.xact == 1)) {
+    launch_chain<PREC, 16, 8, 8, 10, true, 1, 1, 0, 1>(a, s);
+  } else {
+    return false;
+  }
   return true;
 }
 
@@ -487,6 +547,6 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx
   hipStream_t s = mms::as_stream(stream);
   const bool ok = prec == 1 ? dispatch_chain<1>(ks0, nt[0], nt[1], nt[2], backward != 0, a, s)
                             : dispatch_chain<2>(ks0, nt[0], nt[1], nt[2], backward != 0, a, s);
-  MMS_REQUIRE(ok, fn, "unsupported chain shape (SDF 71-256-256-257 and radiance 317-256-256-256 chains only)");
+  MMS_REQUIRE(ok, fn, "unsupported chain shape or activations (SDF 71-256-256-257 Softplus and radiance 317-256-256-256 ReLU chains only)");
   return mms::check_launch(fn);
 }
