@@ -24,7 +24,10 @@ def label(name):
     m = re.search(r"gemm_kernel<(\d), (true|false), (true|false), (true|false)>", name)
     if m:
         return f"mms_gemm:{PREC[m.group(1)]}:{MODE.get((m.group(2), m.group(3)), '??')}"
-    if "hashgrid_bwd_kernel" in name:
+    m = re.search(r"chain_kernel<(\d), \d+, \d+, \d+, \d+, (true|false)", name)
+    if m:
+        return f"mms_mlp_chain:{PREC[m.group(1)]}:chain_{'bwd' if m.group(2) == 'true' else 'fwd'}"
+    if "hashgrid_bwd" in name:
         return "mms_hashgrid_bwd_grouped"
     if "hashgrid_fwd_kernel" in name:
         return "mms_hashgrid_fwd"
