@@ -215,13 +215,18 @@ int mms_geo_loss_bwd_masked(const float* grads, const float* hess, int64_t M, in
                             const float* inv_total, const float* deik, float eik_scale, const float* dcurv,
                             float curv_scale, float* dgrads, float* dhess, void* stream);
 
-/* ---- optimizer (pipelines/base_pipeline.py:232-248 clip_gradients, torch.optim.AdamW): acc += sum x^2 ;
- * AdamW with clip coefficient min(1, max_norm / (sqrt(*sumsq) + 1e-6)) read on device */
+/* ---- optimizer (pipelines/base_pipeline.py:232-248 clip_gradients, torch.optim.AdamW single-tensor step,
+ * method_configs.py:260-269): acc += sum x^2 ; AdamW with clip coefficient min(1, max_norm / (sqrt(*sumsq) + 1e-6))
+ * read on device.  lr / wd / betas / eps are torch.optim.AdamW's hyper-parameters, step the optimizer's step count
+ * (1 on the first update); the scalars are formed in double like torch's Python code and rounded to float. */
 int mms_sumsq(const float* x, int64_t n, float* acc, void* stream);
-int mms_adamw(float* p, const float* g, float* m, float* v, int64_t n, const float* sumsq, float max_norm, float lr,
-              float wd, float beta1, float beta2, float eps, float step_size, float bc2_sqrt, void* stream);
-/* the same step with its per-step scalars read on the device: hyper = [lr, wd, beta1, beta2, eps, step_size,
- * bc2_sqrt] (graph replays: the host rewrites the 7 floats before each launch) */
+int mms_adamw(float* p, const float* g, float* m, float* v, int64_t n, const float* sumsq, float max_norm, double lr,
+              double wd, double beta1, double beta2, double eps, int64_t step, void* stream);
+/* HOST function: the 7 per-step floats the kernel uses, into host memory hyper[7] = [1 - lr wd, 1 - beta1, beta2,
+ * 1 - beta2, eps, -lr / (1 - beta1^step), (1 - beta2^step)^0.5] */
+int mms_adamw_scalars(double lr, double wd, double beta1, double beta2, double eps, int64_t step, float* hyper);
+/* the same step with its per-step scalars read on the device from hyper[7] (mms_adamw_scalars' layout; graph replays:
+ * the host rewrites the 7 floats before each launch) */
 int mms_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* sumsq, float max_norm,
                   const float* hyper, void* stream);
 

@@ -51,6 +51,73 @@ inline unsigned grid_for(int64_t n, int block, int64_t cap = 1 << 20) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// torch.exp / torch.sigmoid as the reference's CPU build evaluates them, bit for bit: ATen's vectorised float
+// sigmoid is reciprocal(1 + exp(0 - x)) with Vectorized<float>::exp = SLEEF's expf_u10 (Cody-Waite reduction
+// by ln2 in two FMA steps, degree-6 polynomial in FMA Horner form, ldexp in two halves).  Checked against
+// torch.sigmoid on 2e7 floats in [-90, 90] and N(0, 30): 0 mismatches (tests/test_oracle_golden.py pins the
+// host restatement).  The NeuS sampler needs it: its searchsorted indices and bins are compared bit-exactly
+// with the reference (ray_samplers.py:545-546).
+__device__ __forceinline__ float pow2i_(int q) { return __int_as_float((q + 0x7f) << 23); }
+
+__device__ __forceinline__ float sleef_expf_u10(float d) {
+#pragma clang fp contract(off)
+  const int q = (int)__builtin_rintf(d * 1.442695040888963407359924681001892137426645954152985934135449406931f);
+  const float qf = (float)q;
+  float s = __builtin_fmaf(qf, -0.693145751953125f, d);
+  s = __builtin_fmaf(qf, -1.428606765330187045e-06f, s);
+  float u = 0.000198527617612853646278381f;
+  u = __builtin_fmaf(u, s, 0.00139304355252534151077271f);
+  u = __builtin_fmaf(u, s, 0.00833336077630519866943359f);
+  u = __builtin_fmaf(u, s, 0.0416664853692054748535156f);
+  u = __builtin_fmaf(u, s, 0.166666671633720397949219f);
+  u = __builtin_fmaf(u, s, 0.5f);
+  u = 1.0f + __builtin_fmaf(s * s, u, s);
+  const int q1 = q >> 1;
+  u = u * pow2i_(q1);
+  u = u * pow2i_(q - q1);
+  if (d < -104.f) u = 0.f;
+  if (d > 100.f) u = __builtin_inff();
+  return u;
+}
+
+__device__ __forceinline__ float torch_cpu_sigmoid(float x) { return 1.0f / (1.0f + sleef_expf_u10(0.0f - x)); }
+
+// torch.sum(x[0:n]) of a contiguous float row as ATen's CPU reduction orders it (SumKernel.cpp cascade_sum ->
+// vectorized_inner_sum with 8-wide vectors, row_sum's 4 ILP partials, scalar tail first, then the 8 partial lanes):
+// matches torch.sum over dim=-1 bit for bit for rows of 33..65 elements (checked in this container).  n < 8 rows
+// take ATen's scalar path, a plain sequential sum.
+__device__ __forceinline__ float torch_cpu_row_sum(const float* x, int n) {
+#pragma clang fp contract(off)
+  if (n < 8) {
+    float s = 0.f;
+    for (int k = 0; k < n; ++k) s = s + x[k];
+    return s;
+  }
+  float P[4][8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int l = 0; l < 8; ++l) P[k][l] = 0.f;
+  const int V = n >> 3, nI = V >> 2;
+  for (int i = 0; i < nI; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int l = 0; l < 8; ++l) P[k][l] = P[k][l] + x[8 * (4 * i + k) + l];
+  for (int i = 4 * nI; i < V; ++i)
+#pragma unroll
+    for (int l = 0; l < 8; ++l) P[0][l] = P[0][l] + x[8 * i + l];
+#pragma unroll
+  for (int k = 1; k < 4; ++k)
+#pragma unroll
+    for (int l = 0; l < 8; ++l) P[0][l] = P[0][l] + P[k][l];
+  float fin = 0.f;
+  for (int k = 8 * V; k < n; ++k) fin = fin + x[k];
+#pragma unroll
+  for (int l = 0; l < 8; ++l) fin = fin + P[0][l];
+  return fin;
+}
+
 // MLP activations for GEMM epilogues (ids: 0 none, 1 ReLU, 2 Softplus(beta, threshold), 3 Sigmoid).
 // Built on the hardware transcendentals (v_exp_f32 = 2^x, v_log_f32 = log2, v_rcp_f32; ~1 ulp): the
 // accurate libm log1pf/expf forms cost ~150 VALU ops per element, which made the epilogue of a 270k x 256

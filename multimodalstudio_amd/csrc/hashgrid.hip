@@ -75,6 +75,7 @@ __device__ __forceinline__ Corners make_corners(float x, float y, float z, float
   return c;
 }
 
+template <bool ALIGNED>
 __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(const float* __restrict__ pos, int64_t M,
                                                            int64_t ldx, const float2* __restrict__ table,
                                                            GridParams p, float* __restrict__ out,
@@ -102,7 +103,13 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(const float* __restri
     r.x = f0312.x * oz + f4756.x * nz;
     r.y = f0312.y * oz + f4756.y * nz;
   }
-  *reinterpret_cast<float2*>(out + pt * ldo + 2 * level) = r;
+  float* o = out + pt * ldo + 2 * level;
+  if (ALIGNED) {
+    *reinterpret_cast<float2*>(o) = r;  // 8-B aligned: one dwordx2 store
+  } else {
+    o[0] = r.x;  // panels with the grid at an odd column (SDF panel col 39): two dword stores
+    o[1] = r.y;
+  }
 }
 
 // Backward ("walk"): one workgroup = 16 level groups x 16 lanes and owns CH consecutive point groups (rows
@@ -243,10 +250,15 @@ MMS_EXPORT int mms_hashgrid_fwd(const float* pos, int64_t M, int64_t ldx, const 
   if (rc) return rc;
   if (M == 0) return 0;
   MMS_REQUIRE(pos && table && out, fn, "null pointer");
+  MMS_REQUIRE(((uintptr_t)out & 3) == 0, fn, "output must be 4-B aligned");
   const int64_t threads = M * 16;
-  hipLaunchKernelGGL(hashgrid_fwd_kernel, dim3(mms::grid_for(threads, 256, INT32_MAX)), dim3(256), 0,
-                     mms::as_stream(stream), pos, M, ldx, reinterpret_cast<const float2*>(table), p, out,
-                     ldo);
+  const bool aligned = ((uintptr_t)out & 7) == 0 && (ldo & 1) == 0;
+  if (aligned)
+    hipLaunchKernelGGL(hashgrid_fwd_kernel<true>, dim3(mms::grid_for(threads, 256, INT32_MAX)), dim3(256), 0,
+                       mms::as_stream(stream), pos, M, ldx, reinterpret_cast<const float2*>(table), p, out, ldo);
+  else
+    hipLaunchKernelGGL(hashgrid_fwd_kernel<false>, dim3(mms::grid_for(threads, 256, INT32_MAX)), dim3(256), 0,
+                       mms::as_stream(stream), pos, M, ldx, reinterpret_cast<const float2*>(table), p, out, ldo);
   return mms::check_launch(fn);
 }
 

@@ -10,6 +10,8 @@
 // Every scalar stays on the device (no host synchronisation inside a step).
 #include "common.h"
 
+#include <math.h>
+
 namespace {
 
 __device__ __forceinline__ float block_reduce_sum(float v) {
@@ -142,25 +144,30 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
   if (threadIdx.x == 0) atomicAdd(acc, s);
 }
 
-// AdamW with the clip coefficient coef = min(1, max_norm / (sqrt(sumsq) + 1e-6)) applied to g.
+// AdamW with the clip coefficient coef = min(1, max_norm / (sqrt(sumsq) + 1e-6)) applied to g, in the operation
+// order of torch.optim.AdamW's single-tensor CPU step (the reference's optimizer):
+//   p *= decay;  m = lerp(m, g, 1 - b1) = fma(1 - b1, g - m, m)  (ATen's vectorised lerp, small weight);
+//   v = v * b2 + ((1 - b2) * g) * g  (addcmul);  p = p + ((-step_size) * m) / (sqrt(v) / bc2_sqrt + eps)  (addcdiv)
+// with the scalars rounded from the double values Python computes (mms_adamw_scalars): hyper = [decay, 1 - b1, b2,
+// 1 - b2, eps, -step_size, bc2_sqrt].  Contraction off: only the lerp is fused, as in ATen.
 __device__ __forceinline__ void adamw_apply(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                             float* __restrict__ v, int64_t n, const float* __restrict__ sumsq,
-                                            float max_norm, float lr, float wd, float beta1, float beta2, float eps,
-                                            float step_size, float bc2_sqrt) {
+                                            float max_norm, float decay, float w1, float b2, float w2, float eps,
+                                            float neg_step, float bc2_sqrt) {
+#pragma clang fp contract(off)
   float coef = 1.0f;
   if (sumsq != nullptr && max_norm > 0.f) {
     const float total = sqrtf(sumsq[0]);
     coef = fminf(max_norm / (total + 1e-6f), 1.0f);
   }
-  const float decay = 1.0f - lr * wd;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float gi = g[i] * coef;
     float pi = p[i] * decay;
     float mi = m[i];
-    mi = mi + (1.0f - beta1) * (gi - mi);
-    float vi = v[i] * beta2 + (1.0f - beta2) * gi * gi;
+    mi = __builtin_fmaf(w1, gi - mi, mi);
+    const float vi = v[i] * b2 + (w2 * gi) * gi;
     const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    pi = pi - step_size * (mi / denom);
+    pi = pi + (neg_step * mi) / denom;
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;
@@ -169,13 +176,13 @@ __device__ __forceinline__ void adamw_apply(float* __restrict__ p, const float* 
 
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, int64_t n,
-                                                    const float* __restrict__ sumsq, float max_norm, float lr, float wd,
-                                                    float beta1, float beta2, float eps, float step_size,
+                                                    const float* __restrict__ sumsq, float max_norm, float decay,
+                                                    float w1, float b2, float w2, float eps, float neg_step,
                                                     float bc2_sqrt) {
-  adamw_apply(p, g, m, v, n, sumsq, max_norm, lr, wd, beta1, beta2, eps, step_size, bc2_sqrt);
+  adamw_apply(p, g, m, v, n, sumsq, max_norm, decay, w1, b2, w2, eps, neg_step, bc2_sqrt);
 }
 
-// the per-step scalars read on the device: hyper = [lr, wd, beta1, beta2, eps, step_size, bc2_sqrt]
+// the per-step scalars read on the device (graph replays): hyper = mms_adamw_scalars' 7 floats
 __global__ __launch_bounds__(256) void adamw_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                         const float* __restrict__ sumsq, float max_norm,
@@ -262,13 +269,33 @@ MMS_EXPORT int mms_sumsq(const float* x, int64_t n, float* acc, void* stream) {
   return mms::check_launch(fn);
 }
 
+MMS_EXPORT int mms_adamw_scalars(double lr, double wd, double beta1, double beta2, double eps, int64_t step,
+                                 float* hyper) {
+  const char* fn = "mms_adamw_scalars";
+  MMS_REQUIRE(hyper != nullptr, fn, "null output");
+  MMS_REQUIRE(step >= 1, fn, "step counts from 1 (torch.optim.AdamW increments before use)");
+  // torch/optim/adamw.py (single-tensor): Python doubles, rounded to float where they meet a float tensor
+  const double bc1 = 1.0 - pow(beta1, (double)step);
+  const double bc2 = 1.0 - pow(beta2, (double)step);
+  hyper[0] = (float)(1.0 - lr * wd);
+  hyper[1] = (float)(1.0 - beta1);
+  hyper[2] = (float)beta2;
+  hyper[3] = (float)(1.0 - beta2);
+  hyper[4] = (float)eps;
+  hyper[5] = (float)(-(lr / bc1));
+  hyper[6] = (float)pow(bc2, 0.5);
+  return 0;
+}
+
 MMS_EXPORT int mms_adamw(float* p, const float* g, float* m, float* v, int64_t n, const float* sumsq, float max_norm,
-                         float lr, float wd, float beta1, float beta2, float eps, float step_size, float bc2_sqrt,
-                         void* stream) {
+                         double lr, double wd, double beta1, double beta2, double eps, int64_t step, void* stream) {
   const char* fn = "mms_adamw";
+  float h[7];
+  const int rc = mms_adamw_scalars(lr, wd, beta1, beta2, eps, step, h);
+  if (rc) return rc;
   if (n == 0) return 0;
   hipLaunchKernelGGL(adamw_kernel, dim3(mms::grid_for(n, 256, 8192)), dim3(256), 0, mms::as_stream(stream), p, g, m, v,
-                     n, sumsq, max_norm, lr, wd, beta1, beta2, eps, step_size, bc2_sqrt);
+                     n, sumsq, max_norm, h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
   return mms::check_launch(fn);
 }
 

@@ -140,11 +140,14 @@ constexpr int nimg() { return PREC == 2 ? 2 : 1; }
 template <int PREC, int NTL>
 constexpr int stage_per() { return (nimg<PREC>() * NTL + 3) / 4; }
 
-// wait until at most N vector-memory operations of this wave are outstanding, then the block barrier (one asm
-// statement with a memory clobber: no LDS read of the ring moves above either)
+// wait until at most N vector-memory operations of this wave are outstanding and its LDS reads have returned,
+// then the block barrier (one asm statement with a memory clobber: no LDS read of the ring moves above either).
+// lgkmcnt(0): gfx950's back-off barrier gets no compiler-inserted wait before an asm s_barrier, so without it a
+// lagging wave's ds_read of slot (s - 1) % 3 could still be in flight when another wave's LDS-DMA overwrites that
+// slot as (s + 2) % 3.  The MFMAs already wait on those reads, so the extra wait costs nothing.
 template <int N>
 __device__ __forceinline__ void wait_vm_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
 // 16 B per lane, global -> LDS (lane-linear at lds_addr), issued as inline asm: the compiler does not see an LDS

@@ -204,7 +204,8 @@ __global__ void collider_fwd_kernel(const float* __restrict__ origins, const flo
     float dot = d[0] * o[0];
     dot = dot + d[1] * o[1];
     dot = dot + d[2] * o[2];
-    const float on = sqrtf(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+    // origins.norm(p=2): ATen's CPU norm accumulates the squares with FMAs (bit-exact to torch.norm)
+    const float on = sqrtf(__builtin_fmaf(o[2], o[2], __builtin_fmaf(o[1], o[1], o[0] * o[0])));
     const float under = dot * dot - (on * on - radius * radius);
     const bool hit = under > 0.01f;
     const float sq = sqrtf(fmaxf(under, 0.01f));
@@ -229,7 +230,8 @@ __global__ void collider_bwd_kernel(const float* __restrict__ origins, const flo
     float dot = d[0] * o[0];
     dot = dot + d[1] * o[1];
     dot = dot + d[2] * o[2];
-    const float on = sqrtf(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+    // origins.norm(p=2): ATen's CPU norm accumulates the squares with FMAs (bit-exact to torch.norm)
+    const float on = sqrtf(__builtin_fmaf(o[2], o[2], __builtin_fmaf(o[1], o[1], o[0] * o[0])));
     const float under = dot * dot - (on * on - radius * radius);
     const bool hit = under > 0.01f;
     const float sq = sqrtf(fmaxf(under, 0.01f));

@@ -10,16 +10,19 @@
 //   merge_ray_samples                   :38-68     (sort of the two start lists + max end)
 // and cameras/rays.py:201-217 (weights from alphas), :69-81 (start positions o + d * start).
 //
-// Bin values depend only on float32 arithmetic performed in the reference's order (no contraction);
-// the PDF cumulative sums and transmittance products are sequential like torch.cumsum / cumprod on
-// CPU, so searchsorted indices and merge order (sorted_index) match the reference.
+// Bin values depend only on float32 arithmetic performed in the reference's order (no contraction): the
+// transmittance product and the CDF are sequential in double like torch.cumprod / cumsum on CPU, the weight sum
+// follows ATen's vectorised CPU reduction order and the sigmoid is torch's CPU SLEEF form (common.h), so bins,
+// searchsorted indices and the merge order (sorted_index) equal the reference's bit for bit
+// (tests/test_gpu_sampler.py against tests/golden/neus_sampler.npz).
 #include "common.h"
 
 #pragma clang fp contract(off)
 
 namespace {
 
-__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// torch.sigmoid exactly as the reference's CPU path computes it (common.h: SLEEF expf_u10 + IEEE division)
+__device__ __forceinline__ float sigm(float x) { return mms::torch_cpu_sigmoid(x); }
 
 // stratified bins: lin [S+1]; t either per ray ([R,1], tstride=1, tcols=1) or per bin ([R, S+1])
 __global__ void stratified_bins_kernel(const float* __restrict__ lin, int nb, const float* __restrict__ t, int tcols,
@@ -186,12 +189,9 @@ __global__ __launch_bounds__(64) void neus_step_kernel(
   }
   cdf[S] = 0.0f;
   // (e) pdf / cdf with padding 1e-5 (histogram_padding) and eps 1e-5
-  float wsum = 0.f;
-  for (int k = 0; k < S; ++k) {
-    const float w = cdf[k + 1] + 1e-5f;
-    cdf[k + 1] = w;
-    wsum = wsum + w;
-  }
+  for (int k = 0; k < S; ++k) cdf[k + 1] = cdf[k + 1] + 1e-5f;
+  // torch.sum(weights, -1) in ATen's CPU summation order (not sequential), so weights_sum has the same bits
+  float wsum = mms::torch_cpu_row_sum(cdf + 1, S);
   const float pad = fmaxf(1e-5f - wsum, 0.f);
   const float padk = pad / (float)S;
   wsum = wsum + pad;

@@ -130,7 +130,7 @@ class GraphTrainer:
                 c = self.coords[m]
                 band = t.masks[m][c[:, 1].long(), c[:, 2].long()].long()[:, None]
                 outputs[m][m] = select_right_channel(outputs[m][m], band)
-        losses, total = compute_loss(outputs, targets, t.modalities, t.step)
+        losses, total = compute_loss(outputs, targets, t.modalities, t.step, max_iters=t.cfg.max_iters)
         total.backward()
         return losses, total
 

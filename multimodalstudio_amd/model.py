@@ -335,6 +335,58 @@ def _linspace(n: int, lo: float = 0.0, hi: float = 1.0) -> torch.Tensor:
     return torch.linspace(lo, hi, n)
 
 
+def sample_start_positions(bins, n, f, o, d) -> torch.Tensor:
+    """Start positions o + d * start of the uniform-spacing samples of ``bins`` [R, S+1] (rays.py:69-81), [R*S, 3]."""
+    R, nb = bins.shape
+    pos = torch.empty(R * (nb - 1), 3, device=bins.device)
+    _lib.call("mms_samples_fwd", bins.data_ptr(), nb, nb, n.data_ptr(), f.data_ptr(), o.data_ptr(), d.data_ptr(),
+              0, R, None, None, None, pos.data_ptr(), fx._s())
+    return pos
+
+
+@torch.no_grad()
+def neus_sample(n_h, f_h, o_h, d_h, t_rand, pdf_rands, sdf_fn, num_samples: int = 32, num_importance: int = 32,
+                upsample_steps: int = 4, base_variance: float = 64.0, lin=None, history: Optional[list] = None):
+    """NeuSSampler.generate_ray_samples (ray_samplers.py:448-514) for one modality's hit rays on the HIP kernels.
+
+    n_h / f_h [R] nears / fars, o_h / d_h [R, 3]; t_rand [R, 1] single-jitter uniforms of the uniform sampler (or
+    None: evaluation, no jitter), pdf_rands: ``upsample_steps`` [R, 1] PDF-sampler uniforms (or None).
+    ``sdf_fn(positions [R*S, 3]) -> sdf [R*S]`` is evaluated at sample starts (the reference's sdf_fn(ray_samples)).
+    Returns the final spacing bins [R, num_samples + num_importance + 1]; ``history`` (a list) receives each
+    iteration's ``sorted_index`` [R, S + n_new] (merge_ray_samples :38-68) -- bit-exact to the reference's."""
+    R = n_h.shape[0]
+    dev = n_h.device
+    if lin is None:
+        lin = lambda n, hi, device: _linspace(n, 0.0, hi).to(device)  # noqa: E731
+    S = num_samples
+    bins = torch.empty(R, S + 1, device=dev)
+    _lib.call("mms_stratified_bins", lin(S + 1, 1.0, dev).data_ptr(), S + 1, fx._p(t_rand), 1, R, bins.data_ptr(),
+              fx._s())
+    n_new = num_importance // upsample_steps
+    u_lin = lin(n_new + 1, 1.0 - 1.0 / (n_new + 1), dev)
+    sdf_prev, prev_idx, s_prev, n_prev_new = None, None, 0, S
+    new_bins = bins
+    for it in range(upsample_steps):
+        sdf_new = sdf_fn(sample_start_positions(new_bins, n_h, f_h, o_h, d_h)).reshape(-1).contiguous()
+        sdf_out = torch.empty(R, S, device=dev)
+        new_bins = torch.empty(R, n_new + 1, device=dev)
+        merged = torch.empty(R, S + n_new + 1, device=dev)
+        sidx = torch.empty(R, S + n_new, dtype=torch.int32, device=dev)
+        rnd = pdf_rands[it] if pdf_rands is not None else None
+        if rnd is not None:
+            rnd = rnd.contiguous()
+        _lib.call("mms_neus_step", R, S, bins.data_ptr(), fx._p(sdf_prev), s_prev, sdf_new.data_ptr(), n_prev_new,
+                  fx._p(prev_idx), n_h.data_ptr(), f_h.data_ptr(), float(base_variance * 2 ** it), fx._p(rnd),
+                  u_lin.data_ptr(), n_new, sdf_out.data_ptr(), new_bins.data_ptr(), merged.data_ptr(),
+                  sidx.data_ptr(), fx._s())
+        if history is not None:
+            history.append(sidx)
+        sdf_prev, prev_idx, s_prev, n_prev_new = sdf_out, sidx, S, n_new
+        bins = merged
+        S += n_new
+    return bins
+
+
 class BaseModel(nn.Module):
     """BaseModel (base_model.py:38-199) — collider -> NeuS sampler -> background -> surface -> radiance -> render."""
 
@@ -392,41 +444,8 @@ class BaseModel(nn.Module):
     @torch.no_grad()
     def neus_bins(self, n_h, f_h, o_h, d_h, t_rand, pdf_rands):
         sp = self.spec
-        R = n_h.shape[0]
-        dev = n_h.device
-        S = sp.num_samples
-        lin = self._lin_dev(S + 1, 1.0, dev)
-        bins = torch.empty(R, S + 1, device=dev)
-        _lib.call("mms_stratified_bins", lin.data_ptr(), S + 1, fx._p(t_rand), 1, R, bins.data_ptr(), fx._s())
-        n_new = sp.num_importance // sp.upsample_steps
-        u_lin = self._lin_dev(n_new + 1, 1.0 - 1.0 / (n_new + 1), dev)
-        pos = self._positions(bins, n_h, f_h, o_h, d_h)
-        sdf_new = self.surface_model.get_sdf(pos)
-        sdf_prev, prev_idx, s_prev, n_prev_new = None, None, 0, S
-        new_bins = None
-        for it in range(sp.upsample_steps):
-            if it > 0:
-                sdf_new = self.surface_model.get_sdf(self._positions(new_bins, n_h, f_h, o_h, d_h))
-            sdf_out = torch.empty(R, S, device=dev)
-            new_bins = torch.empty(R, n_new + 1, device=dev)
-            merged = torch.empty(R, S + n_new + 1, device=dev)
-            sidx = torch.empty(R, S + n_new, dtype=torch.int32, device=dev)
-            rnd = pdf_rands[it] if pdf_rands is not None else None
-            _lib.call("mms_neus_step", R, S, bins.data_ptr(), fx._p(sdf_prev), s_prev, sdf_new.data_ptr(), n_prev_new,
-                      fx._p(prev_idx), n_h.data_ptr(), f_h.data_ptr(), float(sp.base_variance * 2 ** it),
-                      fx._p(rnd), u_lin.data_ptr(), n_new, sdf_out.data_ptr(), new_bins.data_ptr(), merged.data_ptr(),
-                      sidx.data_ptr(), fx._s())
-            sdf_prev, prev_idx, s_prev, n_prev_new = sdf_out, sidx, S, n_new
-            bins = merged
-            S += n_new
-        return bins
-
-    def _positions(self, bins, n, f, o, d):
-        R, nb = bins.shape
-        pos = torch.empty(R * (nb - 1), 3, device=bins.device)
-        _lib.call("mms_samples_fwd", bins.data_ptr(), nb, nb, n.data_ptr(), f.data_ptr(), o.data_ptr(), d.data_ptr(),
-                  0, R, None, None, None, pos.data_ptr(), fx._s())
-        return pos
+        return neus_sample(n_h, f_h, o_h, d_h, t_rand, pdf_rands, self.surface_model.get_sdf, sp.num_samples,
+                           sp.num_importance, sp.upsample_steps, sp.base_variance, lin=self._lin_dev)
 
     # -- forward ----------------------------------------------------------------------------------------
     def forward(self, rays: Dict[str, Dict[str, torch.Tensor]], rng: Optional[RNG] = None, cap: Optional[int] = None):

@@ -139,7 +139,7 @@ class FlatGroup:
         self.m = torch.zeros(n + pad, device=dev)
         self.v = torch.zeros(n + pad, device=dev)
         self.sumsq = torch.zeros(1, device=dev)
-        # this step's AdamW scalars for graph replays (mms_adamw_dev): [lr, wd, beta1, beta2, eps, step_size, bc2_sqrt]
+        # this step's AdamW scalars for graph replays (mms_adamw_dev; layout of mms_adamw_scalars)
         self.hyper = torch.zeros(8, device=dev)
         self._hyper_host = torch.zeros(8).pin_memory() if dev.type == "cuda" else torch.zeros(8)
         off = 0
@@ -171,26 +171,26 @@ class FlatGroup:
             off += k
 
     def _advance(self, lr_factor: float):
-        """Advance the step counter; torch AdamW's scalars for this step."""
+        """Advance the optimizer's step counter (torch AdamW's state['step'], 1 on the first update); this step's
+        base-scheduled learning rate."""
         self.step_count += 1
-        t = self.step_count
-        b1, b2 = self.betas
-        lr = self.lr * lr_factor
-        return [lr, self.wd, b1, b2, self.eps, lr / (1 - b1 ** t), math.sqrt(1 - b2 ** t)]
+        return self.lr * lr_factor
 
     def step(self, lr_factor: float, max_norm: float = 2.0):
         """clip_grad_norm_(max_norm) then torch AdamW math (single launch each; scalars stay on device)."""
         self.check_grads_attached()
-        h = self._advance(lr_factor)
+        lr = self._advance(lr_factor)
         self.sumsq.zero_()
         _lib.call("mms_sumsq", self.grad.data_ptr(), self.n, self.sumsq.data_ptr(), _s())
         _lib.call("mms_adamw", self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.n,
-                  self.sumsq.data_ptr(), float(max_norm), *[float(x) for x in h], _s())
+                  self.sumsq.data_ptr(), float(max_norm), float(lr), float(self.wd), float(self.betas[0]),
+                  float(self.betas[1]), float(self.eps), int(self.step_count), _s())
 
     def load_hyper(self, lr_factor: float):
         """Graph mode, before a replay: advance the step and upload its scalars (read by the captured launch)."""
-        h = self._advance(lr_factor)
-        self._hyper_host[:7] = torch.tensor(h, dtype=torch.float32)
+        lr = self._advance(lr_factor)
+        _lib.call("mms_adamw_scalars", float(lr), float(self.wd), float(self.betas[0]), float(self.betas[1]),
+                  float(self.eps), int(self.step_count), self._hyper_host.data_ptr())
         self.hyper.copy_(self._hyper_host, non_blocking=True)
 
     def step_captured(self, max_norm: float = 2.0):
@@ -226,8 +226,9 @@ def curvature_factor(step: int, max_iters: int = 100000, num_levels=16, min_res=
 # losses
 # ------------------------------------------------------------------------------------------------
 def compute_loss(outputs, targets: Dict[str, torch.Tensor], modalities: List[str], step: int,
-                 sat_threshold: float = 0.9980):
-    """LossManager.compute_loss (losses.py:224-265) for the grid / grid_raw configs."""
+                 sat_threshold: float = 0.9980, max_iters: int = 100000):
+    """LossManager.compute_loss (losses.py:224-265) for the grid / grid_raw configs.  ``max_iters`` is the run's
+    num_iterations: the curvature weight's warm-up / level schedule follows it (schedulers.py:320-343)."""
     losses = {}
     total = None
     for mod in modalities:
@@ -244,7 +245,7 @@ def compute_loss(outputs, targets: Dict[str, torch.Tensor], modalities: List[str
         eik, curv = fx.GeoLossMaskedFunction.apply(S, counts, *grads, *hess)
     else:
         eik, curv = fx.GeoLossFunction.apply(*grads, *hess)
-    cf = curvature_factor(step)
+    cf = curvature_factor(step, max_iters)
     losses["eikonal_loss"] = eik
     losses["curvature_loss"] = curv
     total = total + 0.1 * eik + (5e-4 * cf) * curv
@@ -312,11 +313,11 @@ class Trainer:
         return out
 
     def set_step(self, step: int):
+        """Position the schedules (LR, callbacks) at ``step``.  The optimizers keep their own update counts: a
+        trainer positioned at step 95000 with fresh moments is a fresh torch AdamW (state['step'] starts at 0)
+        under a LambdaLR at 95000."""
         self.step = step
         self.model.set_step(step, self.cfg.max_iters)
-        self.fields.step_count = step
-        if self.poses is not None:
-            self.poses.step_count = step
 
     def train_step(self, coords=None, targets=None, rng: Optional[RNG] = None, ddp=None):
         """One training iteration (raw_pipeline.py:67-82); the BEFORE_TRAIN_ITERATION callbacks (coarse-to-fine
@@ -335,7 +336,7 @@ class Trainer:
             for m in self.modalities:
                 band = self.masks[m][coords_d[m][:, 1].long(), coords_d[m][:, 2].long()].long()[:, None]
                 outputs[m][m] = select_right_channel(outputs[m][m], band)
-        losses, total = compute_loss(outputs, targets_d, self.modalities, self.step)
+        losses, total = compute_loss(outputs, targets_d, self.modalities, self.step, max_iters=self.cfg.max_iters)
         self.fields.zero_grad()
         if self.poses is not None:
             self.poses.zero_grad()

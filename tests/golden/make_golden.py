@@ -271,8 +271,32 @@ def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=F
     sampler.generator.manual_seed(654824)
     coords, pixels = sampler.sample(frames)
     rb = gen(coords)
-    with record_rand() as draws:
-        outputs = model(rb)
+    # record the collider masks and the sampler's final spacing bins per modality (base_model.py:86-95)
+    import model_components.scene_colliders as scm
+    import model_components.ray_samplers as rsm
+    seen = {}
+    orig_update = scm.ColliderInstancer.update_ray_bundles
+    orig_gen = rsm.NeuSSampler.generate_ray_samples
+
+    def update(self, bundles):
+        masks = orig_update(self, bundles)
+        seen.setdefault("masks", {k: v.clone() for k, v in masks.items()})
+        return masks
+
+    def generate(self, *a, **k):
+        out = orig_gen(self, *a, **k)
+        seen["bins"] = {m: torch.cat([rs.spacing_starts[..., 0], rs.spacing_ends[..., -1:, 0]], -1).detach().clone()
+                        for m, rs in out["ray_samples_per_modality"].items()}
+        return out
+
+    scm.ColliderInstancer.update_ray_bundles = update
+    rsm.NeuSSampler.generate_ray_samples = generate
+    try:
+        with record_rand() as draws:
+            outputs = model(rb)
+    finally:
+        scm.ColliderInstancer.update_ray_bundles = orig_update
+        rsm.NeuSSampler.generate_ray_samples = orig_gen
     # loss (raw_pipeline.py:112-122 + losses.py)
     lm = cfg.pipeline.loss_manager.setup(modalities=list(mods), num_iterations=100000, model=model)
     if raw:
@@ -300,6 +324,8 @@ def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=F
         arrays[f"{m}:dpose"] = opt.pose_adjustment[m].grad
         for k in ["c2w", "fx", "fy", "cx", "cy", "distortion"]:
             arrays[f"{m}:{k}"] = getattr(cams[m], k)
+        arrays[f"{m}:mask"] = seen["masks"][m]
+        arrays[f"{m}:bins"] = seen["bins"][m]
         o = outputs[m]
         for k in ["normals", "depth", "accumulation", "gradients", "hessians", "inv_s"]:
             arrays[f"{m}:out:{k}"] = o[k].detach()

@@ -78,8 +78,26 @@ def test_ops_fail_loudly_on_cpu_tensors():
 def test_lr_and_curvature_schedules_match_oracle():
     from multimodalstudio_amd import pipeline
     from oracle import model as om
-    for step in (0, 1, 999, 10000, 10001, 49999, 50000, 75000, 90000, 99999):
-        assert pipeline.lr_factor(step, 100000) == pytest.approx(om.lr_factor(step, 100000), rel=0, abs=0)
+    for max_iters in (100000, 50000, 20000):
+        for step in (0, 1, 999, 4999, 10000, 10001, 19999, 49999, 50000, 75000, 90000, 99999):
+            if step >= max_iters:
+                continue
+            assert pipeline.lr_factor(step, max_iters) == om.lr_factor(step, max_iters)
+            st = om.StepState(step=step, max_iters=max_iters)
+            assert pipeline.curvature_factor(step, max_iters) == st.curvature_factor, (step, max_iters)
+
+
+def test_compute_loss_uses_the_runs_max_iters():
+    """The curvature weight follows num_iterations (schedulers.py:320-343): compute_loss must not fall back to the
+    100k default.  Checked on the host through the factor compute_loss passes to the weight."""
+    import inspect
+    from multimodalstudio_amd import pipeline
+    src = inspect.getsource(pipeline.compute_loss)
+    assert "curvature_factor(step, max_iters)" in src
+    assert "max_iters=self.cfg.max_iters" in inspect.getsource(pipeline.Trainer.train_step)
+    from multimodalstudio_amd import graphs
+    assert "max_iters=t.cfg.max_iters" in inspect.getsource(graphs.GraphTrainer._forward_backward)
+    assert pipeline.curvature_factor(45000, 50000) != pipeline.curvature_factor(45000, 100000)
 
 
 def _ddp_worker(rank, world, port, q):

@@ -37,17 +37,20 @@ def test_e2e_fixed_capacity(dev, name):
     assert worst < 5e-2
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fast"])
-def test_graph_trainer_matches_eager(dev, precision):
+@pytest.mark.parametrize("precision,max_iters,start", [("fp32", 100000, 95000), ("fast", 100000, 95000),
+                                                       ("fp32", 50000, 45000)])
+def test_graph_trainer_matches_eager(dev, precision, max_iters, start):
+    """max_iters 50000: the curvature factor (and every other schedule) follow the run's num_iterations in the
+    graph key and in the loss alike."""
     from multimodalstudio_amd import functions as fx
     from multimodalstudio_amd import graphs
     from multimodalstudio_amd import pipeline as pl
     cfg = pl.TrainConfig(method="grid", modalities=("rgb",), num_rays_per_modality=512, log2T=14, n_views=10,
-                         width=160, height=128)
+                         width=160, height=128, max_iters=max_iters)
 
     def make():
         tr = pl.Trainer(cfg, dev)
-        tr.set_step(95000)
+        tr.set_step(start)
         tr.model.eval()       # no sampler jitter: both paths see identical samples
         return tr
 
