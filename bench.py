@@ -31,6 +31,9 @@ CONFIGS = {
     "grid_rgb": ("grid", ("rgb",), "confs/grid.yaml, RGB-only (modalities: [rgb]), hash grid + MLPs, 1 GPU"),
     "grid_raw5": ("grid_raw", ("rgb", "infrared", "mono", "polarization", "multispectral"),
                   "confs/grid_raw.yaml, 5-modality mosaicked, per-modality heads"),
+    "grid_bg5": ("grid_raw_grid_bg_unbalanced", ("rgb", "polarization"),
+                 "confs/grid_raw_rgb_all_views_pol_10_views.yaml, rgb + polarization (10 pol views), hash-grid "
+                 "background, pose refinement"),
 }
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -75,7 +78,11 @@ def chain_work(a):
     else:
         flops = 2.0 * M * (K0 * n0 + n0 * n1) + 2.0 * (rf * n2 + (M - rf)) * n1
         nbytes = 4.0 * (M * K0 + M * (n0 * st[0] + n1 * st[1]) + (rf * n2 + (M - rf)) * st[2])
-    return f"{PREC_NAMES[prec]}:chain{'_bwd' if bwd else '_fwd'}", (flops, nbytes)
+    # which MLP: the SDF field (71 input columns; its backward's last layer has 71 outputs) or the radiance field;
+    # rows_full = 0 marks the sampler's inference-only SDF evaluations
+    narrow_in = (N[2] if bwd else K0) < 128
+    role = ("sdf" if narrow_in else "radiance") + ("_infer" if (not bwd and rf == 0) else "")
+    return f"{PREC_NAMES[prec]}:{role}{'_bwd' if bwd else '_fwd'}", (flops, nbytes)
 
 
 def work_fns():
@@ -85,6 +92,41 @@ def work_fns():
         "mms_hashgrid_fwd": lambda a: float(a[1]) * HASH_FWD_B,
         "mms_hashgrid_bwd_grouped": lambda a: float(a[1]) * a[2] * HASH_BWD_B,
     }
+
+
+def kernel_records(summ, timing_steps: int, precision: str):
+    """One record per watched launch kind: MLP launches (GEMMs, chains) rated by their algorithmic 2MNK flops against
+    the dense bf16 MFMA peak (split-bf16x3 also against its own third-rate ceiling, fp32 against the f32 MFMA peak),
+    hash-grid launches by their SURVEY §8(d) bytes against HBM.  ``traffic`` = HBM bytes per launch from the
+    committed rocprofv3 PMC passes of this workload (profiles/pmc_traffic_<precision>.json), null if not collected."""
+    kernels = []
+    for name, (n, ms, work) in summ.items():
+        launches_per_step = n / timing_steps
+        rec = {"kernel": name, "avg_ms": round(ms, 5), "launches_per_step": launches_per_step,
+               "ms_per_step": round(ms * launches_per_step, 4), "traffic": None}
+        if name.startswith("mms_gemm") or name.startswith("mms_mlp_chain"):
+            flops, nbytes = work
+            mode = name.split(":")[1]      # "mms_gemm:<precision>:<NT|NN|TN>", "mms_mlp_chain:<precision>:<role>"
+            peak = F32_MFMA_PEAK_TF if mode == "fp32" else BF16_MFMA_PEAK_TF
+            ach = flops / (ms * 1e-3) / 1e12
+            rec.update({"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+                        "frac": round(ach / peak, 4), "gbs": round(nbytes / (ms * 1e-3) / 1e9, 1)})
+            if mode == "bf16x3":
+                rec.update({"mode_peak": round(MFMA_PEAK_TF[mode], 1),
+                            "frac_of_mode_peak": round(ach / MFMA_PEAK_TF[mode], 4)})
+        else:
+            ach = work / (ms * 1e-3) / 1e9
+            rec.update({"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4)})
+        kernels.append(rec)
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{precision}.json")
+    pmc = json.load(open(pmc_path))["kernels"] if os.path.exists(pmc_path) else {}
+    for rec in kernels:
+        if rec["kernel"] in pmc:
+            rec["traffic"] = pmc[rec["kernel"]]["hbm_bytes_per_launch"]
+            rec["traffic_unit"] = "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
+    kernels.sort(key=lambda k: -k["ms_per_step"])
+    return kernels
 
 
 def cpu_baseline(trainer, cfg, seconds: float):
@@ -129,6 +171,52 @@ def cpu_baseline(trainer, cfg, seconds: float):
     }
 
 
+def timed_run(config: str, args, dev, rank: int, ddp, steps: int, warmup: int) -> dict:
+    """Build the trainer for ``config``, run ``warmup`` untimed steps, then time exactly ``steps`` steps bracketed by a
+    barrier + device synchronise on both sides; the time is the max over ranks."""
+    from multimodalstudio_amd.pipeline import Trainer, TrainConfig
+    method, mods, _ = CONFIGS[config]
+    world = ddp.world if ddp is not None else 1
+    from multimodalstudio_amd.pipeline import POL_10_VIEWS_SKIP
+    skip = {"polarization": POL_10_VIEWS_SKIP} if config == "grid_bg5" else None
+    cfg = TrainConfig(method=method, modalities=mods, num_rays_per_modality=args.rays, log2T=args.log2T,
+                      skip_views=skip)
+    trainer = Trainer(cfg, dev, rank=rank)
+    trainer.set_step(args.start_step)
+    runner = None
+    if args.mode == "graph":
+        from multimodalstudio_amd.graphs import GraphTrainer
+        runner = GraphTrainer(trainer, ddp=ddp)
+        step = runner.step
+    else:
+        step = lambda: trainer.train_step(ddp=ddp)  # noqa: E731
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if ddp:
+        ddp.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if ddp:
+        ddp.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if ddp:
+        elapsed = ddp.max_over_ranks(elapsed, dev)
+    if runner is not None:
+        print(f"[bench] {config}: graph steps: {runner.stats}, {len(runner.graphs)} graphs"
+              + (f", capture disabled: {runner.disabled}" if runner.disabled else ""), file=sys.stderr)
+    rays_per_step = args.rays * len(mods) * world
+    mode = ("hipgraph replay (fixed-capacity foreground batches)" if runner is not None and runner.disabled is None
+            else "eager")
+    return {"trainer": trainer, "runner": runner, "elapsed": elapsed, "cfg": cfg, "rays_per_step": rays_per_step,
+            "value": rays_per_step * steps / elapsed, "ms_per_step": 1000.0 * elapsed / steps, "step_mode": mode,
+            "steps": steps, "warmup": warmup}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -145,6 +233,8 @@ def main():
                     help="MLP GEMM precision preset (functions.PRESETS); fp32 = reference-parity mode")
     ap.add_argument("--mode", default="graph", choices=["graph", "eager"],
                     help="graph: hipGraph-captured steps (multimodalstudio_amd/graphs.py); eager: Python-launched")
+    ap.add_argument("--secondary", default="grid_raw5", help="also time this config (nested 'secondary' record); "
+                    "'' to skip")
     ap.add_argument("--timing-steps", type=int, default=5,
                     help="eager steps after the timed region whose watched launches are timed with HIP events")
     args = ap.parse_args()
@@ -163,36 +253,8 @@ def main():
     ddp = mddp.init_from_env("nccl") if world > 1 else None
 
     method, mods, desc = CONFIGS[args.config]
-    cfg = TrainConfig(method=method, modalities=mods, num_rays_per_modality=args.rays, log2T=args.log2T)
-    trainer = Trainer(cfg, dev, rank=rank)
-    trainer.set_step(args.start_step)
-    runner = None
-    if args.mode == "graph":
-        from multimodalstudio_amd.graphs import GraphTrainer
-        runner = GraphTrainer(trainer, ddp=ddp)
-        step = runner.step
-    else:
-        step = lambda: trainer.train_step(ddp=ddp)  # noqa: E731
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if ddp:
-        ddp.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if ddp:
-        ddp.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if ddp:
-        elapsed = ddp.max_over_ranks(elapsed, dev)
-    if runner is not None:
-        print(f"[bench] graph steps: {runner.stats}, {len(runner.graphs)} graphs"
-              + (f", capture disabled: {runner.disabled}" if runner.disabled else ""), file=sys.stderr)
+    run = timed_run(args.config, args, dev, rank, ddp, args.steps, args.warmup)
+    trainer, runner, elapsed, cfg = run["trainer"], run["runner"], run["elapsed"], run["cfg"]
     # per-kernel durations: eager steps of the same workload right after the timed region, every watched launch
     # bracketed by HIP events on the stream it is launched on (a graph replay cannot bracket single kernels)
     timing_steps = max(1, args.timing_steps)
@@ -203,61 +265,39 @@ def main():
         torch.cuda.synchronize()
         _lib.TIMER.stop()
 
-    rays_per_step = args.rays * len(mods) * world
-    value = rays_per_step * args.steps / elapsed
-    ms_per_step = 1000.0 * elapsed / args.steps
+    rays_per_step, value, ms_per_step, run_mode = run["rays_per_step"], run["value"], run["ms_per_step"], run["step_mode"]
 
-    roof = None
-    kernels = []
+    roof, hash_roof, kernels = None, None, []
     if not args.no_kernel_timing:
-        summ = _lib.TIMER.summary()
-        for name, (n, ms, work) in summ.items():
-            launches_per_step = n / timing_steps
-            if name.startswith("mms_gemm") or name.startswith("mms_mlp_chain"):
-                # roofline = the slower of the MFMA and the HBM bound for this launch mix
-                flops, nbytes = work
-                peak = MFMA_PEAK_TF[name.split(":")[1]]       # "mms_gemm:<precision>:<NT|NN|TN>", "mms_mlp_chain:..."
-                t_mfma = flops / (peak * 1e12)
-                t_hbm = nbytes / (HBM_PEAK_GBS * 1e9)
-                if t_mfma >= t_hbm:
-                    ach = flops / (ms * 1e-3) / 1e12
-                    rec = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
-                           "frac": round(ach / peak, 4)}
-                else:
-                    ach = nbytes / (ms * 1e-3) / 1e9
-                    rec = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(ach / HBM_PEAK_GBS, 4)}
-                rec.update({"kernel": name, "avg_ms": round(ms, 5), "launches_per_step": launches_per_step,
-                            "ms_per_step": round(ms * launches_per_step, 4), "traffic": None,
-                            "tflops": round(flops / (ms * 1e-3) / 1e12, 3),
-                            "gbs": round(nbytes / (ms * 1e-3) / 1e9, 1)})
-                kernels.append(rec)
-            else:
-                ach = work / (ms * 1e-3) / 1e9
-                kernels.append({"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "avg_ms": round(ms, 5),
-                                "launches_per_step": launches_per_step,
-                                "ms_per_step": round(ms * launches_per_step, 4), "traffic": None})
-        # HBM traffic per launch from the committed rocprofv3 PMC passes of this workload (scripts/gpu_pmc.sh ->
-        # scripts/pmc_traffic.py -> profiles/pmc_traffic_<precision>.json); null when not collected
-        pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.precision}.json")
-        pmc = json.load(open(pmc_path))["kernels"] if os.path.exists(pmc_path) else {}
-        for rec in kernels:
-            if rec["kernel"] in pmc:
-                rec["traffic"] = pmc[rec["kernel"]]["hbm_bytes_per_launch"]
-                rec["traffic_unit"] = "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
-        kernels.sort(key=lambda k: -k["ms_per_step"])
-        if kernels:
-            top = kernels[0]
-            roof = {k: top[k] for k in ["bound", "achieved", "peak", "unit", "frac", "traffic"]}
-            if "traffic_unit" in top:
-                roof["traffic_unit"] = top["traffic_unit"]
-            roof["kernel"] = top["kernel"]
-            roof["avg_ms"] = top["avg_ms"]
+        kernels = kernel_records(_lib.TIMER.summary(), timing_steps, args.precision)
+        # headline (north_star / SURVEY §8(d)): MFMA utilisation of the fused geometry-MLP chain, forward, rated by
+        # its algorithmic 2MNK flops against the dense bf16 MFMA peak; the hash-grid lookups against HBM beside it
+        by_name = {k["kernel"]: k for k in kernels}
+        sdf = [k for k in kernels if k["kernel"].startswith("mms_mlp_chain:") and k["kernel"].endswith(":sdf_fwd")]
+        top = sdf[0] if sdf else (kernels[0] if kernels else None)
+        if top is not None:
+            roof = {k: top[k] for k in ["bound", "achieved", "peak", "unit", "frac", "traffic"] if k in top}
+            for k in ["kernel", "avg_ms", "frac_of_mode_peak", "mode_peak", "traffic_unit"]:
+                if k in top:
+                    roof[k] = top[k]
+        hash_roof = {d: {k: by_name[n][k] for k in ["achieved", "peak", "unit", "frac", "avg_ms", "traffic"]}
+                     for d, n in [("fwd", "mms_hashgrid_fwd"), ("bwd", "mms_hashgrid_bwd_grouped")] if n in by_name}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(trainer, cfg, args.cpu_seconds)
+
+    secondary = None
+    if args.secondary and args.secondary != args.config:
+        # a second driver-timed line for the 5-modality workload (BASELINE configs[2] per GPU), same process
+        del trainer, runner, run
+        torch.cuda.empty_cache()
+        r2 = timed_run(args.secondary, args, dev, rank, ddp, max(1, min(args.steps, 20)), max(1, min(args.warmup, 5)))
+        secondary = {"config": {"workload": CONFIGS[args.secondary][2], "modalities": list(CONFIGS[args.secondary][1]),
+                                "num_rays_per_modality": args.rays, "rays_per_step": r2["rays_per_step"]},
+                     "value": round(r2["value"], 1), "unit": "rays/s", "steps": r2["steps"], "warmup": r2["warmup"],
+                     "ms_per_step": round(r2["ms_per_step"], 3), "step_mode": r2["step_mode"]}
+        del r2
 
     if rank == 0:
         line = {
@@ -276,13 +316,14 @@ def main():
             "config": {"workload": desc, "num_rays_per_modality": args.rays, "modalities": list(mods),
                        "rays_per_step": rays_per_step, "log2_hashmap_size": args.log2T,
                        "model_step": args.start_step, "precision": args.precision, "parallelism": f"dp{world}",
-                       "step_mode": ("hipgraph replay (fixed-capacity foreground batches)" if runner is not None and
-                                     runner.disabled is None else "eager")},
+                       "step_mode": run_mode},
             "kernel_timing": (f"{timing_steps} eager steps of the same workload after the timed region, HIP events "
                               "around every watched launch on its stream" if not args.no_kernel_timing else None),
             "roofline": roof,
+            "roofline_hash_grid": hash_roof,
             "roofline_kernels": kernels,
             "cpu_baseline": cpu,
+            "secondary": secondary,
         }
         print(json.dumps(line))
     if ddp:

@@ -29,7 +29,9 @@ const char* mms_last_error(void);
 /* ---- multires hash grid: HashEncoding (field_components/encodings.py:184-310) inside FeatureGrid
  * (field_components/feature_structures.py:78-88).  pos [M, ldx] (cols 0..2), table [L*2^log2T, F=2],
  * scales [L] host array (floor(min_res*g^l)), out [M, ldo] cols 0..2L-1.  Levels >= active_levels are
- * zero (coarse-to-fine mask).  bwd: dtable += (atomic), dpos[:, 0:3] += (either may be NULL). */
+ * zero (coarse-to-fine mask).  bwd: dtable += (atomic), dpos[:, 0:3] += (either may be NULL).
+ * radius r > 0: pos is the FeatureGrid input, x_hat = (x + r) / (2 r); r = 0: pos is already x_hat (a bare
+ * HashEncoding.forward, encodings.py:263-304). */
 int mms_hashgrid_fwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L, int log2T, int F,
                      const float* scales, float radius, int active_levels, float* out, int64_t ldo, void* stream);
 int mms_hashgrid_bwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L, int log2T, int F,
@@ -43,19 +45,12 @@ int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group, int64_t gs
                              int active_levels, const float* dout, int64_t ldd, float* dtable, float* dpos,
                              int64_t lddx, void* stream);
 
-/* ---- fp32 MFMA GEMM with fused MLP epilogue: nn.Linear + activation (field_components/mlp.py:152-171).
- * mode 0 NT: C = A[M,K] B[N,K]^T ; 1 NN: C = A[M,K] B[K,N] ; 2 TN: C = A[K,M]^T B[K,N].
- * Epilogue: v = acc + bias[n]; Z[m,n] = v (optional); v = act(v); v *= dact'(aux[m,n]) (optional);
- * C = v or C += v (accumulate; atomic when splits > 1).  act/dact: 0 none, 1 ReLU, 2 Softplus(beta,thr),
- * 3 Sigmoid. */
-int mms_gemm_f32(int mode, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
-                 int64_t ldb, float* C, int64_t ldc, const float* bias, float* Z, int64_t ldz, const float* aux,
-                 int64_t ldaux, int act, int dact, float beta, float thr, int accumulate, int splits, void* stream);
-
 /* ---- MLP GEMM engine (field_components/mlp.py:152-171): C = epilogue(op(A) op(B)^T).
  * trans_a = 0: A is [M, K] (lda); 1: A is stored [K, M].  trans_b = 0: B is [N, K]; 1: B is stored [K, N].
  * prec 0 = exact fp32 MFMA, 1 = bf16 MFMA (fp32 accumulate), 2 = split bf16x3 (near-fp32 operands).
- * Epilogue as mms_gemm_f32; ones_col >= 0 also writes 1.0 at column ones_col of every output row. */
+ * Epilogue: v = acc + bias[n]; Z[m,n] = v (optional); v = act(v); v *= dact'(aux[m,n]) (optional);
+ * C = v or C += v (accumulate; atomic when splits > 1).  act/dact: 0 none, 1 ReLU, 2 Softplus(beta,thr),
+ * 3 Sigmoid.  ones_col >= 0 also writes 1.0 at column ones_col of every output row. */
 int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
              const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, float* Z, int64_t ldz,
              const float* aux, int64_t ldaux, int act, int dact, float beta, float thr, int accumulate, int splits,

@@ -50,10 +50,12 @@ __device__ __forceinline__ Corners make_corners(float x, float y, float z, float
   Corners c;
   // (x + r) / (2r): reference computes a true division by (2r); for r in {1, 2} the reciprocal
   // multiply is exact, but keep the division for bit-exact corner indices in general.
+  // radius 0: the input is already x_hat (HashEncoding called directly, encodings.py:263-304)
   const float two_r = 2.0f * radius;
-  const float hx = (x + radius) / two_r;
-  const float hy = (y + radius) / two_r;
-  const float hz = (z + radius) / two_r;
+  const bool norm = radius > 0.f;
+  const float hx = norm ? (x + radius) / two_r : x;
+  const float hy = norm ? (y + radius) / two_r : y;
+  const float hz = norm ? (z + radius) / two_r : z;
   (void)inv_2r;
   const float sx = hx * s, sy = hy * s, sz = hz * s;
   const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
@@ -148,6 +150,7 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
     const uint32_t hmask = (1u << p.log2T) - 1u;
     const uint32_t base = (uint32_t)level << p.log2T;
     const float two_r = 2.0f * p.radius;
+    const bool norm = p.radius > 0.f;
     uint32_t pidx = 0u;
     float pacc = 0.f;
     for (int k = 0; k < nck; ++k) {
@@ -165,9 +168,9 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
 #pragma unroll
       for (int j = 0; j < G; ++j) {
         // same rounded values as make_corners (bit-exact corners)
-        const float sx = ((px[j] + p.radius) / two_r) * s;
-        const float sy = ((py[j] + p.radius) / two_r) * s;
-        const float sz = ((pz[j] + p.radius) / two_r) * s;
+        const float sx = (norm ? (px[j] + p.radius) / two_r : px[j]) * s;
+        const float sy = (norm ? (py[j] + p.radius) / two_r : py[j]) * s;
+        const float sz = (norm ? (pz[j] + p.radius) / two_r : pz[j]) * s;
         const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
         const float ox = sx - fx, oy = sy - fy, oz = sz - fz;
         const int cx = xc ? (int)ceilf(sx) : (int)fx;
@@ -211,7 +214,7 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
   }
   if (dpos != nullptr) {
     __syncthreads();
-    const float two_r = 2.0f * p.radius;
+    const float two_r = p.radius > 0.f ? 2.0f * p.radius : 1.0f;
     for (int i = t; i < nck * G; i += 256) {
       const int k = i / G, j = i - k * G;
       const int64_t pt = g0 + k + (int64_t)j * gstride;
@@ -227,12 +230,12 @@ int fill_params(const char* fn, GridParams& p, int L, int log2T, const float* sc
                 int active_levels) {
   if (L < 1 || L > kMaxLevels) return mms::set_error(fn, "num_levels must be in [1, 16]");
   if (log2T < 1 || log2T > 24) return mms::set_error(fn, "log2_hashmap_size must be in [1, 24]");
-  if (!(radius > 0.f)) return mms::set_error(fn, "radius must be > 0");
+  if (!(radius >= 0.f)) return mms::set_error(fn, "radius must be >= 0 (0: inputs already in [0, 1])");
   p.levels = L;
   p.active_levels = active_levels < 0 ? L : (active_levels > L ? L : active_levels);
   p.log2T = log2T;
   p.radius = radius;
-  p.inv_2r = 1.0f / (2.0f * radius);
+  p.inv_2r = radius > 0.f ? 1.0f / (2.0f * radius) : 1.0f;
   for (int i = 0; i < kMaxLevels; ++i) p.scale[i] = i < L ? scales[i] : 0.f;
   return 0;
 }

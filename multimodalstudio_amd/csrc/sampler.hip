@@ -204,10 +204,11 @@ __global__ __launch_bounds__(64) void neus_step_kernel(
   }
   // (f-g) inverse CDF at u_j = lin_j + rand / nb (searchsorted right)
   const int nb = n_new + 1;
-  const float rj = rand ? rand[r] / (float)nb : 0.0f;
+  // training: u_j = lin_j + rand / nb (single jitter); eval: u_j = lin_j + 1 / (2 nb) (ray_samplers.py:365-377)
+  const float rj = rand ? rand[r] / (float)nb : (float)(1.0 / (2.0 * nb));
   float* nbo = new_bins + r * nb;
   for (int j = 0; j < nb; ++j) {
-    const float u = rand ? u_lin[j] + rj : u_lin[j];
+    const float u = u_lin[j] + rj;
     int lo = 0, hi = S + 1;  // first index with cdf > u
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;

@@ -472,6 +472,123 @@ def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> to
     return out[:, 0]
 
 
+def _chain_shape(params, acts) -> bool:
+    """True when the fused chain kernel serves this MLP: the SDF (71-256-256-257, Softplus, Softplus, none) or the
+    radiance (317-256-256-256, ReLU x 3) shape (mms_mlp_chain's dispatch table)."""
+    if len(params) != 9:
+        return False
+    dims = [params[1].shape[1]] + [params[3 * l + 1].shape[0] for l in range(3)]
+    a = tuple(x[0] for x in acts)
+    return (dims == [71, 256, 256, 257] and a == (2, 2, 0)) or (dims == [317, 256, 256, 256] and a == (1, 1, 1))
+
+
+def mlp_runner(params, acts, prec: int):
+    """The MLP engine for a weight-normed MLP: the fused 3-layer chain kernel in the bf16 modes where its shape is
+    served, else the per-layer GEMM engine (every shape, every precision)."""
+    if prec != 0 and _chain_shape(params, acts):
+        return ChainRun(params, acts, prec)
+    return MLPRun(params, acts, prec)
+
+
+def _run_forward(run, X, keep: bool):
+    return run.forward(X, keep=keep)
+
+
+def _run_backward(run, dy):
+    """dX of an MLP runner; parameter gradients are accumulated in place (grad_target)."""
+    if isinstance(run, ChainRun):
+        return run.backward(dy if dy.stride(1) == 1 and dy.stride(0) % 4 == 0 else _copy_aligned(dy))
+    dx, _ = run.backward(dy.contiguous(), need_dx=True)
+    return dx
+
+
+class SDFFieldFunction(torch.autograd.Function):
+    """SDFField.forward (surface_field.py:99-116) for the grid methods: PE(x) (encodings.py:161-182, 6 frequencies,
+    input included) -> FeatureGridAndMLP (feature_structures.py:153-169) -> (sdf [M,1], geo [M,G]).  No taps: the
+    plain field evaluation the reference's SDFField / single_output perform; autograd to x, the table and the MLP."""
+
+    @staticmethod
+    def forward(ctx, pos, table, grid: GridCfg, active: int, *params):
+        M = pos.shape[0]
+        dev = pos.device
+        pos = pos.contiguous()
+        K0 = 3 + 36 + grid.out_dim
+        X = _alloc(M, K0, dev)
+        _lib.call("mms_geo_input_fwd", pos.data_ptr(), 3, M, 0, 0.0, 6, X.data_ptr(), X.stride(0), _s())
+        grid_fwd(grid, X, X.stride(0), M, table, active, X, 39)
+        run = mlp_runner(params, SDF_ACTS, PRECISION["sdf"])
+        out = _run_forward(run, X, keep=True)
+        ctx.run, ctx.X, ctx.grid, ctx.active, ctx.table = run, X, grid, active, table
+        ctx.save_for_backward(pos, table)
+        G = out.shape[1] - 1
+        return out[:, :1].contiguous(), out[:, 1:].contiguous() if G > 0 else out[:, :0]
+
+    @staticmethod
+    def backward(ctx, dsdf, dgeo):
+        pos, table = ctx.saved_tensors
+        M = pos.shape[0]
+        dev = pos.device
+        G = dgeo.shape[1] if dgeo is not None else ctx.run.params[-2].shape[0] - 1
+        dout = _alloc(M, G + 1, dev)
+        dout[:, :1] = dsdf if dsdf is not None else 0.0
+        dout[:, 1:] = dgeo if dgeo is not None else 0.0
+        dX = _run_backward(ctx.run, dout)
+        X = ctx.X
+        need_pos = ctx.needs_input_grad[0]
+        dP = torch.zeros(M, 3, device=dev) if need_pos else None
+        dtable = grad_target(ctx.table) if ctx.needs_input_grad[1] else None
+        grid_bwd(ctx.grid, X, X.stride(0), M, table, ctx.active, dX, 39, dtable, dP)
+        dpos = None
+        if need_pos:
+            dpos = torch.zeros(M, 3, device=dev)
+            _lib.call("mms_geo_input_bwd", X.data_ptr(), X.stride(0), dX.data_ptr(), dX.stride(0), dP.data_ptr(), 3, M,
+                      0, 6, dpos.data_ptr(), 3, _s())
+        n = len(ctx.run.params)
+        ctx.run = ctx.X = ctx.table = None
+        return (dpos, None, None, None, *([None] * n))
+
+
+class FeatureGridMLPFunction(torch.autograd.Function):
+    """FeatureGridAndMLP.forward (feature_structures.py:153-169) for any input width: the MLP panel is
+    [input (x = columns 0..2, then the auxiliary columns), grid(x)], the grid written straight into the panel by the
+    hash kernel; MLP on the chain kernel or the GEMM engine (mlp_runner).  Returns the MLP output (and, with
+    return_features, the grid features)."""
+
+    @staticmethod
+    def forward(ctx, inp, table, grid: GridCfg, active: int, acts, prec: int, *params):
+        M, K_in = inp.shape
+        dev = inp.device
+        X = _alloc(M, K_in + grid.out_dim, dev)
+        X[:, :K_in] = inp
+        grid_fwd(grid, X, X.stride(0), M, table, active, X, K_in)
+        run = mlp_runner(params, acts, prec)
+        out = _run_forward(run, X, keep=True)
+        ctx.run, ctx.X, ctx.grid, ctx.active, ctx.table, ctx.K_in = run, X, grid, active, table, K_in
+        ctx.save_for_backward(table)
+        feats = X[:, K_in:].clone()
+        ctx.mark_non_differentiable(feats)
+        return out, feats
+
+    @staticmethod
+    def backward(ctx, dout, dfeats):
+        (table,) = ctx.saved_tensors
+        X, K_in = ctx.X, ctx.K_in
+        M = X.shape[0]
+        dev = X.device
+        dX = _run_backward(ctx.run, dout)
+        need_in = ctx.needs_input_grad[0]
+        dP = torch.zeros(M, 3, device=dev) if need_in else None
+        dtable = grad_target(ctx.table) if ctx.needs_input_grad[1] else None
+        grid_bwd(ctx.grid, X, X.stride(0), M, table, ctx.active, dX, K_in, dtable, dP)
+        dinp = None
+        if need_in:
+            dinp = dX[:, :K_in].clone()
+            dinp[:, :3] += dP
+        n = len(ctx.run.params)
+        ctx.run = ctx.X = ctx.table = None
+        return (dinp, None, None, None, None, None, *([None] * n))
+
+
 # ------------------------------------------------------------------------------------------------
 # radiance field
 # ------------------------------------------------------------------------------------------------
@@ -554,26 +671,33 @@ class MLPFunction(torch.autograd.Function):
 # ------------------------------------------------------------------------------------------------
 # background NeRF field: contraction + PE -> base MLP -> density head ; [feat, PE(d)] -> head MLP
 # ------------------------------------------------------------------------------------------------
-BG_BASE_ACTS = ((1, 1.0, 20.0),) * 4
+BG_BASE_ACTS = ((1, 1.0, 20.0),) * 4      # ReLU hidden + ReLU out (NeRF MLP and the config-5 grid MLP alike)
 BG_DENS_ACTS = ((2, 1.0, 20.0),)
 BG_HEAD_ACTS = ((1, 1.0, 20.0),) * 4
 
 
 class BackgroundFunction(torch.autograd.Function):
-    """pos [M,3] (raw sample starts), dirs [R,3] -> density [M,1], feature [M,128]."""
+    """pos [M,3] (raw sample starts), dirs [R,3] -> density [M,1], feature [M,F].  ``grid``/``table``: the config-5
+    background base field is a FeatureGridAndMLP (hash grid r = 2 on the contracted x, method_configs.py:428-444);
+    None for the NeRF MLP base field."""
 
     @staticmethod
-    def forward(ctx, pos, dirs, S: int, nb: int, nd: int, *params):
+    def forward(ctx, pos, dirs, table, S: int, nb: int, nd: int, grid: Optional[GridCfg], active: int, *params):
         M = pos.shape[0]
         dev = pos.device
         base_p, dens_p, head_p = params[:3 * nb], params[3 * nb:3 * (nb + nd)], params[3 * (nb + nd):]
-        X = _alloc(M, 39, dev)
+        # base input panel [contracted x, PE tail (36)] (+ the grid features of the contracted x for the config-5
+        # FeatureGridAndMLP base field, feature_structures.py:153-169, written straight into columns 39..70)
+        X = _alloc(M, 39 + (grid.out_dim if grid is not None else 0), dev)
         Fb = base_p[-2].shape[0]
         H = _alloc(M, Fb + 27, dev)
         pos = pos.contiguous()
         dirs = dirs.contiguous()
         _lib.call("mms_bg_input_fwd", pos.data_ptr(), M, dirs.data_ptr(), S, X.data_ptr(), X.stride(0), H.data_ptr(),
                   H.stride(0), Fb, _s())
+        if grid is not None:
+            grid_fwd(grid, X, X.stride(0), M, table, active, X, 39)
+        ctx.grid, ctx.active, ctx.table = grid, active, table
         base = MLPRun(base_p, BG_BASE_ACTS[:nb], PRECISION["background"])
         base.forward(X, keep=True, last_out=H)          # writes cols [0, Fb) of the head panel
         dens = MLPRun(dens_p, BG_DENS_ACTS, PRECISION["background"])
@@ -597,12 +721,18 @@ class BackgroundFunction(torch.autograd.Function):
         dFb_d, dgrads_dens = _mlp_strided_bwd(ctx.dens, ddensity.contiguous(), ctx.H, Fb)
         dbase_out = dH[:, :Fb] + dFb_d
         dX, bgrads = ctx.base.backward(dbase_out.contiguous(), need_dx=True)
+        if ctx.grid is not None:
+            # grid features of the contracted x: table gradients, and d(contracted x) into the panel's x columns
+            dtable = grad_target(ctx.table) if ctx.needs_input_grad[2] else None
+            dP = torch.zeros(M, 3, device=dev)
+            grid_bwd(ctx.grid, ctx.X, ctx.X.stride(0), M, ctx.table, ctx.active, dX, 39, dtable, dP)
+            dX[:, :3] += dP
         dpos = torch.empty(M, 3, device=dev) if ctx.needs_input_grad[0] else None
         ddirs = torch.zeros(R, 3, device=dev) if ctx.needs_input_grad[1] else None
         _lib.call("mms_bg_input_bwd", pos.data_ptr(), ctx.X.data_ptr(), ctx.X.stride(0), dX.data_ptr(), dX.stride(0),
                   dirs.data_ptr(), dH.data_ptr(), dH.stride(0), Fb, R, S, _p(dpos), _p(ddirs), _s())
-        ctx.base = ctx.dens = ctx.head = ctx.X = ctx.H = None
-        return (dpos, ddirs, None, None, None, *bgrads, *dgrads_dens, *hgrads)
+        ctx.base = ctx.dens = ctx.head = ctx.X = ctx.H = ctx.table = None
+        return (dpos, ddirs, None, None, None, None, None, None, *bgrads, *dgrads_dens, *hgrads)
 
 
 def _mlp_strided(run: MLPRun, H: torch.Tensor, Fb: int) -> torch.Tensor:

@@ -105,15 +105,6 @@ def gemm(mode: int, M: int, N: int, K: int, A: torch.Tensor, lda: int, B: torch.
               float(beta), float(thr), int(bool(accumulate)), int(splits), int(ones_col), _ptr(colsum), _stream())
 
 
-def gemm_f32_legacy(mode: int, M: int, N: int, K: int, A, lda, B, ldb, C, ldc, **kw):
-    """The first-generation fp32 GEMM (mms_gemm_f32), kept for A/B comparisons."""
-    _lib.call("mms_gemm_f32", int(mode), int(M), int(N), int(K), A.data_ptr(), int(lda), B.data_ptr(), int(ldb),
-              C.data_ptr(), int(ldc), _ptr(kw.get("bias")), _ptr(kw.get("Z")), int(kw.get("ldz", 0)),
-              _ptr(kw.get("aux")), int(kw.get("ldaux", 0)), int(kw.get("act", 0)), int(kw.get("dact", 0)),
-              float(kw.get("beta", 1.0)), float(kw.get("thr", 20.0)), int(bool(kw.get("accumulate", False))),
-              int(kw.get("splits", 1)), _stream())
-
-
 def weight_norm_fwd(g, v, W, norms):
     N, K = v.shape
     _lib.call("mms_weight_norm_fwd", g.data_ptr(), v.data_ptr(), N, K, W.data_ptr(), W.stride(0), norms.data_ptr(),

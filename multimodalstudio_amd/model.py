@@ -289,10 +289,19 @@ class BackgroundModel(nn.Module):
 
     def field(self, pos, dirs, S):
         bf = self.background_field
-        base = bf.base_field.params()
+        grid, table, active = None, None, 0
+        if isinstance(bf.base_field, FeatureGridAndMLP):
+            # config 5: hash grid (r = 2) + MLP base field; its coarse-to-fine callback is never registered
+            # (BackgroundModel.get_training_callbacks returns [], background_model.py:118-123): all levels active
+            g = bf.base_field.feature_grid
+            grid, table, active = g.cfg, g.encoding.hash_table, g.active_levels
+            base = bf.base_field.mlp_head.params()
+        else:
+            base = bf.base_field.params()
         dens = bf.density_head.field.params()
         head = bf.head_field.params()
-        return fx.BackgroundFunction.apply(pos, dirs, S, len(base) // 3, len(dens) // 3, *base, *dens, *head)
+        return fx.BackgroundFunction.apply(pos, dirs, table, S, len(base) // 3, len(dens) // 3, grid, active, *base,
+                                           *dens, *head)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -312,6 +321,10 @@ class ModelSpec:
     upsample_steps: int = 4
     base_variance: float = 64.0
     bg_samples: int = 16
+    # background field: "nerf" (PE -> 39-256x4 MLP, head 283-256x3-128, 1-layer heads; method 'grid' / 'grid_raw') or
+    # "grid" (config 5 'grid_raw_grid_bg_unbalanced', method_configs.py:428-444: hash grid r = 2 + 71-128-128-256 MLP,
+    # head 283-256x3-256, the radiance model's 3-layer heads)
+    bg_kind: str = "nerf"
 
 
 @dataclass
@@ -411,15 +424,25 @@ class BaseModel(nn.Module):
             else:
                 heads[m] = ModalityHead("plain", 256, c, 3, 64, "Sigmoid")
         self.radiance_model = RadianceModel(RadianceField(FeatureGridAndMLP(grid(), rad_mlp)), heads)
-        bg_base = MLP(MLPConfig(num_layers=4, hidden_dim=256, out_activation="ReLU"), 39, 256)
-        bg_head = MLP(MLPConfig(num_layers=4, hidden_dim=256, out_activation="ReLU"), 256 + 27, 128)
         dens = ModalityHead("plain", 256, 1, 1, 64, "Softplus")
         bg_heads = {}
-        for m, c in mods.items():
-            if m == "polarization":
-                bg_heads[m] = ModalityHead("polarization", 128, c, 1, 64, "None")
-            else:
-                bg_heads[m] = ModalityHead("plain", 128, c, 1, 64, "Sigmoid")
+        if spec.bg_kind == "grid":
+            bg_base = FeatureGridAndMLP(grid(2.0), MLP(MLPConfig(num_layers=3, hidden_dim=128, out_activation="ReLU"),
+                                                       3 + 36 + 32, 256))
+            bg_head = MLP(MLPConfig(num_layers=4, hidden_dim=256, out_activation="ReLU"), 256 + 27, 256)
+            for m, c in mods.items():
+                if m == "polarization":
+                    bg_heads[m] = ModalityHead("polarization", 256, c, 3, 256, "None")
+                else:
+                    bg_heads[m] = ModalityHead("plain", 256, c, 3, 64, "Sigmoid")
+        else:
+            bg_base = MLP(MLPConfig(num_layers=4, hidden_dim=256, out_activation="ReLU"), 39, 256)
+            bg_head = MLP(MLPConfig(num_layers=4, hidden_dim=256, out_activation="ReLU"), 256 + 27, 128)
+            for m, c in mods.items():
+                if m == "polarization":
+                    bg_heads[m] = ModalityHead("polarization", 128, c, 1, 64, "None")
+                else:
+                    bg_heads[m] = ModalityHead("plain", 128, c, 1, 64, "Sigmoid")
         self.background_model = BackgroundModel(NeRFField(bg_base, bg_head, dens), bg_heads)
         self._lin = {}
 

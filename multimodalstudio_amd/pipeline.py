@@ -260,9 +260,21 @@ def select_right_channel(rendered: torch.Tensor, band: torch.Tensor) -> torch.Te
 # ------------------------------------------------------------------------------------------------
 # trainer
 # ------------------------------------------------------------------------------------------------
+# per-modality training views skipped by confs/grid_raw_rgb_all_views_pol_10_views.yaml (config 5: the unbalanced
+# dataset keeps 10 polarization training views out of 45)
+POL_10_VIEWS_SKIP = [0, 1, 2, 3, 5, 7, 8, 10, 11, 13, 15, 16, 17, 18, 20, 21, 23, 24, 26, 28, 30, 31, 32, 33, 35, 36,
+                     37, 38, 40, 42, 43, 45, 46, 47, 48]
+METHODS = {
+    # method name: (raw mosaicked frames, background field kind)
+    "grid": (False, "nerf"),
+    "grid_raw": (True, "nerf"),
+    "grid_raw_grid_bg_unbalanced": (True, "grid"),
+}
+
+
 @dataclass
 class TrainConfig:
-    method: str = "grid"                 # "grid" (demosaicked) or "grid_raw"
+    method: str = "grid"                 # a METHODS key
     modalities: tuple = ("rgb",)
     num_rays_per_modality: int = 2048
     log2T: int = 19
@@ -272,6 +284,7 @@ class TrainConfig:
     max_iters: int = 100000
     pose_mode: str = "SO3xR3"
     seed: int = 654824
+    skip_views: Optional[Dict[str, List[int]]] = None   # skip_image_indices_per_modality (datamanager config)
 
 
 class Trainer:
@@ -280,13 +293,16 @@ class Trainer:
     def __init__(self, cfg: TrainConfig, device, rank: int = 0, frames_on_device: bool = True):
         self.cfg = cfg
         self.device = device
-        self.raw = cfg.method == "grid_raw"
+        self.raw, bg_kind = METHODS[cfg.method]
         mods = list(cfg.modalities)
         self.modalities = mods
         channels = {m: mscene.CHANNELS[m] for m in mods}
         torch.manual_seed(654824)
-        self.model = BaseModel(ModelSpec(channels, log2T=cfg.log2T)).to(device)
+        self.model = BaseModel(ModelSpec(channels, log2T=cfg.log2T, bg_kind=bg_kind)).to(device)
         cams = mscene.make_cameras(mods, cfg.n_views, cfg.width, cfg.height, seed=0, train=True)
+        for m, skip in (cfg.skip_views or {}).items():
+            if m in cams:
+                cams[m] = mscene.select_views(cams[m], [v for v in cams[m].view_ids if v not in set(skip)])
         self.cams = {m: DeviceCameras(cams[m], device) for m in mods}
         self.pose = CameraOptimizer(mods, {m: self.cams[m].num for m in mods}, mode=cfg.pose_mode).to(device)
         self.raygen = RayGenerator(self.cams, self.pose, 0.0)

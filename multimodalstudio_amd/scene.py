@@ -83,6 +83,14 @@ def make_cameras(modalities: List[str], n_views: int = 50, width: int = 640, hei
     return out
 
 
+def select_views(cams: ModalityCameras, view_ids: List[int]) -> ModalityCameras:
+    """The cameras of the given frame ids (a dataset split / skip_image_indices_per_modality)."""
+    keep = [cams.view_ids.index(v) for v in view_ids]
+    t = torch.tensor(keep, dtype=torch.long)
+    return ModalityCameras(cams.c2w[t], cams.fx[t], cams.fy[t], cams.cx[t], cams.cy[t], cams.distortion[t],
+                           cams.width, cams.height, list(view_ids))
+
+
 def mosaick_mask(mod: str, width: int, height: int) -> torch.Tensor:
     """RawDataset.build_mosaick_mask (datasets.py:229-254): tiled pattern cropped to H x W, int8."""
     pat = torch.tensor(MOSAICK[mod])

@@ -5,7 +5,7 @@ Records every hip_ops.gemm call of one bench-config training step, then times ea
 (mode, M, N, K, strides, splits) in isolation for the requested precisions, next to torch.mm
 (hipBLASLt) fp32 / bf16 for orientation.  Prints one line per shape and the per-step totals.
 
-    python scripts/gemm_bench.py [--precs=-1,0,1,2]  (-1 = first-generation fp32 kernel) [--reps 20] [--torch]
+    python scripts/gemm_bench.py [--precs=0,1,2] [--reps 20] [--torch]
 """
 from __future__ import annotations
 
@@ -73,9 +73,6 @@ def main():
         line = f"{names[mode]:4s} {M:7d} {N:5d} {K:7d} {splits:4d} {n:2d} {fl / 1e9:7.2f} "
         for p in precs:
             def run():
-                if p < 0:   # first-generation fp32 kernel
-                    return hip_ops.gemm_f32_legacy(mode, M, N, K, A, lda, B, ldb, C, ldc, bias=bias, Z=Z, ldz=N, aux=aux,
-                                                   ldaux=ldc, act=act, dact=act, accumulate=accum, splits=splits)
                 orig(mode, M, N, K, A, lda, B, ldb, C, ldc, bias=bias, Z=Z, ldz=N, aux=aux, ldaux=ldc, act=act,
                      dact=act, accumulate=accum, splits=splits, prec=p)
             for _ in range(3):

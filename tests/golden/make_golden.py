@@ -233,7 +233,7 @@ def set_callbacks(model, step, max_iters=100000):
     return level, delta * 2.0
 
 
-def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=False):
+def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=False, grid_bg=False):
     from cameras.camera_optimizers import CameraOptimizerConfig
     from cameras.pixel_samplers import UniformPixelSamplerConfig
     from model_components.ray_generators import RayGenerator
@@ -243,6 +243,9 @@ def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=F
         "surface_model": {"surface_field": {"field": {"feature_grid": {"encoding": {"log2_hashmap_size": log2T}}}}},
         "radiance_model": {"radiance_field": {"base_field": {"feature_grid": {"encoding": {"log2_hashmap_size": log2T}}}}},
     }}}
+    if grid_bg:
+        overrides["pipeline"]["model"]["background_model"] = {"background_field": {"base_field": {
+            "feature_grid": {"encoding": {"log2_hashmap_size": log2T}}}}}
     cfg, model = refimport.build_model(method, f"/root/reference/confs/{yaml_name}", modalities, overrides)
     model.train()
     with torch.no_grad():
@@ -335,8 +338,138 @@ def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=F
     save(f"e2e_{tag}", **arrays)
 
 
+def gen_eval(method="grid", yaml_name="grid.yaml", mods=("rgb",), step=95000, tag="eval_grid_rgb", raw=False):
+    """Evaluation-mode full-view rendering (Evaluator.render_view -> eval_model_query, evaluator.py:100-178,
+    eval_utils.py:31-76): every pixel of one small view, model in eval mode under no_grad (no jitter anywhere)."""
+    from cameras.camera_optimizers import CameraOptimizerConfig
+    from model_components.ray_generators import RayGenerator
+    torch.manual_seed(1234)
+    modalities = {m: mscene.CHANNELS[m] for m in mods}
+    overrides = {"pipeline": {"model": {
+        "surface_model": {"surface_field": {"field": {"feature_grid": {"encoding": {"log2_hashmap_size": 12}}}}},
+        "radiance_model": {"radiance_field": {"base_field": {"feature_grid": {"encoding": {"log2_hashmap_size": 12}}}}},
+    }}}
+    cfg, model = refimport.build_model(method, f"/root/reference/confs/{yaml_name}", modalities, overrides)
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            if n.endswith("hash_table"):
+                p.mul_(50.0)
+    set_callbacks(model, step)
+    model.eval()
+    W, H = 24, 20
+    cams = mscene.make_cameras(list(mods), n_views=12, width=W, height=H, seed=4)
+    data = {m: {"cameras": ref_cameras(cams[m])} for m in mods}
+    opt = CameraOptimizerConfig(mode="SO3xR3", shared_optimization=True,
+                                modalities_to_optimize={m: True for m in mods}).setup(num_cameras=len(cams[mods[0]].view_ids))
+    with torch.no_grad():
+        for i, m in enumerate(mods):
+            opt.pose_adjustment[m].copy_(torch.tensor([[0.004 * (i + 1), -0.003, 0.002, 0.003, -0.002 * (i + 1), 0.001]]))
+    gen = RayGenerator(data, opt, pixel_offset=0.0)
+    view = 3
+    ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+    coords = {m: torch.stack([torch.full((H * W,), view), ys.reshape(-1), xs.reshape(-1)], -1).to(torch.int32)
+              for m in mods}
+    with torch.no_grad():
+        rb = gen(coords)
+        outputs = model(rb)
+    arrays = {"step": step, "W": W, "H": H, "view": view, "raw": raw, "mods": np.array(mods)}
+    for k, v in model.state_dict().items():
+        arrays["p:" + k] = v
+    gt = torch.rand(H, W, 3, generator=torch.Generator().manual_seed(3))
+    arrays["gt"] = gt
+    for m in mods:
+        arrays[f"{m}:pose"] = opt.pose_adjustment[m].detach()
+        for k in ["c2w", "fx", "fy", "cx", "cy", "distortion"]:
+            arrays[f"{m}:{k}"] = getattr(cams[m], k)
+        o = outputs[m]
+        for k in ["normals", "depth", "accumulation", m]:
+            arrays[f"{m}:out:{k}"] = o[k].detach().reshape(H, W, -1)
+    save(tag, **arrays)
+
+
+def gen_plugins():
+    """Reference-signature modules on their own: SDFField.forward (surface_field.py:99-116), RadianceField.forward
+    (radiance_field.py:72-77) and Renderer.render (renderers.py:75-136), forward and backward."""
+    from cameras.rays import Frustums
+    from model_components.renderers import RadianceRenderer, RendererConfig
+    overrides = {"pipeline": {"model": {
+        "surface_model": {"surface_field": {"field": {"feature_grid": {"encoding": {"log2_hashmap_size": 12}}}}},
+        "radiance_model": {"radiance_field": {"base_field": {"feature_grid": {"encoding": {"log2_hashmap_size": 12}}}}},
+    }}}
+    torch.manual_seed(21)
+    _, model = refimport.build_model("grid", "/root/reference/confs/grid.yaml", {"rgb": 3}, overrides)
+    sf = model.surface_model.surface_field
+    rf = model.radiance_model.radiance_field
+    with torch.no_grad():
+        for n, p in list(sf.named_parameters()) + list(rf.named_parameters()):
+            if n.endswith("hash_table"):
+                p.mul_(50.0)
+    sf.field.feature_grid.update_mask(12)
+    rf.base_field.feature_grid.update_mask(14)
+    g = torch.Generator().manual_seed(22)
+    M = 256
+    arrays = {"sdf_level": 12, "rad_level": 14}
+    # SDFField
+    x = (torch.rand(M, 3, generator=g) * 2.2 - 1.1).requires_grad_(True)
+    sdf, geo = sf(x)
+    dsdf, dgeo = torch.randn(sdf.shape, generator=g), torch.randn(geo.shape, generator=g) * 0.01
+    (sdf * dsdf).sum().add_((geo * dgeo).sum()).backward()
+    arrays.update({"sdf:x": x.detach(), "sdf:sdf": sdf.detach(), "sdf:geo": geo.detach(), "sdf:dsdf": dsdf,
+                   "sdf:dgeo": dgeo, "sdf:dx": x.grad})
+    for k, v in sf.state_dict().items():
+        arrays["sdf:p:" + k] = v
+    for k, p in sf.named_parameters():
+        arrays["sdf:g:" + k] = p.grad
+    # RadianceField: positions, SH(4) directions (25), additional [geo 256, n.v]
+    pos = (torch.rand(M, 3, generator=g) * 2 - 1).requires_grad_(True)
+    vd = (torch.rand(M, rf.input_dim - 3 - 257, generator=g) * 2 - 1).requires_grad_(True)
+    extra = (torch.randn(M, 257, generator=g) * 0.3).requires_grad_(True)
+    feat = rf(pos, vd, extra)
+    dfeat = torch.randn(feat.shape, generator=g)
+    (feat * dfeat).sum().backward()
+    arrays.update({"rad:pos": pos.detach(), "rad:vd": vd.detach(), "rad:extra": extra.detach(),
+                   "rad:out": feat.detach(), "rad:dout": dfeat, "rad:dpos": pos.grad, "rad:dvd": vd.grad,
+                   "rad:dextra": extra.grad})
+    for k, v in rf.state_dict().items():
+        arrays["rad:p:" + k] = v
+    for k, p in rf.named_parameters():
+        arrays["rad:g:" + k] = p.grad
+    # Renderer: rgb composited over a background, normals, depth, accumulation
+    N, S = 96, 16
+    mask = torch.rand(N, generator=g) < 0.7
+    R = int(mask.sum())
+    w = (torch.rand(R, S, 1, generator=g) * 0.12).requires_grad_(True)
+    rgb = torch.rand(R, S, 3, generator=g).requires_grad_(True)
+    bg = torch.rand(N, 3, generator=g).requires_grad_(True)
+    normals = torch.randn(R, S, 3, generator=g)
+    starts = torch.sort(torch.rand(R, S, 1, generator=g) * 2 + 0.5, dim=1)[0]
+    ends = starts + 0.05
+    fr = Frustums(origins=torch.zeros(R, S, 3), directions=torch.zeros(R, S, 3), starts=starts, ends=ends,
+                  pixel_area=torch.ones(R, S, 1))
+
+    class _RS:
+        frustums = fr
+
+    renderer = RendererConfig(renderers={"rgb": RadianceRenderer}).setup()
+    # render() writes the hit rows into the background tensor it is given (renderers.py:97-105): pass a non-leaf copy
+    outs = renderer.render(w, {"rgb": rgb, "background": {"rgb": bg.clone()}, "normals": normals, "depth": _RS()},
+                           mask)
+    drgb = torch.randn(N, 3, generator=g)
+    (outs["rgb"] * drgb).sum().add_(outs["accumulation"].sum()).backward()
+    arrays.update({"ren:mask": mask, "ren:w": w.detach(), "ren:rgb": rgb.detach(), "ren:bg": bg.detach(),
+                   "ren:normals": normals, "ren:starts": starts, "ren:ends": ends, "ren:drgb": drgb,
+                   "ren:dw": w.grad, "ren:dvals": rgb.grad, "ren:dbg": bg.grad})
+    for k in ["rgb", "normals", "depth", "accumulation"]:
+        arrays["ren:out:" + k] = outs[k].detach()
+    save("plugins", **arrays)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["hashgrid", "mlp", "raygen", "sampler", "e2e"]
+    which = sys.argv[1:] or ["hashgrid", "mlp", "raygen", "sampler", "e2e", "plugins", "eval"]
+    if "eval" in which:
+        gen_eval()
+    if "plugins" in which:
+        gen_plugins()
     if "hashgrid" in which:
         gen_hashgrid()
     if "mlp" in which:
@@ -357,3 +490,7 @@ if __name__ == "__main__":
         np.savez_compressed(os.path.join(OUT, "e2e_grid_rgb_s30000.npz"), **b)
         gen_end_to_end("grid_raw", "grid_raw.yaml", ["rgb", "infrared", "mono", "polarization", "multispectral"],
                        95000, "grid_raw_5mod_s95000", raw=True)
+    if "e2e_gridbg" in which or "e2e" in which:
+        # config 5: grid background (hash grid r = 2 + MLP), 3-layer background heads, rgb + polarization
+        gen_end_to_end("grid_raw_grid_bg_unbalanced", "grid_raw_rgb_all_views_pol_10_views.yaml",
+                       ["rgb", "polarization"], 95000, "grid_raw_gridbg_s95000", raw=True, grid_bg=True)

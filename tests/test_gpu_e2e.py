@@ -42,7 +42,9 @@ def run_hip_e2e(f, dev, cap=None):
     mods = [str(m) for m in f["mods"]]
     log2T = int(np.log2(f["p:surface_model.surface_field.field.feature_grid.encoding.hash_table"].shape[0] // 16))
     raw = bool(f["raw"])
-    model = mm.BaseModel(mm.ModelSpec({m: ms.CHANNELS[m] for m in mods}, log2T=log2T)).to(dev)
+    bg_kind = "grid" if "p:background_model.background_field.base_field.feature_grid.encoding.hash_table" in f \
+        else "nerf"
+    model = mm.BaseModel(mm.ModelSpec({m: ms.CHANNELS[m] for m in mods}, log2T=log2T, bg_kind=bg_kind)).to(dev)
     model.load_state_dict({k[2:]: torch.from_numpy(v) for k, v in f.items() if k.startswith("p:")}, strict=True)
     model.train()
     model.set_step(int(f["step"]))
@@ -78,7 +80,8 @@ def run_hip_e2e(f, dev, cap=None):
     return mods, model, pose, outs, losses, total
 
 
-@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_rgb_s30000", "e2e_grid_raw_5mod_s95000"])
+@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_rgb_s30000", "e2e_grid_raw_5mod_s95000",
+                                  "e2e_grid_raw_gridbg_s95000"])
 def test_e2e_train_step(dev, name):
     f = load(name)
     mods, model, pose, outs, losses, total = run_hip_e2e(f, dev)

@@ -18,7 +18,7 @@ from test_gpu_e2e import load, rel_err, run_hip_e2e
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000"])
+@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000", "e2e_grid_raw_gridbg_s95000"])
 def test_e2e_fixed_capacity(dev, name):
     f = load(name)
     N = f[f"{str(f['mods'][0])}:coords"].shape[0]
