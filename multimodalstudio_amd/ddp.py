@@ -28,6 +28,51 @@ class DDP:
     def __init__(self, world_size: int, bucket_bytes: int = 256 << 20):
         self.world = world_size
         self.bucket = bucket_bytes // 4
+        self.pending = []
+
+    # -- overlapped exchange (eager steps) ----------------------------------------------------------------
+    def begin_step(self) -> None:
+        """Start a step: no region of any flat gradient buffer has been launched yet."""
+        self.pending = []          # (work, buffer, start, stop)
+
+    def grad_ready(self, grad: torch.Tensor, groups: List) -> None:
+        """Backward hook (functions.GRAD_READY_HOOKS): ``grad`` -- a view into one group's flat gradient buffer -- is
+        final, so its all-reduce starts now on the collective stream (ordered after the kernels already queued on
+        the current stream) and overlaps the rest of the backward.  Used for the hash-table gradients (97 % of the
+        payload); the radiance table's finishes half-way through the backward."""
+        if self.world <= 1:
+            return
+        for g in groups:
+            buf = g.grad
+            base = buf.data_ptr()
+            off = (grad.data_ptr() - base) // 4
+            if 0 <= off and off + grad.numel() <= buf.numel() and grad.is_contiguous():
+                for a in range(off, off + grad.numel(), self.bucket):
+                    b = min(a + self.bucket, off + grad.numel())
+                    self.pending.append((dist.all_reduce(buf[a:b], op=dist.ReduceOp.SUM, async_op=True), buf, a, b))
+                return
+
+    def finish_step(self, groups: List) -> None:
+        """All-reduce every region not launched early, wait for all of them, average."""
+        if self.world <= 1:
+            return
+        done = {}
+        for _, buf, a, b in self.pending:
+            done.setdefault(buf.data_ptr(), []).append((a, b))
+        works = [w for w, *_ in self.pending]
+        for g in groups:
+            buf = g.grad
+            spans = sorted(done.get(buf.data_ptr(), []))
+            pos = 0
+            for a, b in spans + [(buf.numel(), buf.numel())]:
+                for c in range(pos, a, self.bucket):
+                    works.append(dist.all_reduce(buf[c:min(c + self.bucket, a)], op=dist.ReduceOp.SUM, async_op=True))
+                pos = max(pos, b)
+        for w in works:
+            w.wait()
+        for g in groups:
+            g.grad.mul_(1.0 / self.world)
+        self.pending = []
 
     def allreduce_grads(self, groups: List) -> None:
         """Average flat gradient buffers across ranks (in place), in buckets of <= bucket_bytes."""

@@ -71,6 +71,35 @@ def _s() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+# Called with a parameter's gradient buffer as soon as the backward kernels have finished writing it (queued on the
+# current stream): the data-parallel trainer starts that gradient's all-reduce there (ddp.DDP.grad_ready).
+GRAD_READY_HOOKS: List = []
+_PENDING_USES = {}   # parameter data_ptr -> backward contributions still to come this step
+
+
+def reset_grad_uses() -> None:
+    _PENDING_USES.clear()
+
+
+def _grad_use(p: torch.Tensor) -> None:
+    """A differentiable forward use of parameter ``p`` (its backward will add one gradient contribution)."""
+    _PENDING_USES[p.data_ptr()] = _PENDING_USES.get(p.data_ptr(), 0) + 1
+
+
+def _grad_ready(p: torch.Tensor, g: Optional[torch.Tensor]) -> None:
+    """One backward contribution to ``p``'s gradient ``g`` is queued; the last one of the step fires the hooks (a
+    table used by several modalities' fields is final only after every modality's backward)."""
+    if g is None:
+        return
+    k = p.data_ptr()
+    left = _PENDING_USES.get(k, 1) - 1
+    _PENDING_USES[k] = left
+    if left <= 0:
+        _PENDING_USES.pop(k, None)
+        for h in GRAD_READY_HOOKS:
+            h(g)
+
+
 def _p(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
@@ -362,7 +391,9 @@ class SurfaceFunction(torch.autograd.Function):
         sdf = out[:M, 0:1].contiguous()
         geo = out[:M, 1:].contiguous()
         ctx.grid, ctx.active, ctx.M, ctx.G = grid, active, M, G
-        ctx.table = table          # the Parameter itself: its .grad is accumulated in place
+        ctx.table = ctx.table_p = table          # the Parameter itself: its .grad is accumulated in place
+        if ctx.needs_input_grad[1]:
+            _grad_use(table)
         ctx.four_delta, ctx.delta_sq = four_delta, delta_sq
         ctx.X = X
         ctx.save_for_backward(pos, table, grads, *params)
@@ -395,6 +426,7 @@ class SurfaceFunction(torch.autograd.Function):
         dtable = grad_target(ctx.table) if need_table else None
         dP = torch.zeros(5 * M, 3, device=dev) if need_pos else None
         grid_bwd(ctx.grid, X, K0, 5 * M, table, ctx.active, dX, 39, dtable, dP, group=5)
+        _grad_ready(ctx.table_p, dtable)
         dpos = None
         if need_pos:
             dpos = torch.zeros(M, 3, device=dev)
@@ -616,7 +648,9 @@ class RadianceFunction(torch.autograd.Function):
         run = ChainRun(params, RAD_ACTS, prec) if prec != 0 else MLPRun(params, RAD_ACTS, prec)
         feat = run.forward(X, keep=True)
         ctx.run, ctx.X, ctx.grid, ctx.active, ctx.S, ctx.G = run, X, grid, active, S, G
-        ctx.table = table
+        ctx.table = ctx.table_p = table
+        if ctx.needs_input_grad[4]:
+            _grad_use(table)
         ctx.save_for_backward(pos, dirs, normals, table, *params)
         return feat
 
@@ -637,6 +671,7 @@ class RadianceFunction(torch.autograd.Function):
         need_pos = ctx.needs_input_grad[0]
         dP = torch.zeros(M, 3, device=dev) if need_pos else None
         grid_bwd(ctx.grid, X, K0, M, table, ctx.active, dX, 29 + G, dtable, dP)
+        _grad_ready(ctx.table_p, dtable)   # the radiance table's last contribution: its all-reduce overlaps the rest
         dpos = torch.zeros(M, 3, device=dev) if need_pos else None
         dgeo = torch.empty(M, G, device=dev) if ctx.needs_input_grad[3] else None
         ddirs = torch.zeros(R, 3, device=dev) if ctx.needs_input_grad[1] else None

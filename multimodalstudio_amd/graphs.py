@@ -40,6 +40,9 @@ from . import functions as fx
 from .pipeline import Trainer, compute_loss, curvature_factor, lr_factor, select_right_channel
 
 
+CAPTURE_MODE = None   # override of the capture_error_mode (probes)
+
+
 def bucket_capacity(counts, granule: int, n: int) -> int:
     """Fixed foreground capacity for hit counts ``counts``: the largest, rounded up to ``granule``, at most n."""
     c = max(counts)
@@ -143,7 +146,7 @@ class GraphTrainer:
     def capture(self, key: tuple) -> None:
         cap = key[0]
         # thread-local capture mode when a process group is up: RCCL's watchdog thread queries events meanwhile
-        mode = "thread_local" if self.ddp is not None else "global"
+        mode = CAPTURE_MODE or ("thread_local" if self.ddp is not None else "global")
         torch.cuda.synchronize()
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, pool=self.pool, capture_error_mode=mode):

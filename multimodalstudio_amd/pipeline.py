@@ -339,6 +339,17 @@ class Trainer:
         """One training iteration (raw_pipeline.py:67-82); the BEFORE_TRAIN_ITERATION callbacks (coarse-to-fine
         mask, tap delta, cos anneal: feature_structures.py:97-108, surface_model.py:254-271,
         volume_rendering.py:227-230) are applied for the current step first, as the reference's trainer does."""
+        losses, total, outputs = self.compute_grads(coords, targets, rng, ddp)
+        f = lr_factor(self.step, self.cfg.max_iters)
+        self.fields.step(f)
+        if self.poses is not None:
+            self.poses.step(f)
+        self.step += 1
+        return losses, total, outputs
+
+    def compute_grads(self, coords=None, targets=None, rng: Optional[RNG] = None, ddp=None):
+        """Forward, losses, backward and (data parallel) the averaged gradient exchange: the train step up to the
+        optimizer (fabric.backward, raw_pipeline.py:67-77)."""
         self.model.set_step(self.step, self.cfg.max_iters)
         if coords is None:
             coords, sel = self.sampler.sample(self.frames)
@@ -347,6 +358,7 @@ class Trainer:
         coords_d = {m: c.to(dev, non_blocking=True) for m, c in coords.items()}
         targets_d = {m: t.to(dev, non_blocking=True) for m, t in targets.items()}
         rays = self.raygen(coords_d)
+        fx.reset_grad_uses()
         outputs = self.model(rays, rng)
         if self.raw:
             for m in self.modalities:
@@ -356,12 +368,18 @@ class Trainer:
         self.fields.zero_grad()
         if self.poses is not None:
             self.poses.zero_grad()
-        total.backward()
-        if ddp is not None:
-            ddp.allreduce_grads([self.fields] + ([self.poses] if self.poses is not None else []))
-        f = lr_factor(self.step, self.cfg.max_iters)
-        self.fields.step(f)
-        if self.poses is not None:
-            self.poses.step(f)
-        self.step += 1
+        groups = [self.fields] + ([self.poses] if self.poses is not None else [])
+        if ddp is not None and ddp.world > 1:
+            # hash-table gradients are all-reduced as soon as their backward kernels are queued (overlapping the rest
+            # of the backward), everything else after it
+            ddp.begin_step()
+            hook = lambda g: ddp.grad_ready(g, groups)  # noqa: E731
+            fx.GRAD_READY_HOOKS.append(hook)
+            try:
+                total.backward()
+            finally:
+                fx.GRAD_READY_HOOKS.remove(hook)
+            ddp.finish_step(groups)
+        else:
+            total.backward()
         return losses, total, outputs

@@ -1,0 +1,100 @@
+"""Two-rank check of the real data-parallel training paths, run by tests/test_gpu_ddp.py as
+``python -m torch.distributed.run --nproc-per-node 2 tests/ddp_check.py <out.json>`` (both ranks on cuda:0, gloo
+collectives: RCCL needs one GPU per rank).  Not a pytest module.
+
+0. GraphTrainer(ddp) x 5 (graph replays with the all-reduce between the two captured graphs): parameters identical
+   on both ranks and the steps were replayed.
+1. Trainer.compute_grads(ddp) -- hash-table gradients all-reduced while the backward still runs, the rest after --
+   equals the average of the two ranks' local gradients (local pass = same batch, same device RNG seed, no ddp).
+2. Trainer.train_step(ddp) x 2: parameters identical on both ranks.
+"""
+import json
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def gather(t):
+    parts = [torch.empty_like(t.cpu()) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t.detach().cpu().contiguous())
+    return parts
+
+
+def log(msg):
+    print(f"[rank {os.environ.get('RANK')}] {msg}", flush=True)
+
+
+def main():
+    import faulthandler
+    faulthandler.enable()
+    out_path = sys.argv[1]
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    from multimodalstudio_amd import ddp as mddp
+    from multimodalstudio_amd import functions as fx
+    from multimodalstudio_amd.graphs import GraphTrainer
+    from multimodalstudio_amd.pipeline import TrainConfig, Trainer
+    fx.set_precision("fp32")
+    cfg = TrainConfig(method="grid_raw", modalities=("rgb", "polarization"), num_rays_per_modality=256, log2T=14,
+                      width=64, height=48)
+    ddp = mddp.DDP(world, bucket_bytes=1 << 20)
+    res = {"world": world}
+    # graph-replayed data-parallel steps on a fresh trainer (as bench.py drives it: no eager default-stream steps
+    # before the captures)
+    tg = Trainer(cfg, dev, rank=rank)
+    tg.set_step(95000)
+    g = GraphTrainer(tg, ddp=ddp)
+    for _ in range(5):
+        g.step()
+    torch.cuda.synchronize()
+    p = gather(tg.fields.flat)
+    q = gather(tg.poses.flat)
+    res["graph_params_equal"] = bool(torch.equal(p[0], p[1]) and torch.equal(q[0], q[1]))
+    res["graph_stats"] = g.stats
+    res["graph_disabled"] = g.disabled
+    log("graph steps")
+    del g, tg
+    # 1. averaged gradients
+    t = Trainer(cfg, dev, rank=rank)
+    t.set_step(95000)
+    coords, sel = t.sampler.sample(t.frames)
+    targets = t.targets_for(coords, sel)
+    torch.cuda.manual_seed(100 + rank)
+    t.compute_grads(coords, targets)
+    local = t.fields.grad.clone()
+    local_pose = t.poses.grad.clone()
+    log("local grads")
+    torch.cuda.manual_seed(100 + rank)
+    t.compute_grads(coords, targets, ddp=ddp)
+    torch.cuda.synchronize()
+    log("reduced grads")
+    mean = sum(gather(local)) / world
+    mean_pose = sum(gather(local_pose)) / world
+    red = t.fields.grad.cpu()
+    scale = float(mean.abs().max())
+    res["grad_err"] = float((red - mean).abs().max()) / scale
+    res["pose_grad_err"] = float((t.poses.grad.cpu() - mean_pose).abs().max()) / max(float(mean_pose.abs().max()), 1e-30)
+    res["grads_differ_across_ranks"] = float((gather(local)[0] - gather(local)[1]).abs().max()) / scale
+    res["reduced_equal_across_ranks"] = bool(torch.equal(*gather(t.fields.grad)))
+    # 2. eager data-parallel steps
+    for _ in range(2):
+        t.train_step(ddp=ddp)
+    torch.cuda.synchronize()
+    p = gather(t.fields.flat)
+    res["eager_params_equal"] = bool(torch.equal(p[0], p[1]))
+    log("eager steps")
+    if rank == 0:
+        with open(out_path, "w") as f:
+            json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
