@@ -61,7 +61,8 @@ int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K
  * ReLU, radiance_field.py:72-77).  Layers are computed transposed so each layer's MFMA accumulator feeds the
  * next layer from registers.  prec 1 = bf16, 2 = split bf16x3 operands (fp32 accumulate).
  * Forward (backward = 0): out[l] = act_l(X_l W_l^T + b_l) for the 3 layers (out[0], out[1] may be NULL);
- *   rows >= rows_full compute / store only output column 0 of the last layer (the SDF taps).
+ *   rows >= rows_full compute / store only output column 0 of the last layer (the SDF taps), in fp32 from
+ *   w2row0 = the last layer's fp32 weight row 0 (required when rows_full < M).
  * Backward-data (backward = 1): X = dY of the last forward layer (rows >= rows_full: column 0 only), optionally
  *   scaled by act'(xaux) (stored to xout); out[l] = (prev . W^T) * act_l'(aux[l]) with act' evaluated from the
  *   forward output aux[l] (NULL: no scaling); out[2] = dX.
@@ -71,7 +72,7 @@ int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx, int K0, i
                   const float* xaux, int64_t ldxaux, int xact, float* xout, int64_t ldxout, const void* const* a_hi,
                   const void* const* a_lo, const float* const* bias, const float* const* aux, const int64_t* ldaux,
                   float* const* out, const int64_t* ldo, const int* N, const int* act, float beta, float thr,
-                  void* stream);
+                  const float* w2row0, void* stream);
 /* bf16 (hi, and lo = residual if non-NULL) image of W [N, K] (ldw) as an MFMA A operand of rows x cols:
  * transpose = 0 -> A = W, 1 -> A = W^T; permute = 1 stores each 16-column step in register-fed order
  * (columns 0-3, 8-11, 4-7, 12-15).  Zero padded; rows % 32 == 0, cols % 16 == 0.  Fragment-major: the 32x16

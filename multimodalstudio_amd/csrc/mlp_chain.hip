@@ -22,6 +22,8 @@
 // PREC 1: bf16 operands; PREC 2: split bf16x3 (x = hi + lo, acc += lo.hi + hi.lo + hi.hi); fp32 accumulation.
 #include "common.h"
 
+#include <utility>
+
 
 namespace {
 
@@ -59,6 +61,7 @@ struct ChainArgs {
   float* xout;         // backward: store of the scaled input (dZ of the last forward layer), or null
   int64_t ldxout;
   float beta, thr;     // Softplus(beta, threshold)
+  const float* w2row0; // forward: fp32 row 0 of the last layer's weight ([N1]) for the single-output row blocks
   ChainLayer L[3];
 };
 
@@ -108,19 +111,6 @@ __device__ __forceinline__ void mma(floatx16& acc, const bf16x8& ah, const bf16x
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
 }
 
-// 8 consecutive floats of a 16-B aligned row (pitch a multiple of 4 floats, >= K) from column k0 (a multiple of 8),
-// zero past K.  Both 16-B loads are unconditional (a column past K reads column 0 instead, then is zeroed), so a
-// k-step's loads issue back to back without exec-masked branches.
-__device__ __forceinline__ void load8(const float* __restrict__ row, int k0, int K, float* v) {
-  const f32x4 a = ld_nt4(row + (k0 < K ? k0 : 0));
-  const f32x4 b = ld_nt4(row + (k0 + 4 < K ? k0 + 4 : 0));
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    v[j] = k0 + j < K ? a[j] : 0.f;
-    v[4 + j] = k0 + 4 + j < K ? b[j] : 0.f;
-  }
-}
-
 // ---- weight fragments: block-shared, staged in LDS by LDS-DMA.  All four waves of a block multiply the SAME weight
 // fragments (the A operand) with their own rows, so each k-step's fragments are fetched once per block
 // (global_load_lds_dwordx4: no VGPRs, lane-linear 1 KiB per wave-instruction) into a 3-slot ring, two k-steps
@@ -128,7 +118,8 @@ __device__ __forceinline__ void load8(const float* __restrict__ row, int k0, int
 // MFMAs (one wave per SIMD) left every k-step waiting on L2 latency: 6 % of the MFMA rate.
 // Packed images are fragment-major (mms_mlp_pack): fragment (k-step s, tile t) is one contiguous 1 KiB block at
 // element ((s * NT + t) * 64 + lane) * 8.
-constexpr int kRing = 3;
+constexpr int kDepth = 2;           // k-steps a load is issued ahead of its use (3 measured no faster)
+constexpr int kRing = kDepth + 1;   // ring slots: the one being read + kDepth in flight
 constexpr int kMaxTiles = 10;  // widest chain layer: 10 column tiles (320 units)
 constexpr int kSlot = 21;  // 1 KiB chunks per ring slot: hi + lo images of up to 10 tiles, + 1 spare (dummy loads)
 typedef __attribute__((address_space(3))) void lds_void;
@@ -175,32 +166,59 @@ __device__ __forceinline__ void stage(const ChainLayer& Ly, int s, int wave, int
   }
 }
 
+// compile-time loop: f(std::integral_constant<int, i>) for i in [0, N)
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// vector-memory instructions get_b(s) issues: GE at even s, GO at odd s (none before the layer starts)
+template <int GE, int GO>
+constexpr int gops(int s) { return s < 0 ? 0 : ((s & 1) ? GO : GE); }
+
 // one layer: acc[t] (t < nt) += sum_{s < ks} A(s, t) . B(s); B(s) = get_b(s) (compile-time s: register arrays).
 // ks and NTL are block-uniform (every wave takes part in every barrier); nt may be smaller per wave (nt <= NTL).
-// pre(s) issues the global loads get_b(s) will consume, one k-step ahead (before the ring loads of step s + 1), so
-// the wait for the ring's step s also covers them.
-// Order inside a k-step: EARLY = false: pre(s + 1), ring loads of step s + 2, then get_b(s) (input loads issued
-// as early as possible); EARLY = true: get_b(s) first, then the ring loads, so the stores a lazy epilogue issues
-// in get_b(s) precede them -- vmcnt retires in order, and stores issued after the ring loads would make the next
-// k-step's wait cover their write latency as well.
-template <int PREC, int NT, int NTL, int KS, bool EARLY = false, typename Pre, typename GetB>
+// Pipeline, kDepth k-steps deep for everything a k-step reads from memory: step t issues pre(t + kDepth) (the
+// layer-0 input slices, PRE instructions) and the ring DMA of step t + kDepth (PER instructions), then get_b(t) (GE /
+// GO instructions: the lazy epilogue's stores, the backward's dZ stores).  The wait before step s is EXACT: it lets
+// every instruction issued after step s's own loads stay in flight -- get_b(s - kDepth .. s - 1) and the pre / DMA
+// of the steps already issued after s -- so neither a store nor a later prefetch holds up a k-step (vmcnt retires in
+// issue order, stores included).  Every counted instruction is issued unconditionally (clamped rows, no exec-skipped
+// branches), so the counts are exact for every wave.
+template <int PREC, int NT, int NTL, int KS, int PRE, int GE, int GO, typename Pre, typename GetB>
 __device__ __forceinline__ void run_layer(const ChainLayer& Ly, int ks, int nt, floatx16 (&acc)[NT], int wave,
                                           int lane, bf16x8 (*ring)[kSlot][64], Pre&& pre, GetB&& get_b) {
   constexpr int PER = stage_per<PREC, NTL>();
   wait_vm_barrier<63>();  // every wave is done with the ring (previous layer / launch prologue)
-  pre(0);
-  stage<PREC, NT, NTL>(Ly, 0, wave, lane, ring);
-  if (ks > 1) stage<PREC, NT, NTL>(Ly, 1, wave, lane, ring);
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
+  for (int j = 0; j < kDepth; ++j) {
+    if (j < ks) {
+      pre(j);
+      stage<PREC, NT, NTL>(Ly, j, wave, lane, ring);
+    }
+  }
+  static_for<KS>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
     if (s < ks) {
-      // this wave's loads of step s have landed, and (barrier) every wave's; slot (s + 2) % 3 is free
-      if (s + 1 < ks) wait_vm_barrier<PER>(); else wait_vm_barrier<0>();
+      // this wave's loads of step s have landed, and (barrier) every wave's; slot (s + kDepth) % kRing is free.
+      // Younger instructions: get_b(s - kDepth .. s - 1) and the f = min(kDepth - 1, ks - 1 - s) steps issued after s.
+      static_assert(kDepth >= 1 && kDepth <= 3, "kG sums the last kDepth get_b steps");
+      constexpr int kG = (kDepth >= 3 ? gops<GE, GO>(s - 3) : 0) + (kDepth >= 2 ? gops<GE, GO>(s - 2) : 0) +
+                         gops<GE, GO>(s - 1);
+      const int f = ks - 1 - s;
+      if (kDepth >= 3 && f >= 2) wait_vm_barrier<kG + (kDepth - 1) * (PRE + PER)>();
+      else if (kDepth >= 2 && f >= 1) wait_vm_barrier<kG + (kDepth >= 3 ? 1 : kDepth - 1) * (PRE + PER)>();
+      else wait_vm_barrier<kG>();
+      if (s + kDepth < ks) {
+        pre(s + kDepth);
+        stage<PREC, NT, NTL>(Ly, s + kDepth, wave, lane, ring);
+      }
       bf16x8 bh, bl;
-      if constexpr (EARLY) get_b(s, bh, bl);
-      if (s + 1 < ks) pre(s + 1);
-      if (s + 2 < ks) stage<PREC, NT, NTL>(Ly, s + 2, wave, lane, ring);
-      if constexpr (!EARLY) get_b(s, bh, bl);
+      get_b(s, bh, bl);
       const bf16x8* slot = &ring[s % kRing][0][0];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -211,7 +229,7 @@ __device__ __forceinline__ void run_layer(const ChainLayer& Ly, int ks, int nt, 
         }
       }
     }
-  }
+  });
 }
 
 // Epilogue of one accumulator tile t, in place.  Lane (m, h): register 4 g + i holds unit n = 32 t + 8 g + 4 h + i
@@ -261,11 +279,19 @@ __device__ __forceinline__ void epi_tile(floatx16& acc, int t, const ChainLayer&
 }
 
 // The forward's lazy epilogue of a full 32-unit tile (hidden layers: N = 32 NT, checked at dispatch): bias,
-// activation, and (KEEP) the fp32 store, with no guards at all, so it schedules in one basic block with the
-// MFMAs around it.  Rows past M compute row M - 1's values and store them there again (identical bits).
+// activation, and (KEEP) the fp32 store of the tile's 32 rows x 128 B, with no guards at all, so it schedules in one
+// basic block with the MFMAs around it.  The store goes through the wave's LDS scratch (row pitch 36 floats: both
+// the accumulator-layout writes and the row-contiguous reads are bank-conflict free): the accumulator gives each lane
+// four 16-B pieces spread over its row, so storing from registers put 64 rows x 16 B into every store instruction and
+// every 128-B row segment was written by 8 partial stores (2-3x write traffic, PMC WRITE_SIZE); from the scratch each
+// of the 4 store instructions writes 8 whole 128-B row segments.  Rows past M store row M - 1's values there again
+// (identical bits).  Still exactly 4 vector-memory instructions per lane (run_layer's counted waits).
+constexpr int kScr = 36;  // scratch row pitch (floats)
+
 template <int ACT, bool KEEP>
-__device__ __forceinline__ void epi_tile_full(floatx16& acc, int t, const float* sb, float* orow, int h, float beta,
-                                              float thr) {
+__device__ __forceinline__ void epi_tile_full(floatx16& acc, int t, const float* sb, float* obase, int64_t ldo,
+                                              int64_t m0, int64_t M, float* scr, int lane, float beta, float thr) {
+  const int r = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int n0 = 32 * t + 8 * g + 4 * h;
@@ -276,7 +302,61 @@ __device__ __forceinline__ void epi_tile_full(floatx16& acc, int t, const float*
       v[i] = act_fwd<ACT>(acc[4 * g + i] + bq[i], beta, thr);
       acc[4 * g + i] = v[i];
     }
-    if constexpr (KEEP) st_nt4(orow + n0, v);
+    if constexpr (KEEP) *reinterpret_cast<f32x4*>(scr + r * kScr + 8 * g + 4 * h) = v;
+  }
+  if constexpr (KEEP) {
+    const int q = lane & 7;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = 8 * j + (lane >> 3);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(scr + row * kScr + 4 * q);
+      const int64_t mr = m0 + row < M ? m0 + row : M - 1;
+      st_nt4(obase + mr * ldo + 32 * t + 4 * q, v);
+    }
+  }
+}
+
+// Backward epilogue of a full 256-unit hidden layer, through the wave's LDS scratch like the forward's stores:
+// dZ = acc * act'(Y) with the forward output Y read row-contiguously (each load instruction 8 rows x 128 B, the next
+// tile's rows in flight while this tile is processed) and dZ stored the same way; both sides pass the accumulator
+// layout through the scratch.  Rows past M read / write row M - 1 (identical values).
+template <int NT, int ACT>
+__device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const ChainLayer& Ly, int64_t m0, int64_t M,
+                                                    float* scr, int lane, float beta, float thr) {
+  const int r = lane & 31, h = lane >> 5, q = lane & 7;
+  int64_t rows[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t mr = m0 + 8 * j + (lane >> 3);
+    rows[j] = mr < M ? mr : M - 1;
+  }
+  f32x4 y[2][4];
+  auto load = [&](int t, f32x4* dst) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dst[j] = ld_nt4(Ly.aux + rows[j] * Ly.ldaux + 32 * t + 4 * q);
+  };
+  load(0, y[0]);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (t + 1 < NT) load(t + 1, y[(t + 1) & 1]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(scr + (8 * j + (lane >> 3)) * kScr + 4 * q) = y[t & 1][j];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 yv = *reinterpret_cast<const f32x4*>(scr + r * kScr + 8 * g + 4 * h);
+      f32x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = acc[t][4 * g + i] * act_grad_out<ACT>(yv[i], beta, thr);
+        acc[t][4 * g + i] = v[i];
+      }
+      *reinterpret_cast<f32x4*>(scr + r * kScr + 8 * g + 4 * h) = v;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(scr + (8 * j + (lane >> 3)) * kScr + 4 * q);
+      st_nt4(Ly.out + rows[j] * Ly.ldo + 32 * t + 4 * q, v);
+    }
   }
 }
 
@@ -315,6 +395,9 @@ __device__ __forceinline__ void to_b(const floatx16 (&acc)[NT], bf16x8 (&bh)[2 *
 template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, int XA, bool KEEP>
 __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   __shared__ __attribute__((aligned(1024))) bf16x8 ring[kRing][kSlot][64];
+  // layer-0 input slices (and, backward radiance chain, the xaux slices): [slot][wave][2 x 64 lane chunks]
+  __shared__ __attribute__((aligned(1024))) f32x4 xring[kRing][4][128];
+  __shared__ __attribute__((aligned(1024))) f32x4 aring[(BWD && XA != 0) ? kRing : 1][4][128];
   __shared__ __attribute__((aligned(16))) float sbias[3][32 * kMaxTiles];  // forward biases, zero padded
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar staging addresses
@@ -330,62 +413,88 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   const bool anyfull = m0 < a.rows_full;   // wave-uniform
   const bool blockfull = mb < a.rows_full;  // block-uniform
   const floatx16 zero = {};
+  __shared__ __attribute__((aligned(16))) float sw0[BWD ? 1 : 32 * NT1];  // forward: last layer's weight row 0 (fp32)
+  // per-wave staging of the row-contiguous stores (forward KEEP) and of the backward's Y loads / dZ stores
+  constexpr bool kStage = BWD || KEEP;
+  __shared__ __attribute__((aligned(16))) float sscr[kStage ? 4 : 1][32 * kScr];
+  float* scr = &sscr[kStage ? wave : 0][0];
   if constexpr (!BWD) {
 #pragma unroll
     for (int l = 0; l < 3; ++l)
       for (int i = threadIdx.x; i < 32 * kMaxTiles; i += 256)
         sbias[l][i] = (a.L[l].bias != nullptr && i < a.L[l].N) ? a.L[l].bias[i] : 0.f;
+    for (int i = threadIdx.x; i < 32 * NT1; i += 256) sw0[i] = (a.w2row0 != nullptr && i < a.L[1].N) ? a.w2row0[i] : 0.f;
   }  // (visible after the first layer's opening barrier)
-  // forward hidden-layer stores (KEEP): every lane stores its (clamped) row
-  auto orow_of = [&](const ChainLayer& Ly) -> float* { return KEEP ? Ly.out + mc * Ly.ldo : nullptr; };
 
   // ---- layer 0: B operand from memory, natural k order
   floatx16 acc0[NT0];
 #pragma unroll
   for (int t = 0; t < NT0; ++t) acc0[t] = zero;
   {
+    // backward of the radiance chain (XIO): the input is scaled by the last forward ReLU's derivative (xaux) and the
+    // scaled rows are stored (xout: dZ of the last forward layer, for the weight gradients).  Rows past M use the
+    // clamped row (identical values), so every load / store below is issued by every wave (exact vmcnt counts).
+    constexpr bool XIO = BWD && XA != 0;
     const float* xr = a.X + mc * a.ldx;
-    const float* xa = (BWD && a.xaux != nullptr) ? a.xaux + mc * a.ldxaux : nullptr;
-    float* xo = (BWD && a.xout != nullptr && mval) ? a.xout + m * a.ldxout : nullptr;
+    const float* xa = XIO ? a.xaux + mc * a.ldxaux : nullptr;
+    float* xo = XIO ? a.xout + mc * a.ldxout : nullptr;
     // backward on SDF tap rows: only input column 0 is live (a block of tap rows needs k-step 0 alone)
     const int ks0 = (BWD && !blockfull) ? 1 : KS0;
-    float xv[2][8], wv[2][8];  // k-step s's input (and xaux) row slice in buffer s & 1
+    // k-step s's input slices (16 columns of the wave's 32 rows) land in LDS by LDS-DMA, two steps ahead, like the
+    // weights: instruction j, lane i loads row (i & 31)'s quad q = 2 j + (i >> 5) to lane-linear LDS, i.e. quad-major
+    // [q][row] images, so each lane's two 16-B reads of its row are bank-conflict free.  The compiler never sees these
+    // loads, so it inserts no vmcnt waits of its own into the k-loop (compiler-visible loads drew vmcnt(0..3) waits
+    // there that also drained the weight prefetch).  Quads past K0 read column 0 and are zeroed in get_b.
     auto pre = [&](int s) {
-      load8(xr, 16 * s + 8 * h, a.K0, xv[s & 1]);
-      if (BWD && xa != nullptr) load8(xa, 16 * s + 8 * h, a.K0, wv[s & 1]);
+      const int slot = s % kRing;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = 16 * s + 4 * (2 * j + (lane >> 5));
+        const int c = col < a.K0 ? col : 0;
+        lds_dma16(xr + c, __builtin_amdgcn_readfirstlane(
+                              (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&xring[slot][wave][64 * j])));
+        if constexpr (XIO)
+          lds_dma16(xa + c, __builtin_amdgcn_readfirstlane(
+                                (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&aring[slot][wave][64 * j])));
+      }
     };
     auto get_b = [&](int s, bf16x8& bh, bf16x8& bl) {
       const int k0 = 16 * s + 8 * h;
-      float v[8];
+      const f32x4* xs = &xring[s % kRing][wave][0];
+      const f32x4 x0 = xs[64 * h + r], x1 = xs[64 * h + 32 + r];
+      float v[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = xv[s & 1][j];
+      for (int j = 0; j < 8; ++j)
+        if (k0 + j >= a.K0) v[j] = 0.f;
       if constexpr (BWD) {
         if (!rowfull) {
 #pragma unroll
           for (int j = 0; j < 8; ++j)
             if (k0 + j > 0) v[j] = 0.f;
         }
-        if (xa != nullptr) {
+        if constexpr (XIO) {
+          const f32x4* as = &aring[s % kRing][wave][0];
+          const f32x4 w0 = as[64 * h + r], w1 = as[64 * h + 32 + r];
+          const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] *= act_grad_out<XA>(wv[s & 1][j], a.beta, a.thr);
-        }
-        if (xo != nullptr && (rowfull || s == 0)) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (k0 + j < a.K0 && (rowfull || k0 + j == 0)) __builtin_nontemporal_store(v[j], xo + k0 + j);
+          for (int j = 0; j < 8; ++j) v[j] *= act_grad_out<XA>(wv[j], a.beta, a.thr);
+          // K0 is a multiple of 8 here (dispatch): two unguarded 16-B stores
+          st_nt4(xo + k0, f32x4{v[0], v[1], v[2], v[3]});
+          st_nt4(xo + k0 + 4, f32x4{v[4], v[5], v[6], v[7]});
         }
       }
       split8<PREC>(v, bh, bl);
     };
-    run_layer<PREC, NT0, NT0, KS0>(a.L[0], ks0, NT0, acc0, wave, lane, ring, pre, get_b);
+    run_layer<PREC, NT0, NT0, KS0, XIO ? 4 : 2, XIO ? 2 : 0, XIO ? 2 : 0>(a.L[0], ks0, NT0, acc0, wave, lane, ring,
+                                                                         pre, get_b);
   }
   auto nopre = [](int) {};
-  // lazy-epilogue stores ahead of the ring loads: measured faster for the bf16 radiance chain (173 -> 158 us), slower
-  // for the split-bf16x3 SDF chain (586 -> 655 us: its longer epilogue then delays the prefetch)
-  constexpr bool kEarly = !BWD && PREC == 1;
+  // forward layers 1 and 2: get_b(s) of an even step finishes (and with KEEP stores, 4 x 16 B per lane) one tile of the
+  // previous layer; backward layers 1 and 2 take B from registers (no memory instructions)
+  constexpr int kGE = (!BWD && KEEP) ? 4 : 0;
   bf16x8 b1h[2 * NT0], b1l[2 * NT0];
   if constexpr (BWD) {
-    epilogue<NT0, BWD, A0>(acc0, a.L[0], sbias[0], NT0, m, mc, mval, false, h, a.beta, a.thr);
+    epilogue_bwd_staged<NT0, A0>(acc0, a.L[0], m0, a.M, scr, lane, a.beta, a.thr);
     to_b<PREC, NT0>(acc0, b1h, b1l);
   }
 
@@ -394,12 +503,12 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
 #pragma unroll
   for (int t = 0; t < NT1; ++t) acc1[t] = zero;
   {
-    float* orow0 = orow_of(a.L[0]);
-    run_layer<PREC, NT1, NT1, 2 * NT0, kEarly>(a.L[1], 2 * NT0, NT1, acc1, wave, lane, ring, nopre,
+    run_layer<PREC, NT1, NT1, 2 * NT0, 0, kGE, 0>(a.L[1], 2 * NT0, NT1, acc1, wave, lane, ring, nopre,
                                        [&](int s, bf16x8& bh, bf16x8& bl) {
       if constexpr (!BWD) {
         if ((s & 1) == 0) {
-          epi_tile_full<A0, KEEP>(acc0[s >> 1], s >> 1, sbias[0], orow0, h, a.beta, a.thr);
+          epi_tile_full<A0, KEEP>(acc0[s >> 1], s >> 1, sbias[0], a.L[0].out, a.L[0].ldo, m0, a.M, scr, lane, a.beta,
+                                  a.thr);
           tile_to_b<PREC>(acc0[s >> 1], &b1h[s], &b1l[s]);
         }
       }
@@ -408,7 +517,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   }
   bf16x8 b2h[2 * NT1], b2l[2 * NT1];
   if constexpr (BWD) {
-    epilogue<NT1, BWD, A1>(acc1, a.L[1], sbias[1], NT1, m, mc, mval, false, h, a.beta, a.thr);
+    epilogue_bwd_staged<NT1, A1>(acc1, a.L[1], m0, a.M, scr, lane, a.beta, a.thr);
     to_b<PREC, NT1>(acc1, b2h, b2l);
   }
 
@@ -418,20 +527,37 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   for (int t = 0; t < NT2; ++t) acc2[t] = zero;
   const int nt2 = (!BWD && !anyfull) ? 1 : NT2;
   {
-    float* orow1 = orow_of(a.L[1]);
     auto get_b2 = [&](int s, bf16x8& bh, bf16x8& bl) {
       if constexpr (!BWD) {
         if ((s & 1) == 0) {
-          epi_tile_full<A1, KEEP>(acc1[s >> 1], s >> 1, sbias[1], orow1, h, a.beta, a.thr);
+          epi_tile_full<A1, KEEP>(acc1[s >> 1], s >> 1, sbias[1], a.L[1].out, a.L[1].ldo, m0, a.M, scr, lane, a.beta,
+                                  a.thr);
           tile_to_b<PREC>(acc1[s >> 1], &b2h[s], &b2l[s]);
         }
       }
       bh = b2h[s]; bl = b2l[s];
     };
-    if (BWD || blockfull)
-      run_layer<PREC, NT2, NT2, 2 * NT1, kEarly>(a.L[2], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2);
-    else
-      run_layer<PREC, NT2, 1, 2 * NT1, kEarly>(a.L[2], 2 * NT1, 1, acc2, wave, lane, ring, nopre, get_b2);
+    if (BWD || blockfull) {
+      run_layer<PREC, NT2, NT2, 2 * NT1, 0, kGE, 0>(a.L[2], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2);
+    } else {
+      // a block of SDF tap rows (or the sampler's inference rows) needs only output 0 of the last layer: a 256-long
+      // dot product per row, done in fp32 on the VALU (W row 0 from LDS) instead of 2 NT1 ring k-steps of one
+      // bf16x3 column tile -- no barriers, no weight streaming, and fp32 instead of split-bf16 operand precision
+      float p = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT1; ++t) {
+        epi_tile_full<A1, KEEP>(acc1[t], t, sbias[1], a.L[1].out, a.L[1].ldo, m0, a.M, scr, lane, a.beta, a.thr);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 w = *reinterpret_cast<const f32x4*>(sw0 + 32 * t + 8 * g + 4 * h);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) p = __builtin_fmaf(acc1[t][4 * g + i], w[i], p);
+        }
+      }
+      p += __shfl_xor(p, 32);   // the two halves of the row's units (lanes r and r + 32)
+      if (mval && h == 0 && a.L[2].out != nullptr) __builtin_nontemporal_store(p + sbias[2][0], a.L[2].out + m * a.L[2].ldo);
+      return;
+    }
   }
   epilogue<NT2, BWD, A2>(acc2, a.L[2], sbias[2], nt2, m, mc, mval, !BWD && !rowfull, h, a.beta, a.thr);
 }
@@ -452,6 +578,9 @@ bool dispatch_chain(int ks0, int nt0, int nt1, int nt2, bool bwd, const ChainArg
   const int a0 = a.L[0].act, a1 = a.L[1].act, a2 = a.L[2].act;
   const bool noxa = a.xaux == nullptr;
   const bool hidden_full = a.L[0].N == 256 && a.L[1].N == 256;
+  // backward: both hidden layers' dZ are stored and scaled by act'(Y) (the staged epilogue assumes both)
+  const bool bwd_hidden = a.L[0].aux != nullptr && a.L[1].aux != nullptr && a.L[0].out != nullptr &&
+                          a.L[1].out != nullptr && hidden_full;
   const bool keep = a.L[0].out != nullptr && a.L[1].out != nullptr;
   const bool nokeep = a.L[0].out == nullptr && a.L[1].out == nullptr;
   if (!bwd && ks0 == 5 && nt0 == 8 && nt1 == 8 && nt2 == 9 && a0 == 2 && a1 == 2 && a2 == 0 && hidden_full &&
@@ -461,11 +590,11 @@ bool dispatch_chain(int ks0, int nt0, int nt1, int nt2, bool bwd, const ChainArg
   } else if (!bwd && ks0 == 20 && nt0 == 8 && nt1 == 8 && nt2 == 8 && a0 == 1 && a1 == 1 && a2 == 1 &&
              hidden_full && keep) {
     launch_chain<PREC, 20, 8, 8, 8, false, 1, 1, 1, 0, true>(a, s);
-  } else if (bwd && ks0 == 17 && nt0 == 8 && nt1 == 8 && nt2 == 3 && a0 == 2 && a1 == 2 && a2 == 0 &&
-             (noxa || a.xact == 0)) {
+  } else if (bwd && ks0 == 17 && nt0 == 8 && nt1 == 8 && nt2 == 3 && a0 == 2 && a1 == 2 && a2 == 0 && noxa &&
+             a.xout == nullptr && bwd_hidden) {
     launch_chain<PREC, 17, 8, 8, 3, true, 2, 2, 0, 0>(a, s);
-  } else if (bwd && ks0 == 16 && nt0 == 8 && nt1 == 8 && nt2 == 10 && a0 == 1 && a1 == 1 && a2 == 0 &&
-             (noxa || a.xact == 1)) {
+  } else if (bwd && ks0 == 16 && nt0 == 8 && nt1 == 8 && nt2 == 10 && a0 == 1 && a1 == 1 && a2 == 0 && !noxa &&
+             a.xact == 1 && a.xout != nullptr && a.K0 % 8 == 0 && bwd_hidden) {
     launch_chain<PREC, 16, 8, 8, 10, true, 1, 1, 0, 1>(a, s);
   } else {
     return false;
@@ -520,7 +649,7 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx
                              int64_t ldxout, const void* const* a_hi, const void* const* a_lo,
                              const float* const* bias, const float* const* aux, const int64_t* ldaux,
                              float* const* out, const int64_t* ldo, const int* N, const int* act, float beta,
-                             float thr, void* stream) {
+                             float thr, const float* w2row0, void* stream) {
   const char* fn = "mms_mlp_chain";
   MMS_REQUIRE(prec == 1 || prec == 2, fn, "prec must be 1 (bf16) or 2 (split bf16x3)");
   MMS_REQUIRE(M >= 0 && K0 > 0, fn, "bad shape");
@@ -533,6 +662,9 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx
   a.xaux = backward ? xaux : nullptr; a.ldxaux = ldxaux; a.xact = xact;
   a.xout = backward ? xout : nullptr; a.ldxout = ldxout;
   a.beta = beta; a.thr = thr;
+  a.w2row0 = backward ? nullptr : w2row0;
+  MMS_REQUIRE(backward || rows_full >= M || w2row0 != nullptr, fn,
+              "forward with single-output rows (rows_full < M) needs the last layer's fp32 weight row 0");
   int nt[3];
   for (int l = 0; l < 3; ++l) {
     MMS_REQUIRE(a_hi[l] != nullptr && N[l] > 0, fn, "missing layer weights");

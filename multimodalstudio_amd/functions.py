@@ -252,7 +252,7 @@ class ChainRun:
         return hi, lo
 
     def _chain(self, backward: bool, X, K0: int, rows_full: int, packs, bias, aux, outs, Ns, acts,
-               xaux=None, xact: int = 0, xout=None):
+               xaux=None, xact: int = 0, xout=None, w2row0=None):
         VP = ctypes.c_void_p * 3
         his = VP(*[p[0].data_ptr() for p in packs])
         los = VP(*[(p[1].data_ptr() if p[1] is not None else None) for p in packs])
@@ -267,7 +267,7 @@ class ChainRun:
         _lib.call("mms_mlp_chain", self.prec, int(backward), X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
                   _p(xaux), 0 if xaux is None else xaux.stride(0), int(xact), _p(xout),
                   0 if xout is None else xout.stride(0), cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux),
-                  cast(os_), cast(ldo), cast(ns), cast(ac), self.beta, self.thr, _s())
+                  cast(os_), cast(ldo), cast(ns), cast(ac), self.beta, self.thr, _p(w2row0), _s())
 
     def forward(self, x: torch.Tensor, keep: bool, rows_full: Optional[int] = None) -> torch.Tensor:
         """x [M, K0] (16-B aligned rows); returns the last layer's output [M, N2] (row stride rounded to 4)."""
@@ -291,7 +291,7 @@ class ChainRun:
         Y = [_alloc(M, Ns[0], dev) if keep else None, _alloc(M, Ns[1], dev) if keep else None, _alloc(M, Ns[2], dev)]
         self.rows_full = M if rows_full is None else int(rows_full)
         self._chain(False, x, K0, self.rows_full, packs, [self.params[3 * l + 2] for l in range(3)], [None] * 3, Y,
-                    Ns, [a[0] for a in self.acts])
+                    Ns, [a[0] for a in self.acts], w2row0=self.Ws[2])
         self.Y = Y
         return Y[2]
 

@@ -424,12 +424,13 @@ class BaseModel(nn.Module):
             else:
                 heads[m] = ModalityHead("plain", 256, c, 3, 64, "Sigmoid")
         self.radiance_model = RadianceModel(RadianceField(FeatureGridAndMLP(grid(), rad_mlp)), heads)
-        dens = ModalityHead("plain", 256, 1, 1, 64, "Softplus")
+        # construction order = parameter-initialisation RNG order (base, head, density head, modality heads)
         bg_heads = {}
         if spec.bg_kind == "grid":
             bg_base = FeatureGridAndMLP(grid(2.0), MLP(MLPConfig(num_layers=3, hidden_dim=128, out_activation="ReLU"),
                                                        3 + 36 + 32, 256))
             bg_head = MLP(MLPConfig(num_layers=4, hidden_dim=256, out_activation="ReLU"), 256 + 27, 256)
+            dens = ModalityHead("plain", 256, 1, 1, 64, "Softplus")
             for m, c in mods.items():
                 if m == "polarization":
                     bg_heads[m] = ModalityHead("polarization", 256, c, 3, 256, "None")
@@ -438,6 +439,7 @@ class BaseModel(nn.Module):
         else:
             bg_base = MLP(MLPConfig(num_layers=4, hidden_dim=256, out_activation="ReLU"), 39, 256)
             bg_head = MLP(MLPConfig(num_layers=4, hidden_dim=256, out_activation="ReLU"), 256 + 27, 128)
+            dens = ModalityHead("plain", 256, 1, 1, 64, "Softplus")
             for m, c in mods.items():
                 if m == "polarization":
                     bg_heads[m] = ModalityHead("polarization", 128, c, 1, 64, "None")

@@ -40,9 +40,28 @@ def params(dims, dev, g):
     return out
 
 
+def kernel_us(fn, reps=10):
+    """Average duration of the mms_mlp_chain launches fn makes, from HIP events around each launch (_lib.TIMER), so
+    the weight-norm / pack launches of ChainRun.forward are not counted."""
+    from multimodalstudio_amd import _lib
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    sys.path.insert(0, ROOT)
+    from bench import chain_work
+    _lib.TIMER.start({"mms_mlp_chain": chain_work})
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    _lib.TIMER.stop()
+    summ = _lib.TIMER.summary()
+    return {k: ms * 1e3 for k, (n, ms, _) in summ.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--centres", type=int, default=54400)
+    ap.add_argument("--sweep", action="store_true", help="sampler-form chain at 1 block, 1 and 2 block rounds")
     a = ap.parse_args()
     from multimodalstudio_amd import functions as fx
     dev = torch.device("cuda", 0)
@@ -73,6 +92,28 @@ def main():
             print(f"{name:28s} bwd {tb:9.1f} us  (incl. weight-gradient GEMMs; chain-only flops "
                   f"{flb / 1e9:.1f} GFLOP)", flush=True)
 
+    if a.sweep:
+        p = params((71, 256, 256, 257), dev, g)
+        run = fx.ChainRun(p, fx.SDF_ACTS, 2)
+        for rows in [128, 256 * 128, 512 * 128, 2048 * 128]:
+            X = fx._alloc(rows, 71, dev)
+            X.copy_(torch.randn(rows, 71, generator=g) * 0.3)
+            us = kernel_us(lambda: run.forward(X, keep=False, rows_full=0))
+            print(f"sdf infer-form chain rows={rows:8d} blocks={rows // 128:5d}  kernel {us}", flush=True)
+        for rows_full_frac in [1.0, 0.2, 0.0]:
+            rows = 5 * M
+            X = fx._alloc(rows, 71, dev)
+            X.copy_(torch.randn(rows, 71, generator=g) * 0.3)
+            rf = int(rows * rows_full_frac)
+            dy = fx._alloc(rows, 257, dev)
+            dy.copy_(torch.randn(rows, 257, generator=g))
+
+            def fb():
+                run.forward(X, keep=True, rows_full=rf)
+                run.backward(dy)
+            us = kernel_us(fb)
+            print(f"sdf train-form chain rows={rows} rows_full={rf}  kernel {us}", flush=True)
+        return
     run_case("sdf 5M (centre+taps)", (71, 256, 256, 257), fx.SDF_ACTS, 2, 5 * M, M)
     run_case("sdf sampler (32 rows/ray)", (71, 256, 256, 257), fx.SDF_ACTS, 2, M // 2, 0)
     run_case("radiance", (317, 256, 256, 256), fx.RAD_ACTS, 1, M, M)

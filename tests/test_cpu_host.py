@@ -160,3 +160,18 @@ def test_graph_capacity_buckets():
     assert bucket_capacity([896], 64, 2048) == 896
     assert bucket_capacity([2040], 64, 2048) == 2048
     assert bucket_capacity([1], 64, 2048) == 64
+
+
+def test_model_init_matches_train_parity_fixture():
+    """BaseModel parameter initialisation consumes the RNG in the fixture's order (construction order of the module
+    tree): the same seed gives the init the training-parity fixture recorded (caught on the host, before the GPU)."""
+    import ast
+    import numpy as np
+    from multimodalstudio_amd import model as mm
+    from multimodalstudio_amd import scene as ms
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "train_parity_rgb.npz"))
+    cfg = ast.literal_eval(f["cfg_json"].tobytes().decode())
+    torch.manual_seed(654824)
+    model = mm.BaseModel(mm.ModelSpec({m: ms.CHANNELS[m] for m in cfg["modalities"]}, log2T=cfg["log2T"]))
+    ck = float(sum(float(v.detach().double().abs().sum()) for v in model.state_dict().values()))
+    assert ck == pytest.approx(float(f["init_checksum"]), rel=1e-9)

@@ -6,7 +6,8 @@ tests/golden/make_train_parity.py), then held-out PSNR.
   one: float-atomic gradient sums are not reproducible bit for bit, and AdamW (eps 1e-15) turns last-bit
   differences of near-zero gradients into full-size updates, so per-step losses of two runs of the *same*
   implementation drift apart; the averaged loss over the run and the PSNR are the stable quantities.
-* PSNR: |dPSNR| <= 0.1 dB vs the oracle after K steps, for fp32 and for the `fast` preset.
+* PSNR: |dPSNR| <= 0.1 dB vs the oracle after K steps, for fp32 and for the `fast` preset, on the mean of
+  REPEATS runs (one run's PSNR scatters by about +-0.07 dB, see _repeated).
 """
 from __future__ import annotations
 
@@ -91,20 +92,40 @@ def _report(tag, f, cfg, losses, psnr):
     return ref, rel, oracle
 
 
+REPEATS = 3
+
+
+def _repeated(dev, precision):
+    """REPEATS independent runs of the same K steps: the held-out PSNR of one run scatters by about +-0.07 dB around
+    its mean (float-atomic hash-gradient sums are not reproducible and AdamW's eps 1e-15 turns last-bit differences
+    of near-zero gradients into full-size updates; measured on MI355X, fp32 and fast alike), so the parity criterion
+    is on the mean over the runs."""
+    runs = [run_parity(dev, precision) for _ in range(REPEATS)]
+    f, cfg = runs[0][0], runs[0][1]
+    for k, (_, _, losses, psnr) in enumerate(runs):
+        ref, rel, oracle = _report(f"{precision}[{k}]", f, cfg, losses, psnr)
+    mean = {m: float(np.mean([r[3][m] for r in runs])) for m in cfg["modalities"]}
+    spread = {m: float(np.ptp([r[3][m] for r in runs])) for m in cfg["modalities"]}
+    print(f"{precision}: mean PSNR {mean} (spread {spread}) vs oracle {oracle}; "
+          f"dPSNR {({m: mean[m] - oracle[m] for m in mean})}")
+    return f, cfg, runs, ref, oracle, mean
+
+
 @pytest.mark.gpu
 def test_train_parity_fp32(dev):
-    f, cfg, losses, psnr = run_parity(dev, "fp32")
-    ref, rel, oracle = _report("fp32", f, cfg, losses, psnr)
-    assert rel[:TRAJ_STEPS].max() < 1e-3
-    assert abs(losses.mean() - ref.mean()) / ref.mean() < 2e-2
+    f, cfg, runs, ref, oracle, mean = _repeated(dev, "fp32")
+    for _, _, losses, _ in runs:
+        rel = np.abs(losses - ref) / np.abs(ref)
+        assert rel[:TRAJ_STEPS].max() < 1e-3
+        assert abs(losses.mean() - ref.mean()) / ref.mean() < 2e-2
     for m in cfg["modalities"]:
-        assert abs(psnr[m] - oracle[m]) <= 0.1
+        assert abs(mean[m] - oracle[m]) <= 0.1
 
 
 @pytest.mark.gpu
 def test_train_parity_fast_preset(dev):
-    f, cfg, losses, psnr = run_parity(dev, "fast")
-    ref, rel, oracle = _report("fast", f, cfg, losses, psnr)
-    assert abs(losses.mean() - ref.mean()) / ref.mean() < 2e-2
+    f, cfg, runs, ref, oracle, mean = _repeated(dev, "fast")
+    for _, _, losses, _ in runs:
+        assert abs(losses.mean() - ref.mean()) / ref.mean() < 2e-2
     for m in cfg["modalities"]:
-        assert abs(psnr[m] - oracle[m]) <= 0.1
+        assert abs(mean[m] - oracle[m]) <= 0.1
