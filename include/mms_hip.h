@@ -226,6 +226,24 @@ int mms_adamw_scalars(double lr, double wd, double beta1, double beta2, double e
 int mms_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* sumsq, float max_norm,
                   const float* hyper, void* stream);
 
+/* ---- GPU-resident uniform pixel sampler (UniformPixelSampler.sample, cameras/pixel_samplers.py:71-89, over the
+ * frames CacheDataloader caches, data/dataloaders.py:107-167): n draws of (frame, x, y) from Philox4x32-10
+ * (key seed, counter *counter + i, stream_id; *counter += n on the device afterwards, so graph replays advance it).
+ * coords [n, 3] int32 = [frame_ids[frame] (or frame), y, x]; sel [n] int64 = frame (optional); values [n, C]
+ * = images[frame, y, x, :] of images [n_frames, H, W, C] f32 (optional). */
+int mms_pixel_sample(uint64_t seed, uint32_t stream_id, uint64_t* counter, int64_t n, int n_frames, int H, int W,
+                     const int32_t* frame_ids, const float* images, int C, int32_t* coords, int64_t* sel,
+                     float* values, void* stream);
+
+/* ---- iso-surface of a dense SDF grid (mesh export: MeshExtractor.extract, evaluator_components/mesh_extractors.py:63;
+ * utils/marching_cubes.py:35).  values [nx * ny * nz] x-major; cells split into 6 tetrahedra (marching tetrahedra).
+ * count: counts[cell] = triangles of the cell ((nx-1)(ny-1)(nz-1) cells); emit: with offsets = exclusive scan of
+ * counts (int64), verts [T * 3, 3] f32 (outward-oriented triangles) and keys [T * 3] int64 (grid-edge id of each
+ * vertex, for welding).  origin / spacing: HOST arrays of 3 floats (point (i,j,k) = origin + spacing * (i,j,k)). */
+int mms_iso_count(const float* vals, int nx, int ny, int nz, float level, int32_t* counts, void* stream);
+int mms_iso_emit(const float* vals, int nx, int ny, int nz, float level, const float* origin, const float* spacing,
+                 const int64_t* offsets, float* verts, int64_t* keys, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

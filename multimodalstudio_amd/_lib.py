@@ -27,7 +27,8 @@ def _ctype(arg: str):
     if "*" in a:
         return ctypes.c_void_p
     t = a.rsplit(" ", 1)[0].strip()
-    return {"int64_t": ctypes.c_int64, "int": ctypes.c_int, "float": ctypes.c_float, "double": ctypes.c_double}[t]
+    return {"int64_t": ctypes.c_int64, "int": ctypes.c_int, "float": ctypes.c_float, "double": ctypes.c_double,
+            "uint64_t": ctypes.c_uint64, "uint32_t": ctypes.c_uint32}[t]
 
 
 def parse_header(path: Path = HEADER):

@@ -61,8 +61,12 @@ class GraphTrainer:
         n = trainer.cfg.num_rays_per_modality
         self.n = n
         mods = trainer.modalities
-        self.coords = {m: torch.zeros(n, 3, dtype=torch.int32, device=dev) for m in mods}
-        self.sel = {m: torch.zeros(n, dtype=torch.int64, device=dev) for m in mods}
+        if trainer.gpu_sampler is not None:
+            # device-drawn pixels: the sampler's persistent buffers are the graphs' static inputs
+            self.coords, self.sel = trainer.gpu_sampler.coords, trainer.gpu_sampler.sel
+        else:
+            self.coords = {m: torch.zeros(n, 3, dtype=torch.int32, device=dev) for m in mods}
+            self.sel = {m: torch.zeros(n, dtype=torch.int64, device=dev) for m in mods}
         self.h_coords = {m: torch.zeros(n, 3, dtype=torch.int32).pin_memory() for m in mods}
         self.h_sel = {m: torch.zeros(n, dtype=torch.int64).pin_memory() for m in mods}
         self.count_dev = torch.zeros(len(mods), dtype=torch.int64, device=dev)
@@ -90,6 +94,9 @@ class GraphTrainer:
     def _stage_inputs(self):
         """Host pixel sampling (reference RNG order) into pinned buffers, then async upload to the static ones."""
         t = self.t
+        if t.gpu_sampler is not None:
+            coords, _, _ = t.gpu_sampler.sample()
+            return coords
         coords, sel = t.sampler.sample(t.frames)
         for m in t.modalities:
             self.h_coords[m].copy_(coords[m])

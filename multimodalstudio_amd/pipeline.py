@@ -285,6 +285,8 @@ class TrainConfig:
     pose_mode: str = "SO3xR3"
     seed: int = 654824
     skip_views: Optional[Dict[str, List[int]]] = None   # skip_image_indices_per_modality (datamanager config)
+    data_dir: Optional[str] = None      # an on-disk MMS-DATA scene (data.MMSDataset) instead of the analytic one
+    gpu_sampler: bool = False           # draw pixels on the device (data.GPUPixelSampler) instead of the host
 
 
 class Trainer:
@@ -299,20 +301,40 @@ class Trainer:
         channels = {m: mscene.CHANNELS[m] for m in mods}
         torch.manual_seed(654824)
         self.model = BaseModel(ModelSpec(channels, log2T=cfg.log2T, bg_kind=bg_kind)).to(device)
-        cams = mscene.make_cameras(mods, cfg.n_views, cfg.width, cfg.height, seed=0, train=True)
-        for m, skip in (cfg.skip_views or {}).items():
-            if m in cams:
-                cams[m] = mscene.select_views(cams[m], [v for v in cams[m].view_ids if v not in set(skip)])
+        self.dataset = None
+        if cfg.data_dir is not None:
+            # the train split of an on-disk scene: every frame but the eval views and the skipped ones
+            from .data import MMSDataset
+            excl = {m: list(mscene.EVAL_VIEWS) + list((cfg.skip_views or {}).get(m, [])) for m in mods}
+            self.dataset = MMSDataset(cfg.data_dir, mods, indexes_to_exclude=excl)
+            if self.dataset.raw != self.raw:
+                raise ValueError(f"method {cfg.method} needs {'raw' if self.raw else 'demosaicked'} frames")
+            cams = dict(self.dataset.cameras)
+        else:
+            cams = mscene.make_cameras(mods, cfg.n_views, cfg.width, cfg.height, seed=0, train=True)
+            for m, skip in (cfg.skip_views or {}).items():
+                if m in cams:
+                    cams[m] = mscene.select_views(cams[m], [v for v in cams[m].view_ids if v not in set(skip)])
         self.cams = {m: DeviceCameras(cams[m], device) for m in mods}
         self.pose = CameraOptimizer(mods, {m: self.cams[m].num for m in mods}, mode=cfg.pose_mode).to(device)
         self.raygen = RayGenerator(self.cams, self.pose, 0.0)
         self.sampler = UniformPixelSampler(cfg.num_rays_per_modality, cfg.seed + rank)
         # frames cached in HBM (the reference caches all training frames in RAM, dataloaders.py:135-162)
-        self.images = {m: mscene.render_frames(cams[m], channels[m], device, m if self.raw else None) for m in mods}
+        if self.dataset is not None:
+            self.images = {m: self.dataset.images[m].to(device) for m in mods}
+        else:
+            self.images = {m: mscene.render_frames(cams[m], channels[m], device, m if self.raw else None) for m in mods}
         self.host_cams = cams
-        self.frames = {m: {"shape": (cams[m].c2w.shape[0], cfg.height, cfg.width),
+        self.frames = {m: {"shape": tuple(self.images[m].shape[:3]),
                            "indexes": torch.arange(cams[m].c2w.shape[0], dtype=torch.int32)} for m in mods}
-        self.masks = {m: mscene.mosaick_mask(m, cfg.width, cfg.height).to(device) for m in mods} if self.raw else {}
+        if self.dataset is not None:
+            self.masks = {m: k.to(device) for m, k in self.dataset.mosaick_masks.items()} if self.raw else {}
+        else:
+            self.masks = {m: mscene.mosaick_mask(m, cfg.width, cfg.height).to(device) for m in mods} if self.raw else {}
+        self.gpu_sampler = None
+        if cfg.gpu_sampler:
+            from .data import GPUPixelSampler
+            self.gpu_sampler = GPUPixelSampler(self.images, cfg.num_rays_per_modality, cfg.seed, rank)
         self.fields = FlatGroup(list(self.model.parameters()), lr=1e-3, weight_decay=0.01, eps=1e-15)
         pose_params = list(self.pose.parameters())
         self.poses = FlatGroup(pose_params, lr=1e-4, weight_decay=0.01, eps=1e-15) if pose_params else None
@@ -351,7 +373,9 @@ class Trainer:
         """Forward, losses, backward and (data parallel) the averaged gradient exchange: the train step up to the
         optimizer (fabric.backward, raw_pipeline.py:67-77)."""
         self.model.set_step(self.step, self.cfg.max_iters)
-        if coords is None:
+        if coords is None and self.gpu_sampler is not None:
+            coords, _, targets = self.gpu_sampler.sample()
+        elif coords is None:
             coords, sel = self.sampler.sample(self.frames)
             targets = self.targets_for(coords, sel)
         dev = self.device

@@ -57,9 +57,10 @@ def look_at(cam_pos: np.ndarray) -> np.ndarray:
 
 
 def make_cameras(modalities: List[str], n_views: int = 50, width: int = 640, height: int = 512,
-                 seed: int = 0, train: bool = True) -> Dict[str, ModalityCameras]:
+                 seed: int = 0, train: Optional[bool] = True) -> Dict[str, ModalityCameras]:
+    """Cameras of the train split (train=True), the eval split (EVAL_VIEWS, train=False) or every view (None)."""
     rng = np.random.default_rng(seed)
-    views = [v for v in range(n_views) if (v not in EVAL_VIEWS) == train]
+    views = [v for v in range(n_views) if train is None or (v not in EVAL_VIEWS) == train]
     golden = np.pi * (3.0 - np.sqrt(5.0))
     out = {}
     for mi, mod in enumerate(modalities):

@@ -1,0 +1,69 @@
+"""On-disk MMS-DATA format (data.py) on the host: the writer's scene reads back as the analytic frames, cameras,
+splits and mosaick masks (datasets.py:229-254, 444-529 semantics), and the frame I/O keeps cv2's channel order."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from multimodalstudio_amd import data as md
+from multimodalstudio_amd import scene as ms
+
+
+@pytest.fixture(scope="module")
+def scenes(tmp_path_factory):
+    root = tmp_path_factory.mktemp("mmsdata")
+    mods = ["rgb", "infrared", "polarization", "multispectral"]
+    raw = md.write_synthetic_scene(str(root / "raw"), mods, n_views=12, width=40, height=30, raw=True)
+    dem = md.write_synthetic_scene(str(root / "dem"), mods, n_views=12, width=40, height=30, raw=False)
+    return mods, raw, dem
+
+
+def test_metadata_schema(scenes):
+    mods, raw, _ = scenes
+    meta = json.load(open(os.path.join(raw, "meta_data.json")))
+    assert meta["raw"] is True and meta["undistorted"] is False and meta["pixel_offset"] == 0.0
+    assert meta["scene_box"]["collider_type"] == "sphere"
+    for m in mods:
+        e = meta["modalities"][m]
+        assert len(e["distortion_params"]) == 6 and e["mosaick_pattern"] == ms.MOSAICK[m]
+        assert [f["frame_id"] for f in e["frames"]] == list(range(12))
+        assert np.asarray(e["frames"][0]["camtoworld"]).shape == (3, 4)
+
+
+@pytest.mark.parametrize("raw", [True, False])
+def test_dataset_reads_back_the_scene(scenes, raw):
+    mods, raw_dir, dem_dir = scenes
+    path = raw_dir if raw else dem_dir
+    excl = {m: list(ms.EVAL_VIEWS) for m in mods}
+    ds = md.MMSDataset(path, mods, indexes_to_exclude=excl)
+    ref_cams = ms.make_cameras(mods, 12, 40, 30, seed=0, train=True)
+    assert ds.raw == raw
+    for m in mods:
+        c = ds.cameras[m]
+        assert c.view_ids == [v for v in range(12) if v not in ms.EVAL_VIEWS]
+        assert torch.allclose(c.c2w, ref_cams[m].c2w)
+        assert torch.allclose(c.distortion, ref_cams[m].distortion)
+        ref = ms.render_frames(ref_cams[m], ms.CHANNELS[m], torch.device("cpu"), m if raw else None)
+        got = ds.images[m]
+        assert got.shape == ref.shape, (m, got.shape, ref.shape)
+        nc = got.shape[-1]
+        tol = 0.5 / 65535 + 1e-7 if nc == 1 else (0.5 / 255 + 1e-7 if nc == 3 else 0.0)
+        assert float((got - ref).abs().max()) <= tol, m
+        if raw:
+            assert torch.equal(ds.mosaick_masks[m], ms.mosaick_mask(m, 40, 30))
+    assert ds.get_channels_per_modality() == {m: ms.CHANNELS[m] for m in mods}
+    ev = md.MMSDataset(path, ["rgb"], indexes_to_choose={"rgb": [9]})
+    assert ev.cameras["rgb"].view_ids == [9] and len(ev) == 1
+
+
+def test_frame_io_channel_order(tmp_path):
+    bgr = (np.arange(5 * 4 * 3) % 256).astype(np.uint8).reshape(5, 4, 3)
+    p = str(tmp_path / "f.png")
+    md.write_frame(p, bgr)
+    assert np.array_equal(md.read_frame(p), bgr)        # cv2 semantics: what is written BGR reads back BGR
+    g16 = (np.arange(20) * 3000).astype(np.uint16).reshape(5, 4, 1)
+    md.write_frame(str(tmp_path / "g.png"), g16)
+    assert np.array_equal(md.read_frame(str(tmp_path / "g.png")), g16)
+    assert md.normalize_frame(g16).max() == pytest.approx(57000 / 65535)
