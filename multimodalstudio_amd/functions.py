@@ -30,13 +30,14 @@ from .hip_ops import NN, NT, TN, _splits_for, act_bwd, gemm, weight_norm_bwd, we
 ACT = {None: 0, "None": 0, "ReLU": 1, "Softplus": 2, "Sigmoid": 3}
 
 # GEMM operand precision per MLP family: 0 exact fp32 MFMA (parity mode), 1 bf16, 2 split bf16x3.
-PRECISION = {"sdf": 0, "radiance": 0, "heads": 0, "background": 0}
+PRECISION = {"sdf": 0, "radiance": 0, "heads": 0, "background": 0, "mlp": 0}
 PRESETS = {
-    "fp32": {"sdf": 0, "radiance": 0, "heads": 0, "background": 0},
+    "fp32": {"sdf": 0, "radiance": 0, "heads": 0, "background": 0, "mlp": 0},
     # throughput mode: the SDF MLP keeps ~fp32 operand precision (its 4-tap finite differences divide
-    # sdf differences by 4 delta ~ 4.5e-3), everything else runs bf16 MFMA with fp32 accumulation
-    "fast": {"sdf": 2, "radiance": 1, "heads": 1, "background": 1},
-    "bf16x3": {"sdf": 2, "radiance": 2, "heads": 2, "background": 2},
+    # sdf differences by 4 delta ~ 4.5e-3), everything else runs bf16 MFMA with fp32 accumulation; the analytic-
+    # gradient MLP fields (mlp methods, differentiated twice) stay on the exact fp32 MFMA
+    "fast": {"sdf": 2, "radiance": 1, "heads": 1, "background": 1, "mlp": 0},
+    "bf16x3": {"sdf": 2, "radiance": 2, "heads": 2, "background": 2, "mlp": 2},
 }
 
 
@@ -681,6 +682,36 @@ class RadianceFunction(torch.autograd.Function):
         ctx.X = None
         ctx.table = None
         return (dpos, ddirs, None, dgeo, None, None, None, None, *pgrads)
+
+
+class RadInputFunction(torch.autograd.Function):
+    """The radiance MLP input [x, SH4(d), geo, n.v] (radiance_model.py:114-132) without grid columns, for the mlp
+    methods' RadianceField(MLP): mms_rad_input_fwd / _bwd (normals detached, base_model.py:129)."""
+
+    @staticmethod
+    def forward(ctx, pos, dirs, normals, geo, S: int):
+        M, G = geo.shape
+        dev = pos.device
+        X = _alloc(M, 3 + 25 + G + 1, dev)
+        pos, dirs, normals, geo = pos.contiguous(), dirs.contiguous(), normals.contiguous(), geo.contiguous()
+        _lib.call("mms_rad_input_fwd", pos.data_ptr(), 3, dirs.data_ptr(), normals.data_ptr(), geo.data_ptr(),
+                  geo.stride(0), M, S, G, X.data_ptr(), X.stride(0), _s())
+        ctx.save_for_backward(dirs, normals)
+        ctx.S, ctx.G, ctx.M = S, G, M
+        return X
+
+    @staticmethod
+    def backward(ctx, dX):
+        dirs, normals = ctx.saved_tensors
+        M, S, G = ctx.M, ctx.S, ctx.G
+        dev = dX.device
+        dX = dX if dX.stride(1) == 1 else dX.contiguous()
+        dpos = torch.zeros(M, 3, device=dev) if ctx.needs_input_grad[0] else None
+        dgeo = torch.empty(M, G, device=dev) if ctx.needs_input_grad[3] else None
+        ddirs = torch.zeros(M // S, 3, device=dev) if ctx.needs_input_grad[1] else None
+        _lib.call("mms_rad_input_bwd", dX.data_ptr(), dX.stride(0), None, 3, dirs.data_ptr(), normals.data_ptr(), M // S,
+                  S, G, _p(dpos), 3, _p(dgeo), G, _p(ddirs), _s())
+        return dpos, ddirs, None, dgeo, None
 
 
 # ------------------------------------------------------------------------------------------------

@@ -66,27 +66,30 @@ class MLP(nn.Module):
 
     def __init__(self, config: MLPConfig, input_dim: int, output_dim: Optional[int] = None):
         super().__init__()
-        if config.skip_connections:
-            raise NotImplementedError("skip connections (mlp_raw surface field) are not on the HIP path yet")
         if not config.weight_norm:
             raise NotImplementedError("the HIP MLP implements the weight-normed layers used by every method config")
         self.config = config
         self.input_dim = input_dim
         self.output_dim = output_dim if output_dim is not None else config.hidden_dim
-        dims = [input_dim] + [config.hidden_dim] * (config.num_layers - 1) + [self.output_dim]
+        self.skips = tuple(config.skip_connections or ())
+        # mlp.py:115-137: a skip layer i takes cat[h, input] / sqrt(2); the layer before it is narrowed so the
+        # concatenation is hidden_dim + input_dim wide
+        dims = [input_dim] + [config.hidden_dim + (input_dim if i + 1 in self.skips else 0)
+                              for i in range(config.num_layers - 1)] + [self.output_dim]
+        shapes = [(dims[i], dims[i + 1] - (dims[0] if i + 1 in self.skips else 0)) for i in range(len(dims) - 1)]
         weights, biases = [], []
-        for i in range(len(dims) - 1):
-            lin = nn.Linear(dims[i], dims[i + 1])
+        for k, n in shapes:
+            lin = nn.Linear(k, n)
             weights.append(lin.weight.data)
             biases.append(lin.bias.data)
         if config.geometric_init:
-            self._geometric_init(weights, biases, config.geometric_init_bias, input_dim > 3)
+            self._geometric_init(weights, biases, config.geometric_init_bias, input_dim > 3, self.skips)
         else:
             for w, b in zip(weights, biases):
                 nn.init.kaiming_uniform_(w)
                 nn.init.zeros_(b)
-        self.layers = nn.ModuleList([WeightNormLinear(dims[i], dims[i + 1], weights[i], biases[i])
-                                     for i in range(len(dims) - 1)])
+        self.layers = nn.ModuleList([WeightNormLinear(k, n, weights[i], biases[i])
+                                     for i, (k, n) in enumerate(shapes)])
         hidden = fx.ACT[config.activation]
         beta = float(config.activation_params.get("beta", 1.0))
         thr = float(config.activation_params.get("threshold", 20.0))
@@ -94,7 +97,7 @@ class MLP(nn.Module):
         self.acts = tuple([(hidden, beta, thr)] * (len(dims) - 2) + [(out, 1.0, 20.0)])
 
     @staticmethod
-    def _geometric_init(weights, biases, bias, additional_input):
+    def _geometric_init(weights, biases, bias, additional_input, skips=()):
         """MLP.geometric_init (mlp.py:173-198)."""
         L = len(weights)
         for l in range(L):
@@ -106,6 +109,10 @@ class MLP(nn.Module):
                 nn.init.constant_(biases[l], 0.0)
                 nn.init.constant_(weights[l][:, 3:], 0.0)
                 nn.init.normal_(weights[l][:, :3], 0.0, np.sqrt(2) / np.sqrt(out_dim))
+            elif additional_input and l in skips:
+                nn.init.constant_(biases[l], 0.0)
+                nn.init.normal_(weights[l], 0.0, np.sqrt(2) / np.sqrt(out_dim))
+                nn.init.constant_(weights[l][:, -(weights[0].shape[1] - 3):], 0.0)
             else:
                 nn.init.constant_(biases[l], 0.0)
                 nn.init.normal_(weights[l], 0.0, np.sqrt(2) / np.sqrt(out_dim))
@@ -117,7 +124,39 @@ class MLP(nn.Module):
         return out
 
     def forward(self, x):
+        if self.skips:
+            return self.forward_diff(x)
         return fx.MLPFunction.apply(x, self.acts, *self.params())
+
+    def forward_diff(self, x: torch.Tensor) -> torch.Tensor:
+        """MLP.forward (mlp.py:152-171) with every product on the twice-differentiable HIP GEMM (autodiff.MatMul) and
+        the reference's torch element-wise operators, for fields whose input gradient is differentiated again."""
+        from . import autodiff
+        c = self.config
+        h = x
+        L = len(self.layers)
+        for i, layer in enumerate(self.layers):
+            if i in self.skips:
+                h = torch.cat([h, x], -1) / np.sqrt(2)
+            w = layer.parametrizations["weight"]
+            W = w.original0 * (w.original1 / torch.linalg.vector_norm(w.original1, dim=1, keepdim=True))
+            h = autodiff.linear(h, W, layer.bias)
+            if i < L - 1:
+                h = _act_torch(c.activation, c.activation_params, h)
+        if c.out_activation not in (None, "None"):
+            h = _act_torch(c.out_activation, {}, h)
+        return h
+
+
+def _act_torch(name: str, params: dict, x: torch.Tensor) -> torch.Tensor:
+    if name == "Softplus":
+        return torch.nn.functional.softplus(x, beta=float(params.get("beta", 1.0)),
+                                            threshold=float(params.get("threshold", 20.0)))
+    if name == "ReLU":
+        return torch.relu(x)
+    if name == "Sigmoid":
+        return torch.sigmoid(x)
+    raise ValueError(name)
 
 
 class HashEncoding(nn.Module):
@@ -236,16 +275,48 @@ class SurfaceModel(nn.Module):
         f = self.surface_field.field
         return f.feature_grid, f.mlp_head.params()
 
+    @property
+    def analytic(self) -> bool:
+        """mlp methods: a plain MLP field with autograd gradients (use_numerical_gradients False)."""
+        return isinstance(self.surface_field.field, MLP)
+
     def forward(self, pos: torch.Tensor):
+        if self.analytic:
+            return self._forward_analytic(pos)
         grid, params = self._grid_and_params()
         delta = self.numerical_gradients_delta / np.sqrt(3)
         return fx.SurfaceFunction.apply(pos, grid.encoding.hash_table, grid.cfg, grid.active_levels, float(delta),
                                         *params)
 
+    def _forward_analytic(self, pos: torch.Tensor):
+        """SurfaceModel.forward + gradient() of the mlp methods (surface_model.py:66-91, 192-198): sdf, geo from
+        SDFField(PE(x)) and the gradient d sdf / dx by autograd with create_graph (so the eikonal loss trains through
+        it: the MLP's backward is differentiated again, on the HIP GEMM, autodiff.MatMul); no hessian
+        (compute_hessian False)."""
+        x = pos if pos.requires_grad else pos.detach().requires_grad_(True)
+        with torch.enable_grad():
+            out = self.surface_field.field.forward_diff(nerf_encoding(x, 6))
+            sdf, geo = out[:, :1], out[:, 1:]
+            grads = torch.autograd.grad(sdf, x, torch.ones_like(sdf), create_graph=torch.is_grad_enabled() or
+                                        self.training, retain_graph=True)[0]
+        normals = torch.nn.functional.normalize(grads, p=2, dim=-1)
+        return sdf, geo, grads, None, normals
+
     def get_sdf(self, pos: torch.Tensor) -> torch.Tensor:
+        if self.analytic:
+            with torch.no_grad():
+                return self.surface_field.field.forward_diff(nerf_encoding(pos, 6))[:, 0].contiguous()
         grid, params = self._grid_and_params()
         with torch.no_grad():
             return fx.sdf_only(pos, grid.encoding.hash_table, grid.cfg, grid.active_levels, params)
+
+
+def nerf_encoding(x: torch.Tensor, F: int) -> torch.Tensor:
+    """NeRFEncoding.forward (encodings.py:161-182), frequencies 2^0 .. 2^(F-1), input included, in torch operators
+    (twice differentiable: the analytic-gradient fields differentiate through it again)."""
+    freqs = 2.0 ** torch.linspace(0.0, F - 1, F, device=x.device)
+    scaled = (x[..., None] * freqs).reshape(*x.shape[:-1], -1)
+    return torch.cat([x, torch.sin(torch.cat([scaled, scaled + torch.pi / 2.0], dim=-1))], dim=-1)
 
 
 class RadianceField(nn.Module):
@@ -264,6 +335,9 @@ class RadianceModel(nn.Module):
 
     def features(self, pos, dirs, normals, geo, S):
         bf = self.radiance_field.base_field
+        if isinstance(bf, MLP):
+            # mlp methods: RadianceField(MLP) on [x, SH4(d), geo, n.v] (radiance_model.py:114-141)
+            return bf.forward_diff(fx.RadInputFunction.apply(pos, dirs, normals, geo, S))
         g = bf.feature_grid
         return fx.RadianceFunction.apply(pos, dirs, normals, geo, g.encoding.hash_table, g.cfg, g.active_levels, S,
                                          *bf.mlp_head.params())
@@ -321,6 +395,9 @@ class ModelSpec:
     upsample_steps: int = 4
     base_variance: float = 64.0
     bg_samples: int = 16
+    # field kind: "grid" (hash grid + 3-layer MLPs, 4-tap numerical gradients: methods grid / grid_raw) or "mlp"
+    # (8-layer skip MLPs on PE(x), autograd SDF gradients, no hessian: methods mlp / mlp_raw, method_configs.py:303-353)
+    fields: str = "grid"
     # background field: "nerf" (PE -> 39-256x4 MLP, head 283-256x3-128, 1-layer heads; method 'grid' / 'grid_raw') or
     # "grid" (config 5 'grid_raw_grid_bg_unbalanced', method_configs.py:428-444: hash grid r = 2 + 71-128-128-256 MLP,
     # head 283-256x3-256, the radiance model's 3-layer heads)
@@ -412,18 +489,27 @@ class BaseModel(nn.Module):
             enc = HashEncoding(spec.num_levels, 2, spec.min_res, spec.max_res, spec.log2T)
             return FeatureGrid(enc, radius)
 
-        sdf_mlp = MLP(MLPConfig(num_layers=3, hidden_dim=256, activation="Softplus", activation_params={"beta": 100},
-                                out_activation="None", geometric_init=True, geometric_init_bias=0.4),
-                      3 + 36 + 32, 257)
-        self.surface_model = SurfaceModel(SDFField(FeatureGridAndMLP(grid(), sdf_mlp)))
-        rad_mlp = MLP(MLPConfig(num_layers=3, hidden_dim=256, out_activation="ReLU"), 3 + 25 + 257 + 32, 256)
+        if spec.fields == "mlp":
+            sdf_mlp = MLP(MLPConfig(num_layers=8, hidden_dim=256, activation="Softplus",
+                                    activation_params={"beta": 100}, out_activation="None", skip_connections=(4,),
+                                    geometric_init=True, geometric_init_bias=0.4), 3 + 36, 257)
+            self.surface_model = SurfaceModel(SDFField(sdf_mlp))
+            rad_field = MLP(MLPConfig(num_layers=8, hidden_dim=256, out_activation="ReLU", skip_connections=(4,)),
+                            3 + 25 + 257, 256)
+        else:
+            sdf_mlp = MLP(MLPConfig(num_layers=3, hidden_dim=256, activation="Softplus",
+                                    activation_params={"beta": 100}, out_activation="None", geometric_init=True,
+                                    geometric_init_bias=0.4), 3 + 36 + 32, 257)
+            self.surface_model = SurfaceModel(SDFField(FeatureGridAndMLP(grid(), sdf_mlp)))
+            rad_mlp = MLP(MLPConfig(num_layers=3, hidden_dim=256, out_activation="ReLU"), 3 + 25 + 257 + 32, 256)
+            rad_field = FeatureGridAndMLP(grid(), rad_mlp)   # MLP before grid: the init RNG order
         heads = {}
         for m, c in mods.items():
             if m == "polarization":
                 heads[m] = ModalityHead("polarization", 256, c, 3, 256, "None")
             else:
                 heads[m] = ModalityHead("plain", 256, c, 3, 64, "Sigmoid")
-        self.radiance_model = RadianceModel(RadianceField(FeatureGridAndMLP(grid(), rad_mlp)), heads)
+        self.radiance_model = RadianceModel(RadianceField(rad_field), heads)
         # construction order = parameter-initialisation RNG order (base, head, density head, modality heads)
         bg_heads = {}
         if spec.bg_kind == "grid":
@@ -452,8 +538,9 @@ class BaseModel(nn.Module):
     def set_step(self, step: int, max_iters: int = 100000):
         spl = min(int(max_iters * 1.0), int(max_iters / self.spec.num_levels))
         level = min(max(int(step / spl) + 1, 1), self.spec.num_levels)
-        self.surface_model.surface_field.field.feature_grid.update_mask(level)
-        self.radiance_model.radiance_field.base_field.feature_grid.update_mask(level)
+        if self.spec.fields == "grid":
+            self.surface_model.surface_field.field.feature_grid.update_mask(level)
+            self.radiance_model.radiance_field.base_field.feature_grid.update_mask(level)
         g = float(np.exp((np.log(self.spec.max_res) - np.log(self.spec.min_res)) / (self.spec.num_levels - 1)))
         delta = max(1.0 / self.spec.max_res, 1.0 / (self.spec.min_res * g ** int(step / spl)))
         self.surface_model.set_numerical_gradients_delta(delta * (self.spec.radius * 2.0))
@@ -552,7 +639,7 @@ class BaseModel(nn.Module):
             out["accumulation"] = acc[:N]
             out["count"] = count
             out["gradients"] = grads.view(R, S, 3)
-            out["hessians"] = hess.view(R, S, 3)
+            out["hessians"] = hess.view(R, S, 3) if hess is not None else None
             out["inv_s"] = 1.0 / self.surface_model.volume_rendering.density_fn.variance_network.get_inv_variance()
             out["weights"] = w
             out["bins"] = bins

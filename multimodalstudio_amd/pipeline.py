@@ -237,7 +237,10 @@ def compute_loss(outputs, targets: Dict[str, torch.Tensor], modalities: List[str
         losses[mod] = l
         total = l if total is None else total + l
     grads = [outputs[m]["gradients"].reshape(-1, 3) for m in modalities]
-    hess = [outputs[m]["hessians"].reshape(-1, 3) for m in modalities]
+    # mlp methods: no hessian and no curvature loss (method_configs.py:350-352: geometry losses = eikonal only)
+    analytic = outputs[modalities[0]]["hessians"] is None
+    hess = [torch.zeros_like(g) if analytic else outputs[m]["hessians"].reshape(-1, 3)
+            for m, g in zip(modalities, grads)]
     counts = [outputs[m].get("count") for m in modalities]
     if any(c is not None for c in counts):
         # fixed-capacity batches (graph-captured steps): padding rows carry no geometric loss
@@ -245,10 +248,12 @@ def compute_loss(outputs, targets: Dict[str, torch.Tensor], modalities: List[str
         eik, curv = fx.GeoLossMaskedFunction.apply(S, counts, *grads, *hess)
     else:
         eik, curv = fx.GeoLossFunction.apply(*grads, *hess)
-    cf = curvature_factor(step, max_iters)
     losses["eikonal_loss"] = eik
-    losses["curvature_loss"] = curv
-    total = total + 0.1 * eik + (5e-4 * cf) * curv
+    total = total + 0.1 * eik
+    if not analytic:
+        cf = curvature_factor(step, max_iters)
+        losses["curvature_loss"] = curv
+        total = total + (5e-4 * cf) * curv
     return losses, total
 
 
@@ -265,10 +270,12 @@ def select_right_channel(rendered: torch.Tensor, band: torch.Tensor) -> torch.Te
 POL_10_VIEWS_SKIP = [0, 1, 2, 3, 5, 7, 8, 10, 11, 13, 15, 16, 17, 18, 20, 21, 23, 24, 26, 28, 30, 31, 32, 33, 35, 36,
                      37, 38, 40, 42, 43, 45, 46, 47, 48]
 METHODS = {
-    # method name: (raw mosaicked frames, background field kind)
-    "grid": (False, "nerf"),
-    "grid_raw": (True, "nerf"),
-    "grid_raw_grid_bg_unbalanced": (True, "grid"),
+    # method name: (raw mosaicked frames, background field kind, field kind)
+    "grid": (False, "nerf", "grid"),
+    "grid_raw": (True, "nerf", "grid"),
+    "grid_raw_grid_bg_unbalanced": (True, "grid", "grid"),
+    "mlp": (False, "nerf", "mlp"),
+    "mlp_raw": (True, "nerf", "mlp"),
 }
 
 
@@ -295,12 +302,12 @@ class Trainer:
     def __init__(self, cfg: TrainConfig, device, rank: int = 0, frames_on_device: bool = True):
         self.cfg = cfg
         self.device = device
-        self.raw, bg_kind = METHODS[cfg.method]
+        self.raw, bg_kind, fields = METHODS[cfg.method]
         mods = list(cfg.modalities)
         self.modalities = mods
         channels = {m: mscene.CHANNELS[m] for m in mods}
         torch.manual_seed(654824)
-        self.model = BaseModel(ModelSpec(channels, log2T=cfg.log2T, bg_kind=bg_kind)).to(device)
+        self.model = BaseModel(ModelSpec(channels, log2T=cfg.log2T, bg_kind=bg_kind, fields=fields)).to(device)
         self.dataset = None
         if cfg.data_dir is not None:
             # the train split of an on-disk scene: every frame but the eval views and the skipped ones

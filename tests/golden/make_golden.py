@@ -224,8 +224,9 @@ def set_callbacks(model, step, max_iters=100000):
     import numpy as _np
     spl = min(int(max_iters * 1.0), int(max_iters / 16))
     level = min(max(int(step / spl) + 1, 1), 16)
-    model.surface_model.surface_field.field.feature_grid.update_mask(level)
-    model.radiance_model.radiance_field.base_field.feature_grid.update_mask(level)
+    if hasattr(model.surface_model.surface_field.field, "feature_grid"):      # grid methods only
+        model.surface_model.surface_field.field.feature_grid.update_mask(level)
+        model.radiance_model.radiance_field.base_field.feature_grid.update_mask(level)
     gfac = _np.exp((_np.log(1024) - _np.log(16)) / 15)
     delta = max(1.0 / 1024, 1.0 / (16 * gfac ** int(step / spl)))
     model.surface_model.set_numerical_gradients_delta(delta * 2.0)
@@ -233,7 +234,7 @@ def set_callbacks(model, step, max_iters=100000):
     return level, delta * 2.0
 
 
-def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=False, grid_bg=False):
+def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=False, grid_bg=False, grids=True):
     from cameras.camera_optimizers import CameraOptimizerConfig
     from cameras.pixel_samplers import UniformPixelSamplerConfig
     from model_components.ray_generators import RayGenerator
@@ -246,6 +247,8 @@ def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=F
     if grid_bg:
         overrides["pipeline"]["model"]["background_model"] = {"background_field": {"base_field": {
             "feature_grid": {"encoding": {"log2_hashmap_size": log2T}}}}}
+    if not grids:
+        overrides = None
     cfg, model = refimport.build_model(method, f"/root/reference/confs/{yaml_name}", modalities, overrides)
     model.train()
     with torch.no_grad():
@@ -331,7 +334,8 @@ def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=F
         arrays[f"{m}:bins"] = seen["bins"][m]
         o = outputs[m]
         for k in ["normals", "depth", "accumulation", "gradients", "hessians", "inv_s"]:
-            arrays[f"{m}:out:{k}"] = o[k].detach()
+            if o.get(k) is not None:
+                arrays[f"{m}:out:{k}"] = o[k].detach()
         for mm in mods:
             if mm in o:
                 arrays[f"{m}:out:{mm}"] = o[mm].detach()
@@ -490,6 +494,9 @@ if __name__ == "__main__":
         np.savez_compressed(os.path.join(OUT, "e2e_grid_rgb_s30000.npz"), **b)
         gen_end_to_end("grid_raw", "grid_raw.yaml", ["rgb", "infrared", "mono", "polarization", "multispectral"],
                        95000, "grid_raw_5mod_s95000", raw=True)
+    if "e2e_mlp" in which or "e2e" in which:
+        # config 1: mlp_raw, analytic SDF gradients (double backward), skip-connection MLPs, RGB only
+        gen_end_to_end("mlp_raw", "mlp_raw.yaml", ["rgb"], 95000, "mlp_raw_rgb_s95000", raw=True, grids=False)
     if "e2e_gridbg" in which or "e2e" in which:
         # config 5: grid background (hash grid r = 2 + MLP), 3-layer background heads, rgb + polarization
         gen_end_to_end("grid_raw_grid_bg_unbalanced", "grid_raw_rgb_all_views_pol_10_views.yaml",

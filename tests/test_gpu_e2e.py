@@ -40,11 +40,14 @@ def run_hip_e2e(f, dev, cap=None):
     from multimodalstudio_amd import pipeline as pl
     from multimodalstudio_amd import scene as ms
     mods = [str(m) for m in f["mods"]]
-    log2T = int(np.log2(f["p:surface_model.surface_field.field.feature_grid.encoding.hash_table"].shape[0] // 16))
+    key = "p:surface_model.surface_field.field.feature_grid.encoding.hash_table"
+    fields = "grid" if key in f else "mlp"
+    log2T = int(np.log2(f[key].shape[0] // 16)) if key in f else 19
     raw = bool(f["raw"])
     bg_kind = "grid" if "p:background_model.background_field.base_field.feature_grid.encoding.hash_table" in f \
         else "nerf"
-    model = mm.BaseModel(mm.ModelSpec({m: ms.CHANNELS[m] for m in mods}, log2T=log2T, bg_kind=bg_kind)).to(dev)
+    model = mm.BaseModel(mm.ModelSpec({m: ms.CHANNELS[m] for m in mods}, log2T=log2T, bg_kind=bg_kind,
+                                      fields=fields)).to(dev)
     model.load_state_dict({k[2:]: torch.from_numpy(v) for k, v in f.items() if k.startswith("p:")}, strict=True)
     model.train()
     model.set_step(int(f["step"]))
@@ -81,7 +84,7 @@ def run_hip_e2e(f, dev, cap=None):
 
 
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_rgb_s30000", "e2e_grid_raw_5mod_s95000",
-                                  "e2e_grid_raw_gridbg_s95000"])
+                                  "e2e_grid_raw_gridbg_s95000", "e2e_mlp_raw_rgb_s95000"])
 def test_e2e_train_step(dev, name):
     f = load(name)
     mods, model, pose, outs, losses, total = run_hip_e2e(f, dev)
@@ -91,7 +94,8 @@ def test_e2e_train_step(dev, name):
         o = outs[m]
         report[f"{m}:{m}"] = rel_err(o[m].detach().cpu(), f[f"{m}:out:{m}"])
         for k in ["normals", "accumulation", "depth", "gradients", "hessians"]:
-            report[f"{m}:{k}"] = rel_err(o[k].detach().cpu(), f[f"{m}:out:{k}"])
+            if f"{m}:out:{k}" in f:
+                report[f"{m}:{k}"] = rel_err(o[k].detach().cpu(), f[f"{m}:out:{k}"])
         report[f"{m}:dpose"] = rel_err(pose.pose_adjustment[m].grad.cpu(), f[f"{m}:dpose"])
     worst_param = 0.0
     for k, p in model.named_parameters():
@@ -120,6 +124,6 @@ def test_e2e_train_step(dev, name):
         # hessian = (sum of 4 taps / 2 - 2 sdf) / delta^2 with delta^2 ~ 1.3e-6: an fp32 reordering of the
         # SDF GEMM sums (a few ulp of |sdf| ~ 0.5, i.e. ~1e-7) moves it by ~0.1 absolute; the reference's own
         # CPU-vs-GPU runs differ the same way.  Bound: 4 ulp-scale errors amplified by 1/delta^2.
-        assert report[f"{m}:hessians"] < 0.15
+        assert report.get(f"{m}:hessians", 0.0) < 0.15
         assert report[f"{m}:dpose"] < 5e-2
     assert worst_param < 5e-2
