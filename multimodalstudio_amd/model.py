@@ -494,21 +494,22 @@ class BaseModel(nn.Module):
                                     activation_params={"beta": 100}, out_activation="None", skip_connections=(4,),
                                     geometric_init=True, geometric_init_bias=0.4), 3 + 36, 257)
             self.surface_model = SurfaceModel(SDFField(sdf_mlp))
-            rad_field = MLP(MLPConfig(num_layers=8, hidden_dim=256, out_activation="ReLU", skip_connections=(4,)),
-                            3 + 25 + 257, 256)
+            rad_mlp = MLP(MLPConfig(num_layers=8, hidden_dim=256, out_activation="ReLU", skip_connections=(4,)),
+                          3 + 25 + 257, 256)
         else:
             sdf_mlp = MLP(MLPConfig(num_layers=3, hidden_dim=256, activation="Softplus",
                                     activation_params={"beta": 100}, out_activation="None", geometric_init=True,
                                     geometric_init_bias=0.4), 3 + 36 + 32, 257)
             self.surface_model = SurfaceModel(SDFField(FeatureGridAndMLP(grid(), sdf_mlp)))
             rad_mlp = MLP(MLPConfig(num_layers=3, hidden_dim=256, out_activation="ReLU"), 3 + 25 + 257 + 32, 256)
-            rad_field = FeatureGridAndMLP(grid(), rad_mlp)   # MLP before grid: the init RNG order
         heads = {}
         for m, c in mods.items():
             if m == "polarization":
                 heads[m] = ModalityHead("polarization", 256, c, 3, 256, "None")
             else:
                 heads[m] = ModalityHead("plain", 256, c, 3, 64, "Sigmoid")
+        # construction order = the parameter-initialisation RNG order: radiance MLP, heads, then the radiance grid
+        rad_field = rad_mlp if spec.fields == "mlp" else FeatureGridAndMLP(grid(), rad_mlp)
         self.radiance_model = RadianceModel(RadianceField(rad_field), heads)
         # construction order = parameter-initialisation RNG order (base, head, density head, modality heads)
         bg_heads = {}
