@@ -562,6 +562,13 @@ class BaseModel(nn.Module):
 
     # -- forward ----------------------------------------------------------------------------------------
     def forward(self, rays: Dict[str, Dict[str, torch.Tensor]], rng: Optional[RNG] = None, cap: Optional[int] = None):
+        fx.begin_forward()       # weight-norm / packed-weight cache scope (functions.normed_weight)
+        try:
+            return self._forward(rays, rng, cap)
+        finally:
+            fx.end_forward()
+
+    def _forward(self, rays, rng, cap):
         """rays[mod] = {"origins", "directions", "up_directions"} ([N,3] device); returns per-modality outputs.
 
         ``cap``: fixed-capacity foreground batch for graph capture (graphs.py).  Each modality's hit rays are

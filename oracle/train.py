@@ -17,7 +17,8 @@ from . import rays as orr
 
 class OracleTrainer:
     def __init__(self, state_dict: Dict[str, torch.Tensor], modalities: Dict[str, int], cams: dict, log2T: int,
-                 step: int, raw: bool = False, pose: Dict[str, torch.Tensor] = None):
+                 step: int, raw: bool = False, pose: Dict[str, torch.Tensor] = None,
+                 mosaick: Dict[str, torch.Tensor] = None):
         self.P = {k: v.detach().clone().float().cpu().requires_grad_(True) for k, v in state_dict.items()}
         self.spec = om.spec_grid(modalities, log2T=log2T, raw=raw)
         self.cams = cams
@@ -25,6 +26,7 @@ class OracleTrainer:
         self.pose = {m: (pose[m].detach().clone() if pose else torch.zeros(1, 6)).requires_grad_(True)
                      for m in self.mods}
         self.step = step
+        self.mosaick = mosaick or {}      # raw methods: per-modality band masks (select_right_channel)
         self.field_state: dict = {}
         self.pose_state: dict = {}
 
@@ -45,6 +47,10 @@ class OracleTrainer:
             hits = {m: int(orr.sphere_collider(rays[m].origins, rays[m].directions)[2].sum()) for m in self.mods}
         rng = self.rng(hits, {m: coords[m].shape[0] for m in self.mods})
         outs = om.model_forward(rays, self.P, self.spec, st, rng)
+        if self.spec.raw:
+            # RawPipeline.train_step: each pixel's own band (raw_pipeline.py:74-76, 112-122)
+            for m in self.mods:
+                outs[m][m] = om.select_channel(outs[m][m], self.mosaick[m], coords[m])
         losses, total = om.compute_loss(outs, targets, self.spec, st)
         for p in list(self.P.values()) + list(self.pose.values()):
             p.grad = None

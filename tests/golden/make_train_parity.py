@@ -9,7 +9,7 @@ and the uniform draws from a CPU generator in fixed-size blocks (independent of 
 fixture stores only the configuration, the oracle's per-step losses and its held-out PSNR before and
 after training.  tests/test_gpu_train_parity.py replays the same K steps through the HIP path.
 
-    python tests/golden/make_train_parity.py        (CPU, ~3 min on 8 threads; writes train_parity_rgb.npz)
+    python tests/golden/make_train_parity.py [rgb|raw5]   (CPU, ~3 / ~15 min on 8 threads; train_parity_<name>.npz)
 """
 from __future__ import annotations
 
@@ -23,9 +23,17 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
-CFG = dict(method="grid", modalities=("rgb",), rays=256, log2T=12, width=160, height=128, n_views=10,
-           start_step=95000, steps=300, eval_rays=4096, init_seed=654824, sampler_seed=654824, rng_seed=11,
-           eval_seed=5, bg_samples=16)
+CONFIGS = {
+    # BASELINE configs[1] shape: grid, RGB
+    "rgb": dict(method="grid", modalities=("rgb",), rays=256, log2T=12, width=160, height=128, n_views=10,
+                start_step=95000, steps=300, eval_rays=4096, init_seed=654824, sampler_seed=654824, rng_seed=11,
+                eval_seed=5, bg_samples=16),
+    # BASELINE configs[2] shape: grid_raw, five mosaicked modalities (each pixel supervises its own band)
+    "raw5": dict(method="grid_raw", modalities=("rgb", "infrared", "mono", "polarization", "multispectral"),
+                 rays=96, log2T=12, width=96, height=80, n_views=10, start_step=95000, steps=200, eval_rays=2048,
+                 init_seed=654824, sampler_seed=654824, rng_seed=11, eval_seed=5, bg_samples=16),
+}
+CFG = CONFIGS["rgb"]
 
 
 def param_checksum(sd):
@@ -59,7 +67,7 @@ def eval_inputs(cfg, ecams, eimages, m):
     return coords, tgt, draws(eg, n, cfg["bg_samples"])
 
 
-def main():
+def main(name: str = "rgb"):
     from multimodalstudio_amd import scene as ms
     from multimodalstudio_amd.model import BaseModel, ModelSpec
     from multimodalstudio_amd.pipeline import UniformPixelSampler
@@ -68,7 +76,8 @@ def main():
     from oracle.train import OracleTrainer
 
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    cfg = CFG
+    cfg = CONFIGS[name]
+    raw = cfg["method"] == "grid_raw"
     mods = list(cfg["modalities"])
     channels = {m: ms.CHANNELS[m] for m in mods}
     torch.manual_seed(cfg["init_seed"])
@@ -77,12 +86,13 @@ def main():
     cams = ms.make_cameras(mods, cfg["n_views"], cfg["width"], cfg["height"], seed=0, train=True)
     ecams = ms.make_cameras(mods, cfg["n_views"], cfg["width"], cfg["height"], seed=0, train=False)
     cpu = torch.device("cpu")
-    images = {m: ms.render_frames(cams[m], channels[m], cpu) for m in mods}
-    eimages = {m: ms.render_frames(ecams[m], channels[m], cpu) for m in mods}
+    images = {m: ms.render_frames(cams[m], channels[m], cpu, m if raw else None) for m in mods}
+    eimages = {m: ms.render_frames(ecams[m], channels[m], cpu, m if raw else None) for m in mods}
+    masks = {m: ms.mosaick_mask(m, cfg["width"], cfg["height"]) for m in mods}
     frames = {m: {"shape": (cams[m].c2w.shape[0], cfg["height"], cfg["width"]),
                   "indexes": torch.arange(cams[m].c2w.shape[0], dtype=torch.int32)} for m in mods}
     sampler = UniformPixelSampler(cfg["rays"], cfg["sampler_seed"])
-    ot = OracleTrainer(sd, channels, cams, cfg["log2T"], cfg["start_step"], raw=False)
+    ot = OracleTrainer(sd, channels, cams, cfg["log2T"], cfg["start_step"], raw=raw, mosaick=masks)
     gen = torch.Generator().manual_seed(cfg["rng_seed"])
 
     def rng_hook(n_hit, n_rays):
@@ -97,15 +107,21 @@ def main():
 
     def evaluate(tag):
         st = om.StepState(step=ot.step)
+        rays, rng, tgts, coords_e = {}, om.RNG({}, {}, {}), {}, {}
         for m in mods:
             c = ecams[m]
             coords, tgt, (u, p, b) = eval_inputs(cfg, ecams, eimages, m)
-            rays = {m: orr.generate_rays(coords, c.fx, c.fy, c.cx, c.cy, c.c2w, c.distortion, torch.zeros(1, 6), 0.0)}
-            with torch.no_grad():
-                hit = int(orr.sphere_collider(rays[m].origins, rays[m].directions)[2].sum())
-                rng = om.RNG({m: u[:hit]}, {m: [x[:hit] for x in p]}, {m: b})
-                pred = om.model_forward(rays, ot.P, ot.spec, st, rng)[m][m]
-            psnr = -10.0 * np.log10(float(((pred - tgt) ** 2).mean()))
+            rays[m] = orr.generate_rays(coords, c.fx, c.fy, c.cx, c.cy, c.c2w, c.distortion, torch.zeros(1, 6), 0.0)
+            hit = int(orr.sphere_collider(rays[m].origins, rays[m].directions)[2].sum())
+            rng.uniform[m], rng.pdf[m], rng.background[m] = u[:hit], [x[:hit] for x in p], b
+            tgts[m], coords_e[m] = tgt, coords
+        with torch.no_grad():
+            outs = om.model_forward(rays, ot.P, ot.spec, st, rng)
+        for m in mods:
+            pred = outs[m][m]
+            if raw:
+                pred = om.select_channel(pred, masks[m], coords_e[m])
+            psnr = -10.0 * np.log10(float(((pred - tgts[m]) ** 2).mean()))
             print(f"{tag} {m}: PSNR {psnr:.4f} dB", flush=True)
             out[f"{tag}:{m}:psnr"] = np.float64(psnr)
 
@@ -117,8 +133,8 @@ def main():
         if k % 25 == 0:
             print(f"step {k}: loss {float(out[f's{k}:loss']):.6f} ({time.time() - t0:.1f}s)", flush=True)
     evaluate("eval")
-    np.savez_compressed(os.path.join(os.path.dirname(os.path.abspath(__file__)), "train_parity_rgb.npz"), **out)
+    np.savez_compressed(os.path.join(os.path.dirname(os.path.abspath(__file__)), f"train_parity_{name}.npz"), **out)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else "rgb")

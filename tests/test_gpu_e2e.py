@@ -127,3 +127,28 @@ def test_e2e_train_step(dev, name):
         assert report.get(f"{m}:hessians", 0.0) < 0.15
         assert report[f"{m}:dpose"] < 5e-2
     assert worst_param < 5e-2
+
+
+@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000"])
+def test_e2e_fast_preset_deviation(dev, name):
+    """The benchmarked `fast` preset (SDF MLP split-bf16x3, everything else bf16 MFMA) on the reference's fixture:
+    per-modality rendered-radiance deviation, reported and bounded (bf16 is judged by PSNR parity,
+    tests/test_gpu_train_parity.py, plus this measured deviation; the reference's own fp16 autocast is ~1e-3 mean rel
+    and bf16 5e-3 .. 2.5e-2).  Relative to max(|ref|, 1e-2) per element (polarization channels sit near 0)."""
+    from multimodalstudio_amd import functions as fx
+    f = load(name)
+    fx.set_precision("fast")
+    try:
+        mods, model, pose, outs, losses, total = run_hip_e2e(f, dev)
+    finally:
+        fx.set_precision("fp32")
+    loss_rel = abs(total.item() - float(f["loss"])) / abs(float(f["loss"]))
+    print(f"{name} fast: loss rel {loss_rel:.3e}")
+    for m in mods:
+        got = outs[m][m].detach().cpu().numpy().astype(np.float64)
+        ref = f[f"{m}:out:{m}"].astype(np.float64)
+        rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-2)
+        print(f"  {m:14s} radiance rel dev: mean {rel.mean():.3e}  max {rel.max():.3e}")
+        assert rel.mean() < 2.5e-2, (m, rel.mean())
+        assert rel.max() < 0.25, (m, rel.max())
+    assert loss_rel < 2e-2
