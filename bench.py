@@ -6,7 +6,8 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 One step = one full training iteration of RawPipeline/BasePipeline.train_step on synthetic data of the
-MMS-DATA shape: host pixel sampling (reference RNG), ray generation with SO3xR3 pose refinement, the
+MMS-DATA shape: pixel sampling (device Philox draws over HBM-resident frames; --sampler host: the
+reference-order host sampler), ray generation with SO3xR3 pose refinement, the
 collider, the 4-iteration NeuS sampler, hash grids, SDF MLP with 4 numerical-gradient taps, radiance
 MLP, heads, background NeRF, NeuS compositing, losses, backward, grad clipping, AdamW.  Random-init
 weights; model state at step 95000 (all 16 grid levels active).  Prints ONE JSON line on rank 0.
@@ -180,7 +181,7 @@ def timed_run(config: str, args, dev, rank: int, ddp, steps: int, warmup: int) -
     from multimodalstudio_amd.pipeline import POL_10_VIEWS_SKIP
     skip = {"polarization": POL_10_VIEWS_SKIP} if config == "grid_bg5" else None
     cfg = TrainConfig(method=method, modalities=mods, num_rays_per_modality=args.rays, log2T=args.log2T,
-                      skip_views=skip)
+                      skip_views=skip, gpu_sampler=args.sampler == "device")
     trainer = Trainer(cfg, dev, rank=rank)
     trainer.set_step(args.start_step)
     runner = None
@@ -231,6 +232,9 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--precision", default="fast", choices=list(DTYPES),
                     help="MLP GEMM precision preset (functions.PRESETS); fp32 = reference-parity mode")
+    ap.add_argument("--sampler", default="device", choices=["device", "host"],
+                    help="pixel sampler: HBM-resident frames + device Philox draws (default), or the reference-order "
+                         "host sampler with a per-step upload")
     ap.add_argument("--mode", default="graph", choices=["graph", "eager"],
                     help="graph: hipGraph-captured steps (multimodalstudio_amd/graphs.py); eager: Python-launched")
     ap.add_argument("--secondary", default="grid_raw5", help="also time this config (nested 'secondary' record); "
@@ -315,7 +319,8 @@ def main():
             "data": "synthetic (analytic MMS-DATA-shaped scene, 45 train views 640x512, random-init weights)",
             "config": {"workload": desc, "num_rays_per_modality": args.rays, "modalities": list(mods),
                        "rays_per_step": rays_per_step, "log2_hashmap_size": args.log2T,
-                       "model_step": args.start_step, "precision": args.precision, "parallelism": f"dp{world}",
+                       "model_step": args.start_step, "precision": args.precision,
+                       "pixel_sampler": args.sampler, "parallelism": f"dp{world}",
                        "step_mode": run_mode},
             "kernel_timing": (f"{timing_steps} eager steps of the same workload after the timed region, HIP events "
                               "around every watched launch on its stream" if not args.no_kernel_timing else None),

@@ -62,7 +62,8 @@ int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K
  * next layer from registers.  prec 1 = bf16, 2 = split bf16x3 operands (fp32 accumulate).
  * Forward (backward = 0): out[l] = act_l(X_l W_l^T + b_l) for the 3 layers (out[0], out[1] may be NULL);
  *   rows >= rows_full compute / store only output column 0 of the last layer (the SDF taps), in fp32 from
- *   w2row0 = the last layer's fp32 weight row 0 (required when rows_full < M).
+ *   w2row0 = the last layer's fp32 weight row 0 (required when rows_full < M).  With rows_full = 0 the last
+ *   layer's out may have any pitch >= 1 (e.g. a dense [M] sdf vector).
  * Backward-data (backward = 1): X = dY of the last forward layer (rows >= rows_full: column 0 only), optionally
  *   scaled by act'(xaux) (stored to xout); out[l] = (prev . W^T) * act_l'(aux[l]) with act' evaluated from the
  *   forward output aux[l] (NULL: no scaling); out[2] = dX.
@@ -102,8 +103,11 @@ int mms_geo_input_bwd(const float* X, int64_t ldx, const float* dX, int64_t lddx
  * four_delta = 4 delta, delta_sq = delta^2.  bwd writes d sdf into column 0 of dout rows (all 5M). */
 int mms_taps_combine_fwd(const float* out, int64_t ldo, int64_t M, float four_delta, float delta_sq, float* grads,
                          float* hess, float* normals, void* stream);
+/* bwd also adds the centre rows' own d sdf (dsdf [M] with row stride ldds, may be NULL) into column 0 and writes the
+ * geo-feature gradient dgeo [M, G] (ldg; NULL: zeros) into columns 1..G of the centre rows: dout is complete. */
 int mms_taps_combine_bwd(const float* grads, const float* dgrads, const float* dhess, const float* dnormals,
-                         int64_t M, float four_delta, float delta_sq, float* dout, int64_t lddo, void* stream);
+                         int64_t M, float four_delta, float delta_sq, float* dout, int64_t lddo, const float* dsdf,
+                         int64_t ldds, const float* dgeo, int64_t ldg, int G, void* stream);
 
 /* ---- radiance input panel [x, SH4(d), geo, n.v, (grid)] (RadianceModel.forward radiance_model.py:94-151,
  * RadianceField radiance_field.py:72-77, SH utils/math.py:21-83).  One ray = S consecutive rows. */
@@ -137,12 +141,19 @@ int mms_density_weights_bwd(const float* density, int64_t ldd, const float* delt
                             const float* alpha, const float* dweights, float* ddensity, int64_t lddd, float* ddeltas,
                             void* stream);
 /* composite sum_s w c (+ bg (1 - sum w)), scattering compacted rays to rows idx[r]
- * (Renderer.render / RadianceRenderer renderers.py:75-174; BackgroundModel sum background_model.py:101-109) */
+ * (Renderer.render / RadianceRenderer renderers.py:75-174; BackgroundModel sum background_model.py:101-109).
+ * bwd: dvals and dw [R, S] are written (not accumulated); dbg[idx[r]] is overwritten for hit rows (the caller
+ * passes dbg = dout, the pass-through gradient of every other row). */
 int mms_composite_fwd(const float* w, const float* vals, int64_t ldv, int C, const float* bg, int64_t R, int S,
                       const int64_t* idx, float* out, void* stream);
 int mms_composite_bwd(const float* w, const float* vals, int64_t ldv, int C, const float* bg, int64_t R, int S,
                       const int64_t* idx, const float* dout, float* dvals, int64_t lddv, float* dw, float* dbg,
                       void* stream);
+/* Accumulation / normals / depth renderers (renderers.py:176-242, no grad) of compacted rays scattered to rows idx[r]:
+ * out [rows, ldo >= 5] = (sum w, sum w n, sum w mid) per hit row (other rows untouched), depth clipped to the range of
+ * all sample midpoints; range [2] is scratch, (-inf, -inf) on entry. */
+int mms_render_stats(const float* w, const float* normals, const float* starts, const float* ends, int64_t R, int S,
+                     const int64_t* idx, float* out, int64_t ldo, float* range, void* stream);
 
 /* ---- PolarizationHead Stokes alignment + intensities (field_heads.py:90-106; polarizer.py:54-101).
  * stokes [M,3] (MLP output), dirs/ups per ray [M/S, 3]; out [M,4]; bwd dstokes =, ddirs +=, dups += */
@@ -172,6 +183,10 @@ int mms_neus_step(int64_t R, int S, const float* bins, const float* sdf_prev, in
 
 /* ---- rays (cameras/cameras.py:460-703, camera_utils.py:280-383, poses.py:53-67, ray_generators.py:54-81).
  * coords int [N, 3] = (camera, y, x); mats = camera_opt_to_camera [C or 1, 3, 4]; bwd dmats += (atomic). */
+/* SO(3) x R^3 exponential map of the camera-pose deltas (lie_groups.py:28-63, camera_optimizers.py:86-119):
+ * tangent [B, 6] = (t, w) -> mats [B, 3, 4] = [R(w) | t]; bwd writes dtangent [B, 6] from dmats [B, 3, 4]. */
+int mms_pose_exp_fwd(const float* tangent, int64_t B, float* mats, void* stream);
+int mms_pose_exp_bwd(const float* tangent, const float* dmats, int64_t B, float* dtangent, void* stream);
 int mms_raygen_fwd(const int* coords, int64_t N, const float* fx, const float* fy, const float* cx, const float* cy,
                    const float* c2w, const float* dist, const float* mats, int mat_per_cam, float pixel_offset,
                    float* origins, float* dirs, float* ups, float* area, float* dnorm, void* stream);
@@ -186,6 +201,14 @@ int mms_collider_bwd(const float* origins, const float* dirs, int64_t N, float r
                      void* stream);
 /* order-preserving mask compaction (TensorDataclass.__getitem__ with a bool mask, base_model.py:88-93) */
 int mms_compact(const unsigned char* mask, int64_t N, int64_t* idx, int64_t* count, void* stream);
+/* hit-ray gather of the compacted rays (base_model.py:88-93): (o, d, up [N,3], near, far [N]) rows idx[r] ->
+ * [R,3] x 3, [R] x 2; bwd: dorig, ddirs, dups [N,3], dnears, dfars [N] += scatter of the five gradients (any input
+ * gradient may be NULL; atomic: repeated indices allowed). */
+int mms_hit_gather_fwd(const int64_t* idx, int64_t R, const float* o, const float* d, const float* u, const float* n,
+                       const float* f, float* oh, float* dh, float* uh, float* nh, float* fh, void* stream);
+int mms_hit_gather_bwd(const int64_t* idx, int64_t R, const float* doh, const float* ddh, const float* duh,
+                       const float* dnh, const float* dfh, float* dorig, float* ddirs, float* dups, float* dnears,
+                       float* dfars, void* stream);
 /* fixed-capacity form for static-shape (graph-captured) steps: idx [N] buffer, its first cap entries are used;
  * rows [count, cap) are padding (gather index = first hit, scatter index sidx = N, a dummy row); count is
  * clamped to cap on the device.  sidx may be NULL. */
@@ -203,13 +226,13 @@ int mms_geo_loss_fwd(const float* grads, const float* hess, int64_t M, float inv
 int mms_geo_loss_bwd(const float* grads, const float* hess, int64_t M, float inv_total, const float* deik,
                      float eik_scale, const float* dcurv, float curv_scale, float* dgrads, float* dhess,
                      void* stream);
-/* fixed-capacity batches (graph-captured steps): rows >= count[0] * S are padding and skipped, and 1 / total is
- * read on the device (inv_total[0]), so the hit count never reaches the host */
+/* fixed-capacity batches (graph-captured steps): rows >= count[0] * S are padding and skipped, and the mean runs over
+ * 1 / max(1, S * sum(counts_all[0 .. n_counts))) formed on the device, so no hit count reaches the host */
 int mms_geo_loss_fwd_masked(const float* grads, const float* hess, int64_t M, int S, const int64_t* count,
-                            const float* inv_total, float* eik, float* curv, void* stream);
+                            const int64_t* counts_all, int n_counts, float* eik, float* curv, void* stream);
 int mms_geo_loss_bwd_masked(const float* grads, const float* hess, int64_t M, int S, const int64_t* count,
-                            const float* inv_total, const float* deik, float eik_scale, const float* dcurv,
-                            float curv_scale, float* dgrads, float* dhess, void* stream);
+                            const int64_t* counts_all, int n_counts, const float* deik, float eik_scale,
+                            const float* dcurv, float curv_scale, float* dgrads, float* dhess, void* stream);
 
 /* ---- optimizer (pipelines/base_pipeline.py:232-248 clip_gradients, torch.optim.AdamW single-tensor step,
  * method_configs.py:260-269): acc += sum x^2 ; AdamW with clip coefficient min(1, max_norm / (sqrt(*sumsq) + 1e-6))

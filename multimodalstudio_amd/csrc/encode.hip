@@ -118,12 +118,24 @@ __global__ void taps_combine_fwd_kernel(const float* __restrict__ out, int64_t l
   }
 }
 
-// backward: writes d sdf into column 0 of dOut rows (centre + taps) (overwrite)
+// backward: writes d sdf into column 0 of dOut rows (centre + taps) (overwrite), plus the centre rows' own sdf
+// gradient (dsdf) and, in the blocks past tap_blocks, the geo-feature gradient into columns 1..G of the centre rows
+// (one element per thread, coalesced along the row)
 __global__ void taps_combine_bwd_kernel(const float* __restrict__ grads, const float* __restrict__ dgrads,
                                         const float* __restrict__ dhess, const float* __restrict__ dnormals,
                                         int64_t M, float four_delta, float delta_sq, float* __restrict__ dout,
-                                        int64_t lddo) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
+                                        int64_t lddo, const float* __restrict__ dsdf, int64_t ldds,
+                                        const float* __restrict__ dgeo, int64_t ldg, int G, unsigned tap_blocks) {
+  if (blockIdx.x >= tap_blocks) {
+    const int64_t n = M * G;
+    for (int64_t e = (int64_t)(blockIdx.x - tap_blocks) * blockDim.x + threadIdx.x; e < n;
+         e += (int64_t)(gridDim.x - tap_blocks) * blockDim.x) {
+      const int64_t r = e / G, c = e - r * G;
+      dout[r * lddo + 1 + c] = dgeo ? dgeo[r * ldg + c] : 0.f;
+    }
+    return;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)tap_blocks * blockDim.x) {
     float dg[3] = {0.f, 0.f, 0.f};
     if (dgrads) {
 #pragma unroll
@@ -146,7 +158,7 @@ __global__ void taps_combine_bwd_kernel(const float* __restrict__ grads, const f
     }
     float dh = 0.f;
     if (dhess) dh = (dhess[i * 3] + dhess[i * 3 + 1] + dhess[i * 3 + 2]) / 3.0f / delta_sq;
-    dout[i * lddo] = -2.0f * dh;
+    dout[i * lddo] = dsdf ? -2.0f * dh + dsdf[i * ldds] : -2.0f * dh;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const float ds = (kTap[t][0] * dg[0] + kTap[t][1] * dg[1] + kTap[t][2] * dg[2]) / four_delta + 0.5f * dh;
@@ -222,10 +234,23 @@ __device__ __forceinline__ void sh25_bwd(float x, float y, float z, const float*
 
 // Radiance panel [M, ld]: [pos 3 | SH 25 | geo 256 | ndv 1 | grid 32 (hashgrid kernel)]
 // pos rows i; direction per ray = dirs[i / S]; normals [M, 3]; geo from geometry-MLP output rows i, cols 1..256.
+// Blocks [0, row_blocks): one thread per row writes x, SH(d) and n.v; the blocks after them copy the geo feature
+// columns one element per thread (consecutive threads on consecutive columns: coalesced on both sides -- a thread
+// per row copying its own 256 columns touched 64 rows per instruction).
 __global__ void rad_input_fwd_kernel(const float* __restrict__ pos, int64_t ldp, const float* __restrict__ dirs,
                                      const float* __restrict__ normals, const float* __restrict__ geo, int64_t ldg,
-                                     int64_t M, int S, int G, float* __restrict__ X, int64_t ldx) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
+                                     int64_t M, int S, int G, float* __restrict__ X, int64_t ldx,
+                                     unsigned row_blocks) {
+  if (blockIdx.x >= row_blocks) {
+    const int64_t n = M * G;
+    for (int64_t e = (int64_t)(blockIdx.x - row_blocks) * blockDim.x + threadIdx.x; e < n;
+         e += (int64_t)(gridDim.x - row_blocks) * blockDim.x) {
+      const int64_t r = e / G, c = e - r * G;
+      X[r * ldx + 28 + c] = geo[r * ldg + c];
+    }
+    return;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)row_blocks * blockDim.x) {
     const float* d = dirs + (i / S) * 3;
     float* row = X + i * ldx;
     row[0] = pos[i * ldp];
@@ -235,8 +260,6 @@ __global__ void rad_input_fwd_kernel(const float* __restrict__ pos, int64_t ldp,
     sh25(d[0], d[1], d[2], sh);
 #pragma unroll
     for (int k = 0; k < 25; ++k) row[3 + k] = sh[k];
-    const float* gr = geo + i * ldg;
-    for (int k = 0; k < G; ++k) row[28 + k] = gr[k];
     const float* n = normals + i * 3;
     // torch.sum(normals * -directions, dim=-1): left-to-right sum of the three products
     float ndv = n[0] * -d[0];
@@ -419,11 +442,15 @@ MMS_EXPORT int mms_taps_combine_fwd(const float* out, int64_t ldo, int64_t M, fl
 
 MMS_EXPORT int mms_taps_combine_bwd(const float* grads, const float* dgrads, const float* dhess, const float* dnormals,
                                     int64_t M, float four_delta, float delta_sq, float* dout, int64_t lddo,
+                                    const float* dsdf, int64_t ldds, const float* dgeo, int64_t ldg, int G,
                                     void* stream) {
   const char* fn = "mms_taps_combine_bwd";
   if (M == 0) return 0;
-  hipLaunchKernelGGL(taps_combine_bwd_kernel, dim3(mms::grid_for(M, 256, 16384)), dim3(256), 0, mms::as_stream(stream),
-                     grads, dgrads, dhess, dnormals, M, four_delta, delta_sq, dout, lddo);
+  MMS_REQUIRE(G >= 0 && lddo >= G + 1, fn, "dout rows hold the sdf column and G geo columns");
+  const unsigned tb = mms::grid_for(M, 256, 16384);
+  const unsigned gb = G > 0 ? mms::grid_for(M * G, 256, 16384) : 0;
+  hipLaunchKernelGGL(taps_combine_bwd_kernel, dim3(tb + gb), dim3(256), 0, mms::as_stream(stream), grads, dgrads, dhess,
+                     dnormals, M, four_delta, delta_sq, dout, lddo, dsdf, ldds, dgeo, ldg, G, tb);
   return mms::check_launch(fn);
 }
 
@@ -433,8 +460,10 @@ MMS_EXPORT int mms_rad_input_fwd(const float* pos, int64_t ldp, const float* dir
   const char* fn = "mms_rad_input_fwd";
   MMS_REQUIRE(ldx >= 29 + G, fn, "panel too narrow");
   if (M == 0) return 0;
-  hipLaunchKernelGGL(rad_input_fwd_kernel, dim3(mms::grid_for(M, 256, 16384)), dim3(256), 0, mms::as_stream(stream),
-                     pos, ldp, dirs, normals, geo, ldg, M, S, G, X, ldx);
+  const unsigned rb = mms::grid_for(M, 256, 16384);
+  const unsigned gb = G > 0 ? mms::grid_for(M * G, 256, 16384) : 0;
+  hipLaunchKernelGGL(rad_input_fwd_kernel, dim3(rb + gb), dim3(256), 0, mms::as_stream(stream), pos, ldp, dirs, normals,
+                     geo, ldg, M, S, G, X, ldx, rb);
   return mms::check_launch(fn);
 }
 

@@ -75,14 +75,22 @@ __global__ void l1_bwd_kernel(const float* __restrict__ out, int64_t ldo, const 
 
 // eikonal: sum over rows of (||g|| - 1)^2 / M_total ; curvature: sum |h0 + h1 + h2| / M_total.
 // Fixed-capacity batches (graph-captured steps, graphs.py): with `count`, only rows [0, count[0] * S) are real, and
-// 1 / M_total is read from the device (inv_dev[0]) -- the hit count never reaches the host.
+// 1 / M_total = 1 / max(1, S * sum(counts_all)) is formed on the device -- the hit counts never reach the host.
+__device__ __forceinline__ float inv_rows(const int64_t* counts_all, int n_counts, int S, float inv_total) {
+  if (counts_all == nullptr) return inv_total;
+  int64_t t = 0;
+  for (int k = 0; k < n_counts; ++k) t += counts_all[k];
+  t *= S;
+  return 1.0f / (float)(t > 1 ? t : 1);
+}
+
 __global__ __launch_bounds__(256) void geo_loss_fwd_kernel(const float* __restrict__ grads,
                                                            const float* __restrict__ hess, int64_t M,
                                                            const int64_t* __restrict__ count, int S, float inv_total,
-                                                           const float* __restrict__ inv_dev, float* __restrict__ eik,
-                                                           float* __restrict__ curv) {
+                                                           const int64_t* __restrict__ counts_all, int n_counts,
+                                                           float* __restrict__ eik, float* __restrict__ curv) {
   const int64_t lim = count ? (count[0] * S < M ? count[0] * S : M) : M;
-  const float inv = inv_dev ? inv_dev[0] : inv_total;
+  const float inv = inv_rows(counts_all, n_counts, S, inv_total);
   float se = 0.f, sc = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += (int64_t)gridDim.x * blockDim.x) {
     if (grads) {
@@ -103,11 +111,12 @@ __global__ __launch_bounds__(256) void geo_loss_fwd_kernel(const float* __restri
 
 __global__ void geo_loss_bwd_kernel(const float* __restrict__ grads, const float* __restrict__ hess, int64_t M,
                                     const int64_t* __restrict__ count, int S, float inv_total,
-                                    const float* __restrict__ inv_dev, const float* __restrict__ deik, float eik_scale,
+                                    const int64_t* __restrict__ counts_all, int n_counts,
+                                    const float* __restrict__ deik, float eik_scale,
                                     const float* __restrict__ dcurv, float curv_scale, float* __restrict__ dgrads,
                                     float* __restrict__ dhess) {
   const int64_t lim = count ? (count[0] * S < M ? count[0] * S : M) : M;
-  const float inv = inv_dev ? inv_dev[0] : inv_total;
+  const float inv = inv_rows(counts_all, n_counts, S, inv_total);
   const float ge = deik ? deik[0] * eik_scale * inv : 0.f;
   const float gc = dcurv ? dcurv[0] * curv_scale * inv : 0.f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += (int64_t)gridDim.x * blockDim.x) {
@@ -223,18 +232,19 @@ MMS_EXPORT int mms_geo_loss_fwd(const float* grads, const float* hess, int64_t M
   const char* fn = "mms_geo_loss_fwd";
   if (M == 0) return 0;
   hipLaunchKernelGGL(geo_loss_fwd_kernel, dim3(mms::grid_for(M, 256, 1024)), dim3(256), 0, mms::as_stream(stream),
-                     grads, hess, M, nullptr, 1, inv_total, nullptr, eik, curv);
+                     grads, hess, M, nullptr, 1, inv_total, nullptr, 0, eik, curv);
   return mms::check_launch(fn);
 }
 
 MMS_EXPORT int mms_geo_loss_fwd_masked(const float* grads, const float* hess, int64_t M, int S, const int64_t* count,
-                                       const float* inv_total, float* eik, float* curv, void* stream) {
+                                       const int64_t* counts_all, int n_counts, float* eik, float* curv,
+                                       void* stream) {
   const char* fn = "mms_geo_loss_fwd_masked";
-  MMS_REQUIRE(S >= 1 && count != nullptr && inv_total != nullptr, fn,
-              "needs S >= 1, a device hit count and a device 1/total");
+  MMS_REQUIRE(S >= 1 && count != nullptr && counts_all != nullptr && n_counts >= 1, fn,
+              "needs S >= 1, this batch's device hit count and every batch's");
   if (M == 0) return 0;
   hipLaunchKernelGGL(geo_loss_fwd_kernel, dim3(mms::grid_for(M, 256, 1024)), dim3(256), 0, mms::as_stream(stream),
-                     grads, hess, M, count, S, 0.f, inv_total, eik, curv);
+                     grads, hess, M, count, S, 0.f, counts_all, n_counts, eik, curv);
   return mms::check_launch(fn);
 }
 
@@ -244,19 +254,21 @@ MMS_EXPORT int mms_geo_loss_bwd(const float* grads, const float* hess, int64_t M
   const char* fn = "mms_geo_loss_bwd";
   if (M == 0) return 0;
   hipLaunchKernelGGL(geo_loss_bwd_kernel, dim3(mms::grid_for(M, 256, 8192)), dim3(256), 0, mms::as_stream(stream),
-                     grads, hess, M, nullptr, 1, inv_total, nullptr, deik, eik_scale, dcurv, curv_scale, dgrads, dhess);
+                     grads, hess, M, nullptr, 1, inv_total, nullptr, 0, deik, eik_scale, dcurv, curv_scale, dgrads, dhess);
   return mms::check_launch(fn);
 }
 
 MMS_EXPORT int mms_geo_loss_bwd_masked(const float* grads, const float* hess, int64_t M, int S, const int64_t* count,
-                                       const float* inv_total, const float* deik, float eik_scale, const float* dcurv,
-                                       float curv_scale, float* dgrads, float* dhess, void* stream) {
+                                       const int64_t* counts_all, int n_counts, const float* deik, float eik_scale,
+                                       const float* dcurv, float curv_scale, float* dgrads, float* dhess,
+                                       void* stream) {
   const char* fn = "mms_geo_loss_bwd_masked";
-  MMS_REQUIRE(S >= 1 && count != nullptr && inv_total != nullptr, fn,
-              "needs S >= 1, a device hit count and a device 1/total");
+  MMS_REQUIRE(S >= 1 && count != nullptr && counts_all != nullptr && n_counts >= 1, fn,
+              "needs S >= 1, this batch's device hit count and every batch's");
   if (M == 0) return 0;
   hipLaunchKernelGGL(geo_loss_bwd_kernel, dim3(mms::grid_for(M, 256, 8192)), dim3(256), 0, mms::as_stream(stream),
-                     grads, hess, M, count, S, 0.f, inv_total, deik, eik_scale, dcurv, curv_scale, dgrads, dhess);
+                     grads, hess, M, count, S, 0.f, counts_all, n_counts, deik, eik_scale, dcurv, curv_scale, dgrads,
+                     dhess);
   return mms::check_launch(fn);
 }
 

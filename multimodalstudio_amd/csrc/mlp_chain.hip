@@ -679,8 +679,11 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx
     MMS_REQUIRE(L.aux == nullptr || (aligned16(L.aux) && L.ldaux % 4 == 0), fn, "aux rows must be 16-B aligned");
     L.out = out[l];
     L.ldo = ldo[l];
-    MMS_REQUIRE(L.out == nullptr || (aligned16(L.out) && L.ldo % 4 == 0 && L.ldo >= N[l]), fn,
-                "output rows must be 16-B aligned");
+    // a forward whose rows all take the single-output path (rows_full = 0, the sampler's SDF queries) stores only
+    // column 0 of the last layer, one scalar per row: any pitch >= 1 (a dense [M] sdf vector with ldo = 1)
+    const bool col0_only = !backward && l == 2 && a.rows_full == 0;
+    MMS_REQUIRE(L.out == nullptr || (col0_only && L.ldo >= 1) ||
+                    (aligned16(L.out) && L.ldo % 4 == 0 && L.ldo >= N[l]), fn, "output rows must be 16-B aligned");
     L.N = N[l];
     L.act = act[l];
     nt[l] = (N[l] + 31) / 32;

@@ -301,7 +301,178 @@ __global__ __launch_bounds__(1024) void compact_pad_kernel(int64_t N, int64_t ca
   }
 }
 
+// ---- SO(3) x R^3 exponential map of the pose deltas (lie_groups.py:28-63): thread per camera delta.
+// R = I + f1 K + f2 K^2 with K = skew(w), theta = sqrt(max(|w|^2, 1e-4)), f1 = sin(theta) / theta,
+// f2 = (1 - cos(theta)) / theta^2; the translation column is t.  Same float operation order as the reference's
+// torch expression (fac1 * K + fac2 * K K) + I.
+struct Skew {
+  float k[3][3];
+};
+
+__device__ __forceinline__ Skew skew_of(const float* w) {
+  Skew s;
+  s.k[0][0] = 0.f;   s.k[0][1] = -w[2]; s.k[0][2] = w[1];
+  s.k[1][0] = w[2];  s.k[1][1] = 0.f;   s.k[1][2] = -w[0];
+  s.k[2][0] = -w[1]; s.k[2][1] = w[0];  s.k[2][2] = 0.f;
+  return s;
+}
+
+__global__ void pose_exp_fwd_kernel(const float* __restrict__ tangent, int64_t B, float* __restrict__ mats) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* tv = tangent + 6 * b;
+  const float w[3] = {tv[3], tv[4], tv[5]};
+  const float nrm = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  const float ang = sqrtf(fmaxf(nrm, 1e-4f));
+  const float inv = 1.0f / ang;
+  const float f1 = inv * sinf(ang);
+  const float f2 = inv * inv * (1.0f - cosf(ang));
+  const Skew K = skew_of(w);
+  float* o = mats + 12 * b;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float k2 = K.k[i][0] * K.k[0][j] + K.k[i][1] * K.k[1][j] + K.k[i][2] * K.k[2][j];
+      o[4 * i + j] = (f1 * K.k[i][j] + f2 * k2) + (i == j ? 1.f : 0.f);
+    }
+    o[4 * i + 3] = tv[i];
+  }
+}
+
+// d tangent from d mats [B, 3, 4]: dt = dM[:, 3]; dK = f1 G + f2 (G K^T + K^T G), df1 = <G, K>, df2 = <G, K^2>,
+// and through theta (only where |w|^2 > 1e-4: the clamp passes no gradient below it) dtheta / dw = w / theta.
+__global__ void pose_exp_bwd_kernel(const float* __restrict__ tangent, const float* __restrict__ dmats, int64_t B,
+                                    float* __restrict__ dtangent) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* tv = tangent + 6 * b;
+  const float* g = dmats + 12 * b;
+  const float w[3] = {tv[3], tv[4], tv[5]};
+  const float nrm = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  const float ang = sqrtf(fmaxf(nrm, 1e-4f));
+  const float inv = 1.0f / ang;
+  const float sn = sinf(ang), cs = cosf(ang);
+  const float f1 = inv * sn;
+  const float f2 = inv * inv * (1.0f - cs);
+  const Skew K = skew_of(w);
+  float G[3][3], dK[3][3];
+  float df1 = 0.f, df2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) G[i][j] = g[4 * i + j];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float k2 = K.k[i][0] * K.k[0][j] + K.k[i][1] * K.k[1][j] + K.k[i][2] * K.k[2][j];
+      df1 += G[i][j] * K.k[i][j];
+      df2 += G[i][j] * k2;
+      // (G K^T + K^T G)_ij = sum_l G_il K_jl + K_li G_lj
+      float s = 0.f;
+#pragma unroll
+      for (int l = 0; l < 3; ++l) s += G[i][l] * K.k[j][l] + K.k[l][i] * G[l][j];
+      dK[i][j] = f1 * G[i][j] + f2 * s;
+    }
+  }
+  float dw[3] = {dK[2][1] - dK[1][2], dK[0][2] - dK[2][0], dK[1][0] - dK[0][1]};
+  if (nrm > 1e-4f) {
+    const float df1da = cs * inv - sn * inv * inv;
+    const float df2da = sn * inv * inv - 2.0f * (1.0f - cs) * inv * inv * inv;
+    const float da = df1 * df1da + df2 * df2da;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dw[k] += da * w[k] * inv;
+  }
+  float* d = dtangent + 6 * b;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    d[i] = g[4 * i + 3];
+    d[3 + i] = dw[i];
+  }
+}
+
+// ---- hit-ray gather (TensorDataclass.__getitem__ with the collider mask, base_model.py:88-93): one thread per
+// compacted ray copies (origins 3, directions 3, up 3, near 1, far 1) from row idx[r]; the backward scatter-adds the
+// five gradients back (atomics: padding rows of a fixed-capacity batch repeat the first hit's index, with zero
+// gradients).
+__global__ void hit_gather_fwd_kernel(const int64_t* __restrict__ idx, int64_t R, const float* __restrict__ o,
+                                      const float* __restrict__ d, const float* __restrict__ u,
+                                      const float* __restrict__ n, const float* __restrict__ f, float* __restrict__ oh,
+                                      float* __restrict__ dh, float* __restrict__ uh, float* __restrict__ nh,
+                                      float* __restrict__ fh) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const int64_t i = idx[r];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    oh[r * 3 + c] = o[i * 3 + c];
+    dh[r * 3 + c] = d[i * 3 + c];
+    uh[r * 3 + c] = u[i * 3 + c];
+  }
+  nh[r] = n[i];
+  fh[r] = f[i];
+}
+
+__global__ void hit_gather_bwd_kernel(const int64_t* __restrict__ idx, int64_t R, const float* __restrict__ doh,
+                                      const float* __restrict__ ddh, const float* __restrict__ duh,
+                                      const float* __restrict__ dnh, const float* __restrict__ dfh,
+                                      float* __restrict__ dO, float* __restrict__ dD, float* __restrict__ dU,
+                                      float* __restrict__ dN, float* __restrict__ dF) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const int64_t i = idx[r];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    if (doh) atomicAdd(dO + i * 3 + c, doh[r * 3 + c]);
+    if (ddh) atomicAdd(dD + i * 3 + c, ddh[r * 3 + c]);
+    if (duh) atomicAdd(dU + i * 3 + c, duh[r * 3 + c]);
+  }
+  if (dnh) atomicAdd(dN + i, dnh[r]);
+  if (dfh) atomicAdd(dF + i, dfh[r]);
+}
+
 }  // namespace
+
+MMS_EXPORT int mms_hit_gather_fwd(const int64_t* idx, int64_t R, const float* o, const float* d, const float* u,
+                                  const float* n, const float* f, float* oh, float* dh, float* uh, float* nh, float* fh,
+                                  void* stream) {
+  const char* fn = "mms_hit_gather_fwd";
+  if (R == 0) return 0;
+  MMS_REQUIRE(idx && o && d && u && n && f && oh && dh && uh && nh && fh, fn, "null pointer");
+  hipLaunchKernelGGL(hit_gather_fwd_kernel, dim3(mms::grid_for(R, 256, INT32_MAX)), dim3(256), 0,
+                     mms::as_stream(stream), idx, R, o, d, u, n, f, oh, dh, uh, nh, fh);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_hit_gather_bwd(const int64_t* idx, int64_t R, const float* doh, const float* ddh, const float* duh,
+                                  const float* dnh, const float* dfh, float* dorig, float* ddirs, float* dups,
+                                  float* dnears, float* dfars, void* stream) {
+  const char* fn = "mms_hit_gather_bwd";
+  if (R == 0) return 0;
+  MMS_REQUIRE(idx && dorig && ddirs && dups && dnears && dfars, fn, "null pointer");
+  hipLaunchKernelGGL(hit_gather_bwd_kernel, dim3(mms::grid_for(R, 256, INT32_MAX)), dim3(256), 0,
+                     mms::as_stream(stream), idx, R, doh, ddh, duh, dnh, dfh, dorig, ddirs, dups, dnears, dfars);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_pose_exp_fwd(const float* tangent, int64_t B, float* mats, void* stream) {
+  const char* fn = "mms_pose_exp_fwd";
+  if (B == 0) return 0;
+  MMS_REQUIRE(tangent && mats, fn, "null pointer");
+  hipLaunchKernelGGL(pose_exp_fwd_kernel, dim3(mms::grid_for(B, 64)), dim3(64), 0, mms::as_stream(stream), tangent, B,
+                     mats);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_pose_exp_bwd(const float* tangent, const float* dmats, int64_t B, float* dtangent, void* stream) {
+  const char* fn = "mms_pose_exp_bwd";
+  if (B == 0) return 0;
+  MMS_REQUIRE(tangent && dmats && dtangent, fn, "null pointer");
+  hipLaunchKernelGGL(pose_exp_bwd_kernel, dim3(mms::grid_for(B, 64)), dim3(64), 0, mms::as_stream(stream), tangent,
+                     dmats, B, dtangent);
+  return mms::check_launch(fn);
+}
 
 MMS_EXPORT int mms_raygen_fwd(const int* coords, int64_t N, const float* fx, const float* fy, const float* cx,
                               const float* cy, const float* c2w, const float* dist, const float* mats, int mat_per_cam,

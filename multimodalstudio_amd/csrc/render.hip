@@ -257,7 +257,66 @@ __global__ __launch_bounds__(256) void composite_bwd_kernel(const float* __restr
     }
     if (lane == 0 && bg && dbg) dbg[orow * C + c] = g * (1.0f - acc);  // hit rows: overwrite the pass-through dout
   }
-  if (lane < S && dw) dw[i] += gw;
+  if (lane < S && dw) dw[i] = gw;  // every weight of the ray is written (no accumulation: dw needs no zero fill)
+}
+
+// ------------------------------------------------------------------ render statistics (no grad)
+// Accumulation / normals / depth renderers (renderers.py:176-242) for compacted rays scattered to rows idx[r]:
+// acc = sum_s w, nrm = sum_s w n, dep = sum_s w (start + end) / 2, and the depth's clip range: the min / max of all
+// sample midpoints (torch.clip(depth, steps.min(), steps.max()), renderers.py:205-214) reduced into range[2] by
+// float atomics (order-independent: min / max are exact) as range = (max(-mid), max(mid)); range must hold
+// (-inf, -inf) before the launch.
+__global__ __launch_bounds__(256) void render_stats_kernel(const float* __restrict__ w, const float* __restrict__ nrm,
+                                                           const float* __restrict__ starts,
+                                                           const float* __restrict__ ends, int64_t R, int S,
+                                                           const int64_t* __restrict__ idx, float* __restrict__ out,
+                                                           int64_t ldo, float* __restrict__ range) {
+  // a wave per ray, grid-stride over rays; the midpoint range is reduced per wave, then per block in LDS, then one
+  // atomic pair per block (a pair per ray serialised ~1700 same-address atomics: 50 us)
+  __shared__ float sl[4], sh[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float lo = INFINITY, hi = -INFINITY;
+  for (int64_t ray = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; ray < R;
+       ray += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const int64_t i = ray * S + lane;
+    const bool on = lane < S;
+    const float wi = on ? w[i] : 0.f;
+    const float mid = on ? (starts[i] + ends[i]) / 2.0f : 0.f;
+    const float acc = wave_sum(wi);
+    const float n0 = wave_sum(on ? wi * nrm[i * 3] : 0.f);
+    const float n1 = wave_sum(on ? wi * nrm[i * 3 + 1] : 0.f);
+    const float n2 = wave_sum(on ? wi * nrm[i * 3 + 2] : 0.f);
+    const float dep = wave_sum(on ? wi * mid : 0.f);
+    if (on) { lo = fminf(lo, mid); hi = fmaxf(hi, mid); }
+    if (lane == 0) {
+      float* o = out + (idx ? idx[ray] : ray) * ldo;
+      o[0] = acc; o[1] = n0; o[2] = n1; o[3] = n2; o[4] = dep;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    lo = fminf(lo, __shfl_xor(lo, o));
+    hi = fmaxf(hi, __shfl_xor(hi, o));
+  }
+  if (lane == 0) { sl[wave] = lo; sh[wave] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    lo = fminf(fminf(sl[0], sl[1]), fminf(sl[2], sl[3]));
+    hi = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+    if (lo <= hi) {
+      atomicMax(range, -lo);
+      atomicMax(range + 1, hi);
+    }
+  }
+}
+
+// depth of the hit rows clipped to the midpoint range (rows not written by render_stats_kernel stay 0)
+__global__ void render_clip_kernel(int64_t R, const int64_t* __restrict__ idx, float* __restrict__ out, int64_t ldo,
+                                   const float* __restrict__ range) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  float* d = out + (idx ? idx[r] : r) * ldo + 4;
+  d[0] = fminf(fmaxf(d[0], -range[0]), range[1]);
 }
 
 }  // namespace
@@ -314,6 +373,21 @@ MMS_EXPORT int mms_composite_fwd(const float* w, const float* vals, int64_t ldv,
   if (R == 0) return 0;
   hipLaunchKernelGGL(composite_fwd_kernel, dim3(mms::grid_for(R * 64, 256, INT32_MAX)), dim3(256), 0,
                      mms::as_stream(stream), w, vals, ldv, C, bg, R, S, idx, out);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_render_stats(const float* w, const float* normals, const float* starts, const float* ends,
+                                int64_t R, int S, const int64_t* idx, float* out, int64_t ldo, float* range,
+                                void* stream) {
+  const char* fn = "mms_render_stats";
+  MMS_REQUIRE(S >= 1 && S <= 64, fn, "samples per ray must be in [1, 64]");
+  MMS_REQUIRE(ldo >= 5, fn, "output rows hold (acc, n0, n1, n2, depth)");
+  if (R == 0) return 0;
+  hipStream_t s = mms::as_stream(stream);
+  hipLaunchKernelGGL(render_stats_kernel, dim3(mms::grid_for(R * 64, 256, 256)), dim3(256), 0, s, w, normals,
+                     starts, ends, R, S, idx, out, ldo, range);
+  hipLaunchKernelGGL(render_clip_kernel, dim3(mms::grid_for(R, 256, INT32_MAX)), dim3(256), 0, s, R, idx, out, ldo,
+                     range);
   return mms::check_launch(fn);
 }
 

@@ -20,6 +20,7 @@ There is no CPU path: every function requires HIP device tensors.
 from __future__ import annotations
 
 import ctypes
+import math
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -235,13 +236,14 @@ class MLPRun:
         else:
             dZ = dy
         dx = None
+        dWs = _zeroed_views([tuple(self.params[3 * l + 1].shape) for l in range(self.L)], dev)
         for l in range(self.L - 1, -1, -1):
             g, v, b = self.params[3 * l: 3 * l + 3]
             N, K = v.shape
             Xin = x if l == 0 else self.Ys[l - 1]
             gt, vt, bt = grad_target(g), grad_target(v), grad_target(b)
             if gt is not None or vt is not None or bt is not None:
-                dW = torch.zeros(N, K, device=dev)
+                dW = dWs[l]
                 db = bt if bt is not None else torch.zeros(N, device=dev)
                 tiles = ((N + 127) // 128) * ((K + 127) // 128)
                 gemm(TN, N, K, M, dZ, dZ.stride(0), Xin, Xin.stride(0), dW, K, accumulate=True,
@@ -312,8 +314,10 @@ class ChainRun:
                   0 if xout is None else xout.stride(0), cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux),
                   cast(os_), cast(ldo), cast(ns), cast(ac), self.beta, self.thr, _p(w2row0), _s())
 
-    def forward(self, x: torch.Tensor, keep: bool, rows_full: Optional[int] = None) -> torch.Tensor:
-        """x [M, K0] (16-B aligned rows); returns the last layer's output [M, N2] (row stride rounded to 4)."""
+    def forward(self, x: torch.Tensor, keep: bool, rows_full: Optional[int] = None,
+                dense_col0: bool = False) -> torch.Tensor:
+        """x [M, K0] (16-B aligned rows); returns the last layer's output [M, N2] (row stride rounded to 4), or with
+        dense_col0 (rows_full = 0) its column 0 as a dense [M] vector."""
         M, K0 = x.shape
         dev = x.device
         self.x = x
@@ -328,12 +332,15 @@ class ChainRun:
         packs = [self._pack(self.Ws[0], 32 * nt[0], 16 * ((K0 + 15) // 16), False, False),
                  self._pack(self.Ws[1], 32 * nt[1], 32 * nt[0], False, True),
                  self._pack(self.Ws[2], 32 * nt[2], 32 * nt[1], False, True)]
-        Y = [_alloc(M, Ns[0], dev) if keep else None, _alloc(M, Ns[1], dev) if keep else None, _alloc(M, Ns[2], dev)]
         self.rows_full = M if rows_full is None else int(rows_full)
+        if dense_col0 and self.rows_full != 0:
+            raise ValueError("dense_col0 needs rows_full = 0")
+        last = torch.empty(M, device=dev).view(M, 1) if dense_col0 else _alloc(M, Ns[2], dev)
+        Y = [_alloc(M, Ns[0], dev) if keep else None, _alloc(M, Ns[1], dev) if keep else None, last]
         self._chain(False, x, K0, self.rows_full, packs, [self.params[3 * l + 2] for l in range(3)], [None] * 3, Y,
                     Ns, [a[0] for a in self.acts], w2row0=self.Ws[2])
         self.Y = Y
-        return Y[2]
+        return Y[2].view(M) if dense_col0 else Y[2]
 
     def backward(self, dy: torch.Tensor) -> torch.Tensor:
         """dy [M, N2] (rows >= rows_full: column 0 only); accumulates the parameter gradients (grad_target) and
@@ -357,13 +364,14 @@ class ChainRun:
         dZ = [dZ0, dZ1, dZ2 if dZ2 is not None else dy]
         Xin = [x, Y[0], Y[1]]
         rf = self.rows_full
+        dWs = _zeroed_views([tuple(self.params[3 * l + 1].shape) for l in range(3)], dev)
         for l in range(3):
             g, v, b = self.params[3 * l: 3 * l + 3]
             N, K = v.shape
             gt, vt, bt = grad_target(g), grad_target(v), grad_target(b)
             if gt is None and vt is None and bt is None:
                 continue
-            dW = torch.zeros(N, K, device=dev)
+            dW = dWs[l]
             db = bt if bt is not None else torch.zeros(N, device=dev)
             A, B = dZ[l], Xin[l]
             tiles = ((N + 127) // 128) * ((K + 127) // 128)
@@ -380,6 +388,18 @@ class ChainRun:
                             torch.zeros(N, device=dev), vt if vt is not None else torch.zeros(N, K, device=dev))
         self.Y = self.x = None
         return dx
+
+
+def _zeroed_views(shapes, dev) -> List[Optional[torch.Tensor]]:
+    """Zero-filled f32 accumulation buffers carved from one allocation (None for a None shape): one fill launch per
+    backward function instead of one per gradient -- each fill is a graph node of its own (~5 us replayed)."""
+    sizes = [0 if sh is None else math.prod(sh) for sh in shapes]
+    buf = torch.zeros(max(sum(sizes), 1), device=dev)
+    out, off = [], 0
+    for sh, n in zip(shapes, sizes):
+        out.append(None if sh is None else buf[off:off + n].view(tuple(sh)))
+        off += n
+    return out
 
 
 def _copy_aligned(t: torch.Tensor) -> torch.Tensor:
@@ -403,6 +423,7 @@ class SurfaceFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pos, table, grid: GridCfg, active: int, delta: float, *params):
+        ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
         M = pos.shape[0]
         dev = pos.device
         pos = pos.contiguous()
@@ -428,8 +449,9 @@ class SurfaceFunction(torch.autograd.Function):
         normals = torch.empty(M, 3, device=dev)
         _lib.call("mms_taps_combine_fwd", out.data_ptr(), out.stride(0), M, four_delta, delta_sq, grads.data_ptr(),
                   hess.data_ptr(), normals.data_ptr(), _s())
-        sdf = out[:M, 0:1].contiguous()
-        geo = out[:M, 1:].contiguous()
+        # views of the MLP output rows (row stride = the panel pitch): the consumers take strides, no copies
+        sdf = out[:M, 0:1]
+        geo = out[:M, 1:]
         ctx.grid, ctx.active, ctx.M, ctx.G = grid, active, M, G
         ctx.table = ctx.table_p = table          # the Parameter itself: its .grad is accumulated in place
         if ctx.needs_input_grad[1]:
@@ -446,14 +468,11 @@ class SurfaceFunction(torch.autograd.Function):
         dev = pos.device
         # dout: centre rows all 257 columns, tap rows only the sdf column (everything read is written here)
         dout = _alloc(5 * M, G + 1, dev)
-        _lib.call("mms_taps_combine_bwd", grads.data_ptr(), _p(dgrads if dgrads is not None else None),
-                  _p(dhess), _p(dnormals), M, ctx.four_delta, ctx.delta_sq, dout.data_ptr(), dout.stride(0), _s())
-        if dsdf is not None:
-            dout[:M, 0:1] += dsdf
-        if dgeo is not None:
-            dout[:M, 1:] = dgeo
-        else:
-            dout[:M, 1:] = 0.0
+        c = lambda t: None if t is None else (t if t.stride(-1) == 1 else t.contiguous())
+        dsdf, dgeo = c(dsdf), c(dgeo)
+        _lib.call("mms_taps_combine_bwd", grads.data_ptr(), _p(c(dgrads)), _p(c(dhess)), _p(c(dnormals)), M,
+                  ctx.four_delta, ctx.delta_sq, dout.data_ptr(), dout.stride(0), _p(dsdf),
+                  0 if dsdf is None else dsdf.stride(0), _p(dgeo), 0 if dgeo is None else dgeo.stride(0), G, _s())
         need_table = ctx.needs_input_grad[1]
         need_pos = ctx.needs_input_grad[0]
         if ctx.chain is not None:
@@ -464,12 +483,10 @@ class SurfaceFunction(torch.autograd.Function):
         X = ctx.X
         K0 = X.stride(0)
         dtable = grad_target(ctx.table) if need_table else None
-        dP = torch.zeros(5 * M, 3, device=dev) if need_pos else None
+        dP, dpos = _zeroed_views([(5 * M, 3), (M, 3)] if need_pos else [None, None], dev)
         grid_bwd(ctx.grid, X, K0, 5 * M, table, ctx.active, dX, 39, dtable, dP, group=5)
         _grad_ready(ctx.table_p, dtable)
-        dpos = None
         if need_pos:
-            dpos = torch.zeros(M, 3, device=dev)
             _lib.call("mms_geo_input_bwd", X.data_ptr(), K0, dX.data_ptr(), dX.stride(0), dP.data_ptr(), 3, M, 4, 6,
                       dpos.data_ptr(), 3, _s())
         ctx.run = ctx.H = ctx.W3 = ctx.X = ctx.table = ctx.chain = None
@@ -532,9 +549,9 @@ def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> to
     _lib.call("mms_geo_input_fwd", pos.data_ptr(), pos.stride(0), M, 0, 0.0, 6, X.data_ptr(), X.stride(0), _s())
     grid_fwd(grid, X, X.stride(0), M, table, active, X, 39)
     if PRECISION["sdf"] != 0:
-        # fused chain, no hidden-layer stores, only the sdf column tile of the output layer (rows_full = 0)
-        out = ChainRun(params, SDF_ACTS, PRECISION["sdf"]).forward(X, keep=False, rows_full=0)
-        return out[:, 0].contiguous()      # the sampler kernel reads the sdf rows densely
+        # fused chain, no hidden-layer stores, only the sdf column of the output layer (rows_full = 0), written as
+        # the dense [M] vector the sampler kernel reads
+        return ChainRun(params, SDF_ACTS, PRECISION["sdf"]).forward(X, keep=False, rows_full=0, dense_col0=True)
     # only the sdf column of the last layer is needed
     last = list(params[-3:])
     g, v, b = last
@@ -581,6 +598,7 @@ class SDFFieldFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pos, table, grid: GridCfg, active: int, *params):
+        ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
         M = pos.shape[0]
         dev = pos.device
         pos = pos.contiguous()
@@ -607,12 +625,10 @@ class SDFFieldFunction(torch.autograd.Function):
         dX = _run_backward(ctx.run, dout)
         X = ctx.X
         need_pos = ctx.needs_input_grad[0]
-        dP = torch.zeros(M, 3, device=dev) if need_pos else None
+        dP, dpos = _zeroed_views([(M, 3), (M, 3)] if need_pos else [None, None], dev)
         dtable = grad_target(ctx.table) if ctx.needs_input_grad[1] else None
         grid_bwd(ctx.grid, X, X.stride(0), M, table, ctx.active, dX, 39, dtable, dP)
-        dpos = None
         if need_pos:
-            dpos = torch.zeros(M, 3, device=dev)
             _lib.call("mms_geo_input_bwd", X.data_ptr(), X.stride(0), dX.data_ptr(), dX.stride(0), dP.data_ptr(), 3, M,
                       0, 6, dpos.data_ptr(), 3, _s())
         n = len(ctx.run.params)
@@ -628,6 +644,7 @@ class FeatureGridMLPFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, inp, table, grid: GridCfg, active: int, acts, prec: int, *params):
+        ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
         M, K_in = inp.shape
         dev = inp.device
         X = _alloc(M, K_in + grid.out_dim, dev)
@@ -680,7 +697,7 @@ class RadianceFunction(torch.autograd.Function):
         pos = pos.contiguous()
         dirs = dirs.contiguous()
         normals = normals.contiguous()
-        geo = geo.contiguous()
+        geo = geo if geo.stride(1) == 1 else geo.contiguous()    # row-strided views are read in place
         _lib.call("mms_rad_input_fwd", pos.data_ptr(), 3, dirs.data_ptr(), normals.data_ptr(), geo.data_ptr(),
                   geo.stride(0), M, S, G, X.data_ptr(), X.stride(0), _s())
         grid_fwd(grid, X, X.stride(0), M, table, active, X, 29 + G)
@@ -709,14 +726,14 @@ class RadianceFunction(torch.autograd.Function):
         K0 = X.stride(0)
         dtable = grad_target(ctx.table) if ctx.needs_input_grad[4] else None
         need_pos = ctx.needs_input_grad[0]
-        dP = torch.zeros(M, 3, device=dev) if need_pos else None
+        dP, dpos, ddirs = _zeroed_views([(M, 3) if need_pos else None, (M, 3) if need_pos else None,
+                                         (R, 3) if ctx.needs_input_grad[1] else None], dev)
         grid_bwd(ctx.grid, X, K0, M, table, ctx.active, dX, 29 + G, dtable, dP)
         _grad_ready(ctx.table_p, dtable)   # the radiance table's last contribution: its all-reduce overlaps the rest
-        dpos = torch.zeros(M, 3, device=dev) if need_pos else None
-        dgeo = torch.empty(M, G, device=dev) if ctx.needs_input_grad[3] else None
-        ddirs = torch.zeros(R, 3, device=dev) if ctx.needs_input_grad[1] else None
+        # d geo = the panel gradient's geo columns, handed on as a view (no copy)
+        dgeo = dX[:, 28:28 + G] if ctx.needs_input_grad[3] else None
         _lib.call("mms_rad_input_bwd", dX.data_ptr(), dX.stride(0), _p(dP), 3, dirs.data_ptr(), normals.data_ptr(), R,
-                  S, G, _p(dpos), 3, _p(dgeo), G, _p(ddirs), _s())
+                  S, G, _p(dpos), 3, None, G, _p(ddirs), _s())
         ctx.run = None
         ctx.X = None
         ctx.table = None
@@ -732,7 +749,8 @@ class RadInputFunction(torch.autograd.Function):
         M, G = geo.shape
         dev = pos.device
         X = _alloc(M, 3 + 25 + G + 1, dev)
-        pos, dirs, normals, geo = pos.contiguous(), dirs.contiguous(), normals.contiguous(), geo.contiguous()
+        pos, dirs, normals = pos.contiguous(), dirs.contiguous(), normals.contiguous()
+        geo = geo if geo.stride(1) == 1 else geo.contiguous()
         _lib.call("mms_rad_input_fwd", pos.data_ptr(), 3, dirs.data_ptr(), normals.data_ptr(), geo.data_ptr(),
                   geo.stride(0), M, S, G, X.data_ptr(), X.stride(0), _s())
         ctx.save_for_backward(dirs, normals)
@@ -745,11 +763,11 @@ class RadInputFunction(torch.autograd.Function):
         M, S, G = ctx.M, ctx.S, ctx.G
         dev = dX.device
         dX = dX if dX.stride(1) == 1 else dX.contiguous()
-        dpos = torch.zeros(M, 3, device=dev) if ctx.needs_input_grad[0] else None
-        dgeo = torch.empty(M, G, device=dev) if ctx.needs_input_grad[3] else None
-        ddirs = torch.zeros(M // S, 3, device=dev) if ctx.needs_input_grad[1] else None
+        dpos, ddirs = _zeroed_views([(M, 3) if ctx.needs_input_grad[0] else None,
+                                     (M // S, 3) if ctx.needs_input_grad[1] else None], dev)
+        dgeo = dX[:, 28:28 + G] if ctx.needs_input_grad[3] else None      # a view of the panel gradient
         _lib.call("mms_rad_input_bwd", dX.data_ptr(), dX.stride(0), None, 3, dirs.data_ptr(), normals.data_ptr(), M // S,
-                  S, G, _p(dpos), 3, _p(dgeo), G, _p(ddirs), _s())
+                  S, G, _p(dpos), 3, None, G, _p(ddirs), _s())
         return dpos, ddirs, None, dgeo, None
 
 
@@ -788,6 +806,7 @@ class BackgroundFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pos, dirs, table, S: int, nb: int, nd: int, grid: Optional[GridCfg], active: int, *params):
+        ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
         M = pos.shape[0]
         dev = pos.device
         base_p, dens_p, head_p = params[:3 * nb], params[3 * nb:3 * (nb + nd)], params[3 * (nb + nd):]
@@ -891,10 +910,13 @@ class NeusWeightsFunction(torch.autograd.Function):
         M = sdf.shape[0]
         R = M // S
         dev = sdf.device
-        sdf, grads, dirs, deltas = sdf.contiguous(), grads.contiguous(), dirs.contiguous(), deltas.contiguous()
+        if sdf.dim() != 2 or sdf.shape[1] != 1:
+            sdf = sdf.reshape(M, 1)
+        lds = sdf.stride(0)                 # sdf may be a column view of the SDF MLP output
+        grads, dirs, deltas = grads.contiguous(), dirs.contiguous(), deltas.contiguous()
         alpha = torch.empty(R, S, device=dev)
         w = torch.empty(R, S, device=dev)
-        _lib.call("mms_neus_weights_fwd", sdf.data_ptr(), 1, grads.data_ptr(), dirs.data_ptr(), deltas.data_ptr(),
+        _lib.call("mms_neus_weights_fwd", sdf.data_ptr(), lds, grads.data_ptr(), dirs.data_ptr(), deltas.data_ptr(),
                   s_param.data_ptr(), float(cos_anneal), R, S, alpha.data_ptr(), w.data_ptr(), _s())
         ctx.save_for_backward(sdf, grads, dirs, deltas, s_param, alpha)
         ctx.cos_anneal, ctx.S = float(cos_anneal), S
@@ -906,12 +928,9 @@ class NeusWeightsFunction(torch.autograd.Function):
         S = ctx.S
         R = sdf.shape[0] // S
         dev = sdf.device
-        dsdf = torch.empty_like(sdf)
-        dgrads = torch.zeros_like(grads)
-        ddirs = torch.zeros_like(dirs)
-        ddeltas = torch.zeros_like(deltas)
-        ds = torch.zeros_like(s_param)
-        _lib.call("mms_neus_weights_bwd", sdf.data_ptr(), 1, grads.data_ptr(), dirs.data_ptr(), deltas.data_ptr(),
+        dsdf = torch.empty(sdf.shape[0], 1, device=dev)
+        dgrads, ddirs, ddeltas, ds = _zeroed_views([grads.shape, dirs.shape, deltas.shape, s_param.shape], dev)
+        _lib.call("mms_neus_weights_bwd", sdf.data_ptr(), sdf.stride(0), grads.data_ptr(), dirs.data_ptr(), deltas.data_ptr(),
                   s_param.data_ptr(), ctx.cos_anneal, R, S, alpha.data_ptr(), dw.contiguous().data_ptr(),
                   dsdf.data_ptr(), 1, dgrads.data_ptr(), ddirs.data_ptr(), ddeltas.data_ptr(), ds.data_ptr(), _s())
         return dsdf, dgrads, ddirs, ddeltas, ds, None, None
@@ -974,7 +993,7 @@ class CompositeFunction(torch.autograd.Function):
         R, C = w.shape[0], vals.shape[1]
         dout = dout.contiguous()
         dvals = torch.empty_like(vals) if ctx.needs_input_grad[1] else None
-        dw = torch.zeros_like(w)
+        dw = torch.empty_like(w)                 # every weight written by the kernel
         dbg = dout.clone() if ctx.has_bg else None
         _lib.call("mms_composite_bwd", w.data_ptr(), vals.data_ptr(), C, C, _p(bgc), R, S, _p(idx), dout.data_ptr(),
                   _p(dvals), C, dw.data_ptr(), _p(dbg), _s())
@@ -990,6 +1009,7 @@ class SamplesFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, bins, nears, fars, origins, dirs, kind: int):
+        ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
         R, nb = bins.shape
         S = nb - 1
         dev = bins.device
@@ -1011,10 +1031,7 @@ class SamplesFunction(torch.autograd.Function):
     def backward(ctx, dpos, ddeltas, dstarts, dends):
         bins, nears, fars, dirs = ctx.saved_tensors
         R, nb = bins.shape
-        dn = torch.zeros_like(nears)
-        df = torch.zeros_like(fars)
-        do = torch.zeros(R, 3, device=bins.device)
-        dd = torch.zeros(R, 3, device=bins.device)
+        dn, df, do, dd = _zeroed_views([nears.shape, fars.shape, (R, 3), (R, 3)], bins.device)
         _lib.call("mms_samples_bwd", bins.data_ptr(), nb, nb, nears.data_ptr(), fars.data_ptr(), dirs.data_ptr(),
                   ctx.kind, R, _p(None if dpos is None else dpos.contiguous()),
                   _p(None if ddeltas is None else ddeltas.contiguous()),
@@ -1023,11 +1040,63 @@ class SamplesFunction(torch.autograd.Function):
         return None, dn, df, do, dd, None
 
 
+class HitGatherFunction(torch.autograd.Function):
+    """The hit rays' origins, directions, up directions, nears and fars (base_model.py:88-93: the bundle indexed with
+    the collider mask) in one gather launch; the backward scatters all five gradients in one launch."""
+
+    @staticmethod
+    def forward(ctx, idx, o, d, up, nears, fars):
+        ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
+        R, N = idx.shape[0], o.shape[0]
+        dev = o.device
+        o, d, up, nears, fars = o.contiguous(), d.contiguous(), up.contiguous(), nears.contiguous(), fars.contiguous()
+        oh, dh, uh = [torch.empty(R, 3, device=dev) for _ in range(3)]
+        nh, fh = torch.empty(R, device=dev), torch.empty(R, device=dev)
+        _lib.call("mms_hit_gather_fwd", idx.data_ptr(), R, o.data_ptr(), d.data_ptr(), up.data_ptr(), nears.data_ptr(),
+                  fars.data_ptr(), oh.data_ptr(), dh.data_ptr(), uh.data_ptr(), nh.data_ptr(), fh.data_ptr(), _s())
+        ctx.save_for_backward(idx)
+        ctx.N = N
+        return oh, dh, uh, nh, fh
+
+    @staticmethod
+    def backward(ctx, doh, ddh, duh, dnh, dfh):
+        (idx,) = ctx.saved_tensors
+        N = ctx.N
+        go, gd, gu, gn, gf = _zeroed_views([(N, 3), (N, 3), (N, 3), (N,), (N,)], idx.device)
+        c = lambda t: None if t is None else t.contiguous()
+        _lib.call("mms_hit_gather_bwd", idx.data_ptr(), idx.shape[0], _p(c(doh)), _p(c(ddh)), _p(c(duh)), _p(c(dnh)),
+                  _p(c(dfh)), go.data_ptr(), gd.data_ptr(), gu.data_ptr(), gn.data_ptr(), gf.data_ptr(), _s())
+        return None, go, gd, gu, gn, gf
+
+
+class PoseExpFunction(torch.autograd.Function):
+    """exp_map_SO3xR3 (lie_groups.py:28-63): pose deltas [B, 6] = (t, w) -> [R(w) | t] [B, 3, 4], one launch each
+    way (the reference's ~20 tensor ops forward and their autograd backward)."""
+
+    @staticmethod
+    def forward(ctx, tangent):
+        tangent = tangent.contiguous()
+        B = tangent.shape[0]
+        mats = torch.empty(B, 3, 4, device=tangent.device)
+        _lib.call("mms_pose_exp_fwd", tangent.data_ptr(), B, mats.data_ptr(), _s())
+        ctx.save_for_backward(tangent)
+        return mats
+
+    @staticmethod
+    def backward(ctx, dmats):
+        (tangent,) = ctx.saved_tensors
+        dt = torch.empty_like(tangent)
+        _lib.call("mms_pose_exp_bwd", tangent.data_ptr(), dmats.contiguous().data_ptr(), tangent.shape[0],
+                  dt.data_ptr(), _s())
+        return dt
+
+
 class RaysFunction(torch.autograd.Function):
     """camera_opt_to_camera mats [C|1, 3, 4] -> origins, dirs, ups (+ pixel_area, directions_norm)."""
 
     @staticmethod
     def forward(ctx, mats, coords, cams, pixel_offset: float):
+        ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
         N = coords.shape[0]
         dev = coords.device
         mats = mats.contiguous()
@@ -1063,6 +1132,7 @@ class ColliderFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, origins, dirs, radius: float):
+        ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
         N = origins.shape[0]
         dev = origins.device
         origins, dirs = origins.contiguous(), dirs.contiguous()
@@ -1082,8 +1152,7 @@ class ColliderFunction(torch.autograd.Function):
     def backward(ctx, dn, df, dbn, dbf, dmask):
         origins, dirs = ctx.saved_tensors
         N = origins.shape[0]
-        do = torch.zeros_like(origins)
-        dd = torch.zeros_like(dirs)
+        do, dd = _zeroed_views([origins.shape, dirs.shape], origins.device)
         c = lambda t: None if t is None else t.contiguous()
         _lib.call("mms_collider_bwd", origins.data_ptr(), dirs.data_ptr(), N, ctx.radius, _p(c(dn)), _p(c(df)),
                   _p(c(dbn)), _p(c(dbf)), do.data_ptr(), dd.data_ptr(), _s())
@@ -1146,12 +1215,12 @@ class GeoLossFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, *tensors):
+        ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
         n = len(tensors) // 2
         grads, hess = tensors[:n], tensors[n:]
         total = sum(g.shape[0] for g in grads)
         inv = 1.0 / float(total)
-        eik = torch.zeros((), device=grads[0].device)
-        curv = torch.zeros((), device=grads[0].device)
+        eik, curv = _zeroed_views([(), ()], grads[0].device)
         for g, h in zip(grads, hess):
             _lib.call("mms_geo_loss_fwd", g.contiguous().data_ptr(), h.contiguous().data_ptr(), g.shape[0], inv,
                       eik.data_ptr(), curv.data_ptr(), _s())
@@ -1166,8 +1235,7 @@ class GeoLossFunction(torch.autograd.Function):
         outs = []
         dg_list, dh_list = [], []
         for g, h in zip(ts[:n], ts[n:]):
-            dg = torch.zeros_like(g)
-            dh = torch.zeros_like(h)
+            dg, dh = _zeroed_views([g.shape, h.shape], g.device)
             _lib.call("mms_geo_loss_bwd", g.data_ptr(), h.data_ptr(), g.shape[0], ctx.inv,
                       _p(None if deik is None else deik.contiguous()), 1.0,
                       _p(None if dcurv is None else dcurv.contiguous()), 1.0, dg.data_ptr(), dh.data_ptr(), _s())
@@ -1178,35 +1246,33 @@ class GeoLossFunction(torch.autograd.Function):
 
 class GeoLossMaskedFunction(torch.autograd.Function):
     """GeoLossFunction over fixed-capacity batches: modality m's rows >= counts[m] * S are padding and carry no loss,
-    and the mean runs over the true rows (1 / total computed on the device from the hit counts)."""
+    and the mean runs over the true rows (1 / total formed on the device from the hit counts)."""
 
     @staticmethod
     def forward(ctx, S: int, counts, *tensors):
+        ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
         n = len(tensors) // 2
         grads, hess = tensors[:n], tensors[n:]
         dev = grads[0].device
-        tot = torch.stack([c.reshape(()) for c in counts]).sum() * S
-        inv = (1.0 / tot.clamp_min(1).to(torch.float32)).reshape(1)
-        eik = torch.zeros((), device=dev)
-        curv = torch.zeros((), device=dev)
+        call = torch.cat([c.reshape(1) for c in counts]) if len(counts) > 1 else counts[0].reshape(1)
+        eik, curv = _zeroed_views([(), ()], dev)
         ts = [t.contiguous() for t in tensors]
         for g, h, c in zip(ts[:n], ts[n:], counts):
             _lib.call("mms_geo_loss_fwd_masked", g.data_ptr(), h.data_ptr(), g.shape[0], S, c.data_ptr(),
-                      inv.data_ptr(), eik.data_ptr(), curv.data_ptr(), _s())
-        ctx.save_for_backward(inv, *ts)
+                      call.data_ptr(), call.shape[0], eik.data_ptr(), curv.data_ptr(), _s())
+        ctx.save_for_backward(call, *ts)
         ctx.counts, ctx.S, ctx.n = list(counts), S, n
         return eik, curv
 
     @staticmethod
     def backward(ctx, deik, dcurv):
-        inv, *ts = ctx.saved_tensors
+        call, *ts = ctx.saved_tensors
         n, S = ctx.n, ctx.S
         dg_list, dh_list = [], []
         for g, h, c in zip(ts[:n], ts[n:], ctx.counts):
-            dg = torch.zeros_like(g)
-            dh = torch.zeros_like(h)
+            dg, dh = _zeroed_views([g.shape, h.shape], g.device)
             _lib.call("mms_geo_loss_bwd_masked", g.data_ptr(), h.data_ptr(), g.shape[0], S, c.data_ptr(),
-                      inv.data_ptr(), _p(None if deik is None else deik.contiguous()), 1.0,
+                      call.data_ptr(), call.shape[0], _p(None if deik is None else deik.contiguous()), 1.0,
                       _p(None if dcurv is None else dcurv.contiguous()), 1.0, dg.data_ptr(), dh.data_ptr(), _s())
             dg_list.append(dg)
             dh_list.append(dh)
@@ -1232,8 +1298,7 @@ class PolarizerFunction(torch.autograd.Function):
         S = ctx.S
         R = stokes.shape[0] // S
         ds = torch.empty_like(stokes)
-        dd = torch.zeros_like(dirs)
-        du = torch.zeros_like(ups)
+        dd, du = _zeroed_views([dirs.shape, ups.shape], dirs.device)
         _lib.call("mms_polarizer_bwd", stokes.data_ptr(), dirs.data_ptr(), ups.data_ptr(), R, S,
                   dout.contiguous().data_ptr(), ds.data_ptr(), dd.data_ptr(), du.data_ptr(), _s())
         return ds, dd, du, None

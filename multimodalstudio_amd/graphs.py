@@ -78,6 +78,10 @@ class GraphTrainer:
         self.last_sig = None
         self.ran_eager = False
         self.disabled: Optional[str] = None
+        # device sampler: every step (graph or eager) ends by staging the next step's pixels and hit counts
+        self.tail = trainer.gpu_sampler is not None
+        self.staged = False
+        self.count_event = torch.cuda.Event() if torch.cuda.is_available() else None
         self.stats = {"replays": 0, "eager": 0, "captures": 0}
 
     # -- host side ---------------------------------------------------------------------------------
@@ -106,9 +110,9 @@ class GraphTrainer:
         return coords
 
     @torch.no_grad()
-    def hit_counts(self):
-        """N_hit per modality for the staged rays: ray generation (current pose deltas) + collider + compaction
-        count, then one small device->host read (the step's only synchronisation)."""
+    def _count_hits(self):
+        """Enqueue ray generation (current pose deltas) + collider + compaction count for the staged rays and the
+        count's copy into pinned host memory (no synchronisation)."""
         t = self.t
         dev = t.device
         for i, m in enumerate(t.modalities):
@@ -118,12 +122,25 @@ class GraphTrainer:
             _lib.call("mms_compact", mask.data_ptr(), self.n, self.idx_scratch.data_ptr(),
                       self.count_dev[i:i + 1].data_ptr(), fx._s())
         self.count_host.copy_(self.count_dev, non_blocking=True)
+
+    def hit_counts(self):
+        """N_hit per modality for the staged rays, read on the host (the step's only synchronisation)."""
+        self._count_hits()
         torch.cuda.current_stream().synchronize()
         return [int(c) for c in self.count_host.tolist()]
+
+    def _tail(self):
+        """Device-sampler steps end by drawing the NEXT step's pixels and counting its hits (with the poses this step's
+        optimizer just updated), so the host only waits for that count -- no eager ray generation, collider or
+        synchronisation between two replays.  Captured at the end of each graph."""
+        self.t.gpu_sampler.sample()
+        self._count_hits()
 
     # -- the captured work ---------------------------------------------------------------------------
     def _targets(self):
         t = self.t
+        if t.gpu_sampler is not None:
+            return t.gpu_sampler.values      # gathered by the sampler kernel with the coordinates
         return {m: t.images[m][self.sel[m], self.coords[m][:, 1].long(), self.coords[m][:, 2].long()]
                 for m in t.modalities}
 
@@ -160,6 +177,8 @@ class GraphTrainer:
             out = self._forward_backward(cap)
             if self.ddp is None:
                 self._optimizer()
+                if self.tail:
+                    self._tail()
         if self.pool is None:
             self.pool = g1.pool()
         g2 = None
@@ -167,6 +186,8 @@ class GraphTrainer:
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2, pool=self.pool, capture_error_mode=mode):
                 self._optimizer()
+                if self.tail:
+                    self._tail()
         self.graphs[key] = (g1, g2, out)
         self.stats["captures"] += 1
 
@@ -188,15 +209,22 @@ class GraphTrainer:
         the next replay)."""
         t = self.t
         sig = self.scalar_signature()
-        coords = self._stage_inputs()
         if self.disabled is not None:
-            return self.eager_step(coords)
-        counts = self.hit_counts()
+            return self.eager_step(self._stage_inputs())
+        if self.staged:
+            # pixels drawn and hits counted by the previous step's tail: wait for that count only
+            self.count_event.synchronize()
+            counts = [int(c) for c in self.count_host.tolist()]
+            coords = self.coords
+        else:
+            coords = self._stage_inputs()
+            counts = self.hit_counts()
+        self.staged = False
         stable = sig == self.last_sig
         self.last_sig = sig
         if min(counts) == 0 or not (stable and self.ran_eager):
             # a modality without hits, scalars that changed this step, or nothing run yet: one eager step
-            return self.eager_step(coords)
+            return self._eager_with_tail(coords)
         cap = bucket_capacity(counts, self.granule, self.n)
         key = (cap,) + sig
         if key not in self.graphs:
@@ -221,6 +249,17 @@ class GraphTrainer:
         if self.ddp is not None:
             self.ddp.allreduce_grads([t.fields] + ([t.poses] if t.poses is not None else []))
             g2.replay()
+        if self.tail:
+            self.count_event.record()
+            self.staged = True
         t.step += 1
         self.stats["replays"] += 1
+        return out
+
+    def _eager_with_tail(self, coords):
+        out = self.eager_step(coords)
+        if self.tail:
+            self._tail()
+            self.count_event.record()
+            self.staged = True
         return out

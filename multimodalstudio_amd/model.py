@@ -311,6 +311,19 @@ class SurfaceModel(nn.Module):
             return fx.sdf_only(pos, grid.encoding.hash_table, grid.cfg, grid.active_levels, params)
 
 
+def _render_stats(w, normals, starts, ends, R: int, S: int, sidx, rows: int, dev):
+    """[rows, 5] = (accumulation, normals, depth) of the hit rows sidx (zero elsewhere) by mms_render_stats; the depth
+    is clipped to the min / max of all sample midpoints as DepthRenderer does (renderers.py:205-214)."""
+    buf = torch.zeros(rows * 5 + 2, device=dev)
+    stats = buf[:rows * 5].view(rows, 5)
+    rng = buf[rows * 5:]
+    rng.fill_(float("-inf"))
+    with torch.no_grad():
+        _lib.call("mms_render_stats", w.data_ptr(), normals.detach().contiguous().data_ptr(), starts.data_ptr(),
+                  ends.data_ptr(), R, S, sidx.data_ptr(), stats.data_ptr(), 5, rng.data_ptr(), fx._s())
+    return stats, rng
+
+
 def nerf_encoding(x: torch.Tensor, F: int) -> torch.Tensor:
     """NeRFEncoding.forward (encodings.py:161-182), frequencies 2^0 .. 2^(F-1), input included, in torch operators
     (twice differentiable: the analytic-gradient fields differentiate through it again)."""
@@ -580,6 +593,7 @@ class BaseModel(nn.Module):
         sp = self.spec
         outputs = {}
         s_param = self.surface_model.volume_rendering.density_fn.variance_network.s
+        inv_s = 1.0 / self.surface_model.volume_rendering.density_fn.variance_network.get_inv_variance()  # once
         for mod in sp.modalities:
             r = rays[mod]
             o, d, up = r["origins"], r["directions"], r["up_directions"]
@@ -592,8 +606,7 @@ class BaseModel(nn.Module):
             else:
                 idx, sidx, count = fx.compact_padded(mask, min(int(cap), N))
             R = idx.shape[0]
-            o_h, d_h, up_h = o.index_select(0, idx), d.index_select(0, idx), up.index_select(0, idx)
-            n_h, f_h = nears.index_select(0, idx), fars.index_select(0, idx)
+            o_h, d_h, up_h, n_h, f_h = fx.HitGatherFunction.apply(idx, o, d, up, nears, fars)
             t_rand = _pad_rows(rng.uniform.get(mod), R)
             if t_rand is None and self.training:
                 t_rand = torch.rand(R, 1, device=dev)
@@ -633,22 +646,15 @@ class BaseModel(nn.Module):
                 if cap is not None:
                     bg = torch.cat([bg, bg.new_zeros(1, bg.shape[1])])
                 out[m] = fx.CompositeFunction.apply(w, vals, bg, sidx, S)[:N]
-            with torch.no_grad():
-                acc = torch.zeros(rows, 1, device=dev)
-                acc.index_copy_(0, sidx, w.sum(-1, keepdim=True))
-                nrm = torch.zeros(rows, 3, device=dev)
-                nrm.index_copy_(0, sidx, (w[..., None] * normals.view(R, S, 3)).sum(1))
-                steps = ((starts + ends) / 2).view(R, S)
-                dep = torch.zeros(rows, 1, device=dev)
-                if R > 0:
-                    dep.index_copy_(0, sidx, torch.clip((w * steps).sum(-1, keepdim=True), steps.min(), steps.max()))
-            out["normals"] = nrm[:N]
-            out["depth"] = dep[:N]
-            out["accumulation"] = acc[:N]
+            # accumulation / normals / depth renderers (renderers.py:176-242, no grad): one launch pair
+            stats, rng_buf = _render_stats(w, normals, starts, ends, R, S, sidx, rows, dev)
+            out["normals"] = stats[:N, 1:4]
+            out["depth"] = stats[:N, 4:5]
+            out["accumulation"] = stats[:N, 0:1]
             out["count"] = count
             out["gradients"] = grads.view(R, S, 3)
             out["hessians"] = hess.view(R, S, 3) if hess is not None else None
-            out["inv_s"] = 1.0 / self.surface_model.volume_rendering.density_fn.variance_network.get_inv_variance()
+            out["inv_s"] = inv_s
             out["weights"] = w
             out["bins"] = bins
             out["mask"] = mask

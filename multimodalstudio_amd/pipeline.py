@@ -43,20 +43,8 @@ class DeviceCameras:
 
 
 def exp_map_so3xr3(tangent: torch.Tensor) -> torch.Tensor:
-    """lie_groups.py:28-63 on the (1 x 6) / (C x 6) pose deltas: O(1) work, kept in PyTorch autograd."""
-    log_rot = tangent[:, 3:]
-    nrms = (log_rot * log_rot).sum(1)
-    ang = torch.clamp(nrms, 1e-4).sqrt()
-    inv = 1.0 / ang
-    fac1 = inv * ang.sin()
-    fac2 = inv * inv * (1.0 - ang.cos())
-    B = tangent.shape[0]
-    zero = torch.zeros(B, dtype=tangent.dtype, device=tangent.device)
-    wx, wy, wz = log_rot[:, 0], log_rot[:, 1], log_rot[:, 2]
-    skew = torch.stack([zero, -wz, wy, wz, zero, -wx, -wy, wx, zero], -1).view(B, 3, 3)
-    R = fac1[:, None, None] * skew + fac2[:, None, None] * torch.bmm(skew, skew) + \
-        torch.eye(3, dtype=tangent.dtype, device=tangent.device)[None]
-    return torch.cat([R, tangent[:, :3, None]], dim=-1)
+    """lie_groups.py:28-63 on the (1 x 6) / (C x 6) pose deltas: one mms_pose_exp_fwd launch (and one backward)."""
+    return fx.PoseExpFunction.apply(tangent)
 
 
 class CameraOptimizer(nn.Module):

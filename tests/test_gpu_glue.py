@@ -1,0 +1,89 @@
+"""The step's small fused kernels that replace PyTorch glue, each against the PyTorch expression it replaces:
+
+* mms_pose_exp_fwd/_bwd vs exp_map_SO3xR3 (lie_groups.py:28-63) written in torch ops (fp64), forward and gradient,
+  at zero deltas (the clamp branch), small and large rotations;
+* mms_hit_gather_fwd/_bwd vs index_select / its autograd (base_model.py:88-93), with repeated indices (padding rows);
+* mms_render_stats vs the accumulation / normals / depth renderers (renderers.py:176-242) in torch.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def exp_map_torch(t):
+    log_rot = t[:, 3:]
+    nrms = (log_rot * log_rot).sum(1)
+    ang = torch.clamp(nrms, 1e-4).sqrt()
+    inv = 1.0 / ang
+    fac1 = inv * ang.sin()
+    fac2 = inv * inv * (1.0 - ang.cos())
+    B = t.shape[0]
+    zero = torch.zeros(B, dtype=t.dtype, device=t.device)
+    wx, wy, wz = log_rot[:, 0], log_rot[:, 1], log_rot[:, 2]
+    K = torch.stack([zero, -wz, wy, wz, zero, -wx, -wy, wx, zero], -1).view(B, 3, 3)
+    R = fac1[:, None, None] * K + fac2[:, None, None] * torch.bmm(K, K) + torch.eye(3, dtype=t.dtype,
+                                                                                     device=t.device)[None]
+    return torch.cat([R, t[:, :3, None]], dim=-1)
+
+
+@pytest.mark.parametrize("scale", [0.0, 1e-3, 0.3, 2.0])
+def test_pose_exp(dev, scale):
+    from multimodalstudio_amd import functions as fx
+    g = torch.Generator().manual_seed(3)
+    t = (torch.randn(7, 6, generator=g) * scale).to(dev)
+    if scale == 0.0:
+        t[:, :3] = torch.randn(7, 3, generator=g).to(dev)      # translation only: the clamped-angle branch
+    t32 = t.clone().requires_grad_(True)
+    m = fx.PoseExpFunction.apply(t32)
+    t64 = t.double().requires_grad_(True)
+    ref = exp_map_torch(t64)
+    assert (m.double() - ref).abs().max().item() < 1e-6
+    gm = torch.randn(7, 3, 4, generator=g).to(dev)
+    m.backward(gm)
+    ref.backward(gm.double())
+    err = (t32.grad.double() - t64.grad).abs().max().item()
+    assert err < 1e-5 * max(1.0, t64.grad.abs().max().item()), err
+
+
+def test_hit_gather(dev):
+    from multimodalstudio_amd import functions as fx
+    g = torch.Generator().manual_seed(5)
+    N = 1000
+    o, d, u = [torch.randn(N, 3, generator=g).to(dev).requires_grad_(True) for _ in range(3)]
+    n, f = [torch.rand(N, generator=g).to(dev).requires_grad_(True) for _ in range(2)]
+    idx = torch.randperm(N, generator=g)[:600]
+    idx = torch.cat([idx, idx[:1].repeat(40)]).to(dev)           # padding rows repeat the first hit
+    outs = fx.HitGatherFunction.apply(idx, o, d, u, n, f)
+    refs = [t.index_select(0, idx) for t in (o, d, u, n, f)]
+    for a, b in zip(outs, refs):
+        assert torch.equal(a, b)
+    gs = [torch.randn_like(a) for a in outs]
+    got = torch.autograd.grad(outs, (o, d, u, n, f), gs)
+    want = torch.autograd.grad(refs, (o, d, u, n, f), gs)
+    for a, b in zip(got, want):
+        assert (a - b).abs().max().item() < 1e-5
+
+
+def test_render_stats(dev):
+    from multimodalstudio_amd.model import _render_stats
+    g = torch.Generator().manual_seed(7)
+    R, S, N = 300, 64, 512
+    w = torch.rand(R, S, generator=g) / S
+    w[:20] *= 1e-3                                                # nearly empty rays: depth below every midpoint
+    w = w.to(dev)
+    nrm = torch.nn.functional.normalize(torch.randn(R * S, 3, generator=g), dim=-1).to(dev)
+    starts = (torch.rand(R * S, generator=g) * 2 + 0.1).to(dev)
+    ends = starts + torch.rand(R * S, generator=g).to(dev) * 0.05
+    sidx = torch.randperm(N, generator=g)[:R].to(dev)
+    stats, _ = _render_stats(w, nrm, starts, ends, R, S, sidx, N, dev)
+    acc = torch.zeros(N, 1, device=dev).index_copy_(0, sidx, w.sum(-1, keepdim=True))
+    nn_ = torch.zeros(N, 3, device=dev).index_copy_(0, sidx, (w[..., None] * nrm.view(R, S, 3)).sum(1))
+    steps = ((starts + ends) / 2).view(R, S)
+    dep = torch.zeros(N, 1, device=dev).index_copy_(
+        0, sidx, torch.clip((w * steps).sum(-1, keepdim=True), steps.min(), steps.max()))
+    assert (stats[:, 0:1] - acc).abs().max().item() < 1e-5
+    assert (stats[:, 1:4] - nn_).abs().max().item() < 1e-5
+    assert (stats[:, 4:5] - dep).abs().max().item() < 1e-5
+    # the lower clip is active for rays with little accumulated weight
+    assert (dep[sidx] == steps.min()).any()
