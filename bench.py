@@ -63,26 +63,30 @@ def gemm_work(a):
 
 def chain_work(a):
     """(precision label, (algorithmic flops, algorithmic HBM bytes)) of one mms_mlp_chain launch (include/mms_hip.h
-    argument order): the three layers' 2MNK, narrowed on the SDF tap rows (rows >= rows_full: one output column of
-    the last forward layer, one input column of the first backward layer); bytes = input rows + the stores each
-    layer makes (+ the forward outputs the backward reads for its activation derivatives)."""
+    argument order): every layer's 2MNK, narrowed on the SDF tap rows (rows >= rows_full: one output column of the
+    last forward layer, one input column of the first backward layer); bytes = input rows + the stores each layer
+    makes (+ the forward outputs the backward reads for its activation derivatives)."""
     import ctypes
-    prec, bwd, K0, M, rf = a[0], a[1], a[4], a[5], a[6]
+    prec, bwd, nl, K0, M, rf = a[0], a[1], a[2], a[5], a[6], a[7]
     rf = M if rf < 0 else min(rf, M)
-    N = ctypes.cast(a[19], ctypes.POINTER(ctypes.c_int))
-    outs = ctypes.cast(a[17], ctypes.POINTER(ctypes.c_void_p))
-    n0, n1, n2 = N[0], N[1], N[2]
-    st = [outs[i] is not None for i in range(3)]
+    Np = ctypes.cast(a[20], ctypes.POINTER(ctypes.c_int))
+    outs = ctypes.cast(a[18], ctypes.POINTER(ctypes.c_void_p))
+    n = [Np[i] for i in range(nl)]
+    st = [outs[i] is not None for i in range(nl)]
+    mid = sum(n[l - 1] * n[l] for l in range(1, nl - 1))
     if bwd:
-        flops = 2.0 * (rf * K0 + (M - rf)) * n0 + 2.0 * M * (n0 * n1 + n1 * n2)
-        nbytes = 4.0 * ((rf * K0 + (M - rf)) + M * (n0 * st[0] + n1 * st[1] + n2 * st[2]) + M * (n0 + n1))
+        flops = 2.0 * (rf * K0 + (M - rf)) * n[0] + 2.0 * M * (mid + n[nl - 2] * n[nl - 1])
+        nbytes = 4.0 * ((rf * K0 + (M - rf)) + M * sum(n[l] * st[l] for l in range(nl)) + M * sum(n[:nl - 1]))
     else:
-        flops = 2.0 * M * (K0 * n0 + n0 * n1) + 2.0 * (rf * n2 + (M - rf)) * n1
-        nbytes = 4.0 * (M * K0 + M * (n0 * st[0] + n1 * st[1]) + (rf * n2 + (M - rf)) * st[2])
-    # which MLP: the SDF field (71 input columns; its backward's last layer has 71 outputs) or the radiance field;
-    # rows_full = 0 marks the sampler's inference-only SDF evaluations
-    narrow_in = (N[2] if bwd else K0) < 128
-    role = ("sdf" if narrow_in else "radiance") + ("_infer" if (not bwd and rf == 0) else "")
+        flops = 2.0 * M * (K0 * n[0] + mid) + 2.0 * (rf * n[nl - 1] + (M - rf)) * n[nl - 2]
+        nbytes = 4.0 * (M * K0 + M * sum(n[l] * st[l] for l in range(nl - 1)) + (rf * n[nl - 1] + (M - rf)) * st[nl - 1])
+    # which MLP: the SDF field (71 input columns; its backward's last layer has 71 outputs), the radiance field, or
+    # the background NeRF's base / head (4 layers); rows_full = 0 marks the sampler's inference-only SDF evaluations
+    width = n[nl - 1] if bwd else K0
+    if nl == 4:
+        role = "bg_base" if width < 64 else "bg_head"
+    else:
+        role = ("sdf" if width < 128 else "radiance") + ("_infer" if (not bwd and rf == 0) else "")
     return f"{PREC_NAMES[prec]}:{role}{'_bwd' if bwd else '_fwd'}", (flops, nbytes)
 
 

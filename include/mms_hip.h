@@ -50,30 +50,32 @@ int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group, int64_t gs
  * prec 0 = exact fp32 MFMA, 1 = bf16 MFMA (fp32 accumulate), 2 = split bf16x3 (near-fp32 operands).
  * Epilogue: v = acc + bias[n]; Z[m,n] = v (optional); v = act(v); v *= dact'(aux[m,n]) (optional);
  * C = v or C += v (accumulate; atomic when splits > 1).  act/dact: 0 none, 1 ReLU, 2 Softplus(beta,thr),
- * 3 Sigmoid.  ones_col >= 0 also writes 1.0 at column ones_col of every output row. */
+ * 3 Sigmoid; dact 4 = Sigmoid' from the forward OUTPUT (aux = y; ReLU' is the same from y, id 1).  ones_col >= 0 also writes 1.0 at column ones_col of every output row. */
 int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
              const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, float* Z, int64_t ldz,
              const float* aux, int64_t ldaux, int act, int dact, float beta, float thr, int accumulate, int splits,
              int ones_col, float* colsum, void* stream);
 
-/* ---- fused MLP chains (MLP.forward mlp.py:152-171 under weight norm :206-209, three layers per launch) for the
- * SDF field (71-256-256-257, Softplus(100), surface_field.py:99-116) and the radiance field (317-256-256-256,
- * ReLU, radiance_field.py:72-77).  Layers are computed transposed so each layer's MFMA accumulator feeds the
- * next layer from registers.  prec 1 = bf16, 2 = split bf16x3 operands (fp32 accumulate).
- * Forward (backward = 0): out[l] = act_l(X_l W_l^T + b_l) for the 3 layers (out[0], out[1] may be NULL);
- *   rows >= rows_full compute / store only output column 0 of the last layer (the SDF taps), in fp32 from
+/* ---- fused MLP chains (MLP.forward mlp.py:152-171 under weight norm :206-209, all layers in one launch) for the
+ * SDF field (71-256-256-257, Softplus(100), surface_field.py:99-116), the radiance field (317-256-256-256, ReLU,
+ * radiance_field.py:72-77) and the background NeRF (n_layers = 4: base 39-256-256-256-256 and head
+ * 283-256-256-256-128, ReLU, nerf_field.py:92-105).  Layers are computed transposed so each layer's MFMA
+ * accumulator feeds the next layer from registers.  prec 1 = bf16, 2 = split bf16x3 operands (fp32 accumulate).
+ * Per-layer arrays (a_hi, a_lo, bias, aux, ldaux, out, ldo, N, act) have n_layers entries.
+ * Forward (backward = 0): out[l] = act_l(X_l W_l^T + b_l) (the hidden outs are stored together or, 3 layers, not at
+ *   all); rows >= rows_full compute / store only output column 0 of the last layer (the SDF taps), in fp32 from
  *   w2row0 = the last layer's fp32 weight row 0 (required when rows_full < M).  With rows_full = 0 the last
  *   layer's out may have any pitch >= 1 (e.g. a dense [M] sdf vector).
  * Backward-data (backward = 1): X = dY of the last forward layer (rows >= rows_full: column 0 only), optionally
  *   scaled by act'(xaux) (stored to xout); out[l] = (prev . W^T) * act_l'(aux[l]) with act' evaluated from the
- *   forward output aux[l] (NULL: no scaling); out[2] = dX.
- * a_hi / a_lo: per-layer packed weights from mms_mlp_pack (bf16, 32 ceil(N/32) x 16 ceil(K/16)); layers 1, 2 are
+ *   forward output aux[l] (NULL: no scaling); the last out = dX.
+ * a_hi / a_lo: per-layer packed weights from mms_mlp_pack (bf16, 32 ceil(N/32) x 16 ceil(K/16)); layers >= 1 are
  * register-fed and must be packed with permute = 1.  All row pitches multiples of 4 floats, 16-B aligned. */
-int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx, int K0, int64_t M, int64_t rows_full,
-                  const float* xaux, int64_t ldxaux, int xact, float* xout, int64_t ldxout, const void* const* a_hi,
-                  const void* const* a_lo, const float* const* bias, const float* const* aux, const int64_t* ldaux,
-                  float* const* out, const int64_t* ldo, const int* N, const int* act, float beta, float thr,
-                  const float* w2row0, void* stream);
+int mms_mlp_chain(int prec, int backward, int n_layers, const float* X, int64_t ldx, int K0, int64_t M,
+                  int64_t rows_full, const float* xaux, int64_t ldxaux, int xact, float* xout, int64_t ldxout,
+                  const void* const* a_hi, const void* const* a_lo, const float* const* bias, const float* const* aux,
+                  const int64_t* ldaux, float* const* out, const int64_t* ldo, const int* N, const int* act,
+                  float beta, float thr, const float* w2row0, void* stream);
 /* bf16 (hi, and lo = residual if non-NULL) image of W [N, K] (ldw) as an MFMA A operand of rows x cols:
  * transpose = 0 -> A = W, 1 -> A = W^T; permute = 1 stores each 16-column step in register-fed order
  * (columns 0-3, 8-11, 4-7, 12-15).  Zero padded; rows % 32 == 0, cols % 16 == 0.  Fragment-major: the 32x16
@@ -88,7 +90,7 @@ int mms_weight_norm_bwd(const float* g, const float* v, const float* norms, int6
                         int64_t lddw, float* dg, float* dv, void* stream);
 /* bias gradient: out[n] += sum_m A[m, n] */
 int mms_colsum(const float* A, int64_t M, int64_t N, int64_t lda, float* out, void* stream);
-/* dZ = dY * act'(Z) */
+/* dZ = dY * act'(Z)  (act 4: Sigmoid' from the output, Z = y) */
 int mms_act_bwd(const float* dY, int64_t ldy, const float* Z, int64_t ldz, int64_t M, int64_t N, int act,
                 float beta, float thr, float* dZ, int64_t lddz, void* stream);
 
@@ -257,6 +259,13 @@ int mms_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, const
 int mms_pixel_sample(uint64_t seed, uint32_t stream_id, uint64_t* counter, int64_t n, int n_frames, int H, int W,
                      const int32_t* frame_ids, const float* images, int C, int32_t* coords, int64_t* sel,
                      float* values, void* stream);
+/* Training-mode uniform draws of the model's forward (the NeuS jitter, PDF and background draws that the reference
+ * takes from torch.rand, ray_samplers.py:183-296 / :357-403): out[i] ~ U[0, 1) (24-bit), Philox4x32-10 keyed by
+ * seed at counter *counter + offset + i / 4 in stream stream_id (the device counter is read, not advanced:
+ * mms_counter_advance moves it once per step, in a captured graph too). */
+int mms_uniform(uint64_t seed, uint32_t stream_id, const uint64_t* counter, int64_t offset, int64_t n, float* out,
+                void* stream);
+int mms_counter_advance(uint64_t* counter, int64_t n, void* stream);
 
 /* ---- iso-surface of a dense SDF grid (mesh export: MeshExtractor.extract, evaluator_components/mesh_extractors.py:63;
  * utils/marching_cubes.py:35).  values [nx * ny * nz] x-major; cells split into 6 tetrahedra (marching tetrahedra).

@@ -118,7 +118,9 @@ __device__ __forceinline__ float torch_cpu_row_sum(const float* x, int n) {
   return fin;
 }
 
-// MLP activations for GEMM epilogues (ids: 0 none, 1 ReLU, 2 Softplus(beta, threshold), 3 Sigmoid).
+// MLP activations for GEMM epilogues (ids: 0 none, 1 ReLU, 2 Softplus(beta, threshold), 3 Sigmoid; derivative-only
+// id 4: Sigmoid' evaluated from the forward OUTPUT, so the forward stores no pre-activation -- ReLU' is the same from
+// either side, id 1).
 // Built on the hardware transcendentals (v_exp_f32 = 2^x, v_log_f32 = log2, v_rcp_f32; ~1 ulp): the
 // accurate libm log1pf/expf forms cost ~150 VALU ops per element, which made the epilogue of a 270k x 256
 // layer compute-bound (~250 us).  Softplus(x) = ln2 * log2(1 + 2^(beta x log2 e)) / beta, exact to ~1e-7
@@ -152,6 +154,7 @@ __device__ __forceinline__ float act_grad_exact(int act, float z, float beta, fl
     case 1: return z > 0.f ? 1.f : 0.f;
     case 2: { const float bx = z * beta; if (bx > thr) return 1.f; const float e = expf(bx); return e / (e + 1.0f); }
     case 3: { const float s = 1.0f / (1.0f + expf(-z)); return s * (1.0f - s); }
+    case 4: return z * (1.0f - z);  // Sigmoid' from the layer OUTPUT y (torch's sigmoid_backward form)
     default: return 1.f;
   }
 }
@@ -169,6 +172,7 @@ __device__ __forceinline__ float act_grad_fast(int act, float z, float beta, flo
       const float s = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-z * 1.4426950408889634f));
       return s * (1.0f - s);
     }
+    case 4: return z * (1.0f - z);  // Sigmoid' from the layer OUTPUT y
     default: return 1.f;
   }
 }

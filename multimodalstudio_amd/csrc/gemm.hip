@@ -401,7 +401,7 @@ MMS_EXPORT int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N
   MMS_REQUIRE(colsum == nullptr || trans_a, fn, "the fused column sum needs a transposed (T-source) A");
   MMS_REQUIRE(prec >= 0 && prec <= 2, fn, "prec must be 0 (f32), 1 (bf16) or 2 (bf16x3)");
   MMS_REQUIRE(M >= 0 && N >= 0 && K >= 0, fn, "negative size");
-  MMS_REQUIRE(act >= 0 && act <= 3 && dact >= 0 && dact <= 3, fn, "bad activation id");
+  MMS_REQUIRE(act >= 0 && act <= 3 && dact >= 0 && dact <= 4, fn, "bad activation id");
   if (M == 0 || N == 0) return 0;
   MMS_REQUIRE(A && B && C, fn, "null operand");
   if (splits < 1) splits = 1;

@@ -120,7 +120,7 @@ MMS_EXPORT int mms_colsum(const float* A, int64_t M, int64_t N, int64_t lda, flo
 MMS_EXPORT int mms_act_bwd(const float* dY, int64_t ldy, const float* Z, int64_t ldz, int64_t M, int64_t N, int act,
                            float beta, float thr, float* dZ, int64_t lddz, void* stream) {
   const char* fn = "mms_act_bwd";
-  MMS_REQUIRE(act >= 0 && act <= 3, fn, "bad activation");
+  MMS_REQUIRE(act >= 0 && act <= 4, fn, "bad activation");
   if (M == 0 || N == 0) return 0;
   hipLaunchKernelGGL(act_bwd_kernel, dim3(mms::grid_for(M * N, 256, 8192)), dim3(256), 0, mms::as_stream(stream), dY,
                      ldy, Z, ldz, M, N, act, beta, thr, dZ, lddz);

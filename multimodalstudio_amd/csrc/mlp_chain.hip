@@ -61,8 +61,8 @@ struct ChainArgs {
   float* xout;         // backward: store of the scaled input (dZ of the last forward layer), or null
   int64_t ldxout;
   float beta, thr;     // Softplus(beta, threshold)
-  const float* w2row0; // forward: fp32 row 0 of the last layer's weight ([N1]) for the single-output row blocks
-  ChainLayer L[3];
+  const float* w2row0; // forward: fp32 row 0 of the last layer's weight for the single-output row blocks
+  ChainLayer L[4];     // 3 or 4 layers (kernel template NL)
 };
 
 // activation derivative from the forward OUTPUT y (compile-time activation: branch-free epilogues)
@@ -392,13 +392,15 @@ __device__ __forceinline__ void to_b(const floatx16 (&acc)[NT], bf16x8 (&bh)[2 *
 // backward's input scaling).  The forward's epilogue of layer l is LAZY: tile t is finished (bias, activation,
 // store, bf16 split) inside layer l + 1's k-step 2 t, right before the MFMAs that consume it, so its VALU and
 // transcendental work issues between the previous k-step's MFMAs (one wave per SIMD: nothing else hides it).
-template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, int XA, bool KEEP>
+// NL = 4: a middle register-fed layer of NT1 tiles with activation A1 sits between layer 1 and the last layer (the
+// background NeRF MLPs, 4 layers).  Backward: the same structure on the transposed weights, last layer first.
+template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, int XA, bool KEEP, int NL>
 __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   __shared__ __attribute__((aligned(1024))) bf16x8 ring[kRing][kSlot][64];
   // layer-0 input slices (and, backward radiance chain, the xaux slices): [slot][wave][2 x 64 lane chunks]
   __shared__ __attribute__((aligned(1024))) f32x4 xring[kRing][4][128];
   __shared__ __attribute__((aligned(1024))) f32x4 aring[(BWD && XA != 0) ? kRing : 1][4][128];
-  __shared__ __attribute__((aligned(16))) float sbias[3][32 * kMaxTiles];  // forward biases, zero padded
+  __shared__ __attribute__((aligned(16))) float sbias[NL][32 * kMaxTiles];  // forward biases, zero padded
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar staging addresses
   const int r = lane & 31, h = lane >> 5;
@@ -409,7 +411,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   const int64_t m = m0 + r;
   const bool mval = m < a.M;
   const int64_t mc = mval ? m : a.M - 1;
-  const bool rowfull = m < a.rows_full;
+  // clamped rows past M replicate row M - 1 exactly (their stores land on it): the tap-row test uses the clamped row
+  const bool rowfull = mc < a.rows_full;
   const bool anyfull = m0 < a.rows_full;   // wave-uniform
   const bool blockfull = mb < a.rows_full;  // block-uniform
   const floatx16 zero = {};
@@ -420,7 +423,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   float* scr = &sscr[kStage ? wave : 0][0];
   if constexpr (!BWD) {
 #pragma unroll
-    for (int l = 0; l < 3; ++l)
+    for (int l = 0; l < NL; ++l)
       for (int i = threadIdx.x; i < 32 * kMaxTiles; i += 256)
         sbias[l][i] = (a.L[l].bias != nullptr && i < a.L[l].N) ? a.L[l].bias[i] : 0.f;
     for (int i = threadIdx.x; i < 32 * NT1; i += 256) sw0[i] = (a.w2row0 != nullptr && i < a.L[1].N) ? a.w2row0[i] : 0.f;
@@ -515,30 +518,31 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
       bh = b1h[s]; bl = b1l[s];
     });
   }
-  bf16x8 b2h[2 * NT1], b2l[2 * NT1];
-  if constexpr (BWD) {
-    epilogue_bwd_staged<NT1, A1>(acc1, a.L[1], m0, a.M, scr, lane, a.beta, a.thr);
-    to_b<PREC, NT1>(acc1, b2h, b2l);
-  }
-
-  // ---- layer 2 (forward: SDF tap rows need only the sdf column tile; a block of tap rows stages only that tile)
-  floatx16 acc2[NT2];
+  // ---- the last layer (index LL = NL - 1), fed by the registers of layer LP = LL - 1 (NT1 tiles, activation A1).
+  // Forward: SDF tap rows need only the sdf column tile; a block of tap rows stages only that tile.
+  auto last_layer = [&](floatx16 (&accp)[NT1], auto lpc) {
+    constexpr int LP = decltype(lpc)::value, LL = LP + 1;
+    bf16x8 b2h[2 * NT1], b2l[2 * NT1];
+    if constexpr (BWD) {
+      epilogue_bwd_staged<NT1, A1>(accp, a.L[LP], m0, a.M, scr, lane, a.beta, a.thr);
+      to_b<PREC, NT1>(accp, b2h, b2l);
+    }
+    floatx16 acc2[NT2];
 #pragma unroll
-  for (int t = 0; t < NT2; ++t) acc2[t] = zero;
-  const int nt2 = (!BWD && !anyfull) ? 1 : NT2;
-  {
+    for (int t = 0; t < NT2; ++t) acc2[t] = zero;
+    const int nt2 = (!BWD && !anyfull) ? 1 : NT2;
     auto get_b2 = [&](int s, bf16x8& bh, bf16x8& bl) {
       if constexpr (!BWD) {
         if ((s & 1) == 0) {
-          epi_tile_full<A1, KEEP>(acc1[s >> 1], s >> 1, sbias[1], a.L[1].out, a.L[1].ldo, m0, a.M, scr, lane, a.beta,
-                                  a.thr);
-          tile_to_b<PREC>(acc1[s >> 1], &b2h[s], &b2l[s]);
+          epi_tile_full<A1, KEEP>(accp[s >> 1], s >> 1, sbias[LP], a.L[LP].out, a.L[LP].ldo, m0, a.M, scr, lane,
+                                  a.beta, a.thr);
+          tile_to_b<PREC>(accp[s >> 1], &b2h[s], &b2l[s]);
         }
       }
       bh = b2h[s]; bl = b2l[s];
     };
     if (BWD || blockfull) {
-      run_layer<PREC, NT2, NT2, 2 * NT1, 0, kGE, 0>(a.L[2], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2);
+      run_layer<PREC, NT2, NT2, 2 * NT1, 0, kGE, 0>(a.L[LL], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2);
     } else {
       // a block of SDF tap rows (or the sampler's inference rows) needs only output 0 of the last layer: a 256-long
       // dot product per row, done in fp32 on the VALU (W row 0 from LDS) instead of 2 NT1 ring k-steps of one
@@ -546,60 +550,118 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
       float p = 0.f;
 #pragma unroll
       for (int t = 0; t < NT1; ++t) {
-        epi_tile_full<A1, KEEP>(acc1[t], t, sbias[1], a.L[1].out, a.L[1].ldo, m0, a.M, scr, lane, a.beta, a.thr);
+        epi_tile_full<A1, KEEP>(accp[t], t, sbias[LP], a.L[LP].out, a.L[LP].ldo, m0, a.M, scr, lane, a.beta, a.thr);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const f32x4 w = *reinterpret_cast<const f32x4*>(sw0 + 32 * t + 8 * g + 4 * h);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) p = __builtin_fmaf(acc1[t][4 * g + i], w[i], p);
+          for (int i = 0; i < 4; ++i) p = __builtin_fmaf(accp[t][4 * g + i], w[i], p);
         }
       }
       p += __shfl_xor(p, 32);   // the two halves of the row's units (lanes r and r + 32)
-      if (mval && h == 0 && a.L[2].out != nullptr) __builtin_nontemporal_store(p + sbias[2][0], a.L[2].out + m * a.L[2].ldo);
+      if (mval && h == 0 && a.L[LL].out != nullptr)
+        __builtin_nontemporal_store(p + sbias[LL][0], a.L[LL].out + m * a.L[LL].ldo);
       return;
     }
+    epilogue<NT2, BWD, A2>(acc2, a.L[LL], sbias[LL], nt2, m, mc, mval, !BWD && !rowfull, h, a.beta, a.thr);
+  };
+
+  if constexpr (NL == 4) {
+    // ---- middle layer 2: B operand from layer 1's registers (same width and activation as layer 1)
+    bf16x8 bmh[2 * NT1], bml[2 * NT1];
+    if constexpr (BWD) {
+      epilogue_bwd_staged<NT1, A1>(acc1, a.L[1], m0, a.M, scr, lane, a.beta, a.thr);
+      to_b<PREC, NT1>(acc1, bmh, bml);
+    }
+    floatx16 accm[NT1];
+#pragma unroll
+    for (int t = 0; t < NT1; ++t) accm[t] = zero;
+    run_layer<PREC, NT1, NT1, 2 * NT1, 0, kGE, 0>(a.L[2], 2 * NT1, NT1, accm, wave, lane, ring, nopre,
+                                                  [&](int s, bf16x8& bh, bf16x8& bl) {
+      if constexpr (!BWD) {
+        if ((s & 1) == 0) {
+          epi_tile_full<A1, KEEP>(acc1[s >> 1], s >> 1, sbias[1], a.L[1].out, a.L[1].ldo, m0, a.M, scr, lane, a.beta,
+                                  a.thr);
+          tile_to_b<PREC>(acc1[s >> 1], &bmh[s], &bml[s]);
+        }
+      }
+      bh = bmh[s]; bl = bml[s];
+    });
+    last_layer(accm, std::integral_constant<int, 2>{});
+  } else {
+    last_layer(acc1, std::integral_constant<int, 1>{});
   }
-  epilogue<NT2, BWD, A2>(acc2, a.L[2], sbias[2], nt2, m, mc, mval, !BWD && !rowfull, h, a.beta, a.thr);
 }
 
-template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, int XA, bool KEEP = false>
+template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, int XA, bool KEEP = false,
+          int NL = 3>
 void launch_chain(const ChainArgs& a, hipStream_t s) {
   const unsigned blocks = (unsigned)((a.M + 127) / 128);
-  hipLaunchKernelGGL((chain_kernel<PREC, KS0, NT0, NT1, NT2, BWD, A0, A1, A2, XA, KEEP>), dim3(blocks), dim3(256), 0, s,
-                     a);
+  hipLaunchKernelGGL((chain_kernel<PREC, KS0, NT0, NT1, NT2, BWD, A0, A1, A2, XA, KEEP, NL>), dim3(blocks), dim3(256), 0,
+                     s, a);
 }
 
-// the chains of the SDF and radiance fields (ks0 = ceil(K0 / 16), nt_l = ceil(N_l / 32)) with their activations:
-// SDF Softplus(100), Softplus(100), identity; radiance ReLU x 3 (backward: derivative ids of layers 1, 0 and none,
-// the input scaled by the last ReLU's derivative).  Forward: both hidden layers full (256 units) and stored
-// together (keep) or neither.
+// The served chains (ks0 = ceil(K0 / 16), nt_l = ceil(N_l / 32)) with their activations:
+//   3 layers: SDF Softplus(100), Softplus(100), identity; radiance ReLU x 3 (backward: derivative ids of layers 1, 0
+//             and none, the input scaled by the last ReLU's derivative).  Forward: both hidden layers full (256
+//             units) and stored together (keep) or neither.
+//   4 layers: the background NeRF base 39-256-256-256-256 and head 283-256-256-256-128 MLPs, ReLU throughout
+//             (nerf_field.py:92-105), hidden layers stored.
 template <int PREC>
-bool dispatch_chain(int ks0, int nt0, int nt1, int nt2, bool bwd, const ChainArgs& a, hipStream_t s) {
-  const int a0 = a.L[0].act, a1 = a.L[1].act, a2 = a.L[2].act;
+bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a, hipStream_t s) {
+  const int a0 = a.L[0].act, a1 = a.L[1].act, a2 = a.L[2].act, a3 = nl == 4 ? a.L[3].act : -1;
   const bool noxa = a.xaux == nullptr;
-  const bool hidden_full = a.L[0].N == 256 && a.L[1].N == 256;
-  // backward: both hidden layers' dZ are stored and scaled by act'(Y) (the staged epilogue assumes both)
-  const bool bwd_hidden = a.L[0].aux != nullptr && a.L[1].aux != nullptr && a.L[0].out != nullptr &&
-                          a.L[1].out != nullptr && hidden_full;
-  const bool keep = a.L[0].out != nullptr && a.L[1].out != nullptr;
-  const bool nokeep = a.L[0].out == nullptr && a.L[1].out == nullptr;
-  if (!bwd && ks0 == 5 && nt0 == 8 && nt1 == 8 && nt2 == 9 && a0 == 2 && a1 == 2 && a2 == 0 && hidden_full &&
-      (keep || nokeep)) {
-    if (keep) launch_chain<PREC, 5, 8, 8, 9, false, 2, 2, 0, 0, true>(a, s);
-    else launch_chain<PREC, 5, 8, 8, 9, false, 2, 2, 0, 0, false>(a, s);
-  } else if (!bwd && ks0 == 20 && nt0 == 8 && nt1 == 8 && nt2 == 8 && a0 == 1 && a1 == 1 && a2 == 1 &&
-             hidden_full && keep) {
-    launch_chain<PREC, 20, 8, 8, 8, false, 1, 1, 1, 0, true>(a, s);
-  } else if (bwd && ks0 == 17 && nt0 == 8 && nt1 == 8 && nt2 == 3 && a0 == 2 && a1 == 2 && a2 == 0 && noxa &&
-             a.xout == nullptr && bwd_hidden) {
-    launch_chain<PREC, 17, 8, 8, 3, true, 2, 2, 0, 0>(a, s);
-  } else if (bwd && ks0 == 16 && nt0 == 8 && nt1 == 8 && nt2 == 10 && a0 == 1 && a1 == 1 && a2 == 0 && !noxa &&
-             a.xact == 1 && a.xout != nullptr && a.K0 % 8 == 0 && bwd_hidden) {
-    launch_chain<PREC, 16, 8, 8, 10, true, 1, 1, 0, 1>(a, s);
-  } else {
+  const int nh = nl - 1;  // hidden (stored) layers
+  bool hidden_full = true, keep = true, nokeep = true, bwd_hidden = true;
+  for (int l = 0; l < nh; ++l) {
+    hidden_full = hidden_full && a.L[l].N == 256;
+    keep = keep && a.L[l].out != nullptr;
+    nokeep = nokeep && a.L[l].out == nullptr;
+    // backward: every hidden layer's dZ is stored and scaled by act'(Y) (the staged epilogue assumes all)
+    bwd_hidden = bwd_hidden && a.L[l].aux != nullptr && a.L[l].out != nullptr;
+  }
+  bwd_hidden = bwd_hidden && hidden_full;
+  const bool xio = !noxa && a.xact == 1 && a.xout != nullptr && a.K0 % 8 == 0;
+  if (nl == 3) {
+    if (!bwd && ks0 == 5 && nt[0] == 8 && nt[1] == 8 && nt[2] == 9 && a0 == 2 && a1 == 2 && a2 == 0 && hidden_full &&
+        (keep || nokeep)) {
+      if (keep) launch_chain<PREC, 5, 8, 8, 9, false, 2, 2, 0, 0, true>(a, s);
+      else launch_chain<PREC, 5, 8, 8, 9, false, 2, 2, 0, 0, false>(a, s);
+      return true;
+    }
+    if (!bwd && ks0 == 20 && nt[0] == 8 && nt[1] == 8 && nt[2] == 8 && a0 == 1 && a1 == 1 && a2 == 1 &&
+        hidden_full && keep) {
+      launch_chain<PREC, 20, 8, 8, 8, false, 1, 1, 1, 0, true>(a, s);
+      return true;
+    }
+    if (bwd && ks0 == 17 && nt[0] == 8 && nt[1] == 8 && nt[2] == 3 && a0 == 2 && a1 == 2 && a2 == 0 && noxa &&
+        a.xout == nullptr && bwd_hidden) {
+      launch_chain<PREC, 17, 8, 8, 3, true, 2, 2, 0, 0>(a, s);
+      return true;
+    }
+    if (bwd && ks0 == 16 && nt[0] == 8 && nt[1] == 8 && nt[2] == 10 && a0 == 1 && a1 == 1 && a2 == 0 && xio &&
+        bwd_hidden) {
+      launch_chain<PREC, 16, 8, 8, 10, true, 1, 1, 0, 1>(a, s);
+      return true;
+    }
     return false;
   }
-  return true;
+  // 4-layer chains: the background MLPs, bf16 operands only (the background's precision in every preset but bf16x3)
+  if constexpr (PREC == 1) {
+    if (nl != 4 || nt[0] != 8 || nt[1] != 8 || nt[2] != 8 || a0 != 1 || a1 != 1 || a2 != 1) return false;
+    if (!bwd && hidden_full && keep && a3 == 1) {
+      // base 39-256x4 (NeRF background), head 283-256-256-256-128 (NeRF) / -256 (config-5 grid background)
+      if (ks0 == 3 && nt[3] == 8) { launch_chain<PREC, 3, 8, 8, 8, false, 1, 1, 1, 0, true, 4>(a, s); return true; }
+      if (ks0 == 18 && nt[3] == 4) { launch_chain<PREC, 18, 8, 8, 4, false, 1, 1, 1, 0, true, 4>(a, s); return true; }
+      if (ks0 == 18 && nt[3] == 8) { launch_chain<PREC, 18, 8, 8, 8, false, 1, 1, 1, 0, true, 4>(a, s); return true; }
+    }
+    if (bwd && a3 == 0 && xio && bwd_hidden) {
+      if (ks0 == 16 && nt[3] == 2) { launch_chain<PREC, 16, 8, 8, 2, true, 1, 1, 0, 1, false, 4>(a, s); return true; }
+      if (ks0 == 8 && nt[3] == 9) { launch_chain<PREC, 8, 8, 8, 9, true, 1, 1, 0, 1, false, 4>(a, s); return true; }
+      if (ks0 == 16 && nt[3] == 9) { launch_chain<PREC, 16, 8, 8, 9, true, 1, 1, 0, 1, false, 4>(a, s); return true; }
+    }
+  }
+  return false;
 }
 
 // perm(q): swap bits 2 and 3 of the in-step column (units 0-3, 8-11, 4-7, 12-15 of a register-fed k-step)
@@ -644,7 +706,7 @@ MMS_EXPORT int mms_mlp_pack(const float* W, int64_t N, int64_t K, int64_t ldw, i
   return mms::check_launch(fn);
 }
 
-MMS_EXPORT int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx, int K0, int64_t M,
+MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* X, int64_t ldx, int K0, int64_t M,
                              int64_t rows_full, const float* xaux, int64_t ldxaux, int xact, float* xout,
                              int64_t ldxout, const void* const* a_hi, const void* const* a_lo,
                              const float* const* bias, const float* const* aux, const int64_t* ldaux,
@@ -652,6 +714,7 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx
                              float thr, const float* w2row0, void* stream) {
   const char* fn = "mms_mlp_chain";
   MMS_REQUIRE(prec == 1 || prec == 2, fn, "prec must be 1 (bf16) or 2 (split bf16x3)");
+  MMS_REQUIRE(n_layers == 3 || n_layers == 4, fn, "chains of 3 or 4 layers");
   MMS_REQUIRE(M >= 0 && K0 > 0, fn, "bad shape");
   if (M == 0) return 0;
   MMS_REQUIRE(X && a_hi && N && act && out && ldo, fn, "null pointer");
@@ -665,8 +728,10 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx
   a.w2row0 = backward ? nullptr : w2row0;
   MMS_REQUIRE(backward || rows_full >= M || w2row0 != nullptr, fn,
               "forward with single-output rows (rows_full < M) needs the last layer's fp32 weight row 0");
-  int nt[3];
-  for (int l = 0; l < 3; ++l) {
+  MMS_REQUIRE(n_layers == 3 || rows_full < 0 || rows_full >= M, fn, "single-output rows are a 3-layer (SDF) feature");
+  int nt[4] = {0, 0, 0, 0};
+  for (int l = 0; l < 4; ++l) a.L[l] = ChainLayer{};
+  for (int l = 0; l < n_layers; ++l) {
     MMS_REQUIRE(a_hi[l] != nullptr && N[l] > 0, fn, "missing layer weights");
     MMS_REQUIRE(prec == 1 || (a_lo && a_lo[l] != nullptr), fn, "split bf16x3 needs the residual images");
     MMS_REQUIRE(act[l] >= 0 && act[l] <= 3, fn, "bad activation id");
@@ -681,7 +746,7 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx
     L.ldo = ldo[l];
     // a forward whose rows all take the single-output path (rows_full = 0, the sampler's SDF queries) stores only
     // column 0 of the last layer, one scalar per row: any pitch >= 1 (a dense [M] sdf vector with ldo = 1)
-    const bool col0_only = !backward && l == 2 && a.rows_full == 0;
+    const bool col0_only = !backward && l == n_layers - 1 && a.rows_full == 0;
     MMS_REQUIRE(L.out == nullptr || (col0_only && L.ldo >= 1) ||
                     (aligned16(L.out) && L.ldo % 4 == 0 && L.ldo >= N[l]), fn, "output rows must be 16-B aligned");
     L.N = N[l];
@@ -689,10 +754,10 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, const float* X, int64_t ldx
     nt[l] = (N[l] + 31) / 32;
   }
   const int ks0 = (K0 + 15) / 16;
-  // register-fed layers consume exactly the previous layer's padded unit count
   hipStream_t s = mms::as_stream(stream);
-  const bool ok = prec == 1 ? dispatch_chain<1>(ks0, nt[0], nt[1], nt[2], backward != 0, a, s)
-                            : dispatch_chain<2>(ks0, nt[0], nt[1], nt[2], backward != 0, a, s);
-  MMS_REQUIRE(ok, fn, "unsupported chain shape or activations (SDF 71-256-256-257 Softplus and radiance 317-256-256-256 ReLU chains only)");
+  const bool ok = prec == 1 ? dispatch_chain<1>(n_layers, ks0, nt, backward != 0, a, s)
+                            : dispatch_chain<2>(n_layers, ks0, nt, backward != 0, a, s);
+  MMS_REQUIRE(ok, fn, "unsupported chain shape or activations (SDF 71-256-256-257 Softplus, radiance 317-256-256-256 "
+                      "ReLU, background 39-256x4 and 283-256-256-256-128 ReLU chains only)");
   return mms::check_launch(fn);
 }

@@ -56,7 +56,38 @@ __global__ __launch_bounds__(256) void pixel_sample_kernel(uint64_t seed, uint32
 
 __global__ void advance_kernel(uint64_t* counter, int64_t n) { *counter += (uint64_t)n; }
 
+// U[0, 1) floats (24-bit mantissa draws), four per Philox call: out[i] from counter *counter + offset + i / 4
+__global__ __launch_bounds__(256) void uniform_kernel(uint64_t seed, uint32_t stream, const uint64_t* counter,
+                                                      int64_t offset, int64_t n, float* out) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (4 * q >= n) return;
+  uint32_t u[4];
+  philox4x32(seed, *counter + (uint64_t)offset + (uint64_t)q, stream, u);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (4 * q + j < n) out[4 * q + j] = (float)(u[j] >> 8) * (1.0f / 16777216.0f);
+}
+
 }  // namespace
+
+MMS_EXPORT int mms_uniform(uint64_t seed, uint32_t stream_id, const uint64_t* counter, int64_t offset, int64_t n,
+                           float* out, void* stream) {
+  const char* fn = "mms_uniform";
+  MMS_REQUIRE(n >= 0 && offset >= 0, fn, "bad sizes");
+  MMS_REQUIRE(counter && (n == 0 || out), fn, "null pointer");
+  if (n == 0) return 0;
+  const int64_t calls = (n + 3) / 4;
+  hipLaunchKernelGGL(uniform_kernel, dim3((unsigned)((calls + 255) / 256)), dim3(256), 0, mms::as_stream(stream), seed,
+                     stream_id, counter, offset, n, out);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_counter_advance(uint64_t* counter, int64_t n, void* stream) {
+  const char* fn = "mms_counter_advance";
+  MMS_REQUIRE(counter, fn, "null pointer");
+  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(1), 0, mms::as_stream(stream), counter, n);
+  return mms::check_launch(fn);
+}
 
 MMS_EXPORT int mms_pixel_sample(uint64_t seed, uint32_t stream_id, uint64_t* counter, int64_t n, int n_frames, int H,
                                 int W, const int32_t* frame_ids, const float* images, int C, int32_t* coords,

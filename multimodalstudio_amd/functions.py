@@ -211,7 +211,8 @@ class MLPRun:
                 Y = torch.empty(M, N, device=dev)   # leaves the MLP: consumers expect a contiguous tensor
             else:
                 Y = _alloc(M, N, dev)
-            Z = _alloc(M, N, dev) if (keep and act != 0) else None
+            # the backward takes ReLU' / Sigmoid' from the output: only Softplus keeps its pre-activation
+            Z = _alloc(M, N, dev) if (keep and act == 2) else None
             gemm(NT, M, N, K, h, h.stride(0), W, W.stride(0), Y, Y.stride(0), bias=b, Z=Z,
                  ldz=0 if Z is None else Z.stride(0), act=act, beta=beta, thr=thr, prec=self.prec)
             if keep:
@@ -221,6 +222,14 @@ class MLPRun:
                 self.Ys.append(Y)
             h = Y
         return h
+
+    def _grad_src(self, l: int):
+        """(tensor, derivative id) layer l's activation derivative is taken from: the stored pre-activation for
+        Softplus, else the layer output (ReLU: the same test; Sigmoid: id 4, y (1 - y))."""
+        act = self.acts[l][0]
+        if act == 2 or self.Zs[l] is not None:
+            return self.Zs[l], act
+        return self.Ys[l], (4 if act == 3 else act)
 
     def backward(self, dy: torch.Tensor, need_dx: bool,
                  pre_activated: bool = False) -> Tuple[Optional[torch.Tensor], List[torch.Tensor]]:
@@ -232,7 +241,8 @@ class MLPRun:
         act, beta, thr = self.acts[self.L - 1]
         if act != 0 and not pre_activated:
             dZ = _alloc(M, dy.shape[1], dev)
-            act_bwd(dy, self.Zs[-1], act, beta, thr, dZ)
+            aux, did = self._grad_src(self.L - 1)
+            act_bwd(dy, aux, did, beta, thr, dZ)
         else:
             dZ = dy
         dx = None
@@ -254,9 +264,9 @@ class MLPRun:
             if l > 0:
                 pa, pbeta, pthr = self.acts[l - 1]
                 dprev = _alloc(M, K, dev)
-                zaux = self.Zs[l - 1] if pa != 0 else None
+                zaux, did = self._grad_src(l - 1) if pa != 0 else (None, 0)
                 gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[l], self.Ws[l].stride(0), dprev, dprev.stride(0),
-                     aux=zaux, ldaux=0 if zaux is None else zaux.stride(0), dact=pa, beta=pbeta, thr=pthr,
+                     aux=zaux, ldaux=0 if zaux is None else zaux.stride(0), dact=did, beta=pbeta, thr=pthr,
                      prec=self.prec)
                 dZ = dprev
             elif need_dx:
@@ -267,9 +277,10 @@ class MLPRun:
 
 
 class ChainRun:
-    """A weight-normed 3-layer MLP on the fused chain kernel (mms_mlp_chain: all three layers in one launch, bf16 or
-    split-bf16x3 operands) plus the weight-gradient GEMMs.  Serves the SDF (71-256-256-257) and radiance
-    (317-256-256-256) MLPs in the bf16 precision modes; the fp32 parity mode keeps MLPRun.
+    """A weight-normed 3- or 4-layer MLP on the fused chain kernel (mms_mlp_chain: all layers in one launch, bf16 or
+    split-bf16x3 operands) plus the weight-gradient GEMMs.  Serves the SDF (71-256-256-257), radiance
+    (317-256-256-256) and background NeRF (39-256-256-256-256, 283-256-256-256-128) MLPs in the bf16 precision modes;
+    the fp32 parity mode keeps MLPRun.
 
     ``rows_full``: rows >= rows_full only need output column 0 (the SDF's tap rows, surface_model.py:137-153)."""
 
@@ -277,6 +288,9 @@ class ChainRun:
         if prec not in (1, 2):
             raise ValueError("the fused chain runs the bf16 (1) and split-bf16x3 (2) modes")
         self.params, self.acts, self.prec = list(params), list(acts), int(prec)
+        self.L = len(self.params) // 3
+        if self.L not in (3, 4):
+            raise ValueError("chains of 3 or 4 layers")
         self.beta, self.thr = float(acts[0][1]), float(acts[0][2])
 
     def _pack(self, W, rows: int, cols: int, transpose: bool, permute: bool):
@@ -298,74 +312,82 @@ class ChainRun:
 
     def _chain(self, backward: bool, X, K0: int, rows_full: int, packs, bias, aux, outs, Ns, acts,
                xaux=None, xact: int = 0, xout=None, w2row0=None):
-        VP = ctypes.c_void_p * 3
+        n = self.L
+        VP = ctypes.c_void_p * n
         his = VP(*[p[0].data_ptr() for p in packs])
         los = VP(*[(p[1].data_ptr() if p[1] is not None else None) for p in packs])
         bs = VP(*[(b.data_ptr() if b is not None else None) for b in bias])
         auxs = VP(*[(a.data_ptr() if a is not None else None) for a in aux])
-        ldaux = (ctypes.c_int64 * 3)(*[(a.stride(0) if a is not None else 0) for a in aux])
+        ldaux = (ctypes.c_int64 * n)(*[(a.stride(0) if a is not None else 0) for a in aux])
         os_ = VP(*[(o.data_ptr() if o is not None else None) for o in outs])
-        ldo = (ctypes.c_int64 * 3)(*[(o.stride(0) if o is not None else 0) for o in outs])
-        ns = (ctypes.c_int * 3)(*Ns)
-        ac = (ctypes.c_int * 3)(*acts)
+        ldo = (ctypes.c_int64 * n)(*[(o.stride(0) if o is not None else 0) for o in outs])
+        ns = (ctypes.c_int * n)(*Ns)
+        ac = (ctypes.c_int * n)(*acts)
         cast = lambda a: ctypes.cast(a, ctypes.c_void_p)
-        _lib.call("mms_mlp_chain", self.prec, int(backward), X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
+        _lib.call("mms_mlp_chain", self.prec, int(backward), n, X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
                   _p(xaux), 0 if xaux is None else xaux.stride(0), int(xact), _p(xout),
                   0 if xout is None else xout.stride(0), cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux),
                   cast(os_), cast(ldo), cast(ns), cast(ac), self.beta, self.thr, _p(w2row0), _s())
 
     def forward(self, x: torch.Tensor, keep: bool, rows_full: Optional[int] = None,
-                dense_col0: bool = False) -> torch.Tensor:
-        """x [M, K0] (16-B aligned rows); returns the last layer's output [M, N2] (row stride rounded to 4), or with
-        dense_col0 (rows_full = 0) its column 0 as a dense [M] vector."""
+                dense_col0: bool = False, last_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x [M, K0] (16-B aligned rows); returns the last layer's output [M, N_last] (row stride rounded to 4; or
+        ``last_out``, a 16-B aligned [M, N_last] view the caller owns), or with dense_col0 (rows_full = 0) its column 0
+        as a dense [M] vector."""
         M, K0 = x.shape
         dev = x.device
+        L = self.L
         self.x = x
         self.Ws, self.norms = [], []
-        for l in range(3):
+        for l in range(L):
             g, v, _ = self.params[3 * l: 3 * l + 3]
             W, nrm = normed_weight(g, v)
             self.Ws.append(W)
             self.norms.append(nrm)
         Ns = [W.shape[0] for W in self.Ws]
         nt = [(n + 31) // 32 for n in Ns]
-        packs = [self._pack(self.Ws[0], 32 * nt[0], 16 * ((K0 + 15) // 16), False, False),
-                 self._pack(self.Ws[1], 32 * nt[1], 32 * nt[0], False, True),
-                 self._pack(self.Ws[2], 32 * nt[2], 32 * nt[1], False, True)]
+        packs = [self._pack(self.Ws[0], 32 * nt[0], 16 * ((K0 + 15) // 16), False, False)] + \
+                [self._pack(self.Ws[l], 32 * nt[l], 32 * nt[l - 1], False, True) for l in range(1, L)]
         self.rows_full = M if rows_full is None else int(rows_full)
         if dense_col0 and self.rows_full != 0:
             raise ValueError("dense_col0 needs rows_full = 0")
-        last = torch.empty(M, device=dev).view(M, 1) if dense_col0 else _alloc(M, Ns[2], dev)
-        Y = [_alloc(M, Ns[0], dev) if keep else None, _alloc(M, Ns[1], dev) if keep else None, last]
-        self._chain(False, x, K0, self.rows_full, packs, [self.params[3 * l + 2] for l in range(3)], [None] * 3, Y,
-                    Ns, [a[0] for a in self.acts], w2row0=self.Ws[2])
+        if dense_col0:
+            last = torch.empty(M, device=dev).view(M, 1)
+        else:
+            last = last_out if last_out is not None else _alloc(M, Ns[-1], dev)
+        Y = [_alloc(M, Ns[l], dev) if keep else None for l in range(L - 1)] + [last]
+        self._chain(False, x, K0, self.rows_full, packs, [self.params[3 * l + 2] for l in range(L)], [None] * L, Y,
+                    Ns, [a[0] for a in self.acts], w2row0=self.Ws[-1])
         self.Y = Y
-        return Y[2].view(M) if dense_col0 else Y[2]
+        return Y[-1].view(M) if dense_col0 else Y[-1]
 
     def backward(self, dy: torch.Tensor) -> torch.Tensor:
-        """dy [M, N2] (rows >= rows_full: column 0 only); accumulates the parameter gradients (grad_target) and
+        """dy [M, N_last] (rows >= rows_full: column 0 only); accumulates the parameter gradients (grad_target) and
         returns dx [M, K0]."""
         x, Y = self.x, self.Y
         M, K0 = x.shape
         dev = x.device
+        L = self.L
         Ns = [W.shape[0] for W in self.Ws]
-        N0, N1, N2 = Ns
         acts = [a[0] for a in self.acts]
-        # backward chain: f2^T (natural: B = dy from memory), f1^T, f0^T (register-fed, permuted)
-        packs = [self._pack(self.Ws[2], 32 * ((N1 + 31) // 32), 16 * ((N2 + 15) // 16), True, False),
-                 self._pack(self.Ws[1], 32 * ((N0 + 31) // 32), 32 * ((N1 + 31) // 32), True, True),
-                 self._pack(self.Ws[0], 32 * ((K0 + 31) // 32), 32 * ((N0 + 31) // 32), True, True)]
-        dZ2 = _alloc(M, N2, dev) if acts[2] != 0 else None
-        dZ1, dZ0, dx = _alloc(M, N1, dev), _alloc(M, N0, dev), _alloc(M, K0, dev)
+        up = lambda n, k: k * ((n + k - 1) // k)
+        # backward chain: W_last^T (natural: B = dy from memory), then the earlier layers' W^T (register-fed, permuted)
+        packs = [self._pack(self.Ws[L - 1], up(Ns[L - 2], 32), up(Ns[L - 1], 16), True, False)] + \
+                [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 32), up(Ns[l], 32), True, True)
+                 for l in range(L - 2, -1, -1)]
+        dZl = _alloc(M, Ns[L - 1], dev) if acts[L - 1] != 0 else None
+        dZ = [_alloc(M, Ns[l], dev) for l in range(L - 1)]
+        dx = _alloc(M, K0, dev)
         dy = dy if dy.stride(1) == 1 and dy.stride(0) % 4 == 0 else _copy_aligned(dy)
-        self._chain(True, dy, N2, self.rows_full, packs, [None] * 3, [Y[1], Y[0], None], [dZ1, dZ0, dx],
-                    [N1, N0, K0], [acts[1], acts[0], 0], xaux=Y[2] if acts[2] != 0 else None, xact=acts[2],
-                    xout=dZ2)
-        dZ = [dZ0, dZ1, dZ2 if dZ2 is not None else dy]
-        Xin = [x, Y[0], Y[1]]
+        order = list(range(L - 2, -1, -1))           # hidden layers, last first
+        self._chain(True, dy, Ns[L - 1], self.rows_full, packs, [None] * L, [Y[l] for l in order] + [None],
+                    [dZ[l] for l in order] + [dx], [Ns[l] for l in order] + [K0], [acts[l] for l in order] + [0],
+                    xaux=Y[L - 1] if acts[L - 1] != 0 else None, xact=acts[L - 1], xout=dZl)
+        dZ = dZ + [dZl if dZl is not None else dy]
+        Xin = [x] + Y[:L - 1]
         rf = self.rows_full
-        dWs = _zeroed_views([tuple(self.params[3 * l + 1].shape) for l in range(3)], dev)
-        for l in range(3):
+        dWs = _zeroed_views([tuple(self.params[3 * l + 1].shape) for l in range(L)], dev)
+        for l in range(L):
             g, v, b = self.params[3 * l: 3 * l + 3]
             N, K = v.shape
             gt, vt, bt = grad_target(g), grad_target(v), grad_target(b)
@@ -375,7 +397,7 @@ class ChainRun:
             db = bt if bt is not None else torch.zeros(N, device=dev)
             A, B = dZ[l], Xin[l]
             tiles = ((N + 127) // 128) * ((K + 127) // 128)
-            if l == 2 and rf < M:
+            if l == L - 1 and rf < M:
                 # rows past rows_full carry only the output column 0
                 gemm(TN, N, K, rf, A, A.stride(0), B, B.stride(0), dW, K, accumulate=True,
                      splits=_splits_for(rf, tiles), prec=self.prec, colsum=db)
@@ -561,20 +583,23 @@ def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> to
     return out[:, 0]
 
 
-def _chain_shape(params, acts) -> bool:
-    """True when the fused chain kernel serves this MLP: the SDF (71-256-256-257, Softplus, Softplus, none) or the
-    radiance (317-256-256-256, ReLU x 3) shape (mms_mlp_chain's dispatch table)."""
-    if len(params) != 9:
-        return False
-    dims = [params[1].shape[1]] + [params[3 * l + 1].shape[0] for l in range(3)]
+def _chain_shape(params, acts, prec: int = 2) -> bool:
+    """True when the fused chain kernel serves this MLP (mms_mlp_chain's dispatch table): the SDF (71-256-256-257,
+    Softplus, Softplus, none) and radiance (317-256-256-256, ReLU x 3) chains, and in bf16 (prec 1) the background
+    NeRF's 4-layer ReLU MLPs (base 39-256-256-256-256, head 283-256-256-256-128 / -256)."""
+    dims = [params[1].shape[1]] + [params[3 * l + 1].shape[0] for l in range(len(params) // 3)]
     a = tuple(x[0] for x in acts)
-    return (dims == [71, 256, 256, 257] and a == (2, 2, 0)) or (dims == [317, 256, 256, 256] and a == (1, 1, 1))
+    if len(params) == 9:
+        return (dims == [71, 256, 256, 257] and a == (2, 2, 0)) or (dims == [317, 256, 256, 256] and a == (1, 1, 1))
+    if len(params) == 12 and prec == 1 and a == (1, 1, 1, 1):
+        return dims in ([39, 256, 256, 256, 256], [283, 256, 256, 256, 128], [283, 256, 256, 256, 256])
+    return False
 
 
 def mlp_runner(params, acts, prec: int):
     """The MLP engine for a weight-normed MLP: the fused 3-layer chain kernel in the bf16 modes where its shape is
     served, else the per-layer GEMM engine (every shape, every precision)."""
-    if prec != 0 and _chain_shape(params, acts):
+    if prec != 0 and _chain_shape(params, acts, prec):
         return ChainRun(params, acts, prec)
     return MLPRun(params, acts, prec)
 
@@ -822,11 +847,12 @@ class BackgroundFunction(torch.autograd.Function):
         if grid is not None:
             grid_fwd(grid, X, X.stride(0), M, table, active, X, 39)
         ctx.grid, ctx.active, ctx.table = grid, active, table
-        base = MLPRun(base_p, BG_BASE_ACTS[:nb], PRECISION["background"])
-        base.forward(X, keep=True, last_out=H)          # writes cols [0, Fb) of the head panel
+        # base and head MLPs: 4-layer chain kernels in bf16 (mlp_runner), per-layer GEMMs otherwise
+        base = mlp_runner(base_p, BG_BASE_ACTS[:nb], PRECISION["background"])
+        base.forward(X, keep=True, last_out=H[:, :Fb])  # writes cols [0, Fb) of the head panel
         dens = MLPRun(dens_p, BG_DENS_ACTS, PRECISION["background"])
         density = _mlp_strided(dens, H, Fb)             # density head reads the base features in place
-        head = MLPRun(head_p, BG_HEAD_ACTS[:len(head_p) // 3], PRECISION["background"])
+        head = mlp_runner(head_p, BG_HEAD_ACTS[:len(head_p) // 3], PRECISION["background"])
         feat = head.forward(H, keep=True)
         ctx.base, ctx.dens, ctx.head, ctx.X, ctx.H = base, dens, head, X, H
         ctx.S, ctx.nb, ctx.nd, ctx.Fb = S, nb, nd, Fb
@@ -839,12 +865,12 @@ class BackgroundFunction(torch.autograd.Function):
         M, S, Fb = pos.shape[0], ctx.S, ctx.Fb
         R = M // S
         dev = pos.device
-        dH, hgrads = ctx.head.backward(dfeat.contiguous(), need_dx=True)          # [M, Fb+27]
+        dH = _run_backward(ctx.head, dfeat)                                          # [M, Fb+27]
         if ddensity is None:
             ddensity = torch.zeros(M, 1, device=dev)
         dFb_d, dgrads_dens = _mlp_strided_bwd(ctx.dens, ddensity.contiguous(), ctx.H, Fb)
         dbase_out = dH[:, :Fb] + dFb_d
-        dX, bgrads = ctx.base.backward(dbase_out.contiguous(), need_dx=True)
+        dX = _run_backward(ctx.base, dbase_out)
         if ctx.grid is not None:
             # grid features of the contracted x: table gradients, and d(contracted x) into the panel's x columns
             dtable = grad_target(ctx.table) if ctx.needs_input_grad[2] else None
@@ -856,7 +882,7 @@ class BackgroundFunction(torch.autograd.Function):
         _lib.call("mms_bg_input_bwd", pos.data_ptr(), ctx.X.data_ptr(), ctx.X.stride(0), dX.data_ptr(), dX.stride(0),
                   dirs.data_ptr(), dH.data_ptr(), dH.stride(0), Fb, R, S, _p(dpos), _p(ddirs), _s())
         ctx.base = ctx.dens = ctx.head = ctx.X = ctx.H = ctx.table = None
-        return (dpos, ddirs, None, None, None, None, None, None, *bgrads, *dgrads_dens, *hgrads)
+        return (dpos, ddirs, None, None, None, None, None, None, *([None] * len(params)))
 
 
 def _mlp_strided(run: MLPRun, H: torch.Tensor, Fb: int) -> torch.Tensor:

@@ -81,6 +81,7 @@ class GraphTrainer:
         # device sampler: every step (graph or eager) ends by staging the next step's pixels and hit counts
         self.tail = trainer.gpu_sampler is not None
         self.staged = False
+        self.hyper_step = None      # the step whose AdamW scalars are already queued (behind the last replay)
         self.count_event = torch.cuda.Event() if torch.cuda.is_available() else None
         self.stats = {"replays": 0, "eager": 0, "captures": 0}
 
@@ -192,9 +193,27 @@ class GraphTrainer:
         self.stats["captures"] += 1
 
     # -- one training iteration ------------------------------------------------------------------
+    def _queue_hyper(self):
+        """Queue this step's AdamW scalars (advances the optimizers' step counts)."""
+        t = self.t
+        f = lr_factor(t.step, t.cfg.max_iters)
+        t.fields.load_hyper(f)
+        if t.poses is not None:
+            t.poses.load_hyper(f)
+        self.hyper_step = t.step
+
+    def _drop_queued_hyper(self):
+        """An eager step follows a queued scalar upload: undo its step-count advance (the eager optimizer advances)."""
+        if self.hyper_step is not None:
+            self.t.fields.step_count -= 1
+            if self.t.poses is not None:
+                self.t.poses.step_count -= 1
+            self.hyper_step = None
+
     def eager_step(self, coords):
         """Trainer.train_step on the already-staged inputs (dynamic shapes, no graph), on the side stream the
         captures run on (lazy per-stream state is initialised before the first capture)."""
+        self._drop_queued_hyper()
         self.stats["eager"] += 1
         self.ran_eager = True
         cur = torch.cuda.current_stream()
@@ -240,10 +259,10 @@ class GraphTrainer:
                 print(f"[graphs] capture failed, eager steps from now on: {self.disabled}", file=sys.stderr)
                 torch.cuda.synchronize()
                 return self.eager_step(coords)
-        f = lr_factor(t.step, t.cfg.max_iters)
-        t.fields.load_hyper(f)
-        if t.poses is not None:
-            t.poses.load_hyper(f)
+        if self.hyper_step != t.step:
+            self._drop_queued_hyper()
+            self._queue_hyper()
+        self.hyper_step = None
         g1, g2, out = self.graphs[key]
         g1.replay()
         if self.ddp is not None:
@@ -254,6 +273,9 @@ class GraphTrainer:
             self.staged = True
         t.step += 1
         self.stats["replays"] += 1
+        if self.tail:
+            # the next step's scalars, queued behind this replay: the host's next step only waits for the hit count
+            self._queue_hyper()
         return out
 
     def _eager_with_tail(self, coords):

@@ -594,7 +594,8 @@ class BaseModel(nn.Module):
         outputs = {}
         s_param = self.surface_model.volume_rendering.density_fn.variance_network.s
         inv_s = 1.0 / self.surface_model.volume_rendering.density_fn.variance_network.get_inv_variance()  # once
-        for mod in sp.modalities:
+        drew = False
+        for mi, mod in enumerate(sp.modalities):
             r = rays[mod]
             o, d, up = r["origins"], r["directions"], r["up_directions"]
             N = o.shape[0]
@@ -607,19 +608,25 @@ class BaseModel(nn.Module):
                 idx, sidx, count = fx.compact_padded(mask, min(int(cap), N))
             R = idx.shape[0]
             o_h, d_h, up_h, n_h, f_h = fx.HitGatherFunction.apply(idx, o, d, up, nears, fars)
-            t_rand = _pad_rows(rng.uniform.get(mod), R)
-            if t_rand is None and self.training:
-                t_rand = torch.rand(R, 1, device=dev)
-            pdf = rng.pdf.get(mod)
-            if pdf is not None:
-                pdf = [_pad_rows(p, R) for p in pdf]
-            elif self.training:
-                pdf = [torch.rand(R, 1, device=dev) for _ in range(sp.upsample_steps)]
+            fused = self.training and mod not in rng.uniform and mod not in rng.pdf and mod not in rng.background
+            if fused:
+                # this modality's jitter, PDF and background draws in one device launch (mms_uniform)
+                t_rand, pdf, bt_fused = self._device_draws(mi, R, N, dev)
+                drew = True
+            else:
+                t_rand = _pad_rows(rng.uniform.get(mod), R)
+                if t_rand is None and self.training:
+                    t_rand = torch.rand(R, 1, device=dev)
+                pdf = rng.pdf.get(mod)
+                if pdf is not None:
+                    pdf = [_pad_rows(p, R) for p in pdf]
+                elif self.training:
+                    pdf = [torch.rand(R, 1, device=dev) for _ in range(sp.upsample_steps)]
             bins = self.neus_bins(n_h.detach(), f_h.detach(), o_h.detach(), d_h.detach(), t_rand, pdf)
             S = bins.shape[1] - 1
             pos, deltas, starts, ends = fx.SamplesFunction.apply(bins, n_h, f_h, o_h, d_h, 0)
             # background (background_model.py:73-111) on all N rays
-            bt = rng.background.get(mod)
+            bt = bt_fused if fused else rng.background.get(mod)
             if bt is None and self.training:
                 bt = torch.rand(N, sp.bg_samples + 1, device=dev)
             blin = self._lin_dev(sp.bg_samples + 1, 1.0, dev)
@@ -659,4 +666,37 @@ class BaseModel(nn.Module):
             out["bins"] = bins
             out["mask"] = mask
             outputs[mod] = out
+        if drew:
+            _lib.call("mms_counter_advance", self._draw_counter(dev).data_ptr(), 1 << 32, fx._s())
         return outputs
+
+    # -- training-mode uniform draws on the device ----------------------------------------------------
+    def seed_draws(self, seed: int, dev) -> None:
+        """Restart the forward's device draw stream at (seed, counter 0): two forwards after the same seed_draws draw
+        the same values (torch.cuda.manual_seed's role for the reference's torch.rand draws)."""
+        self.draw_seed = int(seed)
+        self._draw_counter(dev).zero_()
+
+    def _draw_counter(self, dev) -> torch.Tensor:
+        """Device Philox counter of the forward's draws (not a registered buffer: the state_dict stays the
+        reference's); advanced once per forward on the device, so captured graphs draw fresh values every replay."""
+        c = getattr(self, "_draw_ctr", None)
+        if c is None or c.device != dev:
+            c = torch.zeros(1, dtype=torch.int64, device=dev)
+            self._draw_ctr = c
+        return c
+
+    def _device_draws(self, mi: int, R: int, N: int, dev):
+        """(jitter [R,1], PDF draws 4 x [R,1], background [N, bg+1]) ~ U[0,1) from one mms_uniform launch, the
+        stream keyed by (draw_seed, modality index); the reference draws these with torch.rand in the same shapes
+        (SURVEY §8(d) 'RNG')."""
+        sp = self.spec
+        nb = sp.bg_samples + 1
+        k = sp.upsample_steps
+        buf = torch.empty(R * (1 + k) + N * nb, device=dev)
+        _lib.call("mms_uniform", int(getattr(self, "draw_seed", 0)) & ((1 << 64) - 1), mi,
+                  self._draw_counter(dev).data_ptr(), 0, buf.numel(), buf.data_ptr(), fx._s())
+        t_rand = buf[:R].view(R, 1)
+        pdf = [buf[R * (1 + j):R * (2 + j)].view(R, 1) for j in range(k)]
+        bt = buf[R * (1 + k):].view(N, nb)
+        return t_rand, pdf, bt

@@ -129,7 +129,10 @@ class FlatGroup:
         self.sumsq = torch.zeros(1, device=dev)
         # this step's AdamW scalars for graph replays (mms_adamw_dev; layout of mms_adamw_scalars)
         self.hyper = torch.zeros(8, device=dev)
-        self._hyper_host = torch.zeros(8).pin_memory() if dev.type == "cuda" else torch.zeros(8)
+        # two pinned staging buffers, alternated: a step's scalars can be queued behind the previous replay while
+        # the copy queued before it may still be pending
+        self._hyper_host = [torch.zeros(8).pin_memory() if dev.type == "cuda" else torch.zeros(8) for _ in range(2)]
+        self._hyper_slot = 0
         off = 0
         for p in self.params:
             k = p.numel()
@@ -177,9 +180,11 @@ class FlatGroup:
     def load_hyper(self, lr_factor: float):
         """Graph mode, before a replay: advance the step and upload its scalars (read by the captured launch)."""
         lr = self._advance(lr_factor)
+        host = self._hyper_host[self._hyper_slot]
+        self._hyper_slot ^= 1
         _lib.call("mms_adamw_scalars", float(lr), float(self.wd), float(self.betas[0]), float(self.betas[1]),
-                  float(self.eps), int(self.step_count), self._hyper_host.data_ptr())
-        self.hyper.copy_(self._hyper_host, non_blocking=True)
+                  float(self.eps), int(self.step_count), host.data_ptr())
+        self.hyper.copy_(host, non_blocking=True)
 
     def step_captured(self, max_norm: float = 2.0):
         """The clip + AdamW launches with device-resident scalars (captured into the step graph)."""
@@ -296,6 +301,7 @@ class Trainer:
         channels = {m: mscene.CHANNELS[m] for m in mods}
         torch.manual_seed(654824)
         self.model = BaseModel(ModelSpec(channels, log2T=cfg.log2T, bg_kind=bg_kind, fields=fields)).to(device)
+        self.model.draw_seed = (cfg.seed << 8) + 1000003 * rank + 17   # per-rank stream of the forward's draws
         self.dataset = None
         if cfg.data_dir is not None:
             # the train split of an on-disk scene: every frame but the eval views and the skipped ones

@@ -65,12 +65,12 @@ def main():
     t.set_step(95000)
     coords, sel = t.sampler.sample(t.frames)
     targets = t.targets_for(coords, sel)
-    torch.cuda.manual_seed(100 + rank)
+    t.model.seed_draws(100 + rank, dev)
     t.compute_grads(coords, targets)
     local = t.fields.grad.clone()
     local_pose = t.poses.grad.clone()
     log("local grads")
-    torch.cuda.manual_seed(100 + rank)
+    t.model.seed_draws(100 + rank, dev)
     t.compute_grads(coords, targets, ddp=ddp)
     torch.cuda.synchronize()
     log("reduced grads")

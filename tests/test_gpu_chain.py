@@ -159,3 +159,60 @@ def test_sdf_only_fast_matches_fp32(dev):
     torch.cuda.synchronize()
     assert out.is_contiguous() and out.shape == ref.shape
     assert rel(out.cpu(), ref.cpu()) < TOL[2]
+
+
+def _masked_ref_n(x, params, acts, Y, dy):
+    """_masked_ref for any layer count (ReLU / none activations)."""
+    L = len(params) // 3
+    ins = [torch.as_tensor(x).double()] + [Y[l].double().cpu() for l in range(L - 1)]
+    d = torch.as_tensor(dy).double()
+    out = [None] * (3 * L)
+    for l in range(L - 1, -1, -1):
+        if acts[l][0] == 1:
+            d = d * (Y[l].double().cpu() > 0)
+        g64 = params[3 * l].detach().double().cpu().requires_grad_(True)
+        v64 = params[3 * l + 1].detach().double().cpu().requires_grad_(True)
+        W = torch._weight_norm(v64, g64, 0)
+        W.backward(d.T @ ins[l])
+        out[3 * l], out[3 * l + 1], out[3 * l + 2] = g64.grad, v64.grad, d.sum(0)
+        d = d @ W.detach()
+    return d, out
+
+
+@pytest.mark.parametrize("dims", [[39, 256, 256, 256, 256], [283, 256, 256, 256, 128], [283, 256, 256, 256, 256],
+                                  [317, 256, 256, 256]])
+def test_chain_relu_layers(dev, dims):
+    """ReLU chains in bf16 -- the background NeRF's 4-layer MLPs and the radiance MLP -- at a row count that is not a
+    multiple of the 128-row block (the clamped rows past M must store exactly row M - 1's values): forward vs an fp64
+    restatement, backward (dx and every weight-norm / bias gradient, i.e. every stored dZ) vs the fp64 backward at
+    the kernel's own activations; the last layer writes into a caller-owned strided view (the background panel)."""
+    from multimodalstudio_amd import functions as fx
+    g = torch.Generator().manual_seed(sum(dims))
+    M = 1500
+    L = len(dims) - 1
+    params = []
+    for l in range(L):
+        k, n = dims[l], dims[l + 1]
+        v = torch.randn(n, k, generator=g) / np.sqrt(k)
+        params += [v.norm(dim=1, keepdim=True).clone(), v, torch.randn(n, generator=g) * 0.1]
+    params = [p.to(dev).requires_grad_(True) for p in params]
+    acts = [(1, 1.0, 20.0)] * L
+    x = torch.randn(M, dims[0], generator=g)
+    X = _panel(x, dev)
+    panel = fx._alloc(M, dims[L] + 27, dev)
+    run = fx.ChainRun(params, acts, 1)
+    y = run.forward(X, keep=True, last_out=panel[:, :dims[L]])
+    assert y.data_ptr() == panel.data_ptr()
+    h = x.double()
+    for l in range(L):
+        gg, v, b = [p.detach().double().cpu() for p in params[3 * l: 3 * l + 3]]
+        h = torch.relu(h @ torch._weight_norm(v, gg, 0).T + b)
+    assert rel(y.detach().cpu(), h) < TOL[1]
+    Y = [t.detach().clone() for t in run.Y]
+    dy = torch.randn(M, dims[L], generator=g)
+    dx = run.backward(_panel(dy, dev))
+    torch.cuda.synchronize()
+    ref_dx, ref_g = _masked_ref_n(x, params, acts, Y, dy)
+    assert rel(dx.cpu(), ref_dx) < TOL[1]
+    for i, p in enumerate(params):
+        assert rel(p.grad.cpu(), ref_g[i]) < TOL[1], (i, rel(p.grad.cpu(), ref_g[i]))
