@@ -47,6 +47,8 @@ DTYPES = {"fp32": "fp32", "fast": "bf16 MFMA (fp32 accumulate; SDF MLP split-bf1
           "bf16x3": "split-bf16x3 MFMA (fp32-accurate), fp32 elsewhere"}
 HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per lookup, forward
 HASH_BWD_B = 128 + 12 + 16 * 8 * 2 * (4 + 4)    # bytes per lookup, backward (table grads)
+HASH_BWD_ATOMIC_B = 16 * 8 * 2 * 4              # the float-atomic bytes one backward lookup adds into the table
+ATOMIC_PEAK_GBS = 1300.0                        # MI355X_MICROARCH.md "Global float atomics": chip-wide added bytes
 
 
 def gemm_work(a):
@@ -90,12 +92,20 @@ def chain_work(a):
     return f"{PREC_NAMES[prec]}:{role}{'_bwd' if bwd else '_fwd'}", (flops, nbytes)
 
 
+def hash_fwd_work(a):
+    """(role, SURVEY §8(d) bytes) of one mms_hashgrid_fwd launch: the SDF batch [centre | 4 taps] (the dominant
+    launch), the sampler's / background's smaller 72-column panels, or the radiance panel."""
+    M, ldx = int(a[1]), int(a[2])
+    role = "sdf_taps" if (ldx == 72 and M > 200000) else ("radiance" if ldx >= 300 else "sampler_or_bg")
+    return role, float(M) * HASH_FWD_B
+
+
 def work_fns():
     return {
         "mms_gemm": gemm_work,
         "mms_mlp_chain": chain_work,
-        "mms_hashgrid_fwd": lambda a: float(a[1]) * HASH_FWD_B,
-        "mms_hashgrid_bwd_grouped": lambda a: float(a[1]) * a[2] * HASH_BWD_B,
+        "mms_hashgrid_fwd": hash_fwd_work,
+        "mms_hashgrid_bwd_grouped": lambda a: (float(a[1]) * a[2] * HASH_BWD_B, float(a[1]) * a[2] * HASH_BWD_ATOMIC_B),
     }
 
 
@@ -120,9 +130,17 @@ def kernel_records(summ, timing_steps: int, precision: str):
                 rec.update({"mode_peak": round(MFMA_PEAK_TF[mode], 1),
                             "frac_of_mode_peak": round(ach / MFMA_PEAK_TF[mode], 4)})
         else:
+            atomic = None
+            if isinstance(work, tuple):
+                work, atomic = work
             ach = work / (ms * 1e-3) / 1e9
             rec.update({"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(ach / HBM_PEAK_GBS, 4)})
+            if atomic is not None:
+                # the backward's binding ceiling: float atomics execute at the memory side at ~1.3 TB/s of added bytes
+                aa = atomic / (ms * 1e-3) / 1e9
+                rec["atomic_ceiling"] = {"achieved": round(aa, 1), "peak": ATOMIC_PEAK_GBS, "unit": "GB/s added",
+                                         "frac": round(aa / ATOMIC_PEAK_GBS, 4)}
         kernels.append(rec)
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{precision}.json")
     pmc = json.load(open(pmc_path))["kernels"] if os.path.exists(pmc_path) else {}
@@ -288,8 +306,10 @@ def main():
             for k in ["kernel", "avg_ms", "frac_of_mode_peak", "mode_peak", "traffic_unit"]:
                 if k in top:
                     roof[k] = top[k]
-        hash_roof = {d: {k: by_name[n][k] for k in ["achieved", "peak", "unit", "frac", "avg_ms", "traffic"]}
-                     for d, n in [("fwd", "mms_hashgrid_fwd"), ("bwd", "mms_hashgrid_bwd_grouped")] if n in by_name}
+        keys = ["kernel", "achieved", "peak", "unit", "frac", "avg_ms", "traffic", "atomic_ceiling"]
+        hash_roof = {d: {k: by_name[n][k] for k in keys if k in by_name[n]}
+                     for d, n in [("fwd", "mms_hashgrid_fwd:sdf_taps"), ("fwd_radiance", "mms_hashgrid_fwd:radiance"),
+                                  ("bwd", "mms_hashgrid_bwd_grouped")] if n in by_name}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

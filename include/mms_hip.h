@@ -83,6 +83,45 @@ int mms_mlp_chain(int prec, int backward, int n_layers, const float* X, int64_t 
 int mms_mlp_pack(const float* W, int64_t N, int64_t K, int64_t ldw, int transpose, int permute, int64_t rows,
                  int64_t cols, void* hi, void* lo, void* stream);
 
+/* ---- batched weight preparation: every weight-normed layer of a model (and every packed MMA image of them) in one
+ * launch each, once per step (the item tables live in device memory; row0 / elem0 = the item's first block row /
+ * element in the concatenation, items in increasing order).  Same arithmetic as mms_weight_norm_fwd /
+ * mms_mlp_pack per item. */
+typedef struct {
+  const float* g;
+  const float* v;
+  int64_t N, K;
+  float* W;
+  int64_t ldw;
+  float* norms;
+  int64_t row0;
+} MmsNormItem;
+typedef struct {
+  const float* W;
+  int64_t N, K, ldw;
+  int64_t transpose, permute;
+  int64_t rows, cols;
+  void* hi;
+  void* lo;
+  int64_t elem0;
+} MmsPackItem;
+int mms_weight_norm_fwd_batched(const void* items, int n_items, int64_t total_rows, void* stream);
+/* a backward's weight-norm gradients (dg += , dv += as mms_weight_norm_bwd), up to 32 layers per launch; items is a
+ * HOST array (copied into the kernel arguments). */
+typedef struct {
+  const float* g;
+  const float* v;
+  const float* norms;
+  int64_t N, K;
+  const float* dW;
+  int64_t lddw;
+  float* dg;
+  float* dv;
+  int64_t row0;
+} MmsWnBwdItem;
+int mms_weight_norm_bwd_batched(const void* items, int n_items, int64_t total_rows, void* stream);
+int mms_mlp_pack_batched(const void* items, int n_items, int64_t total, void* stream);
+
 /* ---- weight norm (mlp.py:206-209; torch weight_norm dim=0): W = v * (g / ||v||_row); bwd dg += , dv += */
 int mms_weight_norm_fwd(const float* g, const float* v, int64_t N, int64_t K, float* W, int64_t ldw, float* norms,
                         void* stream);

@@ -24,11 +24,9 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
-__global__ __launch_bounds__(256) void wn_fwd_kernel(const float* __restrict__ g, const float* __restrict__ v,
-                                                     int64_t N, int64_t K, float* __restrict__ W, int64_t ldw,
-                                                     float* __restrict__ norms) {
-  __shared__ float red[4];
-  const int64_t n = blockIdx.x;
+// one weight row n (a 256-thread block): the same reduction order for the single-layer and the batched launch
+__device__ __forceinline__ void wn_row(const float* __restrict__ g, const float* __restrict__ v, int64_t n, int64_t K,
+                                       float* __restrict__ W, int64_t ldw, float* __restrict__ norms, float* red) {
   const float* vr = v + n * K;
   float s = 0.f;
   for (int64_t k = threadIdx.x; k < K; k += blockDim.x) s += vr[k] * vr[k];
@@ -39,12 +37,26 @@ __global__ __launch_bounds__(256) void wn_fwd_kernel(const float* __restrict__ g
   if (threadIdx.x == 0 && norms) norms[n] = nrm;
 }
 
-__global__ __launch_bounds__(256) void wn_bwd_kernel(const float* __restrict__ g, const float* __restrict__ v,
-                                                     const float* __restrict__ norms, int64_t N, int64_t K,
-                                                     const float* __restrict__ dW, int64_t lddw,
-                                                     float* __restrict__ dg, float* __restrict__ dv) {
+__global__ __launch_bounds__(256) void wn_fwd_kernel(const float* __restrict__ g, const float* __restrict__ v,
+                                                     int64_t N, int64_t K, float* __restrict__ W, int64_t ldw,
+                                                     float* __restrict__ norms) {
   __shared__ float red[4];
-  const int64_t n = blockIdx.x;
+  wn_row(g, v, blockIdx.x, K, W, ldw, norms, red);
+}
+
+// every layer of a model in one launch: block b handles row b - items[i].row0 of the item i it falls in
+__global__ __launch_bounds__(256) void wn_fwd_batched_kernel(const MmsNormItem* __restrict__ items, int n_items) {
+  __shared__ float red[4];
+  int i = 0;
+  while (i + 1 < n_items && (int64_t)blockIdx.x >= items[i + 1].row0) ++i;
+  const MmsNormItem it = items[i];
+  wn_row(it.g, it.v, (int64_t)blockIdx.x - it.row0, it.K, it.W, it.ldw, it.norms, red);
+}
+
+__device__ __forceinline__ void wn_bwd_row(const float* __restrict__ g, const float* __restrict__ v,
+                                           const float* __restrict__ norms, int64_t n, int64_t K,
+                                           const float* __restrict__ dW, int64_t lddw, float* __restrict__ dg,
+                                           float* __restrict__ dv, float* red) {
   const float* vr = v + n * K;
   const float* dr = dW + n * lddw;
   float s = 0.f;
@@ -56,6 +68,30 @@ __global__ __launch_bounds__(256) void wn_bwd_kernel(const float* __restrict__ g
   const float b = g[n] * dgn / (nrm * nrm);
   for (int64_t k = threadIdx.x; k < K; k += blockDim.x) dv[n * K + k] += a * dr[k] - b * vr[k];
   if (threadIdx.x == 0) dg[n] += dgn;
+}
+
+__global__ __launch_bounds__(256) void wn_bwd_kernel(const float* __restrict__ g, const float* __restrict__ v,
+                                                     const float* __restrict__ norms, int64_t N, int64_t K,
+                                                     const float* __restrict__ dW, int64_t lddw,
+                                                     float* __restrict__ dg, float* __restrict__ dv) {
+  __shared__ float red[4];
+  wn_bwd_row(g, v, norms, blockIdx.x, K, dW, lddw, dg, dv, red);
+}
+
+// all of a backward's weight-norm gradients in one launch; the item list travels by value in the kernel arguments
+// (graph-capturable with no device table: every step's dW buffers are new allocations)
+constexpr int kMaxWnBwd = 32;
+struct WnBwdBatch {
+  MmsWnBwdItem it[kMaxWnBwd];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void wn_bwd_batched_kernel(WnBwdBatch b) {
+  __shared__ float red[4];
+  int i = 0;
+  while (i + 1 < b.n && (int64_t)blockIdx.x >= b.it[i + 1].row0) ++i;
+  const MmsWnBwdItem& it = b.it[i];
+  wn_bwd_row(it.g, it.v, it.norms, (int64_t)blockIdx.x - it.row0, it.K, it.dW, it.lddw, it.dg, it.dv, red);
 }
 
 // db[n] += sum over rows; blockDim = 256 columns-chunk, grid.x = column chunks, grid.y = row splits
@@ -83,6 +119,24 @@ __global__ void act_bwd_kernel(const float* __restrict__ dY, int64_t ldy, const 
 }
 
 }  // namespace
+
+MMS_EXPORT int mms_weight_norm_bwd_batched(const void* items, int n_items, int64_t total_rows, void* stream) {
+  const char* fn = "mms_weight_norm_bwd_batched";
+  MMS_REQUIRE(items && n_items > 0 && n_items <= kMaxWnBwd && total_rows > 0, fn, "1 .. 32 items per batch");
+  WnBwdBatch b;
+  memcpy(b.it, items, sizeof(MmsWnBwdItem) * n_items);
+  b.n = n_items;
+  hipLaunchKernelGGL(wn_bwd_batched_kernel, dim3((unsigned)total_rows), dim3(256), 0, mms::as_stream(stream), b);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_weight_norm_fwd_batched(const void* items, int n_items, int64_t total_rows, void* stream) {
+  const char* fn = "mms_weight_norm_fwd_batched";
+  MMS_REQUIRE(items && n_items > 0 && total_rows > 0, fn, "empty batch");
+  hipLaunchKernelGGL(wn_fwd_batched_kernel, dim3((unsigned)total_rows), dim3(256), 0, mms::as_stream(stream),
+                     reinterpret_cast<const MmsNormItem*>(items), n_items);
+  return mms::check_launch(fn);
+}
 
 MMS_EXPORT int mms_weight_norm_fwd(const float* g, const float* v, int64_t N, int64_t K, float* W, int64_t ldw,
                                    float* norms, void* stream) {

@@ -670,28 +670,53 @@ __device__ __forceinline__ int64_t perm_col(int64_t c) {
   return (c & ~(int64_t)15) | (q & 3) | ((q & 4) << 1) | ((q & 8) >> 1);
 }
 
+// one element i of a packed image (fragment-major destination: (k-step s, tile t) block, lane r + 32 h, element j)
+__device__ __forceinline__ void pack_elem(const float* __restrict__ W, int64_t N, int64_t K, int64_t ldw, int transpose,
+                                          int permute, int64_t rows, int64_t cols, __bf16* __restrict__ hi,
+                                          __bf16* __restrict__ lo, int64_t i) {
+  const int64_t R = transpose ? K : N, C = transpose ? N : K;
+  const int64_t nt = rows / 32;
+  const int64_t row = i / cols, c = i - row * cols;
+  const int64_t src = permute ? perm_col(c) : c;
+  float v = 0.f;
+  if (row < R && src < C) v = transpose ? W[src * ldw + row] : W[row * ldw + src];
+  const int64_t s = c >> 4, q = c & 15, t = row >> 5, r = row & 31;
+  const int64_t o = ((s * nt + t) * 64 + r + 32 * (q >> 3)) * 8 + (q & 7);
+  const __bf16 b = (__bf16)v;
+  hi[o] = b;
+  if (lo != nullptr) lo[o] = (__bf16)(v - (float)b);
+}
+
 __global__ void pack_kernel(const float* __restrict__ W, int64_t N, int64_t K, int64_t ldw, int transpose,
                             int permute, int64_t rows, int64_t cols, __bf16* __restrict__ hi, __bf16* __restrict__ lo) {
   const int64_t total = rows * cols;
-  const int64_t R = transpose ? K : N, C = transpose ? N : K;
-  const int64_t nt = rows / 32;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = i / cols, c = i - row * cols;
-    const int64_t src = permute ? perm_col(c) : c;
-    float v = 0.f;
-    if (row < R && src < C) v = transpose ? W[src * ldw + row] : W[row * ldw + src];
-    // fragment-major destination: (k-step s, tile t) block, lane r + 32 h, element j
-    const int64_t s = c >> 4, q = c & 15, t = row >> 5, r = row & 31;
-    const int64_t o = ((s * nt + t) * 64 + r + 32 * (q >> 3)) * 8 + (q & 7);
-    const __bf16 b = (__bf16)v;
-    hi[o] = b;
-    if (lo != nullptr) lo[o] = (__bf16)(v - (float)b);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
+    pack_elem(W, N, K, ldw, transpose, permute, rows, cols, hi, lo, i);
+}
+
+// every packed image of a model in one launch: element e of the concatenation belongs to the item whose elem0 range
+// holds it (items sorted by elem0)
+__global__ void pack_batched_kernel(const MmsPackItem* __restrict__ items, int n_items, int64_t total) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int i = 0;
+    while (i + 1 < n_items && e >= items[i + 1].elem0) ++i;
+    const MmsPackItem& it = items[i];
+    pack_elem(it.W, it.N, it.K, it.ldw, it.transpose, it.permute, it.rows, it.cols,
+              reinterpret_cast<__bf16*>(it.hi), reinterpret_cast<__bf16*>(it.lo), e - it.elem0);
   }
 }
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
+
+MMS_EXPORT int mms_mlp_pack_batched(const void* items, int n_items, int64_t total, void* stream) {
+  const char* fn = "mms_mlp_pack_batched";
+  MMS_REQUIRE(items && n_items > 0 && total > 0, fn, "empty batch");
+  hipLaunchKernelGGL(pack_batched_kernel, dim3(mms::grid_for(total, 256, 8192)), dim3(256), 0, mms::as_stream(stream),
+                     reinterpret_cast<const MmsPackItem*>(items), n_items, total);
+  return mms::check_launch(fn);
+}
 
 MMS_EXPORT int mms_mlp_pack(const float* W, int64_t N, int64_t K, int64_t ldw, int transpose, int permute,
                             int64_t rows, int64_t cols, void* hi, void* lo, void* stream) {

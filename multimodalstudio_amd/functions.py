@@ -55,39 +55,154 @@ def _alloc(rows: int, cols: int, dev, zero: bool = False) -> torch.Tensor:
     return buf[:, :cols]
 
 
-# Weight-normalised weights (and their packed MFMA images) computed once per model forward: the SDF MLP alone is
-# evaluated 5 times per modality and step (4 sampler iterations + the training pass) and every modality reuses the
-# same fields.  BaseModel.forward opens a scope (begin_forward) at its start; inside a graph capture the first use
-# records the computation, later uses read the same buffers, so replays recompute them from the current parameters.
-_WCACHE: dict = {}
-_WCACHE_ON = [False]
+# Weight-normalised weights (and their packed MFMA images) computed once per model forward, all layers in one launch:
+# the SDF MLP alone is evaluated 5 times per modality and step (4 sampler iterations + the training pass) and every
+# modality reuses the same fields.  BaseModel.forward opens a scope (begin_forward) at its start; a captured graph
+# holds the two batched launches, so replays recompute every entry from the current parameters.
+class _NormItem(ctypes.Structure):
+    """MmsNormItem (include/mms_hip.h)."""
+    _fields_ = [("g", ctypes.c_void_p), ("v", ctypes.c_void_p), ("N", ctypes.c_int64), ("K", ctypes.c_int64),
+                ("W", ctypes.c_void_p), ("ldw", ctypes.c_int64), ("norms", ctypes.c_void_p), ("row0", ctypes.c_int64)]
 
 
-def begin_forward() -> None:
-    _WCACHE.clear()
-    _WCACHE_ON[0] = True
+class _PackItem(ctypes.Structure):
+    """MmsPackItem (include/mms_hip.h)."""
+    _fields_ = [("W", ctypes.c_void_p), ("N", ctypes.c_int64), ("K", ctypes.c_int64), ("ldw", ctypes.c_int64),
+                ("transpose", ctypes.c_int64), ("permute", ctypes.c_int64), ("rows", ctypes.c_int64),
+                ("cols", ctypes.c_int64), ("hi", ctypes.c_void_p), ("lo", ctypes.c_void_p), ("elem0", ctypes.c_int64)]
+
+
+class WeightPrep:
+    """A model's weight preparation, batched: every weight-normed layer's W = g v / ||v|| (mlp.py:206-209) and every
+    bf16 MMA image the chain kernels read (forward and backward orientation) are recomputed at the start of each
+    model forward by two launches (mms_weight_norm_fwd_batched, mms_mlp_pack_batched) instead of one per layer and
+    image.  Entries register themselves on first use (computed individually that once) into persistent buffers; the
+    item tables live in device memory, append-only with a fixed capacity, so a captured graph's launches keep reading
+    a valid table.  Outside a model forward nothing is cached (parameters are read afresh)."""
+
+    MAX_NORM, MAX_PACK = 64, 128
+
+    def __init__(self):
+        self.norm = {}      # key -> [g, v, W, nrm, index]
+        self.pack = {}      # key -> [W, hi, lo, index, args]
+        self.norm_items: List[_NormItem] = []
+        self.pack_items: List[_PackItem] = []
+        self.rows = 0
+        self.elems = 0
+        self.dirty = False
+        self.fresh = False
+        self.table_n = None
+        self.table_p = None
+        self.n_up = (0, 0, 0, 0)   # (norm items, rows, pack items, elems) in the device tables
+        self.done = set()          # entries computed individually in the current forward
+        self.dev = None
+
+    def run(self, dev) -> None:
+        """Recompute every registered entry (start of a model forward)."""
+        self.fresh = False
+        self.done.clear()
+        self.dev = dev
+        if not self.norm_items:
+            return
+        if self.dirty:
+            if torch.cuda.is_current_stream_capturing():
+                return                      # no table upload inside a capture: lookups compute individually
+            self._upload(dev)
+        nn_, rows, np_, elems = self.n_up
+        _lib.call("mms_weight_norm_fwd_batched", self.table_n.data_ptr(), nn_, rows, _s())
+        if np_:
+            _lib.call("mms_mlp_pack_batched", self.table_p.data_ptr(), np_, elems, _s())
+        self.fresh = True
+
+    def close(self) -> None:
+        """End of a model forward: entries registered in it go into the device tables now (outside any capture), so
+        the next forward -- possibly a captured one -- prepares them in the batch."""
+        self.fresh = False
+        if self.dirty and self.dev is not None and not torch.cuda.is_current_stream_capturing():
+            self._upload(self.dev)
+
+    def _upload(self, dev) -> None:
+        if self.table_n is None:
+            self.table_n = torch.zeros(self.MAX_NORM * ctypes.sizeof(_NormItem), dtype=torch.uint8, device=dev)
+            self.table_p = torch.zeros(self.MAX_PACK * ctypes.sizeof(_PackItem), dtype=torch.uint8, device=dev)
+        for items, table, T in ((self.norm_items, self.table_n, _NormItem), (self.pack_items, self.table_p, _PackItem)):
+            if items:
+                arr = (T * len(items))(*items)
+                table[:ctypes.sizeof(arr)].copy_(torch.frombuffer(bytearray(arr), dtype=torch.uint8))
+        self.n_up = (len(self.norm_items), self.rows, len(self.pack_items), self.elems)
+        self.dirty = False
+
+    def normed(self, g: torch.Tensor, v: torch.Tensor):
+        key = (v.data_ptr(), g.data_ptr(), tuple(v.shape))
+        e = self.norm.get(key)
+        if e is None:
+            N, K = v.shape
+            W, nrm = _alloc(N, K, v.device), torch.empty(N, device=v.device)
+            idx = None
+            if len(self.norm_items) < self.MAX_NORM:
+                idx = len(self.norm_items)
+                self.norm_items.append(_NormItem(g.data_ptr(), v.data_ptr(), N, K, W.data_ptr(),
+                                                 W.stride(0), nrm.data_ptr(), self.rows))
+                self.rows += N
+                self.dirty = True
+            e = self.norm[key] = [g, v, W, nrm, idx]
+        g, v, W, nrm, idx = e
+        if not (self.fresh and idx is not None and idx < self.n_up[0]) and key not in self.done:
+            weight_norm_fwd(g.reshape(-1), v, W, nrm)
+            self.done.add(key)
+        return W, nrm
+
+    def packed(self, W: torch.Tensor, rows: int, cols: int, transpose: bool, permute: bool, prec: int):
+        key = (W.data_ptr(), tuple(W.shape), rows, cols, bool(transpose), bool(permute), int(prec))
+        e = self.pack.get(key)
+        N, K = W.shape
+        if e is None:
+            hi = torch.empty(rows, cols, dtype=torch.bfloat16, device=W.device)
+            lo = torch.empty_like(hi) if prec == 2 else None
+            idx = None
+            if len(self.pack_items) < self.MAX_PACK:
+                idx = len(self.pack_items)
+                self.pack_items.append(_PackItem(W.data_ptr(), N, K, W.stride(0), int(transpose), int(permute), rows,
+                                                 cols, hi.data_ptr(), _p(lo), self.elems))
+                self.elems += rows * cols
+                self.dirty = True
+            e = self.pack[key] = [W, hi, lo, idx]
+        W, hi, lo, idx = e
+        if not (self.fresh and idx is not None and idx < self.n_up[2]) and key not in self.done:
+            _lib.call("mms_mlp_pack", W.data_ptr(), N, K, W.stride(0), int(transpose), int(permute), rows, cols,
+                      hi.data_ptr(), _p(lo), _s())
+            self.done.add(key)
+        return hi, lo
+
+
+_ACTIVE_PREP: List[Optional[WeightPrep]] = [None]
+
+
+def begin_forward(prep: Optional[WeightPrep] = None, dev=None) -> None:
+    """Open a model-forward scope: the model's weights are prepared in one batch and looked up from it."""
+    _ACTIVE_PREP[0] = prep
+    if prep is not None:
+        prep.run(dev)
 
 
 def end_forward() -> None:
     """Close the scope: outside a model forward (plugin modules, backward passes) nothing is cached, so parameters
     updated in place are always read afresh."""
-    _WCACHE.clear()
-    _WCACHE_ON[0] = False
+    if _ACTIVE_PREP[0] is not None:
+        _ACTIVE_PREP[0].close()
+    _ACTIVE_PREP[0] = None
 
 
 def normed_weight(g: torch.Tensor, v: torch.Tensor):
     """(W = g v / ||v||_row in a 16-B aligned [N, K] view, row norms) of one weight-normed layer (mlp.py:206-209)."""
-    key = ("wn", v.data_ptr(), g.data_ptr())
-    hit = _WCACHE.get(key)
-    if hit is None:
-        N, K = v.shape
-        W = _alloc(N, K, v.device)
-        nrm = torch.empty(N, device=v.device)
-        weight_norm_fwd(g.reshape(-1), v, W, nrm)
-        hit = (W, nrm)
-        if _WCACHE_ON[0]:
-            _WCACHE[key] = hit
-    return hit
+    prep = _ACTIVE_PREP[0]
+    if prep is not None:
+        return prep.normed(g, v)
+    N, K = v.shape
+    W = _alloc(N, K, v.device)
+    nrm = torch.empty(N, device=v.device)
+    weight_norm_fwd(g.reshape(-1), v, W, nrm)
+    return W, nrm
 
 
 def grad_target(p: torch.Tensor) -> Optional[torch.Tensor]:
@@ -246,7 +361,7 @@ class MLPRun:
         else:
             dZ = dy
         dx = None
-        dWs = _zeroed_views([tuple(self.params[3 * l + 1].shape) for l in range(self.L)], dev)
+        dWs = _dw_views([self.params[3 * l + 1] for l in range(self.L)], dev)
         for l in range(self.L - 1, -1, -1):
             g, v, b = self.params[3 * l: 3 * l + 3]
             N, K = v.shape
@@ -260,7 +375,7 @@ class MLPRun:
                      splits=_splits_for(M, tiles), prec=self.prec, colsum=db)
                 dg = gt.reshape(-1) if gt is not None else torch.zeros(N, device=dev)
                 dv = vt if vt is not None else torch.zeros(N, K, device=dev)
-                weight_norm_bwd(g.reshape(-1), v, self.norms[l], dW, dg, dv)
+                _wn_bwd(g.reshape(-1), v, self.norms[l], dW, dg, dv)
             if l > 0:
                 pa, pbeta, pthr = self.acts[l - 1]
                 dprev = _alloc(M, K, dev)
@@ -294,13 +409,10 @@ class ChainRun:
         self.beta, self.thr = float(acts[0][1]), float(acts[0][2])
 
     def _pack(self, W, rows: int, cols: int, transpose: bool, permute: bool):
-        key = ("pack", W.data_ptr(), rows, cols, transpose, permute, self.prec)
-        hit = _WCACHE.get(key)
-        if hit is None:
-            hit = self._pack_new(W, rows, cols, transpose, permute)
-            if _WCACHE_ON[0]:
-                _WCACHE[key] = hit
-        return hit
+        prep = _ACTIVE_PREP[0]
+        if prep is not None:
+            return prep.packed(W, rows, cols, transpose, permute, self.prec)
+        return self._pack_new(W, rows, cols, transpose, permute)
 
     def _pack_new(self, W, rows: int, cols: int, transpose: bool, permute: bool):
         hi = torch.empty(rows, cols, dtype=torch.bfloat16, device=W.device)
@@ -359,7 +471,20 @@ class ChainRun:
         self._chain(False, x, K0, self.rows_full, packs, [self.params[3 * l + 2] for l in range(L)], [None] * L, Y,
                     Ns, [a[0] for a in self.acts], w2row0=self.Ws[-1])
         self.Y = Y
+        # a training forward fetches the backward's transposed images too, so a model forward prepares them in the
+        # same batched launch (WeightPrep) instead of one pack launch each in the backward
+        self.bwd_packs = self._bwd_packs(K0) if keep else None
         return Y[-1].view(M) if dense_col0 else Y[-1]
+
+    def _bwd_packs(self, K0: int):
+        """Backward chain images: W_last^T (natural: B = dy from memory), then the earlier layers' W^T (register-fed,
+        permuted)."""
+        L = self.L
+        Ns = [W.shape[0] for W in self.Ws]
+        up = lambda n, k: k * ((n + k - 1) // k)
+        return [self._pack(self.Ws[L - 1], up(Ns[L - 2], 32), up(Ns[L - 1], 16), True, False)] + \
+               [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 32), up(Ns[l], 32), True, True)
+                for l in range(L - 2, -1, -1)]
 
     def backward(self, dy: torch.Tensor) -> torch.Tensor:
         """dy [M, N_last] (rows >= rows_full: column 0 only); accumulates the parameter gradients (grad_target) and
@@ -370,11 +495,7 @@ class ChainRun:
         L = self.L
         Ns = [W.shape[0] for W in self.Ws]
         acts = [a[0] for a in self.acts]
-        up = lambda n, k: k * ((n + k - 1) // k)
-        # backward chain: W_last^T (natural: B = dy from memory), then the earlier layers' W^T (register-fed, permuted)
-        packs = [self._pack(self.Ws[L - 1], up(Ns[L - 2], 32), up(Ns[L - 1], 16), True, False)] + \
-                [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 32), up(Ns[l], 32), True, True)
-                 for l in range(L - 2, -1, -1)]
+        packs = self.bwd_packs if self.bwd_packs is not None else self._bwd_packs(K0)
         dZl = _alloc(M, Ns[L - 1], dev) if acts[L - 1] != 0 else None
         dZ = [_alloc(M, Ns[l], dev) for l in range(L - 1)]
         dx = _alloc(M, K0, dev)
@@ -386,7 +507,7 @@ class ChainRun:
         dZ = dZ + [dZl if dZl is not None else dy]
         Xin = [x] + Y[:L - 1]
         rf = self.rows_full
-        dWs = _zeroed_views([tuple(self.params[3 * l + 1].shape) for l in range(L)], dev)
+        dWs = _dw_views([self.params[3 * l + 1] for l in range(L)], dev)
         for l in range(L):
             g, v, b = self.params[3 * l: 3 * l + 3]
             N, K = v.shape
@@ -406,10 +527,70 @@ class ChainRun:
             else:
                 gemm(TN, N, K, M, A, A.stride(0), B, B.stride(0), dW, K, accumulate=True,
                      splits=_splits_for(M, tiles), prec=self.prec, colsum=db)
-            weight_norm_bwd(g.reshape(-1), v, self.norms[l], dW, gt.reshape(-1) if gt is not None else
+            _wn_bwd(g.reshape(-1), v, self.norms[l], dW, gt.reshape(-1) if gt is not None else
                             torch.zeros(N, device=dev), vt if vt is not None else torch.zeros(N, K, device=dev))
-        self.Y = self.x = None
+        self.Y = self.x = self.bwd_packs = None
         return dx
+
+
+# Weight-norm backward of the layers, deferred inside a training backward (wn_bwd_begin / wn_bwd_flush, Trainer and
+# GraphTrainer) and then applied in one batched launch; immediate everywhere else (a bare loss.backward()).
+class _WnBwdItem(ctypes.Structure):
+    """MmsWnBwdItem (include/mms_hip.h)."""
+    _fields_ = [("g", ctypes.c_void_p), ("v", ctypes.c_void_p), ("norms", ctypes.c_void_p), ("N", ctypes.c_int64),
+                ("K", ctypes.c_int64), ("dW", ctypes.c_void_p), ("lddw", ctypes.c_int64), ("dg", ctypes.c_void_p),
+                ("dv", ctypes.c_void_p), ("row0", ctypes.c_int64)]
+
+
+_WN_BWD: List[Optional[dict]] = [None]     # v.data_ptr() -> (g, v, norms, dW, dg, dv), one entry per layer
+_WN_DW: List[Optional[dict]] = [None]      # v.data_ptr() -> the layer's dW accumulation buffer of this backward
+_WN_BWD_MAX = 32
+
+
+def wn_bwd_begin() -> None:
+    """Defer the weight-norm backward: every use of a layer in this backward (the SDF and radiance MLPs serve every
+    modality) accumulates its weight gradient into ONE dW buffer, and the flush applies the (linear) weight-norm
+    backward once per layer -- no two blocks of the batched launch update the same parameter."""
+    _WN_BWD[0] = {}
+    _WN_DW[0] = {}
+
+
+def _dw_views(vs, dev) -> List[torch.Tensor]:
+    """Zeroed dW accumulation buffers of layers (their v tensors): fresh per call, or shared per layer while the
+    weight-norm backward is deferred."""
+    st = _WN_DW[0]
+    if st is None:
+        return _zeroed_views([tuple(v.shape) for v in vs], dev)
+    missing = [v for v in vs if v.data_ptr() not in st]
+    if missing:
+        for v, buf in zip(missing, _zeroed_views([tuple(v.shape) for v in missing], dev)):
+            st[v.data_ptr()] = buf
+    return [st[v.data_ptr()] for v in vs]
+
+
+def wn_bwd_flush() -> None:
+    """Apply the deferred weight-norm gradients (batches of up to 32 layers per launch)."""
+    items = list((_WN_BWD[0] or {}).values())
+    _WN_BWD[0] = _WN_DW[0] = None
+    for i in range(0, len(items or []), _WN_BWD_MAX):
+        chunk = items[i:i + _WN_BWD_MAX]
+        arr, row0 = (_WnBwdItem * len(chunk))(), 0
+        for j, (g, v, nrm, dW, dg, dv) in enumerate(chunk):
+            N, K = v.shape
+            arr[j] = _WnBwdItem(g.data_ptr(), v.data_ptr(), nrm.data_ptr(), N, K, dW.data_ptr(), dW.stride(0),
+                                dg.data_ptr(), dv.data_ptr(), row0)
+            row0 += N
+        _lib.call("mms_weight_norm_bwd_batched", ctypes.cast(arr, ctypes.c_void_p), len(chunk), row0, _s())
+
+
+def _wn_bwd(g, v, norms, dW, dg, dv) -> None:
+    st = _WN_BWD[0]
+    if st is not None:
+        # once per layer (dW is the layer's shared accumulation buffer); the tensors stay referenced until the flush
+        if v.data_ptr() not in st:
+            st[v.data_ptr()] = (g, v, norms, dW, dg, dv)
+    else:
+        weight_norm_bwd(g, v, norms, dW, dg, dv)
 
 
 def _zeroed_views(shapes, dev) -> List[Optional[torch.Tensor]]:
@@ -522,9 +703,7 @@ def _sdf_mlp_unfused(ctx, X, M, params, dev):
     H = run.forward(X, keep=True)
     g3, v3, b3 = params[-3:]
     N3, K3 = v3.shape
-    W3 = _alloc(N3, K3, dev)
-    n3 = torch.empty(N3, device=dev)
-    weight_norm_fwd(g3.reshape(-1), v3, W3, n3)
+    W3, n3 = normed_weight(g3, v3)
     out = _alloc(5 * M, N3, dev)
     prec = PRECISION["sdf"]
     gemm(NT, M, N3, K3, H, H.stride(0), W3, W3.stride(0), out, out.stride(0), bias=b3, prec=prec)
@@ -541,13 +720,13 @@ def _sdf_mlp_unfused_bwd(ctx, dout, params, dev):
     N3, K3 = v3.shape
     gt, vt, bt = grad_target(g3), grad_target(v3), grad_target(b3)
     if gt is not None or vt is not None or bt is not None:
-        dW3 = torch.zeros(N3, K3, device=dev)
+        dW3 = _dw_views([v3], dev)[0]
         db3 = bt if bt is not None else torch.zeros(N3, device=dev)
         gemm(TN, N3, K3, M, dout, dout.stride(0), H, H.stride(0), dW3, K3, accumulate=True,
              splits=_splits_for(M, 6), prec=prec, colsum=db3)
         gemm(TN, 1, K3, 4 * M, dout[M:], dout.stride(0), H[M:], H.stride(0), dW3, K3, accumulate=True,
              splits=_splits_for(4 * M, 2), prec=prec, colsum=db3)
-        weight_norm_bwd(g3.reshape(-1), v3, ctx.n3, dW3, gt.reshape(-1) if gt is not None else
+        _wn_bwd(g3.reshape(-1), v3, ctx.n3, dW3, gt.reshape(-1) if gt is not None else
                         torch.zeros(N3, device=dev), vt if vt is not None else torch.zeros(N3, K3, device=dev))
     # dZ of the last hidden layer = (dout W3) * softplus'(Z) -- the activation gradient fused as aux
     run = ctx.run
@@ -891,9 +1070,7 @@ def _mlp_strided(run: MLPRun, H: torch.Tensor, Fb: int) -> torch.Tensor:
     N, K = v.shape
     M = H.shape[0]
     dev = H.device
-    W = _alloc(N, K, dev)
-    nrm = torch.empty(N, device=dev)
-    weight_norm_fwd(g.reshape(-1), v, W, nrm)
+    W, nrm = normed_weight(g, v)
     act, beta, thr = run.acts[0]
     Y = torch.empty(M, N, device=dev)
     Z = _alloc(M, N, dev)
@@ -913,13 +1090,13 @@ def _mlp_strided_bwd(run: MLPRun, dy: torch.Tensor, H: torch.Tensor, Fb: int):
     act_bwd(dy, run.Zs[0], act, beta, thr, dZ)
     gt, vt, bt = grad_target(g), grad_target(v), grad_target(b)
     if gt is not None or vt is not None or bt is not None:
-        dW = torch.zeros(N, K, device=dev)
+        dW = _dw_views([v], dev)[0]
         db = bt if bt is not None else torch.zeros(N, device=dev)
         gemm(TN, N, K, M, dZ, dZ.stride(0), H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1),
              prec=run.prec, colsum=db)
         dg = gt.reshape(-1) if gt is not None else torch.zeros(N, device=dev)
         dv = vt if vt is not None else torch.zeros(N, K, device=dev)
-        weight_norm_bwd(g.reshape(-1), v, run.norms[0], dW, dg, dv)
+        _wn_bwd(g.reshape(-1), v, run.norms[0], dW, dg, dv)
     dxin = _alloc(M, K, dev)
     gemm(NN, M, K, N, dZ, dZ.stride(0), run.Ws[0], run.Ws[0].stride(0), dxin, dxin.stride(0), prec=run.prec)
     return dxin, [None, None, None]

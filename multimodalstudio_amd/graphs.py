@@ -37,7 +37,7 @@ import torch
 
 from . import _lib
 from . import functions as fx
-from .pipeline import Trainer, compute_loss, curvature_factor, lr_factor, select_right_channel
+from .pipeline import Trainer, backward_batched, compute_loss, curvature_factor, lr_factor, select_right_channel
 
 
 CAPTURE_MODE = None   # override of the capture_error_mode (probes)
@@ -159,7 +159,7 @@ class GraphTrainer:
                 band = t.masks[m][c[:, 1].long(), c[:, 2].long()].long()[:, None]
                 outputs[m][m] = select_right_channel(outputs[m][m], band)
         losses, total = compute_loss(outputs, targets, t.modalities, t.step, max_iters=t.cfg.max_iters)
-        total.backward()
+        backward_batched(total)
         return losses, total
 
     def _optimizer(self):

@@ -575,7 +575,10 @@ class BaseModel(nn.Module):
 
     # -- forward ----------------------------------------------------------------------------------------
     def forward(self, rays: Dict[str, Dict[str, torch.Tensor]], rng: Optional[RNG] = None, cap: Optional[int] = None):
-        fx.begin_forward()       # weight-norm / packed-weight cache scope (functions.normed_weight)
+        if getattr(self, "_prep", None) is None:
+            self._prep = fx.WeightPrep()    # not a module attribute: the state_dict stays the reference's
+        dev = next(iter(rays.values()))["origins"].device
+        fx.begin_forward(self._prep, dev)   # every layer's W and MMA images prepared in one batch, looked up below
         try:
             return self._forward(rays, rng, cap)
         finally:

@@ -289,6 +289,15 @@ class TrainConfig:
     gpu_sampler: bool = False           # draw pixels on the device (data.GPUPixelSampler) instead of the host
 
 
+def backward_batched(total: torch.Tensor) -> None:
+    """total.backward() with the layers' weight-norm gradients applied in one batched launch at its end."""
+    fx.wn_bwd_begin()
+    try:
+        total.backward()
+    finally:
+        fx.wn_bwd_flush()
+
+
 class Trainer:
     """Synthetic-scene trainer: frames resident in HBM, host pixel sampler, full train step on the HIP path."""
 
@@ -401,10 +410,10 @@ class Trainer:
             hook = lambda g: ddp.grad_ready(g, groups)  # noqa: E731
             fx.GRAD_READY_HOOKS.append(hook)
             try:
-                total.backward()
+                backward_batched(total)
             finally:
                 fx.GRAD_READY_HOOKS.remove(hook)
             ddp.finish_step(groups)
         else:
-            total.backward()
+            backward_batched(total)
         return losses, total, outputs

@@ -20,17 +20,27 @@ PREC = {"0": "fp32", "1": "bf16", "2": "bf16x3"}
 MODE = {("false", "false"): "NT", ("false", "true"): "NN", ("true", "true"): "TN"}
 
 
-def label(name):
+CHAIN_ROLES = {  # (bwd, KS0, NT2, NL, KEEP) -> the role label bench.py's chain_work gives the same launch
+    (False, 5, 9, 3, True): "sdf_fwd", (False, 5, 9, 3, False): "sdf_infer_fwd",
+    (False, 20, 8, 3, True): "radiance_fwd", (True, 17, 3, 3, False): "sdf_bwd", (True, 16, 10, 3, False): "radiance_bwd",
+    (False, 3, 8, 4, True): "bg_base_fwd", (False, 18, 4, 4, True): "bg_head_fwd", (False, 18, 8, 4, True): "bg_head_fwd",
+    (True, 16, 2, 4, False): "bg_base_bwd", (True, 8, 9, 4, False): "bg_head_bwd", (True, 16, 9, 4, False): "bg_head_bwd",
+}
+
+
+def label(name, grid=0):
     m = re.search(r"gemm_kernel<(\d), (true|false), (true|false), (true|false)>", name)
     if m:
         return f"mms_gemm:{PREC[m.group(1)]}:{MODE.get((m.group(2), m.group(3)), '??')}"
-    m = re.search(r"chain_kernel<(\d), \d+, \d+, \d+, \d+, (true|false)", name)
+    m = re.search(r"chain_kernel<(\d), (\d+), \d+, \d+, (\d+), (true|false), \d, \d, \d, \d, (true|false), (\d)>", name)
     if m:
-        return f"mms_mlp_chain:{PREC[m.group(1)]}:chain_{'bwd' if m.group(2) == 'true' else 'fwd'}"
+        key = (m.group(4) == "true", int(m.group(2)), int(m.group(3)), int(m.group(6)), m.group(5) == "true")
+        return f"mms_mlp_chain:{PREC[m.group(1)]}:{CHAIN_ROLES.get(key, 'other')}"
     if "hashgrid_bwd" in name:
         return "mms_hashgrid_bwd_grouped"
     if "hashgrid_fwd_kernel" in name:
-        return "mms_hashgrid_fwd"
+        # thread per (point, level): the SDF [centre | 4 taps] batch is the launch with > 200k points
+        return "mms_hashgrid_fwd:sdf_taps" if grid > 200000 * 16 else "mms_hashgrid_fwd:other"
     return None
 
 
@@ -39,7 +49,7 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        lab = label(r["Kernel_Name"])
+        lab = label(r["Kernel_Name"], int(float(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)))
         if lab:
             acc[lab].append(float(r["Counter_Value"]) * 1024.0)
     return acc

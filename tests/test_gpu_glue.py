@@ -87,3 +87,65 @@ def test_render_stats(dev):
     assert (stats[:, 4:5] - dep).abs().max().item() < 1e-5
     # the lower clip is active for rays with little accumulated weight
     assert (dep[sidx] == steps.min()).any()
+
+
+def test_weight_prep_batched_matches_single(dev):
+    """WeightPrep: after the registering forward, the two batched launches (mms_weight_norm_fwd_batched,
+    mms_mlp_pack_batched) reproduce every entry bit for bit against the single-layer mms_weight_norm_fwd /
+    mms_mlp_pack, including the backward-orientation images, after a parameter update."""
+    from multimodalstudio_amd import functions as fx
+    from multimodalstudio_amd.pipeline import TrainConfig, Trainer
+    fx.set_precision("fast")
+    try:
+        t = Trainer(TrainConfig(method="grid", modalities=("rgb",), num_rays_per_modality=256, log2T=12, width=64,
+                                height=48, n_views=6), dev)
+        t.set_step(95000)
+        t.train_step()                        # registers every entry (computed one by one), tables uploaded at its end
+        prep = t.model._prep
+        assert prep.norm_items and prep.pack_items and not prep.dirty
+        assert prep.n_up[0] == len(prep.norm_items) and prep.n_up[2] == len(prep.pack_items)
+        t.train_step()                        # batched
+        fx.begin_forward(prep, dev)           # one more batched preparation on the updated parameters
+        fx.end_forward()
+        torch.cuda.synchronize()
+        for g, v, W, nrm, idx in prep.norm.values():
+            W1, n1 = fx.normed_weight(g, v)   # outside a scope: the single-layer kernel
+            assert torch.equal(W, W1) and torch.equal(nrm, n1)
+        for key, (W, hi, lo, idx) in prep.pack.items():
+            _, _, rows, cols, tr, pm, prec = key
+            run = fx.ChainRun([torch.zeros(1)] * 9, [(1, 1.0, 20.0)] * 3, prec)
+            h1, l1 = run._pack_new(W, rows, cols, tr, pm)
+            assert torch.equal(hi, h1) and (lo is None or torch.equal(lo, l1))
+    finally:
+        fx.set_precision("fp32")
+
+
+def test_weight_norm_bwd_batched_matches_immediate(dev):
+    """The training backward's deferred, batched weight-norm gradients (mms_weight_norm_bwd_batched) equal the
+    immediate per-layer mms_weight_norm_bwd on the same forward (to float-atomic summation order)."""
+    from multimodalstudio_amd import functions as fx
+    from multimodalstudio_amd.pipeline import TrainConfig, Trainer
+    fx.set_precision("fast")
+    try:
+        t = Trainer(TrainConfig(method="grid", modalities=("rgb",), num_rays_per_modality=256, log2T=12, width=64,
+                                height=48, n_views=6), dev)
+        t.set_step(95000)
+        coords, sel = t.sampler.sample(t.frames)
+        targets = t.targets_for(coords, sel)
+        grads = []
+        for batched in (True, False):
+            t.model.seed_draws(7, dev)
+            if batched:
+                t.compute_grads(coords, targets)
+            else:
+                begin, fx.wn_bwd_begin = fx.wn_bwd_begin, lambda: None
+                try:
+                    t.compute_grads(coords, targets)
+                finally:
+                    fx.wn_bwd_begin = begin
+            torch.cuda.synchronize()
+            grads.append(t.fields.grad.clone())
+        scale = float(grads[1].abs().max())
+        assert float((grads[0] - grads[1]).abs().max()) <= 1e-4 * scale
+    finally:
+        fx.set_precision("fp32")
