@@ -105,7 +105,8 @@ def work_fns():
         "mms_gemm": gemm_work,
         "mms_mlp_chain": chain_work,
         "mms_hashgrid_fwd": hash_fwd_work,
-        "mms_hashgrid_bwd_grouped": lambda a: (float(a[1]) * a[2] * HASH_BWD_B, float(a[1]) * a[2] * HASH_BWD_ATOMIC_B),
+        "mms_hashgrid_bwd_grouped": lambda a: ("sdf_taps" if a[2] == 5 else "radiance_or_bg",
+                                               (float(a[1]) * a[2] * HASH_BWD_B, float(a[1]) * a[2] * HASH_BWD_ATOMIC_B)),
     }
 
 
@@ -309,7 +310,8 @@ def main():
         keys = ["kernel", "achieved", "peak", "unit", "frac", "avg_ms", "traffic", "atomic_ceiling"]
         hash_roof = {d: {k: by_name[n][k] for k in keys if k in by_name[n]}
                      for d, n in [("fwd", "mms_hashgrid_fwd:sdf_taps"), ("fwd_radiance", "mms_hashgrid_fwd:radiance"),
-                                  ("bwd", "mms_hashgrid_bwd_grouped")] if n in by_name}
+                                  ("bwd", "mms_hashgrid_bwd_grouped:sdf_taps"),
+                                  ("bwd_radiance", "mms_hashgrid_bwd_grouped:radiance_or_bg")] if n in by_name}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -134,110 +134,141 @@ __global__ __launch_bounds__(256) void samples_bwd_kernel(const float* __restric
   }
 }
 
-// ------------------------------------------------------------------ NeuS up-sampling step (one thread per ray)
-constexpr int kMaxBins = 80;
+// ------------------------------------------------------------------ NeuS up-sampling step (one wave per ray)
+// Lane k owns sample k: its sdf gather, section cosine, the two sigmoids and alpha run in parallel across the wave.
+// The transmittance cumprod, the weight sum and the CDF cumsum keep the reference's sequential double order: every
+// lane runs the same uniform loop over the broadcast values, so the results are those of a single sequential thread
+// bit for bit.  The inverse-CDF lookups (lane j = new bin j) and the stable merge (each element's output slot = its
+// own index + the number of elements of the other list before it) are parallel again.  One wave per ray spreads a
+// step over every CU (a thread per ray kept a ~1700-ray step on 27 waves).
+constexpr int kMaxBins = 64;   // samples + 1 edges per ray held on the lanes
+constexpr int kWavesPerBlock = 4;
 
-__global__ __launch_bounds__(64) void neus_step_kernel(
+// the wave's LDS writes are visible to its later LDS reads (program order within one wave; no compiler reordering)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(256) void neus_step_kernel(
     int64_t R, int S, const float* __restrict__ bins, const float* __restrict__ sdf_prev, int s_prev,
     const float* __restrict__ sdf_new, int n_prev_new, const int* __restrict__ prev_idx,
     const float* __restrict__ nears, const float* __restrict__ fars, float inv_s, const float* __restrict__ rand,
     const float* __restrict__ u_lin, int n_new, float* __restrict__ sdf_out, float* __restrict__ new_bins,
     float* __restrict__ merged_bins, int* __restrict__ sorted_idx) {
-  __shared__ float s_cdf[64][kMaxBins + 1];
-  __shared__ float s_sdf[64][kMaxBins];
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
-  float* cdf = s_cdf[threadIdx.x];
-  float* sdf = s_sdf[threadIdx.x];
+  __shared__ float s_b[kWavesPerBlock][kMaxBins];     // bin edges b[0..S]
+  __shared__ float s_w[kWavesPerBlock][kMaxBins];     // padded weights, then the CDF (cdf[0..S])
+  __shared__ float s_n[kWavesPerBlock][kMaxBins];     // new bins
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + wv;
+  if (r >= R) return;                                  // wave-uniform
+  float* sb = s_b[wv];
+  float* sw = s_w[wv];
+  float* sn = s_n[wv];
   const float* b = bins + r * (S + 1);
+  const float bk = lane <= S ? b[lane] : 0.f;
+  if (lane <= S) sb[lane] = bk;
   // (a) merged sdf for the current samples
-  for (int j = 0; j < S; ++j) {
-    float v;
+  float sdf_k = 0.f;
+  if (lane < S) {
     if (prev_idx) {
-      const int id = prev_idx[r * S + j];
-      v = id < s_prev ? sdf_prev[r * s_prev + id] : sdf_new[r * n_prev_new + (id - s_prev)];
+      const int id = prev_idx[r * S + lane];
+      sdf_k = id < s_prev ? sdf_prev[r * s_prev + id] : sdf_new[r * n_prev_new + (id - s_prev)];
     } else {
-      v = sdf_new[r * S + j];
+      sdf_k = sdf_new[r * S + lane];
     }
-    sdf[j] = v;
-    sdf_out[r * S + j] = v;
+    sdf_out[r * S + lane] = sdf_k;
   }
   const float nr = nears[r], fr = fars[r];
-  // (b-d) fixed-inv_s alphas and weights (w_{S-1} = 0), sequential cumprod
-  // torch.cumprod / cumsum on CPU accumulate in double (at::acc_type<float, false>) and round each
-  // output to float: do the same so the CDF (and hence searchsorted) matches.
-  double T = 1.0;
-  float prev_cos = 0.0f;
-  float e_cur = fr * b[0] + nr * (1 - b[0]);
-  for (int k = 0; k < S - 1; ++k) {
-    const float e_nxt = fr * b[k + 1] + nr * (1 - b[k + 1]);
-    const float dl = e_nxt - e_cur;
-    e_cur = e_nxt;
-    const float pv = sdf[k], nx = sdf[k + 1];
-    const float mid = (pv + nx) * 0.5f;
-    float cs = (nx - pv) / (dl + 1e-5f);
-    float cmin = fminf(prev_cos, cs);
-    prev_cos = cs;
-    cmin = fminf(fmaxf(cmin, -1e3f), 0.0f);
-    const float pe = mid - cmin * dl * 0.5f;
-    const float ne = mid + cmin * dl * 0.5f;
+  // (b-d) section k = [k, k+1] (k < S - 1): cosine with the previous section's, alpha
+  const float e_k = fr * bk + nr * (1 - bk);
+  const float e_n = __shfl_down(e_k, 1);
+  const float sdf_n = __shfl_down(sdf_k, 1);
+  const float dl = e_n - e_k;
+  const float mid = (sdf_k + sdf_n) * 0.5f;
+  const float cs = (sdf_n - sdf_k) / (dl + 1e-5f);
+  float prev_cos = __shfl_up(cs, 1);
+  if (lane == 0) prev_cos = 0.0f;
+  float cmin = fminf(prev_cos, cs);
+  cmin = fminf(fmaxf(cmin, -1e3f), 0.0f);
+  const float pe = mid - cmin * dl * 0.5f;
+  const float ne = mid + cmin * dl * 0.5f;
+  float alpha = 0.f;
+  if (lane < S - 1) {
     const float pc = sigm(pe * inv_s), nc = sigm(ne * inv_s);
-    const float alpha = (pc - nc + 1e-5f) / (pc + 1e-5f);
-    const float w = alpha * (float)T;
-    T = T * (double)(1.0f - alpha + 1e-7f);
-    cdf[k + 1] = w;  // stash weights (shifted by one)
+    alpha = (pc - nc + 1e-5f) / (pc + 1e-5f);
   }
-  cdf[S] = 0.0f;
+  // sequential transmittance (torch.cumprod on CPU: double accumulation, float outputs), uniform across the wave
+  double T = 1.0;
+  float w_k = 0.0f;   // w_{S-1} = 0
+  for (int k = 0; k < S - 1; ++k) {
+    const float a = __shfl(alpha, k);
+    const float w = a * (float)T;
+    if (lane == k) w_k = w;
+    T = T * (double)(1.0f - a + 1e-7f);
+  }
   // (e) pdf / cdf with padding 1e-5 (histogram_padding) and eps 1e-5
-  for (int k = 0; k < S; ++k) cdf[k + 1] = cdf[k + 1] + 1e-5f;
+  const float wp = w_k + 1e-5f;
+  if (lane < S) sw[lane] = wp;
+  wave_sync();
   // torch.sum(weights, -1) in ATen's CPU summation order (not sequential), so weights_sum has the same bits
-  float wsum = mms::torch_cpu_row_sum(cdf + 1, S);
+  float wsum = mms::torch_cpu_row_sum(sw, S);
   const float pad = fmaxf(1e-5f - wsum, 0.f);
   const float padk = pad / (float)S;
   wsum = wsum + pad;
   double run = 0.0;
-  cdf[0] = 0.f;
+  float cdf_k1 = 0.f;   // lane k: cdf[k + 1]
   for (int k = 0; k < S; ++k) {
-    const float w = cdf[k + 1] + padk;
+    const float w = __shfl(wp, k) + padk;
     run = run + (double)(w / wsum);
-    cdf[k + 1] = fminf(1.0f, (float)run);
+    if (lane == k) cdf_k1 = fminf(1.0f, (float)run);
   }
-  // (f-g) inverse CDF at u_j = lin_j + rand / nb (searchsorted right)
+  // cdf[0] = 0, cdf[k + 1] from lane k (the weights above are consumed: the array is reused)
+  wave_sync();
+  if (lane < S) sw[lane + 1] = cdf_k1;
+  if (lane == 0) sw[0] = 0.f;
+  wave_sync();
+  // (f-g) inverse CDF at u_j = lin_j + rand / nb (searchsorted right), lane j = new bin j
   const int nb = n_new + 1;
   // training: u_j = lin_j + rand / nb (single jitter); eval: u_j = lin_j + 1 / (2 nb) (ray_samplers.py:365-377)
   const float rj = rand ? rand[r] / (float)nb : (float)(1.0 / (2.0 * nb));
-  float* nbo = new_bins + r * nb;
-  for (int j = 0; j < nb; ++j) {
-    const float u = u_lin[j] + rj;
+  float nbo = 0.f;
+  if (lane < nb) {
+    const float u = u_lin[lane] + rj;
     int lo = 0, hi = S + 1;  // first index with cdf > u
     while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (cdf[mid] > u) hi = mid; else lo = mid + 1;
+      const int m = (lo + hi) >> 1;
+      if (sw[m] > u) hi = m; else lo = m + 1;
     }
     const int inds = lo;
     const int below = min(max(inds - 1, 0), S);
     const int above = min(max(inds, 0), S);
-    const float c0 = cdf[below], c1 = cdf[above];
-    const float b0 = b[below], b1 = b[above];
+    const float c0 = sw[below], c1 = sw[above];
+    const float b0 = sb[below], b1 = sb[above];
     float t = (u - c0) / (c1 - c0);
     if (isnan(t)) t = 0.f;
     t = fminf(fmaxf(t, 0.f), 1.f);
-    nbo[j] = b0 + t * (b1 - b0);
+    nbo = b0 + t * (b1 - b0);
+    new_bins[r * nb + lane] = nbo;
+    sn[lane] = nbo;
   }
-  // (h) stable merge of the start lists; end = max of the ends
+  wave_sync();
+  // (h) stable merge of the start lists (ties: the first list first); end = max of the ends
   float* mb = merged_bins + r * (S + n_new + 1);
   int* si = sorted_idx + r * (S + n_new);
-  int i1 = 0, i2 = 0, o = 0;
-  while (i1 < S || i2 < n_new) {
-    bool take1;
-    if (i1 >= S) take1 = false;
-    else if (i2 >= n_new) take1 = true;
-    else take1 = !(nbo[i2] < b[i1]);  // ties keep the first list first (stable)
-    if (take1) { mb[o] = b[i1]; si[o] = i1; ++i1; }
-    else { mb[o] = nbo[i2]; si[o] = S + i2; ++i2; }
-    ++o;
+  if (lane < S) {
+    int before = 0;
+    for (int j = 0; j < n_new; ++j) before += sn[j] < bk;
+    mb[lane + before] = bk;
+    si[lane + before] = lane;
   }
-  mb[S + n_new] = fmaxf(b[S], nbo[n_new]);
+  if (lane < n_new) {
+    int before = 0;
+    for (int i = 0; i < S; ++i) before += sb[i] <= nbo;
+    mb[lane + before] = nbo;
+    si[lane + before] = S + lane;
+  }
+  if (lane == 0) mb[S + n_new] = fmaxf(sb[S], sn[n_new]);
 }
 
 }  // namespace
@@ -280,10 +311,11 @@ MMS_EXPORT int mms_neus_step(int64_t R, int S, const float* bins, const float* s
                              const float* fars, float inv_s, const float* rand, const float* u_lin, int n_new,
                              float* sdf_out, float* new_bins, float* merged_bins, int* sorted_idx, void* stream) {
   const char* fn = "mms_neus_step";
-  MMS_REQUIRE(S >= 2 && S + n_new <= kMaxBins, fn, "sample count out of range");
+  MMS_REQUIRE(S >= 2 && S + 1 <= kMaxBins && n_new + 1 <= kMaxBins, fn, "sample count out of range (one wave per ray)");
   if (R == 0) return 0;
-  hipLaunchKernelGGL(neus_step_kernel, dim3(mms::grid_for(R, 64, INT32_MAX)), dim3(64), 0, mms::as_stream(stream), R,
-                     S, bins, sdf_prev, s_prev, sdf_new, n_prev_new, prev_idx, nears, fars, inv_s, rand, u_lin, n_new,
-                     sdf_out, new_bins, merged_bins, sorted_idx);
+  hipLaunchKernelGGL(neus_step_kernel, dim3((unsigned)((R + kWavesPerBlock - 1) / kWavesPerBlock)),
+                     dim3(64 * kWavesPerBlock), 0, mms::as_stream(stream), R, S, bins, sdf_prev, s_prev, sdf_new,
+                     n_prev_new, prev_idx, nears, fars, inv_s, rand, u_lin, n_new, sdf_out, new_bins, merged_bins,
+                     sorted_idx);
   return mms::check_launch(fn);
 }

@@ -37,7 +37,8 @@ def label(name, grid=0):
         key = (m.group(4) == "true", int(m.group(2)), int(m.group(3)), int(m.group(6)), m.group(5) == "true")
         return f"mms_mlp_chain:{PREC[m.group(1)]}:{CHAIN_ROLES.get(key, 'other')}"
     if "hashgrid_bwd" in name:
-        return "mms_hashgrid_bwd_grouped"
+        # hashgrid_bwd_walk_kernel<GROUP, ...>: the SDF batch walks 5 rows (centre + 4 taps) per thread
+        return "mms_hashgrid_bwd_grouped:sdf_taps" if "walk_kernel<5" in name else "mms_hashgrid_bwd_grouped:radiance_or_bg"
     if "hashgrid_fwd_kernel" in name:
         # thread per (point, level): the SDF [centre | 4 taps] batch is the launch with > 200k points
         return "mms_hashgrid_fwd:sdf_taps" if grid > 200000 * 16 else "mms_hashgrid_fwd:other"
