@@ -372,7 +372,7 @@ class MLPRun:
                 db = bt if bt is not None else torch.zeros(N, device=dev)
                 tiles = ((N + 127) // 128) * ((K + 127) // 128)
                 gemm(TN, N, K, M, dZ, dZ.stride(0), Xin, Xin.stride(0), dW, K, accumulate=True,
-                     splits=_splits_for(M, tiles), prec=self.prec, colsum=db)
+                     splits=_splits_for(M, tiles, self.prec), prec=self.prec, colsum=db)
                 dg = gt.reshape(-1) if gt is not None else torch.zeros(N, device=dev)
                 dv = vt if vt is not None else torch.zeros(N, K, device=dev)
                 _wn_bwd(g.reshape(-1), v, self.norms[l], dW, dg, dv)
@@ -521,12 +521,12 @@ class ChainRun:
             if l == L - 1 and rf < M:
                 # rows past rows_full carry only the output column 0
                 gemm(TN, N, K, rf, A, A.stride(0), B, B.stride(0), dW, K, accumulate=True,
-                     splits=_splits_for(rf, tiles), prec=self.prec, colsum=db)
+                     splits=_splits_for(rf, tiles, self.prec), prec=self.prec, colsum=db)
                 gemm(TN, 1, K, M - rf, A[rf:], A.stride(0), B[rf:], B.stride(0), dW, K, accumulate=True,
-                     splits=_splits_for(M - rf, 2), prec=self.prec, colsum=db)
+                     splits=_splits_for(M - rf, 2, self.prec), prec=self.prec, colsum=db)
             else:
                 gemm(TN, N, K, M, A, A.stride(0), B, B.stride(0), dW, K, accumulate=True,
-                     splits=_splits_for(M, tiles), prec=self.prec, colsum=db)
+                     splits=_splits_for(M, tiles, self.prec), prec=self.prec, colsum=db)
             _wn_bwd(g.reshape(-1), v, self.norms[l], dW, gt.reshape(-1) if gt is not None else
                             torch.zeros(N, device=dev), vt if vt is not None else torch.zeros(N, K, device=dev))
         self.Y = self.x = self.bwd_packs = None
@@ -723,9 +723,9 @@ def _sdf_mlp_unfused_bwd(ctx, dout, params, dev):
         dW3 = _dw_views([v3], dev)[0]
         db3 = bt if bt is not None else torch.zeros(N3, device=dev)
         gemm(TN, N3, K3, M, dout, dout.stride(0), H, H.stride(0), dW3, K3, accumulate=True,
-             splits=_splits_for(M, 6), prec=prec, colsum=db3)
+             splits=_splits_for(M, 6, prec), prec=prec, colsum=db3)
         gemm(TN, 1, K3, 4 * M, dout[M:], dout.stride(0), H[M:], H.stride(0), dW3, K3, accumulate=True,
-             splits=_splits_for(4 * M, 2), prec=prec, colsum=db3)
+             splits=_splits_for(4 * M, 2, prec), prec=prec, colsum=db3)
         _wn_bwd(g3.reshape(-1), v3, ctx.n3, dW3, gt.reshape(-1) if gt is not None else
                         torch.zeros(N3, device=dev), vt if vt is not None else torch.zeros(N3, K3, device=dev))
     # dZ of the last hidden layer = (dout W3) * softplus'(Z) -- the activation gradient fused as aux
@@ -1092,7 +1092,7 @@ def _mlp_strided_bwd(run: MLPRun, dy: torch.Tensor, H: torch.Tensor, Fb: int):
     if gt is not None or vt is not None or bt is not None:
         dW = _dw_views([v], dev)[0]
         db = bt if bt is not None else torch.zeros(N, device=dev)
-        gemm(TN, N, K, M, dZ, dZ.stride(0), H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1),
+        gemm(TN, N, K, M, dZ, dZ.stride(0), H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1, run.prec),
              prec=run.prec, colsum=db)
         dg = gt.reshape(-1) if gt is not None else torch.zeros(N, device=dev)
         dv = vt if vt is not None else torch.zeros(N, K, device=dev)

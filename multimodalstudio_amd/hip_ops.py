@@ -128,6 +128,11 @@ def act_bwd(dY, Z, act, beta, thr, dZ):
               float(thr), dZ.data_ptr(), dZ.stride(0), _stream())
 
 
-def _splits_for(M_rows: int, tiles: int) -> int:
-    target = max(1, 1024 // max(1, tiles))
+# split-K target: blocks per weight-gradient GEMM (measured, scratch/tn_sweep.py): one 128x128-tile block per CU for
+# bf16 operands (more splits only add float atomics), two for split-bf16x3 (3 MFMAs per product), four for fp32
+_SPLIT_BLOCKS = {0: 1024, 1: 256, 2: 512}
+
+
+def _splits_for(M_rows: int, tiles: int, prec: int = 0) -> int:
+    target = max(1, _SPLIT_BLOCKS.get(int(prec), 1024) // max(1, tiles))
     return int(max(1, min(target, M_rows // 512)))
