@@ -10,6 +10,6 @@ export TMPDIR=/tmp
 cd /tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $C --output-format csv -d $R/gpurun_out/pmc_${PREC}_$C -o run -- \
-    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing --precision $PREC \
+    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing --secondary "" --precision $PREC \
     > $R/gpurun_out/pmc_${PREC}_$C.log 2>&1
 done
