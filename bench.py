@@ -43,7 +43,7 @@ BF16_MFMA_PEAK_TF = 2500.0  # dense bf16 MFMA peak (no sparsity), MI355X_MICROAR
 # split-bf16x3 runs 3 bf16 MFMAs per f32 product: its ceiling for the algorithmic 2MNK flops is a third
 MFMA_PEAK_TF = {"fp32": F32_MFMA_PEAK_TF, "bf16": BF16_MFMA_PEAK_TF, "bf16x3": BF16_MFMA_PEAK_TF / 3}
 PREC_NAMES = {0: "fp32", 1: "bf16", 2: "bf16x3"}
-DTYPES = {"fp32": "fp32", "fast": "bf16 MFMA (fp32 accumulate; SDF MLP split-bf16x3), fp32 elsewhere",
+DTYPES = {"fp32": "fp32", "fast": "bf16 MFMA (fp32 accumulate; SDF MLP and polarization heads split-bf16x3), fp32 elsewhere",
           "bf16x3": "split-bf16x3 MFMA (fp32-accurate), fp32 elsewhere"}
 HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per lookup, forward
 HASH_BWD_B = 128 + 12 + 16 * 8 * 2 * (4 + 4)    # bytes per lookup, backward (table grads)

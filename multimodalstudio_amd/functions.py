@@ -33,12 +33,14 @@ ACT = {None: 0, "None": 0, "ReLU": 1, "Softplus": 2, "Sigmoid": 3}
 # GEMM operand precision per MLP family: 0 exact fp32 MFMA (parity mode), 1 bf16, 2 split bf16x3.
 PRECISION = {"sdf": 0, "radiance": 0, "heads": 0, "background": 0, "mlp": 0}
 PRESETS = {
-    "fp32": {"sdf": 0, "radiance": 0, "heads": 0, "background": 0, "mlp": 0},
+    "fp32": {"sdf": 0, "radiance": 0, "heads": 0, "pol_head": 0, "background": 0, "mlp": 0},
     # throughput mode: the SDF MLP keeps ~fp32 operand precision (its 4-tap finite differences divide
     # sdf differences by 4 delta ~ 4.5e-3), everything else runs bf16 MFMA with fp32 accumulation; the analytic-
     # gradient MLP fields (mlp methods, differentiated twice) stay on the exact fp32 MFMA
-    "fast": {"sdf": 2, "radiance": 1, "heads": 1, "background": 1, "mlp": 0},
-    "bf16x3": {"sdf": 2, "radiance": 2, "heads": 2, "background": 2, "mlp": 2},
+    # (the polarization heads keep split-bf16x3 too: their Stokes outputs are combined into intensities by
+    # differences, and their PSNR after training moved by ~0.2 dB in bf16, tests/test_gpu_train_parity.py)
+    "fast": {"sdf": 2, "radiance": 1, "heads": 1, "pol_head": 2, "background": 1, "mlp": 0},
+    "bf16x3": {"sdf": 2, "radiance": 2, "heads": 2, "pol_head": 2, "background": 2, "mlp": 2},
 }
 
 
@@ -979,9 +981,11 @@ class RadInputFunction(torch.autograd.Function):
 # plain MLP (heads)
 # ------------------------------------------------------------------------------------------------
 class MLPFunction(torch.autograd.Function):
+    """A plain weight-normed MLP (modality heads) on the GEMM engine; ``key`` names its PRECISION entry."""
+
     @staticmethod
-    def forward(ctx, x, acts, *params):
-        run = MLPRun(params, acts, PRECISION["heads"])
+    def forward(ctx, x, acts, key, *params):
+        run = MLPRun(params, acts, PRECISION[key])
         # grad mode is off inside Function.forward: decide from what the graph will need
         y = run.forward(x.contiguous(), keep=any(ctx.needs_input_grad))
         ctx.run = run
@@ -992,7 +996,7 @@ class MLPFunction(torch.autograd.Function):
     def backward(ctx, dy):
         dx, grads = ctx.run.backward(dy.contiguous(), need_dx=ctx.needs_input_grad[0])
         ctx.run = None
-        return (dx, None, *grads)
+        return (dx, None, None, *grads)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -69,6 +69,7 @@ class MLP(nn.Module):
         if not config.weight_norm:
             raise NotImplementedError("the HIP MLP implements the weight-normed layers used by every method config")
         self.config = config
+        self.precision_key = "heads"      # functions.PRECISION entry of its GEMMs when run as a plain MLP
         self.input_dim = input_dim
         self.output_dim = output_dim if output_dim is not None else config.hidden_dim
         self.skips = tuple(config.skip_connections or ())
@@ -126,7 +127,7 @@ class MLP(nn.Module):
     def forward(self, x):
         if self.skips:
             return self.forward_diff(x)
-        return fx.MLPFunction.apply(x, self.acts, *self.params())
+        return fx.MLPFunction.apply(x, self.acts, self.precision_key, *self.params())
 
     def forward_diff(self, x: torch.Tensor) -> torch.Tensor:
         """MLP.forward (mlp.py:152-171) with every product on the twice-differentiable HIP GEMM (autodiff.MatMul) and
@@ -243,6 +244,8 @@ class ModalityHead(nn.Module):
         self.kind = kind
         cfg = MLPConfig(num_layers=num_layers, hidden_dim=hidden_dim, out_activation=out_activation)
         self.field = MLP(cfg, input_dim, 3 if kind == "polarization" else output_dim)
+        if kind == "polarization":
+            self.field.precision_key = "pol_head"
 
     def forward(self, x, directions=None, up_directions=None, S: int = 1):
         y = self.field(x)
@@ -547,6 +550,8 @@ class BaseModel(nn.Module):
                     bg_heads[m] = ModalityHead("plain", 128, c, 1, 64, "Sigmoid")
         self.background_model = BackgroundModel(NeRFField(bg_base, bg_head, dens), bg_heads)
         self._lin = {}
+        # training shortcut (SURVEY §8(d) MLP FLOPs note): heads of other modalities only feed outputs no loss reads
+        self.own_heads_only = False
 
     # -- callbacks (BEFORE_TRAIN_ITERATION), restated from the reference schedules --------------------
     def set_step(self, step: int, max_iters: int = 100000):
@@ -640,7 +645,12 @@ class BaseModel(nn.Module):
             density, bfeat = self.background_model.field(bpos, d, sp.bg_samples)
             bw = fx.DensityWeightsFunction.apply(density, bdeltas, sp.bg_samples)
             bg_out = {}
+            # every head on every modality's rays (radiance_model.py:143-149) -- or, with own_heads_only (training:
+            # only the ray's own modality's output reaches the loss, raw_pipeline.py:112-122), just its own
+            heads_for = [mod] if (self.own_heads_only and torch.is_grad_enabled()) else None
             for m, head in self.background_model.modality_heads.items():
+                if heads_for is not None and m not in heads_for:
+                    continue
                 vals = head(bfeat, d, up, sp.bg_samples)
                 bg_out[m] = fx.CompositeFunction.apply(bw, vals, None, None, sp.bg_samples)
             # surface + radiance
@@ -651,6 +661,8 @@ class BaseModel(nn.Module):
             out = {}
             rows = N if cap is None else N + 1     # padded batches scatter into a dummy row N, cut off below
             for m, head in self.radiance_model.modality_heads.items():
+                if heads_for is not None and m not in heads_for:
+                    continue
                 vals = head(feat, d_h, up_h, S)
                 bg = bg_out[m]
                 if cap is not None:

@@ -287,6 +287,7 @@ class TrainConfig:
     skip_views: Optional[Dict[str, List[int]]] = None   # skip_image_indices_per_modality (datamanager config)
     data_dir: Optional[str] = None      # an on-disk MMS-DATA scene (data.MMSDataset) instead of the analytic one
     gpu_sampler: bool = False           # draw pixels on the device (data.GPUPixelSampler) instead of the host
+    own_heads_only: bool = True         # training renders each modality's rays through its own head only
 
 
 def backward_batched(total: torch.Tensor) -> None:
@@ -311,6 +312,9 @@ class Trainer:
         torch.manual_seed(654824)
         self.model = BaseModel(ModelSpec(channels, log2T=cfg.log2T, bg_kind=bg_kind, fields=fields)).to(device)
         self.model.draw_seed = (cfg.seed << 8) + 1000003 * rank + 17   # per-rank stream of the forward's draws
+        # training renders each modality's rays through its own head only (the loss reads nothing else; gradients are
+        # identical); evaluation (no grad) renders every head as the reference does
+        self.model.own_heads_only = cfg.own_heads_only
         self.dataset = None
         if cfg.data_dir is not None:
             # the train split of an on-disk scene: every frame but the eval views and the skipped ones

@@ -35,7 +35,7 @@ def test_mlp_golden(dev, name):
         for k in ["parametrizations.weight.original0", "parametrizations.weight.original1", "bias"]:
             params.append(torch.from_numpy(f[f"p:layers.{l}.{k}"]).to(dev).requires_grad_(True))
     x = torch.from_numpy(f["x"]).to(dev).requires_grad_(True)
-    y = fx.MLPFunction.apply(x, tuple(acts), *params)
+    y = fx.MLPFunction.apply(x, tuple(acts), "heads", *params)
     y.backward(torch.from_numpy(f["dy"]).to(dev))
     torch.cuda.synchronize()
     close(y.detach().cpu(), f["y"], 2e-6, "y")
