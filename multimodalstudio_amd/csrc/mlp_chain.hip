@@ -466,6 +466,14 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
       const f32x4* xs = &xring[s % kRing][wave][0];
       const f32x4 x0 = xs[64 * h + r], x1 = xs[64 * h + 32 + r];
       float v[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+      if constexpr (XIO) {
+        // scaled first, masked after: columns past K0 hold whatever the padded rows hold (possibly non-finite)
+        const f32x4* as = &aring[s % kRing][wave][0];
+        const f32x4 w0 = as[64 * h + r], w1 = as[64 * h + 32 + r];
+        const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= act_grad_out<XA>(wv[j], a.beta, a.thr);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (k0 + j >= a.K0) v[j] = 0.f;
@@ -476,12 +484,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
             if (k0 + j > 0) v[j] = 0.f;
         }
         if constexpr (XIO) {
-          const f32x4* as = &aring[s % kRing][wave][0];
-          const f32x4 w0 = as[64 * h + r], w1 = as[64 * h + 32 + r];
-          const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] *= act_grad_out<XA>(wv[j], a.beta, a.thr);
-          // K0 is a multiple of 8 here (dispatch): two unguarded 16-B stores
+          // xout rows hold at least 16 ks0 columns (dispatch): two unguarded 16-B stores, zeros past K0
           st_nt4(xo + k0, f32x4{v[0], v[1], v[2], v[3]});
           st_nt4(xo + k0 + 4, f32x4{v[4], v[5], v[6], v[7]});
         }
@@ -612,16 +615,20 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
   const int a0 = a.L[0].act, a1 = a.L[1].act, a2 = a.L[2].act, a3 = nl == 4 ? a.L[3].act : -1;
   const bool noxa = a.xaux == nullptr;
   const int nh = nl - 1;  // hidden (stored) layers
-  bool hidden_full = true, keep = true, nokeep = true, bwd_hidden = true;
+  bool hidden_full = true, keep = true, nokeep = true, bwd_hidden = true, hidden64 = true;
   for (int l = 0; l < nh; ++l) {
     hidden_full = hidden_full && a.L[l].N == 256;
+    hidden64 = hidden64 && a.L[l].N == 64;
     keep = keep && a.L[l].out != nullptr;
     nokeep = nokeep && a.L[l].out == nullptr;
     // backward: every hidden layer's dZ is stored and scaled by act'(Y) (the staged epilogue assumes all)
     bwd_hidden = bwd_hidden && a.L[l].aux != nullptr && a.L[l].out != nullptr;
   }
-  bwd_hidden = bwd_hidden && hidden_full;
-  const bool xio = !noxa && a.xact == 1 && a.xout != nullptr && a.K0 % 8 == 0;
+  const bool bwd_stored = bwd_hidden;
+  bwd_hidden = bwd_stored && hidden_full;
+  // the input scaling stores 16 ks0 columns per row (zeros past K0)
+  const bool xio = !noxa && a.xact == 1 && a.xout != nullptr && a.ldxout >= 16 * ks0;
+  const bool xio3 = !noxa && a.xact == 3 && a.xout != nullptr && a.ldxout >= 16 * ks0;
   if (nl == 3) {
     if (!bwd && ks0 == 5 && nt[0] == 8 && nt[1] == 8 && nt[2] == 9 && a0 == 2 && a1 == 2 && a2 == 0 && hidden_full &&
         (keep || nokeep)) {
@@ -643,6 +650,19 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
         bwd_hidden) {
       launch_chain<PREC, 16, 8, 8, 10, true, 1, 1, 0, 1>(a, s);
       return true;
+    }
+    if constexpr (PREC == 1) {
+      // the plain modality heads 256-64-64-C (ReLU, ReLU, Sigmoid; field_heads.py:71-88), C <= 32, bf16
+      if (!bwd && ks0 == 16 && nt[0] == 2 && nt[1] == 2 && nt[2] == 1 && a0 == 1 && a1 == 1 && a2 == 3 && hidden64 &&
+          keep) {
+        launch_chain<PREC, 16, 2, 2, 1, false, 1, 1, 3, 0, true>(a, s);
+        return true;
+      }
+      if (bwd && ks0 == 1 && nt[0] == 2 && nt[1] == 2 && nt[2] == 8 && a0 == 1 && a1 == 1 && a2 == 0 && xio3 &&
+          bwd_stored && hidden64) {
+        launch_chain<PREC, 1, 2, 2, 8, true, 1, 1, 0, 3>(a, s);
+        return true;
+      }
     }
     return false;
   }

@@ -498,7 +498,8 @@ class ChainRun:
         Ns = [W.shape[0] for W in self.Ws]
         acts = [a[0] for a in self.acts]
         packs = self.bwd_packs if self.bwd_packs is not None else self._bwd_packs(K0)
-        dZl = _alloc(M, Ns[L - 1], dev) if acts[L - 1] != 0 else None
+        # the scaled input's store writes 16 ceil(N/16) columns per row (zeros past N)
+        dZl = _alloc(M, 16 * ((Ns[L - 1] + 15) // 16), dev)[:, :Ns[L - 1]] if acts[L - 1] != 0 else None
         dZ = [_alloc(M, Ns[l], dev) for l in range(L - 1)]
         dx = _alloc(M, K0, dev)
         dy = dy if dy.stride(1) == 1 and dy.stride(0) % 4 == 0 else _copy_aligned(dy)
@@ -771,7 +772,10 @@ def _chain_shape(params, acts, prec: int = 2) -> bool:
     dims = [params[1].shape[1]] + [params[3 * l + 1].shape[0] for l in range(len(params) // 3)]
     a = tuple(x[0] for x in acts)
     if len(params) == 9:
-        return (dims == [71, 256, 256, 257] and a == (2, 2, 0)) or (dims == [317, 256, 256, 256] and a == (1, 1, 1))
+        if (dims == [71, 256, 256, 257] and a == (2, 2, 0)) or (dims == [317, 256, 256, 256] and a == (1, 1, 1)):
+            return True
+        # the plain modality heads 256-64-64-C, C <= 32 (bf16)
+        return prec == 1 and dims[:3] == [256, 64, 64] and dims[3] <= 32 and a == (1, 1, 3)
     if len(params) == 12 and prec == 1 and a == (1, 1, 1, 1):
         return dims in ([39, 256, 256, 256, 256], [283, 256, 256, 256, 128], [283, 256, 256, 256, 256])
     return False
@@ -985,16 +989,21 @@ class MLPFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, acts, key, *params):
-        run = MLPRun(params, acts, PRECISION[key])
+        run = mlp_runner(params, acts, PRECISION[key])
         # grad mode is off inside Function.forward: decide from what the graph will need
-        y = run.forward(x.contiguous(), keep=any(ctx.needs_input_grad))
+        x = x if (x.stride(-1) == 1 and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0) else _copy_aligned(x)
+        y = _run_forward(run, x, keep=any(ctx.needs_input_grad))
         ctx.run = run
         ctx.save_for_backward(*params)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        dx, grads = ctx.run.backward(dy.contiguous(), need_dx=ctx.needs_input_grad[0])
+        if isinstance(ctx.run, ChainRun):
+            dx = _run_backward(ctx.run, dy)
+            grads = [None] * len(ctx.run.params)
+        else:
+            dx, grads = ctx.run.backward(dy.contiguous(), need_dx=ctx.needs_input_grad[0])
         ctx.run = None
         return (dx, None, None, *grads)
 

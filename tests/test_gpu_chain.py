@@ -216,3 +216,50 @@ def test_chain_relu_layers(dev, dims):
     assert rel(dx.cpu(), ref_dx) < TOL[1]
     for i, p in enumerate(params):
         assert rel(p.grad.cpu(), ref_g[i]) < TOL[1], (i, rel(p.grad.cpu(), ref_g[i]))
+
+
+@pytest.mark.parametrize("C", [3, 1, 5])
+def test_chain_head(dev, C):
+    """A modality head 256-64-64-C (ReLU, ReLU, Sigmoid; field_heads.py:71-88) on the bf16 chain kernel: forward vs
+    fp64, backward (dx, every parameter gradient) vs the fp64 backward at the kernel's own activations (Sigmoid' from
+    the output), at a row count that is not a multiple of the 128-row block."""
+    from multimodalstudio_amd import functions as fx
+    dims = [256, 64, 64, C]
+    g = torch.Generator().manual_seed(C)
+    M = 1500
+    params = []
+    for l in range(3):
+        k, n = dims[l], dims[l + 1]
+        v = torch.randn(n, k, generator=g) / np.sqrt(k)
+        params += [v.norm(dim=1, keepdim=True).clone(), v, torch.randn(n, generator=g) * 0.1]
+    params = [p.to(dev).requires_grad_(True) for p in params]
+    acts = [(1, 1.0, 20.0), (1, 1.0, 20.0), (3, 1.0, 20.0)]
+    assert fx._chain_shape(params, acts, 1)
+    x = torch.randn(M, 256, generator=g)
+    run = fx.ChainRun(params, acts, 1)
+    y = run.forward(_panel(x, dev), keep=True)
+    h = x.double()
+    for l in range(3):
+        gg, v, b = [p.detach().double().cpu() for p in params[3 * l: 3 * l + 3]]
+        h = h @ torch._weight_norm(v, gg, 0).T + b
+        h = torch.relu(h) if l < 2 else torch.sigmoid(h)
+    assert rel(y.detach().cpu(), h) < TOL[1]
+    Y = [t.detach().clone().double().cpu() for t in run.Y]
+    dy = torch.randn(M, C, generator=g)
+    dx = run.backward(_panel(dy, dev))
+    torch.cuda.synchronize()
+    d = dy.double() * Y[2] * (1 - Y[2])
+    ins = [x.double(), Y[0], Y[1]]
+    ref = [None] * 9
+    for l in (2, 1, 0):
+        if l < 2:
+            d = d * (Y[l] > 0)
+        g64 = params[3 * l].detach().double().cpu().requires_grad_(True)
+        v64 = params[3 * l + 1].detach().double().cpu().requires_grad_(True)
+        W = torch._weight_norm(v64, g64, 0)
+        W.backward(d.T @ ins[l])
+        ref[3 * l], ref[3 * l + 1], ref[3 * l + 2] = g64.grad, v64.grad, d.sum(0)
+        d = d @ W.detach()
+    assert rel(dx.cpu(), d) < TOL[1]
+    for i, p in enumerate(params):
+        assert rel(p.grad.cpu(), ref[i]) < TOL[1], (i, rel(p.grad.cpu(), ref[i]))
