@@ -63,6 +63,15 @@ def gemm_work(a):
     return f"{PREC_NAMES[prec]}:{mode}", (2.0 * M * N * K, nbytes)
 
 
+def gemm_grouped_work(a):
+    """(precision label, (flops, bytes)) of one mms_gemm_tn_grouped launch: the weight gradients of one MLP's layers
+    (sum over items of 2 M N K flops; bytes = both operands once + dW read and written)."""
+    prec, n, M, N, K = a[0], a[1], a[2], a[3], a[4]
+    flops = sum(2.0 * M[i] * N[i] * K[i] for i in range(n))
+    nbytes = sum(4.0 * (float(K[i]) * (M[i] + N[i]) + 2.0 * M[i] * N[i]) for i in range(n))
+    return f"{PREC_NAMES[prec]}:TN_grouped", (flops, nbytes)
+
+
 def chain_work(a):
     """(precision label, (algorithmic flops, algorithmic HBM bytes)) of one mms_mlp_chain launch (include/mms_hip.h
     argument order): every layer's 2MNK, narrowed on the SDF tap rows (rows >= rows_full: one output column of the
@@ -93,9 +102,10 @@ def chain_work(a):
 
 
 def hash_fwd_work(a):
-    """(role, SURVEY §8(d) bytes) of one mms_hashgrid_fwd launch: the SDF batch [centre | 4 taps] (the dominant
+    """(role, SURVEY §8(d) bytes) of one mms_hashgrid_fwd(_grouped) launch: the SDF batch [centre | 4 taps] (the dominant
     launch), the sampler's / background's smaller 72-column panels, or the radiance panel."""
-    M, ldx = int(a[1]), int(a[2])
+    Mg, group, ldx = int(a[1]), int(a[2]), int(a[4])     # mms_hashgrid_fwd_grouped(pos, Mg, group, gstride, ldx, ...)
+    M = Mg * group
     role = "sdf_taps" if (ldx == 72 and M > 200000) else ("radiance" if ldx >= 300 else "sampler_or_bg")
     return role, float(M) * HASH_FWD_B
 
@@ -103,8 +113,9 @@ def hash_fwd_work(a):
 def work_fns():
     return {
         "mms_gemm": gemm_work,
+        "mms_gemm_tn_grouped": gemm_grouped_work,
         "mms_mlp_chain": chain_work,
-        "mms_hashgrid_fwd": hash_fwd_work,
+        "mms_hashgrid_fwd_grouped": hash_fwd_work,
         "mms_hashgrid_bwd_grouped": lambda a: ("sdf_taps" if a[2] == 5 else "radiance_or_bg",
                                                (float(a[1]) * a[2] * HASH_BWD_B, float(a[1]) * a[2] * HASH_BWD_ATOMIC_B)),
     }
@@ -120,7 +131,7 @@ def kernel_records(summ, timing_steps: int, precision: str):
         launches_per_step = n / timing_steps
         rec = {"kernel": name, "avg_ms": round(ms, 5), "launches_per_step": launches_per_step,
                "ms_per_step": round(ms * launches_per_step, 4), "traffic": None}
-        if name.startswith("mms_gemm") or name.startswith("mms_mlp_chain"):
+        if name.startswith("mms_gemm") or name.startswith("mms_mlp_chain"):   # (incl. mms_gemm_tn_grouped)
             flops, nbytes = work
             mode = name.split(":")[1]      # "mms_gemm:<precision>:<NT|NN|TN>", "mms_mlp_chain:<precision>:<role>"
             peak = F32_MFMA_PEAK_TF if mode == "fp32" else BF16_MFMA_PEAK_TF
@@ -206,6 +217,7 @@ def timed_run(config: str, args, dev, rank: int, ddp, steps: int, warmup: int) -
     cfg = TrainConfig(method=method, modalities=mods, num_rays_per_modality=args.rays, log2T=args.log2T,
                       skip_views=skip, gpu_sampler=args.sampler == "device")
     trainer = Trainer(cfg, dev, rank=rank)
+    trainer.model.concurrent_background = not args.serial_background
     trainer.set_step(args.start_step)
     runner = None
     if args.mode == "graph":
@@ -258,6 +270,8 @@ def main():
     ap.add_argument("--sampler", default="device", choices=["device", "host"],
                     help="pixel sampler: HBM-resident frames + device Philox draws (default), or the reference-order "
                          "host sampler with a per-step upload")
+    ap.add_argument("--serial-background", action="store_true",
+                    help="run the background branch on the main stream (default: its own stream, overlapped)")
     ap.add_argument("--mode", default="graph", choices=["graph", "eager"],
                     help="graph: hipGraph-captured steps (multimodalstudio_amd/graphs.py); eager: Python-launched")
     ap.add_argument("--secondary", default="grid_raw5", help="also time this config (nested 'secondary' record); "
@@ -286,11 +300,15 @@ def main():
     # bracketed by HIP events on the stream it is launched on (a graph replay cannot bracket single kernels)
     timing_steps = max(1, args.timing_steps)
     if not args.no_kernel_timing:
+        # the background branch on the main stream here: a launch's events then bracket that kernel alone, not the
+        # time it shares the chip with the overlapped background stream
+        trainer.model.concurrent_background = False
         _lib.TIMER.start(work_fns())
         for _ in range(timing_steps):
             trainer.train_step(ddp=ddp)
         torch.cuda.synchronize()
         _lib.TIMER.stop()
+        trainer.model.concurrent_background = not args.serial_background
 
     rays_per_step, value, ms_per_step, run_mode = run["rays_per_step"], run["value"], run["ms_per_step"], run["step_mode"]
 
@@ -309,7 +327,7 @@ def main():
                     roof[k] = top[k]
         keys = ["kernel", "achieved", "peak", "unit", "frac", "avg_ms", "traffic", "atomic_ceiling"]
         hash_roof = {d: {k: by_name[n][k] for k in keys if k in by_name[n]}
-                     for d, n in [("fwd", "mms_hashgrid_fwd:sdf_taps"), ("fwd_radiance", "mms_hashgrid_fwd:radiance"),
+                     for d, n in [("fwd", "mms_hashgrid_fwd_grouped:sdf_taps"), ("fwd_radiance", "mms_hashgrid_fwd_grouped:radiance"),
                                   ("bwd", "mms_hashgrid_bwd_grouped:sdf_taps"),
                                   ("bwd_radiance", "mms_hashgrid_bwd_grouped:radiance_or_bg")] if n in by_name}
 
@@ -349,7 +367,8 @@ def main():
                        "pixel_sampler": args.sampler, "parallelism": f"dp{world}",
                        "step_mode": run_mode},
             "kernel_timing": (f"{timing_steps} eager steps of the same workload after the timed region, HIP events "
-                              "around every watched launch on its stream" if not args.no_kernel_timing else None),
+                              "around every watched launch on its stream (background branch serialized for these steps so "
+                              "each launch is timed alone)" if not args.no_kernel_timing else None),
             "roofline": roof,
             "roofline_hash_grid": hash_roof,
             "roofline_kernels": kernels,

@@ -34,6 +34,12 @@ const char* mms_last_error(void);
  * HashEncoding.forward, encodings.py:263-304). */
 int mms_hashgrid_fwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L, int log2T, int F,
                      const float* scales, float radius, int active_levels, float* out, int64_t ldo, void* stream);
+/* Forward over Mg groups of `group` rows (row = g + j * gstride, j < group; group 1 or 5): the SDF batch
+ * [centre | 4 taps] (surface_model.py:138-160) gathered in (sample, tap) order, so a sample's centre and taps --
+ * which share cells at the coarse levels -- hit one L2.  Same values as mms_hashgrid_fwd on every row. */
+int mms_hashgrid_fwd_grouped(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx,
+                             const float* table, int L, int log2T, int F, const float* scales, float radius,
+                             int active_levels, float* out, int64_t ldo, void* stream);
 int mms_hashgrid_bwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L, int log2T, int F,
                      const float* scales, float radius, int active_levels, const float* dout, int64_t ldd,
                      float* dtable, float* dpos, int64_t lddx, void* stream);
@@ -55,6 +61,15 @@ int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N, int64_t K
              const float* B, int64_t ldb, float* C, int64_t ldc, const float* bias, float* Z, int64_t ldz,
              const float* aux, int64_t ldaux, int act, int dact, float beta, float thr, int accumulate, int splits,
              int ones_col, float* colsum, void* stream);
+/* The weight gradients of up to 5 layers in ONE launch (the layers of one MLP after its fused backward): for each
+ * item i, C_i[M_i, N_i] += A_i^T B_i with A_i stored [K_i, M_i] (dZ, lda_i) and B_i stored [K_i, N_i] (X, ldb_i),
+ * K_i = rows, plus colsum_i[m] += sum_k A_i[k][m] (the bias gradient) when colsum (or colsum[i]) is non-null.
+ * Replaces the per-layer mms_gemm(trans_a = trans_b = 1, ...) calls of the nn.Linear weight gradients
+ * (field_components/mlp.py:152-171 under autograd); the K slices (split-K, float atomics) are sized per item for
+ * about target_blocks blocks in all. */
+int mms_gemm_tn_grouped(int prec, int n, const int64_t* M, const int64_t* N, const int64_t* K,
+                        const float* const* A, const int64_t* lda, const float* const* B, const int64_t* ldb,
+                        float* const* C, const int64_t* ldc, float* const* colsum, int target_blocks, void* stream);
 
 /* ---- fused MLP chains (MLP.forward mlp.py:152-171 under weight norm :206-209, all layers in one launch) for the
  * SDF field (71-256-256-257, Softplus(100), surface_field.py:99-116), the radiance field (317-256-256-256, ReLU,

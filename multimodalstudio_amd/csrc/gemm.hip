@@ -31,6 +31,9 @@
 #ifndef MMS_GEMM_ABLATE
 #define MMS_GEMM_ABLATE 0
 #endif
+#ifndef MMS_GEMM_XCDSPLIT
+#define MMS_GEMM_XCDSPLIT 1
+#endif
 
 namespace {
 
@@ -236,11 +239,33 @@ __device__ __forceinline__ void epi_tile(const floatx16& a, int64_t rbase, int64
 }
 
 // ---------------------------------------------------------------------------- kernel
+// split-K tile map: id -> (tile, slice).  XCD-grouped: the tiles of one K slice share an XCD (ids x, x + 8, x + 16, ...
+// under round-robin dispatch), so the slice's rows -- read by every tile of its row / column -- come from HBM into that
+// XCD's L2 once; the slices spread over the 8 XCDs (the slice count is padded to a multiple of 8 at launch).
+// Returns false for a padding id.
+__device__ __forceinline__ bool split_map(int id, int m_tiles_pad, int n_tiles, int splits, int& mt, int& nt,
+                                          int& slice) {
+  const int tiles = m_tiles_pad * n_tiles;
+#if MMS_GEMM_XCDSPLIT
+  const int j = id >> 3;
+  const int t = j % tiles;
+  slice = (j / tiles) * 8 + (id & 7);
+  if (slice >= splits) return false;
+#else
+  const int t = id % tiles;
+  slice = id / tiles;
+#endif
+  mt = t % m_tiles_pad;
+  nt = t / m_tiles_pad;
+  return true;
+}
+
+// one 128 x 128 output tile (mt, nt) over K slice `slice`
 template <int PREC, bool TA, bool TB, bool VEC>
-__global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A,
-                                                   int64_t lda, const float* __restrict__ B, int64_t ldb,
-                                                   float* __restrict__ C, int64_t ldc, Epi ep, int64_t k_per_split,
-                                                   int m_tiles_pad, int n_tiles) {
+__device__ __forceinline__ void gemm_block(int mt, int nt, int slice, int64_t M, int64_t N, int64_t K,
+                                           const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
+                                           int64_t ldb, float* __restrict__ C, int64_t ldc, const Epi& ep,
+                                           int64_t k_per_split) {
   using G = Geo<PREC>;
   using E = typename G::elem;
   constexpr int BK = G::BK;
@@ -250,22 +275,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t
   E* As = lds;
   E* Bs = lds + A_ELEMS;
 
-  // tile map.  Unsplit: XCD-aware -- ids b and b + 8 (same XCD under round-robin dispatch) take the N-tiles
-  // of one M panel, so the panel is fetched into one L2.  Split-K: id -> (tile, slice), consecutive ids on
-  // different tiles/slices, spreading the work over all 8 XCDs.
-  const int id = blockIdx.x;
-  int mt, nt, slice = 0;
-  if (ep.splits > 1) {
-    const int tiles = m_tiles_pad * n_tiles;
-    const int t = id % tiles;
-    slice = id / tiles;
-    mt = t % m_tiles_pad;
-    nt = t / m_tiles_pad;
-  } else {
-    nt = (id >> 3) % n_tiles;
-    mt = (id & 7) + 8 * (id / (8 * n_tiles));
-    if (mt >= m_tiles_pad) return;
-  }
   const int64_t m0 = (int64_t)mt * BM;
   const int64_t n0 = (int64_t)nt * BN;
   if (m0 >= M) return;
@@ -288,23 +297,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t
     }
   };
 
-  float4 ra[BK / 8], rb[BK / 8];
-  uint32_t ma = 0, mb = 0;
-  if (kbeg < kend) {
-    ma = stage_load<BK, TA, VEC>(A, lda, m0, M, kbeg, kend, ra);
-    mb = stage_load<BK, TB, VEC>(B, ldb, n0, N, kbeg, kend, rb);
-  }
-  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();
-    stage_store<PREC, TA>(As, ra, ma);
-    stage_store<PREC, TB>(Bs, rb, mb);
-    if (do_cs) colsum_acc(ra);
-    __syncthreads();
-    if (k0 + BK < kend) {
-      ma = stage_load<BK, TA, VEC>(A, lda, m0, M, k0 + BK, kend, ra);
-      mb = stage_load<BK, TB, VEC>(B, ldb, n0, N, k0 + BK, kend, rb);
-    }
-    const int ar0 = wm * 64, br0 = wn * 64;
+  const int ar0 = wm * 64, br0 = wn * 64;
+  auto compute = [&]() {
     if constexpr ((MMS_GEMM_ABLATE & 2) != 0) {
       acc00[0] += (float)As[lane] + (float)Bs[lane];  // keep the staging alive
     } else if constexpr (PREC == P_F32) {
@@ -343,6 +337,39 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t
         acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc11, 0, 0, 0);
       }
     }
+  };
+
+  // Global loads run DEPTH k-steps ahead of the MFMAs in DEPTH register sets (unrolled, so every set is addressed
+  // statically).
+  constexpr int DEPTH = 1;   // 2 measured no faster for the weight gradients (bf16x3 5 % slower: register pressure)
+  float4 ra[DEPTH][BK / 8], rb[DEPTH][BK / 8];
+  uint32_t ma[DEPTH] = {}, mb[DEPTH] = {};
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) {
+    const int64_t k = kbeg + (int64_t)d * BK;
+    if (k < kend) {
+      ma[d] = stage_load<BK, TA, VEC>(A, lda, m0, M, k, kend, ra[d]);
+      mb[d] = stage_load<BK, TB, VEC>(B, ldb, n0, N, k, kend, rb[d]);
+    }
+  }
+  for (int64_t k0 = kbeg; k0 < kend; k0 += DEPTH * BK) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const int64_t k = k0 + (int64_t)d * BK;
+      if (k < kend) {
+        __syncthreads();
+        stage_store<PREC, TA>(As, ra[d], ma[d]);
+        stage_store<PREC, TB>(Bs, rb[d], mb[d]);
+        if (do_cs) colsum_acc(ra[d]);
+        __syncthreads();
+        const int64_t kn = k + (int64_t)DEPTH * BK;
+        if (kn < kend) {
+          ma[d] = stage_load<BK, TA, VEC>(A, lda, m0, M, kn, kend, ra[d]);
+          mb[d] = stage_load<BK, TB, VEC>(B, ldb, n0, N, kn, kend, rb[d]);
+        }
+        compute();
+      }
+    }
   }
 
   if (do_cs) {  // reduce the 8 threads sharing t % 32 through LDS, then one atomic per column
@@ -365,6 +392,63 @@ __global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t
   epi_tile<PREC>(acc01, rbase, cbase + 32, M, N, C, ldc, ep);
   epi_tile<PREC>(acc10, rbase + 32, cbase, M, N, C, ldc, ep);
   epi_tile<PREC>(acc11, rbase + 32, cbase + 32, M, N, C, ldc, ep);
+}
+
+template <int PREC, bool TA, bool TB, bool VEC>
+__global__ __launch_bounds__(256) void gemm_kernel(int64_t M, int64_t N, int64_t K, const float* __restrict__ A,
+                                                   int64_t lda, const float* __restrict__ B, int64_t ldb,
+                                                   float* __restrict__ C, int64_t ldc, Epi ep, int64_t k_per_split,
+                                                   int m_tiles_pad, int n_tiles) {
+  // Unsplit: XCD-aware -- ids b and b + 8 (same XCD under round-robin dispatch) take the N-tiles of one M panel, so
+  // the panel is fetched into one L2.  Split-K: split_map.
+  const int id = blockIdx.x;
+  int mt, nt, slice = 0;
+  if (ep.splits > 1) {
+    if (!split_map(id, m_tiles_pad, n_tiles, ep.splits, mt, nt, slice)) return;
+  } else {
+    nt = (id >> 3) % n_tiles;
+    mt = (id & 7) + 8 * (id / (8 * n_tiles));
+    if (mt >= m_tiles_pad) return;
+  }
+  gemm_block<PREC, TA, TB, VEC>(mt, nt, slice, M, N, K, A, lda, B, ldb, C, ldc, ep, k_per_split);
+}
+
+// ---------------------------------------------------------------------------- grouped weight gradients
+// The weight gradients of every layer of one MLP in ONE launch: dW_i += dZ_i^T X_i (+ the bias-gradient column sums),
+// item i owning a contiguous, 8-aligned run of block ids.  Sharing the launch lets each layer fill the chip with 8x
+// fewer K slices than a launch of its own (the items' tiles together make the blocks), and the split-K atomics --
+// one 64 KB tile of float adds per block, at the memory side's ~1.3 TB/s -- shrink with the slice count.
+struct TnItem {
+  int64_t M, N, K;   // C[M, N] += A^T B, A [K, M] (lda), B [K, N] (ldb): M = out units, N = in units, K = rows
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  float* C;
+  int64_t ldc;
+  float* colsum;
+  int64_t kps;       // rows per slice
+  int mt, nt, zs;    // tiles and K slices
+  int blocks;        // 8 * ceil(mt nt zs / 8)... (mt nt * zs rounded so every item starts on an XCD-group boundary)
+};
+constexpr int kMaxTnItems = 5;
+struct TnGroup {
+  TnItem it[kMaxTnItems];
+  int n;
+};
+
+template <int PREC, bool VEC>
+__global__ __launch_bounds__(256) void gemm_tn_grouped_kernel(TnGroup g) {
+  int id = blockIdx.x, i = 0;
+  while (i + 1 < g.n && id >= g.it[i].blocks) {
+    id -= g.it[i].blocks;
+    ++i;
+  }
+  const TnItem& t = g.it[i];
+  int mt, nt, slice;
+  if (!split_map(id, t.mt, t.nt, t.zs, mt, nt, slice)) return;
+  Epi ep{nullptr, nullptr, 0, nullptr, 0, ACT_NONE, ACT_NONE, 1.f, 20.f, 1, -1, t.zs > 1 ? t.zs : 2, t.colsum};
+  gemm_block<PREC, true, true, VEC>(mt, nt, slice, t.M, t.N, t.K, t.A, t.lda, t.B, t.ldb, t.C, t.ldc, ep, t.kps);
 }
 
 template <int PREC, bool TA, bool TB>
@@ -418,15 +502,82 @@ MMS_EXPORT int mms_gemm(int prec, int trans_a, int trans_b, int64_t M, int64_t N
   const int64_t mt = (M + BM - 1) / BM;
   const int64_t mtp = zs > 1 ? mt : ((mt + 7) / 8) * 8;
   const int64_t nt = (N + BN - 1) / BN;
-  MMS_REQUIRE(mtp * nt * zs <= INT32_MAX, fn, "grid too large");
+  MMS_REQUIRE(mtp * nt * (zs + 7) <= INT32_MAX, fn, "grid too large");
   Epi ep{bias, Z, ldz, aux, ldaux, act, dact, beta, thr, accumulate, ones_col, (int)zs, colsum};
-  dim3 grid((unsigned)(mtp * nt * zs), 1, 1);
+  const int64_t zs_grid = (zs > 1 && MMS_GEMM_XCDSPLIT) ? (zs + 7) / 8 * 8 : zs;
+  dim3 grid((unsigned)(mtp * nt * zs_grid), 1, 1);
   hipStream_t s = mms::as_stream(stream);
   const int64_t kp = K == 0 ? 0 : kps;
   switch (prec) {
     case P_F32: dispatch_ta_tb<P_F32>(trans_a, trans_b, vec, grid, s, M, N, K, A, lda, B, ldb, C, ldc, ep, kp, (int)mtp, (int)nt); break;
     case P_BF16: dispatch_ta_tb<P_BF16>(trans_a, trans_b, vec, grid, s, M, N, K, A, lda, B, ldb, C, ldc, ep, kp, (int)mtp, (int)nt); break;
     default: dispatch_ta_tb<P_BF16X3>(trans_a, trans_b, vec, grid, s, M, N, K, A, lda, B, ldb, C, ldc, ep, kp, (int)mtp, (int)nt); break;
+  }
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_gemm_tn_grouped(int prec, int n, const int64_t* M, const int64_t* N, const int64_t* K,
+                                   const float* const* A, const int64_t* lda, const float* const* B,
+                                   const int64_t* ldb, float* const* C, const int64_t* ldc, float* const* colsum,
+                                   int target_blocks, void* stream) {
+  const char* fn = "mms_gemm_tn_grouped";
+  MMS_REQUIRE(prec >= 0 && prec <= 2, fn, "prec must be 0 (f32), 1 (bf16) or 2 (bf16x3)");
+  MMS_REQUIRE(n >= 1 && n <= kMaxTnItems, fn, "1 to 5 weight-gradient items per launch");
+  MMS_REQUIRE(M && N && K && A && lda && B && ldb && C && ldc, fn, "null argument array");
+  if (target_blocks < 1) target_blocks = 256;
+  const int BK = prec == P_BF16 ? Geo<P_BF16>::BK : Geo<P_F32>::BK;
+  TnGroup g{};
+  double work = 0.0;
+  for (int i = 0; i < n; ++i) {
+    MMS_REQUIRE(M[i] >= 0 && N[i] >= 0 && K[i] >= 0, fn, "negative size");
+    MMS_REQUIRE(M[i] == 0 || N[i] == 0 || K[i] == 0 || (A[i] && B[i] && C[i]), fn, "null operand");
+    work += (double)((M[i] + BM - 1) / BM) * ((N[i] + BN - 1) / BN) * (double)K[i];
+  }
+  bool vec = true;
+  int64_t total = 0;
+  int m = 0;
+  for (int i = 0; i < n; ++i) {
+    if (M[i] == 0 || N[i] == 0 || K[i] == 0) continue;   // nothing to add
+    TnItem& t = g.it[m++];
+    t.M = M[i]; t.N = N[i]; t.K = K[i];
+    t.A = A[i]; t.lda = lda[i]; t.B = B[i]; t.ldb = ldb[i]; t.C = C[i]; t.ldc = ldc[i];
+    t.colsum = colsum ? colsum[i] : nullptr;
+    t.mt = (int)((t.M + BM - 1) / BM);
+    t.nt = (int)((t.N + BN - 1) / BN);
+    // K slices in proportion to the item's share of the work (every block then streams the same number of rows),
+    // rounded to a multiple of 8 so the slices of each tile spread evenly over the 8 XCDs (split_map), at least
+    // 512 rows each
+    const double share = (double)t.mt * t.nt * (double)t.K / work;
+    int64_t zs = (int64_t)(share * target_blocks / (t.mt * t.nt) + 0.5);
+    zs = zs >= 8 ? (zs + 4) / 8 * 8 : zs;
+    if (zs > t.K / 512) zs = t.K / 512;
+    if (zs < 1) zs = 1;
+    int64_t kps = (t.K + zs - 1) / zs;
+    kps = (kps + BK - 1) / BK * BK;
+    t.kps = kps;
+    t.zs = (int)((t.K + kps - 1) / kps);
+    t.blocks = t.mt * t.nt * ((t.zs + 7) / 8 * 8);
+    total += t.blocks;
+    vec = vec && ((uintptr_t)t.A & 15) == 0 && ((uintptr_t)t.B & 15) == 0 && t.lda % 4 == 0 && t.ldb % 4 == 0;
+  }
+  g.n = m;
+  if (m == 0) return 0;
+  MMS_REQUIRE(total <= INT32_MAX, fn, "grid too large");
+  hipStream_t s = mms::as_stream(stream);
+  dim3 grid((unsigned)total), blk(256);
+  switch (prec) {
+    case P_F32:
+      if (vec) hipLaunchKernelGGL((gemm_tn_grouped_kernel<P_F32, true>), grid, blk, 0, s, g);
+      else hipLaunchKernelGGL((gemm_tn_grouped_kernel<P_F32, false>), grid, blk, 0, s, g);
+      break;
+    case P_BF16:
+      if (vec) hipLaunchKernelGGL((gemm_tn_grouped_kernel<P_BF16, true>), grid, blk, 0, s, g);
+      else hipLaunchKernelGGL((gemm_tn_grouped_kernel<P_BF16, false>), grid, blk, 0, s, g);
+      break;
+    default:
+      if (vec) hipLaunchKernelGGL((gemm_tn_grouped_kernel<P_BF16X3, true>), grid, blk, 0, s, g);
+      else hipLaunchKernelGGL((gemm_tn_grouped_kernel<P_BF16X3, false>), grid, blk, 0, s, g);
+      break;
   }
   return mms::check_launch(fn);
 }

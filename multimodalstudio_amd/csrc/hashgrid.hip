@@ -77,15 +77,21 @@ __device__ __forceinline__ Corners make_corners(float x, float y, float z, float
   return c;
 }
 
-template <bool ALIGNED>
-__global__ __launch_bounds__(256) void hashgrid_fwd_kernel(const float* __restrict__ pos, int64_t M,
-                                                           int64_t ldx, const float2* __restrict__ table,
-                                                           GridParams p, float* __restrict__ out,
-                                                           int64_t ldo) {
+// G > 1 (the SDF panel: centre rows g, tap rows g + j * gstride, j < G): the lanes walk the points in (g, j) order, so
+// the centre and the 4 taps of one sample -- which share their cells at every level coarser than the tap offset --
+// and the next samples of the same ray are gathered by the same wave: their corner lines are fetched from MALL / HBM
+// into one L2 once instead of by five waves on (under round-robin dispatch) five different XCDs.
+template <bool ALIGNED, int G>
+__global__ __launch_bounds__(256) void hashgrid_fwd_kernel(const float* __restrict__ pos, int64_t Mg,
+                                                           int64_t gstride, int64_t ldx,
+                                                           const float2* __restrict__ table, GridParams p,
+                                                           float* __restrict__ out, int64_t ldo) {
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t pt = tid >> 4;
+  const int64_t q = tid >> 4;
   const int level = (int)(tid & 15);
-  if (pt >= M || level >= p.levels) return;
+  const int64_t g = G == 1 ? q : q / G;
+  const int64_t pt = G == 1 ? q : g + (q - g * G) * gstride;
+  if (g >= Mg || level >= p.levels) return;
   float2 r = make_float2(0.f, 0.f);
   if (level < p.active_levels) {
     const float* xp = pos + pt * ldx;
@@ -242,27 +248,48 @@ int fill_params(const char* fn, GridParams& p, int L, int log2T, const float* sc
 
 }  // namespace
 
-MMS_EXPORT int mms_hashgrid_fwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L,
-                                int log2T, int F, const float* scales, float radius, int active_levels,
-                                float* out, int64_t ldo, void* stream) {
-  const char* fn = "mms_hashgrid_fwd";
+MMS_EXPORT int mms_hashgrid_fwd_grouped(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx,
+                                        const float* table, int L, int log2T, int F, const float* scales, float radius,
+                                        int active_levels, float* out, int64_t ldo, void* stream) {
+  const char* fn = "mms_hashgrid_fwd_grouped";
   MMS_REQUIRE(F == 2, fn, "features_per_level must be 2");
-  MMS_REQUIRE(M >= 0 && ldx >= 3 && ldo >= 2 * L, fn, "bad shapes");
+  MMS_REQUIRE(Mg >= 0 && ldx >= 3 && ldo >= 2 * L, fn, "bad shapes");
+  MMS_REQUIRE(group == 1 || group == 5, fn, "group must be 1 (plain) or 5 (centre + 4 taps)");
+  MMS_REQUIRE(group == 1 || gstride >= Mg, fn, "group rows overlap (gstride < groups)");
   GridParams p;
   int rc = fill_params(fn, p, L, log2T, scales, radius, active_levels);
   if (rc) return rc;
-  if (M == 0) return 0;
+  if (Mg == 0) return 0;
   MMS_REQUIRE(pos && table && out, fn, "null pointer");
   MMS_REQUIRE(((uintptr_t)out & 3) == 0, fn, "output must be 4-B aligned");
-  const int64_t threads = M * 16;
+  const int64_t threads = Mg * group * 16;
+  const unsigned blocks = mms::grid_for(threads, 256, INT32_MAX);
   const bool aligned = ((uintptr_t)out & 7) == 0 && (ldo & 1) == 0;
-  if (aligned)
-    hipLaunchKernelGGL(hashgrid_fwd_kernel<true>, dim3(mms::grid_for(threads, 256, INT32_MAX)), dim3(256), 0,
-                       mms::as_stream(stream), pos, M, ldx, reinterpret_cast<const float2*>(table), p, out, ldo);
-  else
-    hipLaunchKernelGGL(hashgrid_fwd_kernel<false>, dim3(mms::grid_for(threads, 256, INT32_MAX)), dim3(256), 0,
-                       mms::as_stream(stream), pos, M, ldx, reinterpret_cast<const float2*>(table), p, out, ldo);
+  const float2* t2 = reinterpret_cast<const float2*>(table);
+  hipStream_t s = mms::as_stream(stream);
+  if (group == 5) {
+    if (aligned)
+      hipLaunchKernelGGL((hashgrid_fwd_kernel<true, 5>), dim3(blocks), dim3(256), 0, s, pos, Mg, gstride, ldx, t2, p,
+                         out, ldo);
+    else
+      hipLaunchKernelGGL((hashgrid_fwd_kernel<false, 5>), dim3(blocks), dim3(256), 0, s, pos, Mg, gstride, ldx, t2, p,
+                         out, ldo);
+  } else {
+    if (aligned)
+      hipLaunchKernelGGL((hashgrid_fwd_kernel<true, 1>), dim3(blocks), dim3(256), 0, s, pos, Mg, Mg, ldx, t2, p, out,
+                         ldo);
+    else
+      hipLaunchKernelGGL((hashgrid_fwd_kernel<false, 1>), dim3(blocks), dim3(256), 0, s, pos, Mg, Mg, ldx, t2, p, out,
+                         ldo);
+  }
   return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_hashgrid_fwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L,
+                                int log2T, int F, const float* scales, float radius, int active_levels,
+                                float* out, int64_t ldo, void* stream) {
+  return mms_hashgrid_fwd_grouped(pos, M, 1, M, ldx, table, L, log2T, F, scales, radius, active_levels, out, ldo,
+                                  stream);
 }
 
 MMS_EXPORT int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx,

@@ -26,7 +26,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from . import _lib
-from .hip_ops import NN, NT, TN, _splits_for, act_bwd, gemm, weight_norm_bwd, weight_norm_fwd
+from .hip_ops import NN, NT, TN, _splits_for, act_bwd, gemm, gemm_tn_grouped, weight_norm_bwd, weight_norm_fwd
 
 ACT = {None: 0, "None": 0, "ReLU": 1, "Softplus": 2, "Sigmoid": 3}
 
@@ -282,9 +282,13 @@ class GridCfg:
         return self.L * self.F
 
 
-def grid_fwd(g: GridCfg, pos: torch.Tensor, ldx: int, M: int, table, active: int, out: torch.Tensor, col: int):
-    _lib.call("mms_hashgrid_fwd", pos.data_ptr(), M, ldx, table.data_ptr(), g.L, g.log2T, g.F, g.scales_ptr,
-              g.radius, active, out.data_ptr() + 4 * col, out.stride(0), _s())
+def grid_fwd(g: GridCfg, pos: torch.Tensor, ldx: int, M: int, table, active: int, out: torch.Tensor, col: int,
+             group: int = 1):
+    """Hash-grid features of M rows into out[:, col:col + 2L]; group=5 for the [centre | 4 taps] SDF batch (gathered
+    in (sample, tap) order, same values)."""
+    Mg = M // group
+    _lib.call("mms_hashgrid_fwd_grouped", pos.data_ptr(), Mg, group, Mg, ldx, table.data_ptr(), g.L, g.log2T, g.F,
+              g.scales_ptr, g.radius, active, out.data_ptr() + 4 * col, out.stride(0), _s())
 
 
 def grid_bwd(g: GridCfg, pos, ldx, M, table, active, dout: torch.Tensor, col: int, dtable, dpos, group: int = 1):
@@ -511,6 +515,8 @@ class ChainRun:
         Xin = [x] + Y[:L - 1]
         rf = self.rows_full
         dWs = _dw_views([self.params[3 * l + 1] for l in range(L)], dev)
+        # every layer's weight gradient dW_l += dZ_l^T X_l (+ bias column sums) in ONE grouped launch
+        items, wn = [], []
         for l in range(L):
             g, v, b = self.params[3 * l: 3 * l + 3]
             N, K = v.shape
@@ -520,18 +526,18 @@ class ChainRun:
             dW = dWs[l]
             db = bt if bt is not None else torch.zeros(N, device=dev)
             A, B = dZ[l], Xin[l]
-            tiles = ((N + 127) // 128) * ((K + 127) // 128)
             if l == L - 1 and rf < M:
                 # rows past rows_full carry only the output column 0
-                gemm(TN, N, K, rf, A, A.stride(0), B, B.stride(0), dW, K, accumulate=True,
-                     splits=_splits_for(rf, tiles, self.prec), prec=self.prec, colsum=db)
-                gemm(TN, 1, K, M - rf, A[rf:], A.stride(0), B[rf:], B.stride(0), dW, K, accumulate=True,
-                     splits=_splits_for(M - rf, 2, self.prec), prec=self.prec, colsum=db)
+                items.append((N, K, rf, A, B, dW, db))
+                items.append((1, K, M - rf, A[rf:], B[rf:], dW, db))
             else:
-                gemm(TN, N, K, M, A, A.stride(0), B, B.stride(0), dW, K, accumulate=True,
-                     splits=_splits_for(M, tiles, self.prec), prec=self.prec, colsum=db)
+                items.append((N, K, M, A, B, dW, db))
+            wn.append((g, v, l, dW, gt, vt, N, K))
+        if items:
+            gemm_tn_grouped(items, self.prec)
+        for g, v, l, dW, gt, vt, N, K in wn:
             _wn_bwd(g.reshape(-1), v, self.norms[l], dW, gt.reshape(-1) if gt is not None else
-                            torch.zeros(N, device=dev), vt if vt is not None else torch.zeros(N, K, device=dev))
+                    torch.zeros(N, device=dev), vt if vt is not None else torch.zeros(N, K, device=dev))
         self.Y = self.x = self.bwd_packs = None
         return dx
 
@@ -637,7 +643,7 @@ class SurfaceFunction(torch.autograd.Function):
         X = _alloc(5 * M, K0, dev)
         d32 = float(torch.tensor(delta, dtype=torch.float32))
         _lib.call("mms_geo_input_fwd", pos.data_ptr(), 3, M, 4, d32, 6, X.data_ptr(), X.stride(0), _s())
-        grid_fwd(grid, X, X.stride(0), 5 * M, table, active, X, 39)
+        grid_fwd(grid, X, X.stride(0), 5 * M, table, active, X, 39, group=5)
         prec = PRECISION["sdf"]
         ctx.chain = None
         if prec != 0:

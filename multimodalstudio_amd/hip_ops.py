@@ -6,6 +6,7 @@ Every function here requires CUDA(HIP) tensors and raises otherwise: there is no
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -134,5 +135,28 @@ _SPLIT_BLOCKS = {0: 1024, 1: 256, 2: 512}
 
 
 def _splits_for(M_rows: int, tiles: int, prec: int = 0) -> int:
+    """K slices of a split-K weight gradient: a multiple of 8 (mms_gemm spreads each tile's slices over the 8 XCDs and
+    pads the count to a multiple of 8: a padded count loads some XCDs with one slice more) within the block target."""
     target = max(1, _SPLIT_BLOCKS.get(int(prec), 1024) // max(1, tiles))
+    if target >= 8:
+        target = target // 8 * 8
     return int(max(1, min(target, M_rows // 512)))
+
+
+# grouped weight-gradient launches (mms_gemm_tn_grouped): blocks per launch for all the MLP's layers together
+_GROUP_BLOCKS = {0: 1024, 1: 256, 2: 512}
+
+
+def gemm_tn_grouped(items, prec: int, target_blocks: Optional[int] = None):
+    """items = [(N_out, K_in, rows, dZ [rows, >=N_out], X [rows, >=K_in], dW [N_out, K_in], db [N_out] or None)]:
+    dW += dZ^T X and db += colsum(dZ) for every item in one launch (<= 5 items)."""
+    n = len(items)
+    I64 = ctypes.c_int64 * n
+    VP = ctypes.c_void_p * n
+    target = int(os.environ.get("MMS_TN_BLOCKS", "0")) or target_blocks or _GROUP_BLOCKS.get(int(prec), 512)
+    _lib.call("mms_gemm_tn_grouped", int(prec), n, I64(*[it[0] for it in items]), I64(*[it[1] for it in items]),
+              I64(*[it[2] for it in items]), VP(*[it[3].data_ptr() for it in items]),
+              I64(*[it[3].stride(0) for it in items]), VP(*[it[4].data_ptr() for it in items]),
+              I64(*[it[4].stride(0) for it in items]), VP(*[it[5].data_ptr() for it in items]),
+              I64(*[it[5].stride(0) for it in items]),
+              VP(*[(it[6].data_ptr() if it[6] is not None else None) for it in items]), target, _stream())

@@ -428,6 +428,42 @@ class RNG:
     background: Dict[str, torch.Tensor] = field(default_factory=dict)
 
 
+_BG_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def background_stream(dev) -> "torch.cuda.Stream":
+    """The per-device HIP stream the background branch runs on (BaseModel.concurrent_background)."""
+    i = torch.device(dev).index or 0
+    if i not in _BG_STREAMS:
+        _BG_STREAMS[i] = torch.cuda.Stream(device=i)
+    return _BG_STREAMS[i]
+
+
+def join_background(dev) -> None:
+    """Order the current stream after everything queued on the background stream (its backward included)."""
+    i = torch.device(dev).index or 0
+    if i in _BG_STREAMS:
+        torch.cuda.current_stream(i).wait_stream(_BG_STREAMS[i])
+
+
+class _JoinBackground(torch.autograd.Function):
+    """Identity on a background output, applied on the main stream after the join.  Its backward queues a final
+    callback that joins the background stream into the caller's stream, so whatever reads the gradients after
+    ``backward()`` returns (the weight-norm flush, the optimizer, a test) is ordered after the background's
+    backward kernels -- which accumulate the parameter gradients in place, outside autograd's own stream sync."""
+
+    @staticmethod
+    def forward(ctx, x, dev_index: int):
+        ctx.dev_index = dev_index
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        i = ctx.dev_index
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: join_background(i))
+        return g, None
+
+
 def _pad_rows(t: Optional[torch.Tensor], R: int) -> Optional[torch.Tensor]:
     """Injected per-hit-ray uniforms padded with zeros to a fixed-capacity batch of R rows (padding rows' samples are
     discarded)."""
@@ -552,6 +588,8 @@ class BaseModel(nn.Module):
         self._lin = {}
         # training shortcut (SURVEY §8(d) MLP FLOPs note): heads of other modalities only feed outputs no loss reads
         self.own_heads_only = False
+        # the background branch on its own HIP stream (overlaps the foreground; same results)
+        self.concurrent_background = True
 
     # -- callbacks (BEFORE_TRAIN_ITERATION), restated from the reference schedules --------------------
     def set_step(self, step: int, max_iters: int = 100000):
@@ -630,29 +668,39 @@ class BaseModel(nn.Module):
                     pdf = [_pad_rows(p, R) for p in pdf]
                 elif self.training:
                     pdf = [torch.rand(R, 1, device=dev) for _ in range(sp.upsample_steps)]
-            bins = self.neus_bins(n_h.detach(), f_h.detach(), o_h.detach(), d_h.detach(), t_rand, pdf)
-            S = bins.shape[1] - 1
-            pos, deltas, starts, ends = fx.SamplesFunction.apply(bins, n_h, f_h, o_h, d_h, 0)
-            # background (background_model.py:73-111) on all N rays
+            # background (background_model.py:73-111) on all N rays.  It depends on the foreground only through the
+            # final composite, so it runs on a second HIP stream (forward here, and -- autograd runs each node's
+            # backward on its forward's stream -- its backward too), overlapping the NeuS sampler and the surface /
+            # radiance work; the main stream joins it right before the composite, and every backward through it ends
+            # with a join (_JoinBackground)
             bt = bt_fused if fused else rng.background.get(mod)
             if bt is None and self.training:
                 bt = torch.rand(N, sp.bg_samples + 1, device=dev)
-            blin = self._lin_dev(sp.bg_samples + 1, 1.0, dev)
-            bbins = torch.empty(N, sp.bg_samples + 1, device=dev)
-            _lib.call("mms_stratified_bins", blin.data_ptr(), sp.bg_samples + 1, fx._p(bt), sp.bg_samples + 1, N,
-                      bbins.data_ptr(), fx._s())
-            bpos, bdeltas, _, _ = fx.SamplesFunction.apply(bbins, bnears, bfars, o, d, 1)
-            density, bfeat = self.background_model.field(bpos, d, sp.bg_samples)
-            bw = fx.DensityWeightsFunction.apply(density, bdeltas, sp.bg_samples)
-            bg_out = {}
+            cur = torch.cuda.current_stream(dev)
+            bgs = background_stream(dev) if self.concurrent_background else cur
+            if bgs is not cur:
+                bgs.wait_stream(cur)
             # every head on every modality's rays (radiance_model.py:143-149) -- or, with own_heads_only (training:
             # only the ray's own modality's output reaches the loss, raw_pipeline.py:112-122), just its own
             heads_for = [mod] if (self.own_heads_only and torch.is_grad_enabled()) else None
-            for m, head in self.background_model.modality_heads.items():
-                if heads_for is not None and m not in heads_for:
-                    continue
-                vals = head(bfeat, d, up, sp.bg_samples)
-                bg_out[m] = fx.CompositeFunction.apply(bw, vals, None, None, sp.bg_samples)
+            with torch.cuda.stream(bgs):
+                blin = self._lin_dev(sp.bg_samples + 1, 1.0, dev)
+                bbins = torch.empty(N, sp.bg_samples + 1, device=dev)
+                _lib.call("mms_stratified_bins", blin.data_ptr(), sp.bg_samples + 1, fx._p(bt), sp.bg_samples + 1, N,
+                          bbins.data_ptr(), fx._s())
+                bpos, bdeltas, _, _ = fx.SamplesFunction.apply(bbins, bnears, bfars, o, d, 1)
+                density, bfeat = self.background_model.field(bpos, d, sp.bg_samples)
+                bw = fx.DensityWeightsFunction.apply(density, bdeltas, sp.bg_samples)
+                bg_out = {}
+                for m, head in self.background_model.modality_heads.items():
+                    if heads_for is not None and m not in heads_for:
+                        continue
+                    vals = head(bfeat, d, up, sp.bg_samples)
+                    bg_out[m] = fx.CompositeFunction.apply(bw, vals, None, None, sp.bg_samples)
+            # NeuS sampling (ray_samplers.py:448-514) -- latency-bound launches the background work overlaps
+            bins = self.neus_bins(n_h.detach(), f_h.detach(), o_h.detach(), d_h.detach(), t_rand, pdf)
+            S = bins.shape[1] - 1
+            pos, deltas, starts, ends = fx.SamplesFunction.apply(bins, n_h, f_h, o_h, d_h, 0)
             # surface + radiance
             sdf, geo, grads, hess, normals = self.surface_model(pos)
             vr = self.surface_model.volume_rendering
@@ -660,6 +708,12 @@ class BaseModel(nn.Module):
             feat = self.radiance_model.features(pos, d_h, normals.detach(), geo, S)
             out = {}
             rows = N if cap is None else N + 1     # padded batches scatter into a dummy row N, cut off below
+            if bgs is not cur:
+                cur.wait_stream(bgs)
+                for m in list(bg_out):
+                    bg_out[m].record_stream(cur)    # made on the background stream, read (and freed) on this one
+                    if torch.is_grad_enabled() and bg_out[m].requires_grad:
+                        bg_out[m] = _JoinBackground.apply(bg_out[m], torch.device(dev).index or 0)
             for m, head in self.radiance_model.modality_heads.items():
                 if heads_for is not None and m not in heads_for:
                     continue

@@ -29,6 +29,9 @@ CHAIN_ROLES = {  # (bwd, KS0, NT2, NL, KEEP) -> the role label bench.py's chain_
 
 
 def label(name, grid=0):
+    m = re.search(r"gemm_tn_grouped_kernel<(\d), (true|false)>", name)
+    if m:
+        return f"mms_gemm_tn_grouped:{PREC[m.group(1)]}:TN_grouped"
     m = re.search(r"gemm_kernel<(\d), (true|false), (true|false), (true|false)>", name)
     if m:
         return f"mms_gemm:{PREC[m.group(1)]}:{MODE.get((m.group(2), m.group(3)), '??')}"
@@ -41,7 +44,7 @@ def label(name, grid=0):
         return "mms_hashgrid_bwd_grouped:sdf_taps" if "walk_kernel<5" in name else "mms_hashgrid_bwd_grouped:radiance_or_bg"
     if "hashgrid_fwd_kernel" in name:
         # thread per (point, level): the SDF [centre | 4 taps] batch is the launch with > 200k points
-        return "mms_hashgrid_fwd:sdf_taps" if grid > 200000 * 16 else "mms_hashgrid_fwd:other"
+        return "mms_hashgrid_fwd_grouped:sdf_taps" if grid > 200000 * 16 else "mms_hashgrid_fwd_grouped:other"
     return None
 
 

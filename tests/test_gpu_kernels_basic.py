@@ -62,6 +62,15 @@ def test_hashgrid_bwd_grouped_taps(dev, log2T):
     torch.cuda.synchronize()
     np.testing.assert_allclose(dtable.cpu().numpy(), tr.grad.numpy(), rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(dpos.cpu().numpy(), xr.grad.numpy(), rtol=1e-3, atol=1e-3)
+    # the grouped forward ((sample, tap) lane order) writes the plain forward's bits into an odd-column panel
+    out_g = torch.full((5 * Mc, 72), 7.0, device=dev)
+    out_g[:, :3] = xd
+    out_p = out_g.clone()
+    F.grid_fwd(cfg, out_g, 72, 5 * Mc, td, L, out_g, 39, group=5)
+    F.grid_fwd(cfg, out_p, 72, 5 * Mc, td, L, out_p, 39, group=1)
+    torch.cuda.synchronize()
+    assert torch.equal(out_g, out_p)
+    np.testing.assert_allclose(out_g[:, 39:71].cpu().numpy(), ref.detach().numpy(), rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 257, 71), (300, 3, 64), (4096, 256, 256), (77, 130, 317)])
