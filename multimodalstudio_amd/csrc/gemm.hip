@@ -339,37 +339,23 @@ __device__ __forceinline__ void gemm_block(int mt, int nt, int slice, int64_t M,
     }
   };
 
-  // Global loads run DEPTH k-steps ahead of the MFMAs in DEPTH register sets (unrolled, so every set is addressed
-  // statically).
-  constexpr int DEPTH = 1;   // 2 measured no faster for the weight gradients (bf16x3 5 % slower: register pressure)
-  float4 ra[DEPTH][BK / 8], rb[DEPTH][BK / 8];
-  uint32_t ma[DEPTH] = {}, mb[DEPTH] = {};
-#pragma unroll
-  for (int d = 0; d < DEPTH; ++d) {
-    const int64_t k = kbeg + (int64_t)d * BK;
-    if (k < kend) {
-      ma[d] = stage_load<BK, TA, VEC>(A, lda, m0, M, k, kend, ra[d]);
-      mb[d] = stage_load<BK, TB, VEC>(B, ldb, n0, N, k, kend, rb[d]);
-    }
+  float4 ra[BK / 8], rb[BK / 8];
+  uint32_t ma = 0, mb = 0;
+  if (kbeg < kend) {
+    ma = stage_load<BK, TA, VEC>(A, lda, m0, M, kbeg, kend, ra);
+    mb = stage_load<BK, TB, VEC>(B, ldb, n0, N, kbeg, kend, rb);
   }
-  for (int64_t k0 = kbeg; k0 < kend; k0 += DEPTH * BK) {
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-      const int64_t k = k0 + (int64_t)d * BK;
-      if (k < kend) {
-        __syncthreads();
-        stage_store<PREC, TA>(As, ra[d], ma[d]);
-        stage_store<PREC, TB>(Bs, rb[d], mb[d]);
-        if (do_cs) colsum_acc(ra[d]);
-        __syncthreads();
-        const int64_t kn = k + (int64_t)DEPTH * BK;
-        if (kn < kend) {
-          ma[d] = stage_load<BK, TA, VEC>(A, lda, m0, M, kn, kend, ra[d]);
-          mb[d] = stage_load<BK, TB, VEC>(B, ldb, n0, N, kn, kend, rb[d]);
-        }
-        compute();
-      }
+  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+    stage_store<PREC, TA>(As, ra, ma);
+    stage_store<PREC, TB>(Bs, rb, mb);
+    if (do_cs) colsum_acc(ra);
+    __syncthreads();
+    if (k0 + BK < kend) {
+      ma = stage_load<BK, TA, VEC>(A, lda, m0, M, k0 + BK, kend, ra);
+      mb = stage_load<BK, TB, VEC>(B, ldb, n0, N, k0 + BK, kend, rb);
     }
+    compute();
   }
 
   if (do_cs) {  // reduce the 8 threads sharing t % 32 through LDS, then one atomic per column

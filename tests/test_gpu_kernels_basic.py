@@ -222,3 +222,54 @@ def test_gemm_tall_skinny_epilogues(dev, prec, tol, M, N, K):
     ref = (dZ.double() @ W.double()) * sg
     e = ((dX.double() - ref).abs().max() / ref.abs().max()).item()
     assert e < tol, e
+
+
+@pytest.mark.parametrize("prec,tol", [(0, 2e-6), (2, 2e-5), (1, 2e-2)])
+def test_gemm_tn_grouped(dev, prec, tol):
+    """mms_gemm_tn_grouped: several layers' weight gradients (+ bias column sums) in one launch vs fp64 -- ragged
+    widths, a single-column item sharing its dW with a full item (the SDF taps), unaligned rows (scalar staging),
+    and slices long enough for the asm-prefetched k-loop to wrap several times."""
+    from multimodalstudio_amd import hip_ops
+    from multimodalstudio_amd.functions import _alloc
+    g = torch.Generator().manual_seed(11 + prec)
+    specs = [(256, 71, 30000), (256, 256, 30000), (257, 256, 9000), (130, 317, 20000)]
+    items, refs = [], []
+    for N, K, M in specs:
+        dZ = torch.randn(M, N, generator=g)
+        X = torch.randn(M, K, generator=g)
+        dZd, Xd = _alloc(M, N, dev), _alloc(M, K, dev)
+        dZd.copy_(dZ.to(dev))
+        Xd.copy_(X.to(dev))
+        dW = torch.zeros(N, K, device=dev)
+        db = torch.zeros(N, device=dev)
+        items.append((N, K, M, dZd, Xd, dW, db))
+        refs.append((dZ.double().T @ X.double(), dZ.double().sum(0)))
+    # the taps item: rows past 9000 of a 257-wide dZ, column 0 only, into the same dW / db as item 2
+    dZt = torch.randn(7000, 257, generator=g)
+    Xt = torch.randn(7000, 256, generator=g)
+    dZtd, Xtd = _alloc(7000, 257, dev), _alloc(7000, 256, dev)
+    dZtd.copy_(dZt.to(dev))
+    Xtd.copy_(Xt.to(dev))
+    items.append((1, 256, 7000, dZtd, Xtd, items[2][5], items[2][6]))
+    r2w = refs[2][0].clone()
+    r2w[0] += dZt.double()[:, 0] @ Xt.double()
+    r2b = refs[2][1].clone()
+    r2b[0] += dZt.double()[:, 0].sum()
+    refs[2] = (r2w, r2b)
+    # an unaligned-row item (scalar staging path): a column slice of a wider panel
+    wide = torch.randn(5000, 40, generator=g)
+    wd = wide.to(dev)
+    dZu, Xu = wd[:, 1:33], wd[:, 3:20]
+    dWu = torch.zeros(32, 17, device=dev)
+    items_u = [(32, 17, 5000, dZu, Xu, dWu, None)]
+    hip_ops.gemm_tn_grouped(items, prec)
+    hip_ops.gemm_tn_grouped(items_u, prec)
+    torch.cuda.synchronize()
+    for (N, K, M, _, _, dW, db), (rw, rb) in zip(items[:4], refs):
+        err = np.abs(dW.cpu().double().numpy() - rw.numpy()).max() / np.abs(rw.numpy()).max()
+        assert err < tol, f"dW {N}x{K} prec={prec}: rel err {err:.2e}"
+        errb = (db.cpu().double() - rb).abs().max() / rb.abs().max()
+        assert errb < 1e-5, f"db {N} prec={prec}: rel err {errb:.2e}"
+    ru = wide.double()[:, 1:33].T @ wide.double()[:, 3:20]
+    err = np.abs(dWu.cpu().double().numpy() - ru.numpy()).max() / np.abs(ru.numpy()).max()
+    assert err < tol, f"unaligned item prec={prec}: rel err {err:.2e}"
