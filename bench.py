@@ -41,9 +41,14 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F32_MFMA_PEAK_TF = 157.3   # dense f32-input MFMA (v_mfma_f32_32x32x2_f32) peak, MI355X_MICROARCH.md
 BF16_MFMA_PEAK_TF = 2500.0  # dense bf16 MFMA peak (no sparsity), MI355X_MICROARCH.md
 # split-bf16x3 runs 3 bf16 MFMAs per f32 product: its ceiling for the algorithmic 2MNK flops is a third
-MFMA_PEAK_TF = {"fp32": F32_MFMA_PEAK_TF, "bf16": BF16_MFMA_PEAK_TF, "bf16x3": BF16_MFMA_PEAK_TF / 3}
-PREC_NAMES = {0: "fp32", 1: "bf16", 2: "bf16x3"}
-DTYPES = {"fp32": "fp32", "fast": "bf16 MFMA (fp32 accumulate; SDF MLP and polarization heads split-bf16x3), fp32 elsewhere",
+# (bf16x2: the SDF chain's split activations x bf16 weights, 2 bf16 MFMAs per product)
+MFMA_PEAK_TF = {"fp32": F32_MFMA_PEAK_TF, "bf16": BF16_MFMA_PEAK_TF, "bf16x3": BF16_MFMA_PEAK_TF / 3,
+                "bf16x2": BF16_MFMA_PEAK_TF / 2}
+PREC_NAMES = {0: "fp32", 1: "bf16", 2: "bf16x3", 3: "bf16x2"}
+DTYPES = {"fp32": "fp32",
+          "fast": "bf16 MFMA (fp32 accumulate; SDF MLP chain bf16 weights x split-bf16 activations, its weight "
+                  "gradients and the polarization heads split-bf16x3), fp32 elsewhere",
+          "fast_x3": "bf16 MFMA (fp32 accumulate; SDF MLP and polarization heads split-bf16x3), fp32 elsewhere",
           "bf16x3": "split-bf16x3 MFMA (fp32-accurate), fp32 elsewhere"}
 HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per lookup, forward
 HASH_BWD_B = 128 + 12 + 16 * 8 * 2 * (4 + 4)    # bytes per lookup, backward (table grads)
@@ -138,7 +143,7 @@ def kernel_records(summ, timing_steps: int, precision: str):
             ach = flops / (ms * 1e-3) / 1e12
             rec.update({"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
                         "frac": round(ach / peak, 4), "gbs": round(nbytes / (ms * 1e-3) / 1e9, 1)})
-            if mode == "bf16x3":
+            if mode in ("bf16x3", "bf16x2"):
                 rec.update({"mode_peak": round(MFMA_PEAK_TF[mode], 1),
                             "frac_of_mode_peak": round(ach / MFMA_PEAK_TF[mode], 4)})
         else:

@@ -19,7 +19,11 @@
 // Backward-data: dZ_l = (W_{l+1}^T dZ_{l+1}) * act'(Y_l), with act' taken from the stored forward OUTPUT
 // (ReLU: Y > 0; Softplus(b): 1 - exp(-b Y) = sigmoid(b Z); Sigmoid: Y (1 - Y)) -- no pre-activation is ever
 // stored -- and an fp32 store of every dZ for the weight-gradient GEMMs.
-// PREC 1: bf16 operands; PREC 2: split bf16x3 (x = hi + lo, acc += lo.hi + hi.lo + hi.hi); fp32 accumulation.
+// PREC 1: bf16 operands; PREC 2: split bf16x3 (x = hi + lo, acc += lo.hi + hi.lo + hi.hi); PREC 3: split
+// activations only (bf16 weights W~ = bf16(W), acc += W~ (h_hi + h_lo): the chain computes the MLP of the rounded
+// weights with ~16-bit activations, so the SDF's tap differences stay exact differences of ONE function -- its
+// weights' rounding is the mixed-precision "bf16 weights, fp32 master" one -- at 2 MFMAs and half the weight
+// traffic of PREC 2); fp32 accumulation.
 #include "common.h"
 
 #include <utility>
@@ -97,7 +101,7 @@ __device__ __forceinline__ void split8(const float* v, bf16x8& hi, bf16x8& lo) {
   for (int j = 0; j < 8; ++j) {
     const __bf16 b = (__bf16)v[j];
     hi[j] = b;
-    if constexpr (PREC == 2) lo[j] = (__bf16)(v[j] - (float)b);
+    if constexpr (PREC >= 2) lo[j] = (__bf16)(v[j] - (float)b);
   }
 }
 
@@ -108,6 +112,7 @@ __device__ __forceinline__ void mma(floatx16& acc, const bf16x8& ah, const bf16x
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
   }
+  if constexpr (PREC == 3) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
 }
 
@@ -636,19 +641,21 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
       else launch_chain<PREC, 5, 8, 8, 9, false, 2, 2, 0, 0, false>(a, s);
       return true;
     }
-    if (!bwd && ks0 == 20 && nt[0] == 8 && nt[1] == 8 && nt[2] == 8 && a0 == 1 && a1 == 1 && a2 == 1 &&
-        hidden_full && keep) {
-      launch_chain<PREC, 20, 8, 8, 8, false, 1, 1, 1, 0, true>(a, s);
-      return true;
+    if constexpr (PREC != 3) {   // (split activations: the SDF chains only)
+      if (!bwd && ks0 == 20 && nt[0] == 8 && nt[1] == 8 && nt[2] == 8 && a0 == 1 && a1 == 1 && a2 == 1 &&
+          hidden_full && keep) {
+        launch_chain<PREC, 20, 8, 8, 8, false, 1, 1, 1, 0, true>(a, s);
+        return true;
+      }
+      if (bwd && ks0 == 16 && nt[0] == 8 && nt[1] == 8 && nt[2] == 10 && a0 == 1 && a1 == 1 && a2 == 0 && xio &&
+          bwd_hidden) {
+        launch_chain<PREC, 16, 8, 8, 10, true, 1, 1, 0, 1>(a, s);
+        return true;
+      }
     }
     if (bwd && ks0 == 17 && nt[0] == 8 && nt[1] == 8 && nt[2] == 3 && a0 == 2 && a1 == 2 && a2 == 0 && noxa &&
         a.xout == nullptr && bwd_hidden) {
       launch_chain<PREC, 17, 8, 8, 3, true, 2, 2, 0, 0>(a, s);
-      return true;
-    }
-    if (bwd && ks0 == 16 && nt[0] == 8 && nt[1] == 8 && nt[2] == 10 && a0 == 1 && a1 == 1 && a2 == 0 && xio &&
-        bwd_hidden) {
-      launch_chain<PREC, 16, 8, 8, 10, true, 1, 1, 0, 1>(a, s);
       return true;
     }
     if constexpr (PREC == 1) {
@@ -758,7 +765,7 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
                              float* const* out, const int64_t* ldo, const int* N, const int* act, float beta,
                              float thr, const float* w2row0, void* stream) {
   const char* fn = "mms_mlp_chain";
-  MMS_REQUIRE(prec == 1 || prec == 2, fn, "prec must be 1 (bf16) or 2 (split bf16x3)");
+  MMS_REQUIRE(prec >= 1 && prec <= 3, fn, "prec must be 1 (bf16), 2 (split bf16x3) or 3 (split activations)");
   MMS_REQUIRE(n_layers == 3 || n_layers == 4, fn, "chains of 3 or 4 layers");
   MMS_REQUIRE(M >= 0 && K0 > 0, fn, "bad shape");
   if (M == 0) return 0;
@@ -778,7 +785,7 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
   for (int l = 0; l < 4; ++l) a.L[l] = ChainLayer{};
   for (int l = 0; l < n_layers; ++l) {
     MMS_REQUIRE(a_hi[l] != nullptr && N[l] > 0, fn, "missing layer weights");
-    MMS_REQUIRE(prec == 1 || (a_lo && a_lo[l] != nullptr), fn, "split bf16x3 needs the residual images");
+    MMS_REQUIRE(prec != 2 || (a_lo && a_lo[l] != nullptr), fn, "split bf16x3 needs the residual images");
     MMS_REQUIRE(act[l] >= 0 && act[l] <= 3, fn, "bad activation id");
     ChainLayer& L = a.L[l];
     L.a_hi = reinterpret_cast<const __bf16*>(a_hi[l]);
@@ -800,8 +807,9 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
   }
   const int ks0 = (K0 + 15) / 16;
   hipStream_t s = mms::as_stream(stream);
-  const bool ok = prec == 1 ? dispatch_chain<1>(n_layers, ks0, nt, backward != 0, a, s)
-                            : dispatch_chain<2>(n_layers, ks0, nt, backward != 0, a, s);
+  const bool ok = prec == 1   ? dispatch_chain<1>(n_layers, ks0, nt, backward != 0, a, s)
+                  : prec == 2 ? dispatch_chain<2>(n_layers, ks0, nt, backward != 0, a, s)
+                              : dispatch_chain<3>(n_layers, ks0, nt, backward != 0, a, s);
   MMS_REQUIRE(ok, fn, "unsupported chain shape or activations (SDF 71-256-256-257 Softplus, radiance 317-256-256-256 "
                       "ReLU, background 39-256x4 and 283-256-256-256-128 ReLU chains only)");
   return mms::check_launch(fn);

@@ -31,7 +31,6 @@ from .hip_ops import NN, NT, TN, _splits_for, act_bwd, gemm, gemm_tn_grouped, we
 ACT = {None: 0, "None": 0, "ReLU": 1, "Softplus": 2, "Sigmoid": 3}
 
 # GEMM operand precision per MLP family: 0 exact fp32 MFMA (parity mode), 1 bf16, 2 split bf16x3.
-PRECISION = {"sdf": 0, "radiance": 0, "heads": 0, "background": 0, "mlp": 0}
 PRESETS = {
     "fp32": {"sdf": 0, "radiance": 0, "heads": 0, "pol_head": 0, "background": 0, "mlp": 0},
     # throughput mode: the SDF MLP keeps ~fp32 operand precision (its 4-tap finite differences divide
@@ -39,13 +38,23 @@ PRESETS = {
     # gradient MLP fields (mlp methods, differentiated twice) stay on the exact fp32 MFMA
     # (the polarization heads keep split-bf16x3 too: their Stokes outputs are combined into intensities by
     # differences, and their PSNR after training moved by ~0.2 dB in bf16, tests/test_gpu_train_parity.py)
-    "fast": {"sdf": 2, "radiance": 1, "heads": 1, "pol_head": 2, "background": 1, "mlp": 0},
+    # "sdf_chain": the SDF chain kernel's operand mode -- 3: bf16 weights x split (hi + lo) activations, i.e. the MLP
+    # of the bf16-rounded weights at ~16-bit activation precision (the tap differences stay exact differences of
+    # one function; 2 MFMAs per product instead of 3); its weight gradients stay split-bf16x3 ("sdf": 2), since the
+    # taps' large, opposite dZ rows cancel in dW.  PSNR parity and radiance deviation: tests/test_gpu_train_parity.py,
+    # tests/test_gpu_e2e.py; the kernel itself: tests/test_gpu_chain.py::test_sdf_chain_split_activations
+    "fast": {"sdf": 2, "sdf_chain": 3, "radiance": 1, "heads": 1, "pol_head": 2, "background": 1, "mlp": 0},
     "bf16x3": {"sdf": 2, "radiance": 2, "heads": 2, "pol_head": 2, "background": 2, "mlp": 2},
 }
+for _p in PRESETS.values():
+    _p.setdefault("sdf_chain", 0)      # 0: the chain runs on the "sdf" GEMM precision
+# the round-2 fast preset (SDF chain split-bf16x3 as well), kept for comparison
+PRESETS["fast_x3"] = dict(PRESETS["fast"], sdf_chain=0)
+PRECISION = dict(PRESETS["fp32"])
 
 
 def set_precision(mode: str) -> None:
-    """Select the MLP GEMM precision preset ('fp32' parity | 'fast' | 'bf16x3')."""
+    """Select the MLP GEMM precision preset ('fp32' parity | 'fast' | 'fast_x3' | 'bf16x3')."""
     PRECISION.update(PRESETS[mode])
 
 
@@ -405,10 +414,13 @@ class ChainRun:
 
     ``rows_full``: rows >= rows_full only need output column 0 (the SDF's tap rows, surface_model.py:137-153)."""
 
-    def __init__(self, params: Sequence[torch.Tensor], acts: Sequence[Tuple[int, float, float]], prec: int):
+    def __init__(self, params: Sequence[torch.Tensor], acts: Sequence[Tuple[int, float, float]], prec: int,
+                 chain_prec: int = 0):
         if prec not in (1, 2):
             raise ValueError("the fused chain runs the bf16 (1) and split-bf16x3 (2) modes")
         self.params, self.acts, self.prec = list(params), list(acts), int(prec)
+        # the chain kernel's operand mode (prec, or 3: split activations x bf16 weights); weight gradients use prec
+        self.cprec = int(chain_prec) or self.prec
         self.L = len(self.params) // 3
         if self.L not in (3, 4):
             raise ValueError("chains of 3 or 4 layers")
@@ -417,12 +429,12 @@ class ChainRun:
     def _pack(self, W, rows: int, cols: int, transpose: bool, permute: bool):
         prep = _ACTIVE_PREP[0]
         if prep is not None:
-            return prep.packed(W, rows, cols, transpose, permute, self.prec)
+            return prep.packed(W, rows, cols, transpose, permute, self.cprec)
         return self._pack_new(W, rows, cols, transpose, permute)
 
     def _pack_new(self, W, rows: int, cols: int, transpose: bool, permute: bool):
         hi = torch.empty(rows, cols, dtype=torch.bfloat16, device=W.device)
-        lo = torch.empty_like(hi) if self.prec == 2 else None
+        lo = torch.empty_like(hi) if self.cprec == 2 else None
         N, K = W.shape
         _lib.call("mms_mlp_pack", W.data_ptr(), N, K, W.stride(0), int(transpose), int(permute), rows, cols,
                   hi.data_ptr(), _p(lo), _s())
@@ -442,7 +454,7 @@ class ChainRun:
         ns = (ctypes.c_int * n)(*Ns)
         ac = (ctypes.c_int * n)(*acts)
         cast = lambda a: ctypes.cast(a, ctypes.c_void_p)
-        _lib.call("mms_mlp_chain", self.prec, int(backward), n, X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
+        _lib.call("mms_mlp_chain", self.cprec, int(backward), n, X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
                   _p(xaux), 0 if xaux is None else xaux.stride(0), int(xact), _p(xout),
                   0 if xout is None else xout.stride(0), cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux),
                   cast(os_), cast(ldo), cast(ns), cast(ac), self.beta, self.thr, _p(w2row0), _s())
@@ -648,7 +660,7 @@ class SurfaceFunction(torch.autograd.Function):
         ctx.chain = None
         if prec != 0:
             # bf16 modes: the whole 3-layer chain in one kernel; tap rows keep only the sdf column
-            chain = ChainRun(params, SDF_ACTS, prec)
+            chain = ChainRun(params, SDF_ACTS, prec, PRECISION["sdf_chain"])
             out = chain.forward(X, keep=True, rows_full=M)
             ctx.chain = chain
         else:
@@ -761,7 +773,8 @@ def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> to
     if PRECISION["sdf"] != 0:
         # fused chain, no hidden-layer stores, only the sdf column of the output layer (rows_full = 0), written as
         # the dense [M] vector the sampler kernel reads
-        return ChainRun(params, SDF_ACTS, PRECISION["sdf"]).forward(X, keep=False, rows_full=0, dense_col0=True)
+        return ChainRun(params, SDF_ACTS, PRECISION["sdf"], PRECISION["sdf_chain"]).forward(X, keep=False, rows_full=0,
+                                                                                         dense_col0=True)
     # only the sdf column of the last layer is needed
     last = list(params[-3:])
     g, v, b = last
