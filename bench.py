@@ -372,8 +372,8 @@ def main():
                        "pixel_sampler": args.sampler, "parallelism": f"dp{world}",
                        "step_mode": run_mode},
             "kernel_timing": (f"{timing_steps} eager steps of the same workload after the timed region, HIP events "
-                              "around every watched launch on its stream (background branch serialized for these steps so "
-                              "each launch is timed alone)" if not args.no_kernel_timing else None),
+                              "around every watched launch on its stream (background branch on the main stream for these "
+                              "steps, so each launch is timed alone)" if not args.no_kernel_timing else None),
             "roofline": roof,
             "roofline_hash_grid": hash_roof,
             "roofline_kernels": kernels,
