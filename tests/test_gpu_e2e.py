@@ -38,7 +38,7 @@ def rel_err(actual, ref):
     return (np.abs(a - r).max() / scale) if scale > 0 else np.abs(a - r).max()
 
 
-def run_hip_e2e(f, dev, cap=None):
+def run_hip_e2e(f, dev, cap=None, concurrent_background=True):
     from multimodalstudio_amd import model as mm
     from multimodalstudio_amd import pipeline as pl
     from multimodalstudio_amd import scene as ms
@@ -53,6 +53,7 @@ def run_hip_e2e(f, dev, cap=None):
                                       fields=fields)).to(dev)
     model.load_state_dict({k[2:]: torch.from_numpy(v) for k, v in f.items() if k.startswith("p:")}, strict=True)
     model.train()
+    model.concurrent_background = concurrent_background
     model.set_step(int(f["step"]))
     cams = {}
     for m in mods:
@@ -155,3 +156,25 @@ def test_e2e_fast_preset_deviation(dev, name):
         assert rel.mean() < 2.5e-2, (m, rel.mean())
         assert rel.max() < 0.25, (m, rel.max())
     assert loss_rel < 2e-2
+
+
+@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_gridbg_s95000"])
+def test_background_stream_matches_single_stream(dev, name):
+    """The background branch on its own HIP stream (forward + backward, joined before the composite and by the
+    backward's final callback) gives the single-stream results: loss, radiance and every parameter / pose gradient to
+    float-atomic summation order (the grid background's table gradient included)."""
+    f = load(name)
+    runs = []
+    for conc in (False, True):
+        mods, model, pose, outs, losses, total = run_hip_e2e(f, dev, concurrent_background=conc)
+        grads = {k: p.grad.detach().cpu().clone() for k, p in model.named_parameters() if p.grad is not None}
+        grads.update({f"pose:{k}": p.grad.detach().cpu().clone() for k, p in pose.named_parameters()
+                      if p.grad is not None})
+        runs.append((float(total), {m: outs[m][m].detach().cpu().clone() for m in mods}, grads))
+    (l0, o0, g0), (l1, o1, g1) = runs
+    assert abs(l0 - l1) <= 1e-6 * abs(l0)
+    for m in o0:
+        assert rel_err(o1[m], o0[m]) < 1e-6, m
+    assert g0.keys() == g1.keys() and any("background" in k for k in g0)
+    for k in g0:
+        assert rel_err(g1[k], g0[k]) < 1e-4, (k, rel_err(g1[k], g0[k]))
