@@ -365,6 +365,85 @@ __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const C
   }
 }
 
+// The backward's last layer (dx, no activation derivative): its tiles through the wave's LDS scratch like the hidden
+// layers' dZ, so each store instruction writes 8 whole 128-B row segments instead of 64 rows x 16 B (the unstaged
+// stores wrote the 71- / 317- / 256-column dx rows in 32-B pieces: 1.3-1.5x the algorithmic write bytes, PMC
+// WRITE_SIZE).  Columns past N are not written (a partial quad stores its valid elements), nor rows past M.
+template <int NT>
+__device__ __forceinline__ void epilogue_out_staged(floatx16 (&acc)[NT], const ChainLayer& Ly, int nt, int64_t m0,
+                                                    int64_t M, float* scr, int lane) {
+  const int r = lane & 31, h = lane >> 5, q = lane & 7;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (t < nt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<f32x4*>(scr + r * kScr + 8 * g + 4 * h) =
+            f32x4{acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = 8 * j + (lane >> 3);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(scr + row * kScr + 4 * q);
+        const int64_t mr = m0 + row;
+        const int col = 32 * t + 4 * q;
+        if (mr < M) {
+          float* o = Ly.out + mr * Ly.ldo + col;
+          if (col + 4 <= Ly.N) {
+            st_nt4(o, v);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (col + e < Ly.N) __builtin_nontemporal_store(v[e], o + e);
+          }
+        }
+      }
+    }
+  }
+}
+
+// The forward's last layer the same way: + bias, activation, then staged row-contiguous stores.  SDF tap rows (rows
+// >= rows_full, only in the one block that straddles the boundary: whole tap blocks take the VALU path) store
+// column 0 alone.
+template <int NT, int ACT>
+__device__ __forceinline__ void epilogue_fwd_out_staged(floatx16 (&acc)[NT], const ChainLayer& Ly, const float* sb,
+                                                        int nt, int64_t m0, int64_t M, int64_t rows_full, float* scr,
+                                                        int lane, float beta, float thr) {
+  const int r = lane & 31, h = lane >> 5, q = lane & 7;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (t < nt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n0 = 32 * t + 8 * g + 4 * h;
+        const f32x4 bq = *reinterpret_cast<const f32x4*>(sb + n0);
+        f32x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = act_fwd<ACT>(acc[t][4 * g + i] + bq[i], beta, thr);
+        *reinterpret_cast<f32x4*>(scr + r * kScr + 8 * g + 4 * h) = v;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = 8 * j + (lane >> 3);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(scr + row * kScr + 4 * q);
+        const int64_t mr = m0 + row;
+        const int col = 32 * t + 4 * q;
+        if (mr < M) {
+          float* o = Ly.out + mr * Ly.ldo + col;
+          if (mr >= rows_full) {
+            if (col == 0) __builtin_nontemporal_store(v[0], o);
+          } else if (col + 4 <= Ly.N) {
+            st_nt4(o, v);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (col + e < Ly.N) __builtin_nontemporal_store(v[e], o + e);
+          }
+        }
+      }
+    }
+  }
+}
+
 template <int NT, bool BWD, int ACT>
 __device__ __forceinline__ void epilogue(floatx16 (&acc)[NT], const ChainLayer& Ly, const float* sb, int nt, int64_t m,
                                          int64_t mc, bool mval, bool only_col0, int h, float beta, float thr) {
@@ -571,7 +650,15 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
         __builtin_nontemporal_store(p + sbias[LL][0], a.L[LL].out + m * a.L[LL].ldo);
       return;
     }
-    epilogue<NT2, BWD, A2>(acc2, a.L[LL], sbias[LL], nt2, m, mc, mval, !BWD && !rowfull, h, a.beta, a.thr);
+    if constexpr (BWD && A2 == 0) {
+      if (a.L[LL].out != nullptr) epilogue_out_staged<NT2>(acc2, a.L[LL], nt2, m0, a.M, scr, lane);
+    } else if constexpr (!BWD && KEEP) {   // (the per-wave scratch exists for KEEP forwards)
+      if (a.L[LL].out != nullptr)
+        epilogue_fwd_out_staged<NT2, A2>(acc2, a.L[LL], sbias[LL], nt2, m0, a.M, a.rows_full, scr, lane, a.beta,
+                                         a.thr);
+    } else {
+      epilogue<NT2, BWD, A2>(acc2, a.L[LL], sbias[LL], nt2, m, mc, mval, !BWD && !rowfull, h, a.beta, a.thr);
+    }
   };
 
   if constexpr (NL == 4) {

@@ -614,15 +614,59 @@ def _wn_bwd(g, v, norms, dW, dg, dv) -> None:
         weight_norm_bwd(g, v, norms, dW, dg, dv)
 
 
+class _ZeroArena:
+    """One zero-filled f32 buffer per training step that the step's scratch gradients are carved from (zero_arena_begin
+    / zero_arena_end around forward + loss + backward): ONE fill launch per step instead of one per backward function
+    (~30 fills, each a graph node of ~5 us).  Sized from the previous step's demand; a step that needs more takes
+    fresh zeroed buffers for the rest.  Buffers a captured graph may reference are never freed."""
+
+    def __init__(self):
+        self.buf: Optional[torch.Tensor] = None
+        self.keep: List[torch.Tensor] = []
+        self.off = 0
+        self.need = 0
+        self.active = False
+
+
+_ARENA = _ZeroArena()
+_ALIGN = 64          # floats: every carved buffer starts on a 256-B boundary (vector / GEMM paths)
+
+
+def zero_arena_begin(dev) -> None:
+    a = _ARENA
+    size = a.buf.numel() if a.buf is not None else 0
+    if a.need > size and not torch.cuda.is_current_stream_capturing():
+        if a.buf is not None:
+            a.keep.append(a.buf)
+        a.buf = torch.empty(int(a.need * 1.25) + 4 * _ALIGN, device=dev)
+    a.need, a.off = 0, 0
+    a.active = a.buf is not None and a.buf.device == torch.device(dev)
+    if a.active:
+        a.buf.zero_()
+
+
+def zero_arena_end() -> None:
+    _ARENA.active = False
+
+
 def _zeroed_views(shapes, dev) -> List[Optional[torch.Tensor]]:
-    """Zero-filled f32 accumulation buffers carved from one allocation (None for a None shape): one fill launch per
-    backward function instead of one per gradient -- each fill is a graph node of its own (~5 us replayed)."""
+    """Zero-filled f32 accumulation buffers (None for a None shape) carved from the step's zero arena, or from one
+    fresh zeroed allocation outside a training step / past the arena."""
     sizes = [0 if sh is None else math.prod(sh) for sh in shapes]
-    buf = torch.zeros(max(sum(sizes), 1), device=dev)
+    padded = [(n + _ALIGN - 1) // _ALIGN * _ALIGN for n in sizes]
+    total = max(sum(padded), 1)
+    a = _ARENA
+    if a.active:
+        a.need += total
+    if a.active and a.off + total <= a.buf.numel():
+        buf = a.buf[a.off:a.off + total]
+        a.off += total
+    else:
+        buf = torch.zeros(total, device=dev)
     out, off = [], 0
-    for sh, n in zip(shapes, sizes):
+    for sh, n, pn in zip(shapes, sizes, padded):
         out.append(None if sh is None else buf[off:off + n].view(tuple(sh)))
-        off += n
+        off += pn
     return out
 
 
@@ -1079,8 +1123,9 @@ class BackgroundFunction(torch.autograd.Function):
         dH = _run_backward(ctx.head, dfeat)                                          # [M, Fb+27]
         if ddensity is None:
             ddensity = torch.zeros(M, 1, device=dev)
-        dFb_d, dgrads_dens = _mlp_strided_bwd(ctx.dens, ddensity.contiguous(), ctx.H, Fb)
-        dbase_out = dH[:, :Fb] + dFb_d
+        # the density head's input gradient accumulates straight into the head panel's base columns
+        _mlp_strided_bwd(ctx.dens, ddensity.contiguous(), ctx.H, Fb, dx_into=dH[:, :Fb])
+        dbase_out = dH[:, :Fb]
         dX = _run_backward(ctx.base, dbase_out)
         if ctx.grid is not None:
             # grid features of the contracted x: table gradients, and d(contracted x) into the panel's x columns
@@ -1089,7 +1134,7 @@ class BackgroundFunction(torch.autograd.Function):
             grid_bwd(ctx.grid, ctx.X, ctx.X.stride(0), M, ctx.table, ctx.active, dX, 39, dtable, dP)
             dX[:, :3] += dP
         dpos = torch.empty(M, 3, device=dev) if ctx.needs_input_grad[0] else None
-        ddirs = torch.zeros(R, 3, device=dev) if ctx.needs_input_grad[1] else None
+        ddirs = _zeroed_views([(R, 3)], dev)[0] if ctx.needs_input_grad[1] else None
         _lib.call("mms_bg_input_bwd", pos.data_ptr(), ctx.X.data_ptr(), ctx.X.stride(0), dX.data_ptr(), dX.stride(0),
                   dirs.data_ptr(), dH.data_ptr(), dH.stride(0), Fb, R, S, _p(dpos), _p(ddirs), _s())
         ctx.base = ctx.dens = ctx.head = ctx.X = ctx.H = ctx.table = None
@@ -1112,7 +1157,8 @@ def _mlp_strided(run: MLPRun, H: torch.Tensor, Fb: int) -> torch.Tensor:
     return Y
 
 
-def _mlp_strided_bwd(run: MLPRun, dy: torch.Tensor, H: torch.Tensor, Fb: int):
+def _mlp_strided_bwd(run: MLPRun, dy: torch.Tensor, H: torch.Tensor, Fb: int, dx_into: Optional[torch.Tensor] = None):
+    """Backward of _mlp_strided; the input gradient is returned, or (dx_into) added into that [M, K] view."""
     g, v, b = run.params
     N, K = v.shape
     M = H.shape[0]
@@ -1129,6 +1175,10 @@ def _mlp_strided_bwd(run: MLPRun, dy: torch.Tensor, H: torch.Tensor, Fb: int):
         dg = gt.reshape(-1) if gt is not None else torch.zeros(N, device=dev)
         dv = vt if vt is not None else torch.zeros(N, K, device=dev)
         _wn_bwd(g.reshape(-1), v, run.norms[0], dW, dg, dv)
+    if dx_into is not None:
+        gemm(NN, M, K, N, dZ, dZ.stride(0), run.Ws[0], run.Ws[0].stride(0), dx_into, dx_into.stride(0),
+             accumulate=True, prec=run.prec)
+        return dx_into, [None, None, None]
     dxin = _alloc(M, K, dev)
     gemm(NN, M, K, N, dZ, dZ.stride(0), run.Ws[0], run.Ws[0].stride(0), dxin, dxin.stride(0), prec=run.prec)
     return dxin, [None, None, None]
@@ -1191,7 +1241,7 @@ class DensityWeightsFunction(torch.autograd.Function):
         S = ctx.S
         R = density.shape[0] // S
         dden = torch.empty_like(density)
-        ddel = torch.zeros_like(deltas)
+        ddel = _zeroed_views([tuple(deltas.shape)], deltas.device)[0]
         _lib.call("mms_density_weights_bwd", density.data_ptr(), 1, deltas.data_ptr(), R, S, alpha.data_ptr(),
                   dw.contiguous().data_ptr(), dden.data_ptr(), 1, ddel.data_ptr(), _s())
         return dden, ddel, None
@@ -1354,7 +1404,7 @@ class RaysFunction(torch.autograd.Function):
         mats, coords = ctx.saved_tensors
         cams = ctx.cams
         N = coords.shape[0]
-        dm = torch.zeros_like(mats)
+        dm = _zeroed_views([tuple(mats.shape)], mats.device)[0]
         _lib.call("mms_raygen_bwd", coords.data_ptr(), N, cams.fx.data_ptr(), cams.fy.data_ptr(), cams.cx.data_ptr(),
                   cams.cy.data_ptr(), cams.c2w.data_ptr(), _p(cams.distortion), mats.data_ptr(), ctx.per_cam,
                   ctx.off, _p(None if do is None else do.contiguous()), _p(None if dd is None else dd.contiguous()),
@@ -1439,7 +1489,7 @@ class L1LossFunction(torch.autograd.Function):
     def backward(ctx, dl):
         out, target, scratch = ctx.saved_tensors
         N, C = target.shape
-        dout = torch.zeros_like(out)
+        dout = _zeroed_views([tuple(out.shape)], out.device)[0]
         _lib.call("mms_l1_loss_bwd", out.data_ptr(), C, target.data_ptr(), N, C, ctx.thr, _p(scratch),
                   dl.contiguous().data_ptr(), 1.0, dout.data_ptr(), C, _s())
         return dout, None, None
@@ -1455,7 +1505,7 @@ class GeoLossFunction(torch.autograd.Function):
         grads, hess = tensors[:n], tensors[n:]
         total = sum(g.shape[0] for g in grads)
         inv = 1.0 / float(total)
-        eik, curv = _zeroed_views([(), ()], grads[0].device)
+        eik, curv = torch.zeros(2, device=grads[0].device).unbind(0)   # outputs: not from the step arena
         for g, h in zip(grads, hess):
             _lib.call("mms_geo_loss_fwd", g.contiguous().data_ptr(), h.contiguous().data_ptr(), g.shape[0], inv,
                       eik.data_ptr(), curv.data_ptr(), _s())
@@ -1490,7 +1540,7 @@ class GeoLossMaskedFunction(torch.autograd.Function):
         grads, hess = tensors[:n], tensors[n:]
         dev = grads[0].device
         call = torch.cat([c.reshape(1) for c in counts]) if len(counts) > 1 else counts[0].reshape(1)
-        eik, curv = _zeroed_views([(), ()], dev)
+        eik, curv = torch.zeros(2, device=dev).unbind(0)   # outputs: not from the step arena
         ts = [t.contiguous() for t in tensors]
         for g, h, c in zip(ts[:n], ts[n:], counts):
             _lib.call("mms_geo_loss_fwd_masked", g.data_ptr(), h.data_ptr(), g.shape[0], S, c.data_ptr(),

@@ -151,6 +151,13 @@ class GraphTrainer:
         t.fields.zero_grad()
         if t.poses is not None:
             t.poses.zero_grad()
+        fx.zero_arena_begin(t.device)
+        try:
+            return self._forward_backward_body(t, targets, cap)
+        finally:
+            fx.zero_arena_end()
+
+    def _forward_backward_body(self, t, targets, cap: int):
         rays = t.raygen(self.coords)
         outputs = t.model(rays, None, cap=cap)
         if t.raw:

@@ -395,6 +395,14 @@ class Trainer:
         dev = self.device
         coords_d = {m: c.to(dev, non_blocking=True) for m, c in coords.items()}
         targets_d = {m: t.to(dev, non_blocking=True) for m, t in targets.items()}
+        fx.zero_arena_begin(dev)
+        try:
+            return self._compute_grads(coords_d, targets_d, rng, ddp)
+        finally:
+            fx.zero_arena_end()
+
+    def _compute_grads(self, coords_d, targets_d, rng, ddp):
+        dev = self.device
         rays = self.raygen(coords_d)
         fx.reset_grad_uses()
         outputs = self.model(rays, rng)

@@ -94,9 +94,9 @@ def test_compute_loss_uses_the_runs_max_iters():
     from multimodalstudio_amd import pipeline
     src = inspect.getsource(pipeline.compute_loss)
     assert "curvature_factor(step, max_iters)" in src
-    assert "max_iters=self.cfg.max_iters" in inspect.getsource(pipeline.Trainer.compute_grads)
+    assert "max_iters=self.cfg.max_iters" in inspect.getsource(pipeline.Trainer._compute_grads)
     from multimodalstudio_amd import graphs
-    assert "max_iters=t.cfg.max_iters" in inspect.getsource(graphs.GraphTrainer._forward_backward)
+    assert "max_iters=t.cfg.max_iters" in inspect.getsource(graphs.GraphTrainer._forward_backward_body)
     assert pipeline.curvature_factor(45000, 50000) != pipeline.curvature_factor(45000, 100000)
 
 
