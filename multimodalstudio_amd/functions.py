@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -625,10 +626,12 @@ class _ZeroArena:
         self.keep: List[torch.Tensor] = []
         self.off = 0
         self.need = 0
+        self.in_step = False   # between begin / end: demand is counted even before the buffer exists
         self.active = False
 
 
 _ARENA = _ZeroArena()
+_ARENA_OFF = os.environ.get("MMS_NO_ZERO_ARENA", "0") == "1"   # debugging: per-function zero fills
 _ALIGN = 64          # floats: every carved buffer starts on a 256-B boundary (vector / GEMM paths)
 
 
@@ -640,6 +643,7 @@ def zero_arena_begin(dev) -> None:
             a.keep.append(a.buf)
         a.buf = torch.empty(int(a.need * 1.25) + 4 * _ALIGN, device=dev)
     a.need, a.off = 0, 0
+    a.in_step = not _ARENA_OFF
     a.active = a.buf is not None and a.buf.device == torch.device(dev)
     if a.active:
         a.buf.zero_()
@@ -647,6 +651,7 @@ def zero_arena_begin(dev) -> None:
 
 def zero_arena_end() -> None:
     _ARENA.active = False
+    _ARENA.in_step = False
 
 
 def _zeroed_views(shapes, dev) -> List[Optional[torch.Tensor]]:
@@ -656,8 +661,8 @@ def _zeroed_views(shapes, dev) -> List[Optional[torch.Tensor]]:
     padded = [(n + _ALIGN - 1) // _ALIGN * _ALIGN for n in sizes]
     total = max(sum(padded), 1)
     a = _ARENA
-    if a.active:
-        a.need += total
+    if a.in_step:
+        a.need += total     # (counted from the first step on: the buffer is sized at the next begin)
     if a.active and a.off + total <= a.buf.numel():
         buf = a.buf[a.off:a.off + total]
         a.off += total

@@ -4,7 +4,9 @@ Steps are delimited by the field group's AdamW launch (one per step).  Over the 
 the summed kernel time per step (> span where the background stream overlaps the main one), and per kernel symbol
 calls / step, average duration and ms / step.
 
-usage: python scripts/step_kernels.py gpurun_out/prof_X/run_kernel_trace.csv [last_steps] [top]
+usage: python scripts/step_kernels.py gpurun_out/prof_X/run_kernel_trace.csv [last_steps] [top] [skip_steps]
+
+skip_steps drops that many step boundaries from the end first (e.g. the bench's secondary grid_raw5 steps).
 """
 import collections
 import csv
@@ -17,6 +19,8 @@ dur = lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"])  # noqa: E73
 ad = [(i, dur(r)) for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
 big = max(d for _, d in ad)
 ends = [i for i, d in ad if d > big / 4]
+skip = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+ends = ends[:len(ends) - skip]
 seg = ends[-last - 1:]
 ks = rows[seg[0] + 1:seg[-1] + 1]
 steps = len(seg) - 1
