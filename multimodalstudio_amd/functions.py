@@ -39,23 +39,24 @@ PRESETS = {
     # gradient MLP fields (mlp methods, differentiated twice) stay on the exact fp32 MFMA
     # (the polarization heads keep split-bf16x3 too: their Stokes outputs are combined into intensities by
     # differences, and their PSNR after training moved by ~0.2 dB in bf16, tests/test_gpu_train_parity.py)
-    # "sdf_chain": the SDF chain kernel's operand mode -- 3: bf16 weights x split (hi + lo) activations, i.e. the MLP
-    # of the bf16-rounded weights at ~16-bit activation precision (the tap differences stay exact differences of
-    # one function; 2 MFMAs per product instead of 3); its weight gradients stay split-bf16x3 ("sdf": 2), since the
-    # taps' large, opposite dZ rows cancel in dW.  PSNR parity and radiance deviation: tests/test_gpu_train_parity.py,
-    # tests/test_gpu_e2e.py; the kernel itself: tests/test_gpu_chain.py::test_sdf_chain_split_activations
-    "fast": {"sdf": 2, "sdf_chain": 3, "radiance": 1, "heads": 1, "pol_head": 2, "background": 1, "mlp": 0},
+    # "sdf_chain": the SDF chain kernel's operand mode (0: the "sdf" GEMM precision).  The benchmarked preset keeps the
+    # chain on split-bf16x3: the curvature loss sees hessians = second differences of the SDF over delta^2 ~ 1.3e-6,
+    # and with bf16-ROUNDED weights (mode 3, "fast_x2") they are the hessians of a different, rippled function --
+    # 56x the reference's hessian scale off on the e2e fixtures and a 24x larger curvature loss over the rgb training
+    # trajectory, although radiance and PSNR are unchanged (tests/test_gpu_e2e.py::test_e2e_fast_preset_deviation)
+    "fast": {"sdf": 2, "radiance": 1, "heads": 1, "pol_head": 2, "background": 1, "mlp": 0},
     "bf16x3": {"sdf": 2, "radiance": 2, "heads": 2, "pol_head": 2, "background": 2, "mlp": 2},
 }
 for _p in PRESETS.values():
     _p.setdefault("sdf_chain", 0)      # 0: the chain runs on the "sdf" GEMM precision
-# the round-2 fast preset (SDF chain split-bf16x3 as well), kept for comparison
-PRESETS["fast_x3"] = dict(PRESETS["fast"], sdf_chain=0)
+# NOT a parity preset: the SDF chain on bf16 weights x split activations (mms_mlp_chain prec 3, two MFMAs per product;
+# its geometry fails the hessian bound above), kept to measure what the curvature parity costs
+PRESETS["fast_x2"] = dict(PRESETS["fast"], sdf_chain=3)
 PRECISION = dict(PRESETS["fp32"])
 
 
 def set_precision(mode: str) -> None:
-    """Select the MLP GEMM precision preset ('fp32' parity | 'fast' | 'fast_x3' | 'bf16x3')."""
+    """Select the MLP GEMM precision preset ('fp32' parity | 'fast' | 'bf16x3' | 'fast_x2')."""
     PRECISION.update(PRESETS[mode])
 
 
@@ -547,12 +548,52 @@ class ChainRun:
                 items.append((N, K, M, A, B, dW, db))
             wn.append((g, v, l, dW, gt, vt, N, K))
         if items:
-            gemm_tn_grouped(items, self.prec)
+            if ASYNC_WGRAD and _WN_BWD[0] is not None:
+                _wgrad_async(items, self.prec, dev)
+            else:
+                gemm_tn_grouped(items, self.prec)
         for g, v, l, dW, gt, vt, N, K in wn:
             _wn_bwd(g.reshape(-1), v, self.norms[l], dW, gt.reshape(-1) if gt is not None else
                     torch.zeros(N, device=dev), vt if vt is not None else torch.zeros(N, K, device=dev))
         self.Y = self.x = self.bwd_packs = None
         return dx
+
+
+# Weight gradients off the critical path.  Inside a training backward (deferred weight norm: nothing reads dW before
+# the flush) an MLP's grouped weight-gradient launch goes to a side stream forked from the caller's: the SDF MLP's
+# 0.46 ms split-K launch then runs beside the hash-grid backward it used to delay (the grid needs only the chain's dx),
+# and the radiance MLP's beside the radiance grid's.  A final autograd callback joins the side stream back into the
+# caller's stream, so the weight-norm flush and the optimizer see every gradient.  MMS_SYNC_WGRAD=1 keeps them inline.
+ASYNC_WGRAD = os.environ.get("MMS_SYNC_WGRAD", "0") != "1"
+_WGRAD_STREAMS: dict = {}
+
+
+def wgrad_stream(dev) -> "torch.cuda.Stream":
+    i = torch.device(dev).index or 0
+    if i not in _WGRAD_STREAMS:
+        _WGRAD_STREAMS[i] = torch.cuda.Stream(device=i)
+    return _WGRAD_STREAMS[i]
+
+
+def join_wgrad(i: int) -> None:
+    if i in _WGRAD_STREAMS:
+        torch.cuda.current_stream(i).wait_stream(_WGRAD_STREAMS[i])
+
+
+def _wgrad_async(items, prec, dev) -> None:
+    cur = torch.cuda.current_stream(dev)
+    side = wgrad_stream(dev)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        gemm_tn_grouped(items, prec)
+    seen = set()
+    for it in items:
+        for t in it[3:]:          # A, B, dW, db: made (or freed) on the caller's stream, read / written on the side
+            if t is not None and t.data_ptr() not in seen:
+                seen.add(t.data_ptr())
+                t.record_stream(side)
+    i = torch.device(dev).index or 0
+    torch.autograd.Variable._execution_engine.queue_callback(lambda: join_wgrad(i))
 
 
 # Weight-norm backward of the layers, deferred inside a training backward (wn_bwd_begin / wn_bwd_flush, Trainer and

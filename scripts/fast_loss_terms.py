@@ -6,7 +6,9 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 import test_gpu_train_parity as tp  # noqa: E402
 from multimodalstudio_amd import pipeline as pl  # noqa: E402
 
@@ -22,7 +24,7 @@ def wrapped(self, *a, **k):
 
 pl.Trainer.train_step = wrapped
 dev = torch.device("cuda", 0)
-for prec in ("fp32", tp.FAST):
+for prec in (sys.argv[1:] or ["fp32", tp.FAST]):
     rec.clear()
     f, cfg, losses, psnr = tp.run_parity(dev, prec, tp.GOLD)
     keys = rec[0].keys()

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 import torch
 
-# the benchmarked preset under test (MMS_FAST_PRESET=fast_x3: the round-2 preset, SDF chain on split-bf16x3)
+# the benchmarked preset under test (MMS_FAST_PRESET overrides it)
 FAST = os.environ.get("MMS_FAST_PRESET", "fast")
 
 pytestmark = pytest.mark.gpu
@@ -155,7 +155,19 @@ def test_e2e_fast_preset_deviation(dev, name):
         print(f"  {m:14s} radiance rel dev: mean {rel.mean():.3e}  max {rel.max():.3e}")
         assert rel.mean() < 2.5e-2, (m, rel.mean())
         assert rel.max() < 0.25, (m, rel.max())
+        # the geometry the eikonal / curvature losses see: 4-tap SDF gradients and hessians (second differences over
+        # delta^2 ~ 1.3e-6, so any activation rounding that differs between the centre and the tap rows shows here)
+        for k in ("gradients", "hessians"):
+            e = rel_err(outs[m][k].detach().cpu(), f[f"{m}:out:{k}"])
+            print(f"  {m:14s} {k} rel err {e:.3e}")
+            assert e < GEO_TOL_FAST[k], (m, k, e)
     assert loss_rel < 2e-2
+
+
+# fast preset geometry bounds (fp32 mode: gradients 2e-3, hessians 0.15)
+# (split-bf16x3 operands carry ~17 significant bits: measured gradients 2.4e-3, hessians 0.9 of the reference's hessian
+# scale on both fixtures; the bf16-weight SDF chain -- preset fast_x2 -- measured 56 and fails)
+GEO_TOL_FAST = {"gradients": 5e-3, "hessians": 1.5}
 
 
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_gridbg_s95000"])

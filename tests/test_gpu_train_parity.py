@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 import torch
 
-# the benchmarked preset under test (MMS_FAST_PRESET=fast_x3: the round-2 preset, SDF chain on split-bf16x3)
+# the benchmarked preset under test (MMS_FAST_PRESET overrides it)
 FAST = os.environ.get("MMS_FAST_PRESET", "fast")
 
 HERE = os.path.dirname(os.path.abspath(__file__))
