@@ -308,13 +308,16 @@ def main():
     if not args.no_kernel_timing:
         # the background branch on the main stream here: a launch's events then bracket that kernel alone, not the
         # time it shares the chip with the overlapped background stream
+        # (and the weight-gradient launches inline, not on their side stream beside the hash-grid backward)
         trainer.model.concurrent_background = False
+        async_wgrad, mfn.ASYNC_WGRAD = mfn.ASYNC_WGRAD, False
         _lib.TIMER.start(work_fns())
         for _ in range(timing_steps):
             trainer.train_step(ddp=ddp)
         torch.cuda.synchronize()
         _lib.TIMER.stop()
         trainer.model.concurrent_background = not args.serial_background
+        mfn.ASYNC_WGRAD = async_wgrad
 
     rays_per_step, value, ms_per_step, run_mode = run["rays_per_step"], run["value"], run["ms_per_step"], run["step_mode"]
 

@@ -667,6 +667,7 @@ class _ZeroArena:
         self.keep: List[torch.Tensor] = []
         self.off = 0
         self.need = 0
+        self.dev = None
         self.in_step = False   # between begin / end: demand is counted even before the buffer exists
         self.active = False
 
@@ -676,13 +677,20 @@ _ARENA_OFF = os.environ.get("MMS_NO_ZERO_ARENA", "0") == "1"   # debugging: per-
 _ALIGN = 64          # floats: every carved buffer starts on a 256-B boundary (vector / GEMM paths)
 
 
-def zero_arena_begin(dev) -> None:
+def _arena_grow(dev) -> None:
+    # outside a capture only (a buffer allocated while capturing would live in that graph's private pool)
     a = _ARENA
     size = a.buf.numel() if a.buf is not None else 0
     if a.need > size and not torch.cuda.is_current_stream_capturing():
         if a.buf is not None:
             a.keep.append(a.buf)
         a.buf = torch.empty(int(a.need * 1.25) + 4 * _ALIGN, device=dev)
+
+
+def zero_arena_begin(dev) -> None:
+    a = _ARENA
+    _arena_grow(dev)
+    a.dev = dev
     a.need, a.off = 0, 0
     a.in_step = not _ARENA_OFF
     a.active = a.buf is not None and a.buf.device == torch.device(dev)
@@ -691,8 +699,13 @@ def zero_arena_begin(dev) -> None:
 
 
 def zero_arena_end() -> None:
-    _ARENA.active = False
-    _ARENA.in_step = False
+    a = _ARENA
+    if a.in_step:
+        # sized right after the step that measured the demand, so the graphs captured next (GraphTrainer captures
+        # straight after one eager step, every later begin runs inside a capture) already carve from it
+        _arena_grow(a.dev)
+    a.active = False
+    a.in_step = False
 
 
 def _zeroed_views(shapes, dev) -> List[Optional[torch.Tensor]]:
