@@ -562,8 +562,9 @@ class ChainRun:
 # Weight gradients off the critical path.  Inside a training backward (deferred weight norm: nothing reads dW before
 # the flush) an MLP's grouped weight-gradient launch goes to a side stream forked from the caller's: the SDF MLP's
 # 0.46 ms split-K launch then runs beside the hash-grid backward it used to delay (the grid needs only the chain's dx),
-# and the radiance MLP's beside the radiance grid's (side-streaming only the SDF MLP's measured 5 % slower than all).  A final autograd callback joins the side stream back into the
-# caller's stream, so the weight-norm flush and the optimizer see every gradient.  MMS_SYNC_WGRAD=1 keeps them inline.
+# and the radiance MLP's beside the radiance grid's (side-streaming only the SDF MLP's measured 5 % slower than
+# all).  A final autograd callback joins the side stream back into the caller's stream, so the weight-norm flush and
+# the optimizer see every gradient.  MMS_SYNC_WGRAD=1 keeps them inline.
 ASYNC_WGRAD = os.environ.get("MMS_SYNC_WGRAD", "0") != "1"
 _WGRAD_STREAMS: dict = {}
 
