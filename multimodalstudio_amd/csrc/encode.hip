@@ -296,32 +296,22 @@ __global__ void rad_input_fwd_kernel(const float* __restrict__ pos, int64_t ldp,
     }
     return;
   }
-  // one thread per (row, column) of the 29 non-geo columns: consecutive lanes store consecutive columns of a row
-  // (a thread per row wrote its 29 columns with the panel's 1280-B lane stride).  Column c < 3: x_c; 3 <= c < 28:
-  // SH_{c-3} of the ray's direction (all 25 evaluated by sh25 and one selected, same bits); c = 28: n.v at 28 + G.
-  const int64_t n = M * 29;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)row_blocks * blockDim.x) {
-    const int64_t i = q / 29;
-    const int c = (int)(q - i * 29);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)row_blocks * blockDim.x) {
     const float* d = dirs + (i / S) * 3;
     float* row = X + i * ldx;
-    if (c < 3) {
-      row[c] = pos[i * ldp + c];
-    } else if (c < 28) {
-      float sh[25];
-      sh25(d[0], d[1], d[2], sh);
-      float v = 0.f;
+    row[0] = pos[i * ldp];
+    row[1] = pos[i * ldp + 1];
+    row[2] = pos[i * ldp + 2];
+    float sh[25];
+    sh25(d[0], d[1], d[2], sh);
 #pragma unroll
-      for (int k = 0; k < 25; ++k) v = (k == c - 3) ? sh[k] : v;
-      row[c] = v;
-    } else {
-      const float* nr = normals + i * 3;
-      // torch.sum(normals * -directions, dim=-1): left-to-right sum of the three products
-      float ndv = nr[0] * -d[0];
-      ndv = ndv + nr[1] * -d[1];
-      ndv = ndv + nr[2] * -d[2];
-      row[28 + G] = ndv;
-    }
+    for (int k = 0; k < 25; ++k) row[3 + k] = sh[k];
+    const float* n = normals + i * 3;
+    // torch.sum(normals * -directions, dim=-1): left-to-right sum of the three products
+    float ndv = n[0] * -d[0];
+    ndv = ndv + n[1] * -d[1];
+    ndv = ndv + n[2] * -d[2];
+    row[28 + G] = ndv;
   }
 }
 
@@ -522,7 +512,7 @@ MMS_EXPORT int mms_rad_input_fwd(const float* pos, int64_t ldp, const float* dir
   const char* fn = "mms_rad_input_fwd";
   MMS_REQUIRE(ldx >= 29 + G, fn, "panel too narrow");
   if (M == 0) return 0;
-  const unsigned rb = mms::grid_for(M * 29, 256, 16384);
+  const unsigned rb = mms::grid_for(M, 256, 16384);
   const unsigned gb = G > 0 ? mms::grid_for(M * G, 256, 16384) : 0;
   hipLaunchKernelGGL(rad_input_fwd_kernel, dim3(rb + gb), dim3(256), 0, mms::as_stream(stream), pos, ldp, dirs, normals,
                      geo, ldg, M, S, G, X, ldx, rb);
