@@ -682,7 +682,8 @@ def _arena_grow(dev) -> None:
     # outside a capture only (a buffer allocated while capturing would live in that graph's private pool)
     a = _ARENA
     size = a.buf.numel() if a.buf is not None else 0
-    if a.need > size and not torch.cuda.is_current_stream_capturing():
+    capturing = torch.device(dev).type == "cuda" and torch.cuda.is_current_stream_capturing()
+    if a.need > size and not capturing:
         if a.buf is not None:
             a.keep.append(a.buf)
         a.buf = torch.empty(int(a.need * 1.25) + 4 * _ALIGN, device=dev)

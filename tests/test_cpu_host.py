@@ -175,3 +175,43 @@ def test_model_init_matches_train_parity_fixture():
     model = mm.BaseModel(mm.ModelSpec({m: ms.CHANNELS[m] for m in cfg["modalities"]}, log2T=cfg["log2T"]))
     ck = float(sum(float(v.detach().double().abs().sum()) for v in model.state_dict().values()))
     assert ck == pytest.approx(float(f["init_checksum"]), rel=1e-9)
+
+
+def test_zero_arena_is_sized_by_the_first_step_and_carved_after():
+    """functions._ZeroArena (host logic, on CPU tensors): the first step only measures its demand (fresh zeroed
+    buffers), the arena is allocated at that step's end -- before the graphs captured next -- and later steps carve
+    zeroed, 256-B aligned, non-overlapping views from it (round-2 fix: the demand used to be counted only once the
+    buffer existed, so the arena never engaged)."""
+    from multimodalstudio_amd import functions as fx
+    a, dev = fx._ARENA, torch.device("cpu")
+    saved = (a.buf, list(a.keep), a.need, a.off, a.in_step, a.active, a.dev)
+    try:
+        a.buf, a.keep, a.need = None, [], 0
+        fx.zero_arena_begin(dev)
+        first = fx._zeroed_views([(5, 3), None, (7,)], dev)
+        assert first[1] is None and a.buf is None and a.need > 0
+        fx.zero_arena_end()
+        assert a.buf is not None and a.buf.numel() >= a.need
+        fx.zero_arena_begin(dev)
+        v1, v2 = fx._zeroed_views([(5, 3), (7,)], dev)
+        base, end = a.buf.data_ptr(), a.buf.data_ptr() + 4 * a.buf.numel()
+        for v in (v1, v2):
+            assert base <= v.data_ptr() < end and v.data_ptr() % 256 == 0 and float(v.abs().sum()) == 0.0
+        assert v2.data_ptr() >= v1.data_ptr() + 4 * v1.numel()
+        v1.fill_(3.0)
+        fx.zero_arena_end()
+        fx.zero_arena_begin(dev)           # the next step's fill zeroes what the last one wrote
+        w1, = fx._zeroed_views([(5, 3)], dev)
+        assert w1.data_ptr() == v1.data_ptr() and float(w1.abs().sum()) == 0.0
+        fx.zero_arena_end()
+    finally:
+        a.buf, a.keep, a.need, a.off, a.in_step, a.active, a.dev = saved
+
+
+def test_benchmarked_preset_keeps_the_sdf_chain_split_bf16x3():
+    """The `fast` preset (bench default) must keep the SDF MLP on split-bf16x3: the bf16-weight chain (prec 3, preset
+    fast_x2) moved the curvature loss's hessians 56x the reference's hessian scale (tests/test_gpu_e2e.py)."""
+    from multimodalstudio_amd import functions as fx
+    fast = fx.PRESETS["fast"]
+    assert fast["sdf"] == 2 and fast["sdf_chain"] in (0, 2) and fast["mlp"] == 0
+    assert fx.PRESETS["fast_x2"]["sdf_chain"] == 3
