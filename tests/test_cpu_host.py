@@ -196,7 +196,7 @@ def test_zero_arena_is_sized_by_the_first_step_and_carved_after():
         v1, v2 = fx._zeroed_views([(5, 3), (7,)], dev)
         base, end = a.buf.data_ptr(), a.buf.data_ptr() + 4 * a.buf.numel()
         for v in (v1, v2):
-            assert base <= v.data_ptr() < end and v.data_ptr() % 256 == 0 and float(v.abs().sum()) == 0.0
+            assert base <= v.data_ptr() < end and (v.data_ptr() - base) % 256 == 0 and float(v.abs().sum()) == 0.0
         assert v2.data_ptr() >= v1.data_ptr() + 4 * v1.numel()
         v1.fill_(3.0)
         fx.zero_arena_end()
