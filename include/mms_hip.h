@@ -210,6 +210,13 @@ int mms_composite_bwd(const float* w, const float* vals, int64_t ldv, int C, con
  * all sample midpoints; range [2] is scratch, (-inf, -inf) on entry. */
 int mms_render_stats(const float* w, const float* normals, const float* starts, const float* ends, int64_t R, int S,
                      const int64_t* idx, float* out, int64_t ldo, float* range, void* stream);
+/* the same for every modality of a batched hit set in one launch pair: segment m = rays [seg_off[m], seg_off[m+1])
+ * (seg_off: HOST array of n_seg + 1 <= 9 offsets), its rays scatter to out rows m * seg_rows + sidx[r] (sidx: the
+ * ray's row within its modality) and its depth clips to its own midpoint range (range [2 n_seg], (-inf, -inf) on
+ * entry) -- one DepthRenderer call per modality's RayBundle (renderers.py:205-214, base_model.py:146-159). */
+int mms_render_stats_segments(const float* w, const float* normals, const float* starts, const float* ends, int n_seg,
+                              const int64_t* seg_off, int S, const int64_t* sidx, float* out, int64_t ldo,
+                              int64_t seg_rows, float* range, void* stream);
 
 /* ---- PolarizationHead Stokes alignment + intensities (field_heads.py:90-106; polarizer.py:54-101).
  * stokes [M,3] (MLP output), dirs/ups per ray [M/S, 3]; out [M,4]; bwd dstokes =, ddirs +=, dups += */
@@ -270,6 +277,13 @@ int mms_hit_gather_bwd(const int64_t* idx, int64_t R, const float* doh, const fl
  * clamped to cap on the device.  sidx may be NULL. */
 int mms_compact_padded(const unsigned char* mask, int64_t N, int64_t cap, int64_t* idx, int64_t* sidx,
                        int64_t* count, void* stream);
+/* every modality's compaction in one launch (BaseModel runs all modalities' rays through the shared fields as one
+ * batch, base_model.py:86-99 per modality): mask [n_seg N] = n_seg segments of N rays; segment m's hits are laid out
+ * in rows [m cap, (m+1) cap) of gidx (global ray index; padding rows past min(hits, cap) repeat the segment's first
+ * hit) and sidx (index within the segment; N for padding rows), count [n_seg] = min(hits, cap); scratch [n_seg N].
+ * cap = N keeps every hit (dynamic-shape steps read count and use the first count rows of each segment). */
+int mms_compact_segments(const unsigned char* mask, int n_seg, int64_t N, int64_t cap, int64_t* scratch, int64_t* gidx,
+                         int64_t* sidx, int64_t* count, void* stream);
 
 /* ---- losses (model_components/losses.py): L1 (+ SkipSaturation fill), eikonal, curvature; scalars on device */
 int mms_l1_loss_fwd(const float* out, int64_t ldo, const float* tgt, int64_t N, int C, float sat_thr,

@@ -301,6 +301,54 @@ __global__ __launch_bounds__(1024) void compact_pad_kernel(int64_t N, int64_t ca
   }
 }
 
+// Every modality's hit rays in one launch (BaseModel batches all modalities through the shared fields): block m
+// compacts segment m = rays [m N, (m + 1) N) of the concatenated batch (order-preserving, as base_model.py:88-93 per
+// modality) into scratch row m, then lays out `cap` rows per segment: gidx = global ray index of the hit (rows past
+// the segment's hit count repeat its first hit, or its first ray when nothing hit: always a valid row), sidx =
+// the hit's index within its modality (N for padding rows: the dummy row one past the modality's rays), count =
+// min(hits, cap).
+__global__ __launch_bounds__(1024) void compact_segments_kernel(const unsigned char* __restrict__ mask, int64_t N,
+                                                                int64_t cap, int64_t* __restrict__ scratch,
+                                                                int64_t* __restrict__ gidx,
+                                                                int64_t* __restrict__ sidx,
+                                                                int64_t* __restrict__ count) {
+  __shared__ int64_t base;
+  __shared__ int wsum[16];
+  const int64_t seg = blockIdx.x;
+  const int64_t g0 = seg * N;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int64_t start = 0; start < N; start += blockDim.x) {
+    const int64_t i = start + threadIdx.x;
+    const int f = (i < N && mask[g0 + i]) ? 1 : 0;
+    const unsigned long long bal = __ballot(f);
+    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int off = 0;
+    for (int k = 0; k < w; ++k) off += wsum[k];
+    if (f) scratch[g0 + base + off + pre] = g0 + i;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int k = 0; k < (int)(blockDim.x >> 6); ++k) tot += wsum[k];
+      base += tot;
+    }
+    __syncthreads();
+  }
+  __threadfence_block();
+  __syncthreads();
+  const int64_t c = base < cap ? base : cap;
+  const int64_t pad = c > 0 ? scratch[g0] : g0;
+  for (int64_t i = threadIdx.x; i < cap; i += blockDim.x) {
+    const int64_t gi = i < c ? scratch[g0 + i] : pad;
+    gidx[seg * cap + i] = gi;
+    if (sidx) sidx[seg * cap + i] = i < c ? gi - g0 : N;
+  }
+  if (threadIdx.x == 0) count[seg] = c;
+}
+
 // ---- SO(3) x R^3 exponential map of the pose deltas (lie_groups.py:28-63): thread per camera delta.
 // R = I + f1 K + f2 K^2 with K = skew(w), theta = sqrt(max(|w|^2, 1e-4)), f1 = sin(theta) / theta,
 // f2 = (1 - cos(theta)) / theta^2; the translation column is t.  Same float operation order as the reference's
@@ -533,5 +581,16 @@ MMS_EXPORT int mms_compact_padded(const unsigned char* mask, int64_t N, int64_t 
   // so the caller passes an [N] buffer and uses its first cap entries
   hipLaunchKernelGGL(compact_kernel, dim3(1), dim3(1024), 0, s, mask, N, idx, count);
   hipLaunchKernelGGL(compact_pad_kernel, dim3(1), dim3(1024), 0, s, N, cap, idx, sidx, count);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_compact_segments(const unsigned char* mask, int n_seg, int64_t N, int64_t cap, int64_t* scratch,
+                                    int64_t* gidx, int64_t* sidx, int64_t* count, void* stream) {
+  const char* fn = "mms_compact_segments";
+  MMS_REQUIRE(n_seg >= 1 && n_seg <= 65535, fn, "segment count must be in [1, 65535]");
+  MMS_REQUIRE(cap >= 1 && cap <= N, fn, "capacity must be in [1, N]");
+  MMS_REQUIRE(mask && scratch && gidx && count, fn, "null pointer");
+  hipLaunchKernelGGL(compact_segments_kernel, dim3(n_seg), dim3(1024), 0, mms::as_stream(stream), mask, N, cap,
+                     scratch, gidx, sidx, count);
   return mms::check_launch(fn);
 }

@@ -319,7 +319,95 @@ __global__ void render_clip_kernel(int64_t R, const int64_t* __restrict__ idx, f
   d[0] = fminf(fmaxf(d[0], -range[0]), range[1]);
 }
 
+// Every modality's statistics in one launch pair: segment m (blockIdx.y) holds the rays [off[m], off[m + 1]) of the
+// batched hit set; its rows scatter to out rows m * seg_rows + sidx[r] and its depth clips to its own midpoint range
+// (range + 2 m), as one DepthRenderer call per modality does (renderers.py:205-214).
+constexpr int kMaxSeg = 8;
+struct SegOff {
+  int64_t off[kMaxSeg + 1];
+};
+
+__global__ __launch_bounds__(256) void render_stats_seg_kernel(const float* __restrict__ w,
+                                                               const float* __restrict__ nrm,
+                                                               const float* __restrict__ starts,
+                                                               const float* __restrict__ ends, SegOff so, int S,
+                                                               const int64_t* __restrict__ sidx,
+                                                               float* __restrict__ out, int64_t ldo, int64_t seg_rows,
+                                                               float* __restrict__ range) {
+  __shared__ float sl[4], sh[4];
+  const int seg = blockIdx.y;
+  const int64_t r0 = so.off[seg], r1 = so.off[seg + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* o_seg = out + seg * seg_rows * ldo;
+  float lo = INFINITY, hi = -INFINITY;
+  for (int64_t ray = r0 + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); ray < r1;
+       ray += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const int64_t i = ray * S + lane;
+    const bool on = lane < S;
+    const float wi = on ? w[i] : 0.f;
+    const float mid = on ? (starts[i] + ends[i]) / 2.0f : 0.f;
+    const float acc = wave_sum(wi);
+    const float n0 = wave_sum(on ? wi * nrm[i * 3] : 0.f);
+    const float n1 = wave_sum(on ? wi * nrm[i * 3 + 1] : 0.f);
+    const float n2 = wave_sum(on ? wi * nrm[i * 3 + 2] : 0.f);
+    const float dep = wave_sum(on ? wi * mid : 0.f);
+    if (on) { lo = fminf(lo, mid); hi = fmaxf(hi, mid); }
+    if (lane == 0) {
+      float* o = o_seg + sidx[ray] * ldo;
+      o[0] = acc; o[1] = n0; o[2] = n1; o[3] = n2; o[4] = dep;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    lo = fminf(lo, __shfl_xor(lo, o));
+    hi = fmaxf(hi, __shfl_xor(hi, o));
+  }
+  if (lane == 0) { sl[wave] = lo; sh[wave] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    lo = fminf(fminf(sl[0], sl[1]), fminf(sl[2], sl[3]));
+    hi = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+    if (lo <= hi) {
+      atomicMax(range + 2 * seg, -lo);
+      atomicMax(range + 2 * seg + 1, hi);
+    }
+  }
+}
+
+__global__ void render_clip_seg_kernel(SegOff so, const int64_t* __restrict__ sidx, float* __restrict__ out,
+                                       int64_t ldo, int64_t seg_rows, const float* __restrict__ range) {
+  const int seg = blockIdx.y;
+  const int64_t r = so.off[seg] + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= so.off[seg + 1]) return;
+  float* d = out + (seg * seg_rows + sidx[r]) * ldo + 4;
+  d[0] = fminf(fmaxf(d[0], -range[2 * seg]), range[2 * seg + 1]);
+}
+
 }  // namespace
+
+MMS_EXPORT int mms_render_stats_segments(const float* w, const float* normals, const float* starts, const float* ends,
+                                         int n_seg, const int64_t* seg_off, int S, const int64_t* sidx, float* out,
+                                         int64_t ldo, int64_t seg_rows, float* range, void* stream) {
+  const char* fn = "mms_render_stats_segments";
+  MMS_REQUIRE(S >= 1 && S <= 64, fn, "samples per ray must be in [1, 64]");
+  MMS_REQUIRE(ldo >= 5, fn, "output rows hold (acc, n0, n1, n2, depth)");
+  MMS_REQUIRE(n_seg >= 1 && n_seg <= kMaxSeg, fn, "segment count must be in [1, 8]");
+  MMS_REQUIRE(seg_off && sidx && out && range, fn, "null pointer");
+  SegOff so{};
+  int64_t most = 0;
+  for (int m = 0; m <= n_seg; ++m) so.off[m] = seg_off[m];
+  for (int m = 0; m < n_seg; ++m) {
+    MMS_REQUIRE(so.off[m + 1] >= so.off[m], fn, "segment offsets must be non-decreasing");
+    most = so.off[m + 1] - so.off[m] > most ? so.off[m + 1] - so.off[m] : most;
+  }
+  if (most == 0) return 0;
+  hipStream_t s = mms::as_stream(stream);
+  hipLaunchKernelGGL(render_stats_seg_kernel, dim3(mms::grid_for(most * 64, 256, 256), n_seg), dim3(256), 0, s, w,
+                     normals, starts, ends, so, S, sidx, out, ldo, seg_rows, range);
+  hipLaunchKernelGGL(render_clip_seg_kernel, dim3(mms::grid_for(most, 256, INT32_MAX), n_seg), dim3(256), 0, s, so,
+                     sidx, out, ldo, seg_rows, range);
+  return mms::check_launch(fn);
+}
 
 MMS_EXPORT int mms_neus_weights_fwd(const float* sdf, int64_t lds, const float* grads, const float* dirs,
                                     const float* deltas, const float* s_param, float cos_anneal, int64_t R, int S,

@@ -363,9 +363,10 @@ class MLPRun:
             return self.Zs[l], act
         return self.Ys[l], (4 if act == 3 else act)
 
-    def backward(self, dy: torch.Tensor, need_dx: bool,
-                 pre_activated: bool = False) -> Tuple[Optional[torch.Tensor], List[torch.Tensor]]:
-        """dy = gradient of the last layer's output, or (pre_activated) already of its pre-activation."""
+    def backward(self, dy: torch.Tensor, need_dx: bool, pre_activated: bool = False,
+                 dx_out: Optional[torch.Tensor] = None) -> Tuple[Optional[torch.Tensor], List[torch.Tensor]]:
+        """dy = gradient of the last layer's output, or (pre_activated) already of its pre-activation; dx is written
+        into ``dx_out`` (a [M, K] view with unit column stride) when given."""
         x = self.x
         M = x.shape[0]
         dev = x.device
@@ -402,7 +403,7 @@ class MLPRun:
                      prec=self.prec)
                 dZ = dprev
             elif need_dx:
-                dx = _alloc(M, K, dev)
+                dx = dx_out if dx_out is not None else _alloc(M, K, dev)
                 gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[0], self.Ws[0].stride(0), dx, dx.stride(0),
                      prec=self.prec)
         return dx, grads
@@ -506,9 +507,9 @@ class ChainRun:
                [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 32), up(Ns[l], 32), True, True)
                 for l in range(L - 2, -1, -1)]
 
-    def backward(self, dy: torch.Tensor) -> torch.Tensor:
+    def backward(self, dy: torch.Tensor, dx_out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """dy [M, N_last] (rows >= rows_full: column 0 only); accumulates the parameter gradients (grad_target) and
-        returns dx [M, K0]."""
+        returns dx [M, K0] (written into ``dx_out``, a [M, K0] view with unit column stride, when given)."""
         x, Y = self.x, self.Y
         M, K0 = x.shape
         dev = x.device
@@ -519,7 +520,7 @@ class ChainRun:
         # the scaled input's store writes 16 ceil(N/16) columns per row (zeros past N)
         dZl = _alloc(M, 16 * ((Ns[L - 1] + 15) // 16), dev)[:, :Ns[L - 1]] if acts[L - 1] != 0 else None
         dZ = [_alloc(M, Ns[l], dev) for l in range(L - 1)]
-        dx = _alloc(M, K0, dev)
+        dx = dx_out if dx_out is not None else _alloc(M, K0, dev)
         dy = dy if dy.stride(1) == 1 and dy.stride(0) % 4 == 0 else _copy_aligned(dy)
         order = list(range(L - 2, -1, -1))           # hidden layers, last first
         self._chain(True, dy, Ns[L - 1], self.rows_full, packs, [None] * L, [Y[l] for l in order] + [None],
@@ -1648,6 +1649,233 @@ class PolarizerFunction(torch.autograd.Function):
         _lib.call("mms_polarizer_bwd", stokes.data_ptr(), dirs.data_ptr(), ups.data_ptr(), R, S,
                   dout.contiguous().data_ptr(), ds.data_ptr(), dd.data_ptr(), du.data_ptr(), _s())
         return ds, dd, du, None
+
+
+# ------------------------------------------------------------------------------------------------
+# modalities batched through the shared fields
+# ------------------------------------------------------------------------------------------------
+def compact_segments(mask: torch.Tensor, n_seg: int, N: int, cap: int):
+    """Every modality's hit-ray compaction in one launch (mms_compact_segments): (gather index [n_seg cap] of global
+    ray indices, index within the modality [n_seg cap] -- N for padding rows --, device hit counts [n_seg])."""
+    dev = mask.device
+    scratch = torch.empty(n_seg * N, dtype=torch.int64, device=dev)
+    gidx = torch.empty(n_seg * cap, dtype=torch.int64, device=dev)
+    sidx = torch.empty(n_seg * cap, dtype=torch.int64, device=dev)
+    cnt = torch.empty(n_seg, dtype=torch.int64, device=dev)
+    _lib.call("mms_compact_segments", mask.data_ptr(), n_seg, N, cap, scratch.data_ptr(), gidx.data_ptr(),
+              sidx.data_ptr(), cnt.data_ptr(), _s())
+    return gidx, sidx, cnt
+
+
+class HeadSpec:
+    """One modality head for HeadsCompositeFunction: 'plain' (MLP + out activation) or 'polarization' (MLP to Stokes +
+    PolarizerFunction), its activations, its PRECISION key and its parameter count."""
+
+    def __init__(self, kind: str, acts, key: str, n_params: int):
+        self.kind, self.acts, self.key, self.n_params = kind, tuple(acts), key, int(n_params)
+
+
+class HeadsCompositeFunction(torch.autograd.Function):
+    """Modality heads + compositing of a batched ray set in ONE autograd node (RadianceModel heads
+    radiance_model.py:143-149 / field_heads.py:71-106, Renderer.render renderers.py:75-136; the background's heads and
+    sum background_model.py:101-109).  All modalities' rays share the field evaluation; each modality's rays are a
+    contiguous segment of the batch, and only heads and compositing are per modality.
+
+    ``jobs``: (head id, first ray, rays) -- a head evaluated on the feature rows of those rays (S rows per ray);
+    ``items``: (job id, first ray within the job, rays, first ray in ``w``, scatter index or None, output rows) -- one
+    composited output each, over the job's values, scattered into a copy of its background (``bgs[i]``, or None: a
+    plain [rays, C] sum).  The backward writes the feature, weight and direction gradients of every segment into one
+    buffer each (no per-modality zero fill + slice-add), and accumulates the head parameters' gradients in place."""
+
+    @staticmethod
+    def forward(ctx, feat, w, dirs, ups, S: int, heads, jobs, items, *rest):
+        ctx.set_materialize_grads(False)
+        n_items = len(items)
+        bgs, params = rest[:n_items], rest[n_items:]
+        offs, o = [], 0
+        for h in heads:
+            offs.append(o)
+            o += h.n_params
+        keep = any(ctx.needs_input_grad)
+        dirs_c, ups_c = dirs.contiguous(), ups.contiguous()
+        runs, vals = [], []
+        for h_id, r0, rays in jobs:
+            h = heads[h_id]
+            ps = params[offs[h_id]:offs[h_id] + h.n_params]
+            x = feat[r0 * S:(r0 + rays) * S]
+            run = mlp_runner(ps, h.acts, PRECISION[h.key])
+            y = _run_forward(run, x, keep=keep)
+            if h.kind == "polarization":
+                st = y if y.is_contiguous() else y.contiguous()
+                v = torch.empty(rays * S, 4, device=feat.device)
+                _lib.call("mms_polarizer_fwd", st.data_ptr(), dirs_c[r0:].data_ptr(), ups_c[r0:].data_ptr(), rays * S,
+                          S, v.data_ptr(), _s())
+                y = st
+            else:
+                v = y
+            runs.append((run, y))
+            vals.append(v)
+        w_c = w.contiguous()
+        outs = []
+        for (j, sub, rays, w0, sidx, rows), bg in zip(items, bgs):
+            v = vals[j]
+            C = v.shape[1]
+            if bg is not None:
+                out = bg.detach().clone().contiguous()
+            else:
+                out = torch.empty(rays if sidx is None else rows, C, device=feat.device)
+            _lib.call("mms_composite_fwd", w_c[w0:].data_ptr(), v[sub * S:].data_ptr(), v.stride(0), C,
+                      _p(None if bg is None else bg.contiguous()), rays, S, _p(sidx), out.data_ptr(), _s())
+            outs.append(out)
+        ctx.heads, ctx.jobs, ctx.items, ctx.S, ctx.runs, ctx.vals = heads, jobs, items, S, runs, vals
+        ctx.n_params = len(params)
+        ctx.save_for_backward(w_c, dirs_c, ups_c, *[None if b is None else b.contiguous() for b in bgs])
+        ctx.feat_shape = tuple(feat.shape)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        w, dirs, ups, *bgs = ctx.saved_tensors
+        heads, jobs, items, S = ctx.heads, ctx.jobs, ctx.items, ctx.S
+        dev = w.device
+        R = w.shape[0]
+        live = [d is not None for d in douts]
+        # weight gradient: one buffer; written directly when the items with gradients partition its rows
+        w_ranges = [(it[3], it[2]) for it, on in zip(items, live) if on]
+        dw = torch.empty_like(w) if _partitions(w_ranges, R) else _zeroed_views([tuple(w.shape)], dev)[0]
+        dw_direct = _partitions(w_ranges, R)
+        dvals = [None] * len(jobs)
+        dbgs = [None] * len(items)
+        for i, ((j, sub, rays, w0, sidx, rows), dout) in enumerate(zip(items, douts)):
+            if dout is None:
+                continue
+            v = ctx.vals[j]
+            C = v.shape[1]
+            if dvals[j] is None:
+                dvals[j] = _alloc(v.shape[0], C, dev) if _job_covered(j, items, live) else \
+                    _zeroed_views([(v.shape[0], (C + 3) // 4 * 4)], dev)[0][:, :C]
+            bg = bgs[i]
+            dbg = dout.clone() if bg is not None else None
+            dwi = dw[w0:] if dw_direct else torch.empty(rays, S, device=dev)
+            _lib.call("mms_composite_bwd", w[w0:].data_ptr(), v[sub * S:].data_ptr(), v.stride(0), C, _p(bg), rays, S,
+                      _p(sidx), dout.contiguous().data_ptr(), dvals[j][sub * S:].data_ptr(), dvals[j].stride(0),
+                      dwi.data_ptr(), _p(dbg), _s())
+            if not dw_direct:
+                dw[w0:w0 + rays] += dwi
+            dbgs[i] = dbg
+        need_feat = ctx.needs_input_grad[0]
+        f_ranges = [(jobs[j][1], jobs[j][2]) for j in range(len(jobs)) if dvals[j] is not None]
+        f_direct = _partitions(f_ranges, ctx.feat_shape[0] // S)
+        dfeat = None
+        if need_feat:
+            dfeat = torch.empty(ctx.feat_shape, device=dev) if f_direct else \
+                _zeroed_views([ctx.feat_shape], dev)[0]
+        need_dir = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        ddirs = dups = None
+        if need_dir and any(heads[jobs[j][0]].kind == "polarization" and dvals[j] is not None
+                            for j in range(len(jobs))):
+            ddirs, dups = _zeroed_views([tuple(dirs.shape), tuple(ups.shape)], dev)
+        for j, (h_id, r0, rays) in enumerate(jobs):
+            if dvals[j] is None:
+                continue
+            run, y = ctx.runs[j]
+            dy = dvals[j]
+            if heads[h_id].kind == "polarization":
+                # Stokes gradient of the intensities' (PolarizerFunction), direction / up gradients accumulated
+                dd = ddirs[r0:] if ddirs is not None else torch.zeros(rays, 3, device=dev)
+                du = dups[r0:] if dups is not None else torch.zeros(rays, 3, device=dev)
+                dyc = dy.contiguous()
+                dsc = torch.empty(rays * S, 3, device=dev)
+                _lib.call("mms_polarizer_bwd", y.data_ptr(), dirs[r0:].data_ptr(), ups[r0:].data_ptr(), rays, S,
+                          dyc.data_ptr(), dsc.data_ptr(), dd.data_ptr(), du.data_ptr(), _s())
+                dy = dsc
+            if not need_feat:
+                _mlp_backward(run, dy, None)
+                continue
+            rows = dfeat[r0 * S:(r0 + rays) * S]
+            if f_direct:
+                _mlp_backward(run, dy, rows)
+            else:
+                rows += _mlp_backward(run, dy, None)
+        ctx.runs = ctx.vals = None
+        return (dfeat, dw if ctx.needs_input_grad[1] else None, ddirs if ctx.needs_input_grad[2] else None,
+                dups if ctx.needs_input_grad[3] else None, None, None, None, None, *dbgs, *([None] * ctx.n_params))
+
+
+def _partitions(ranges, total: int) -> bool:
+    """True when the (start, length) ranges tile [0, total) exactly once."""
+    pos = 0
+    for a, n in sorted(ranges):
+        if a != pos:
+            return False
+        pos += n
+    return pos == total
+
+
+def _job_covered(j: int, items, live) -> bool:
+    """True when job j's items with gradients write every value row of the job exactly once."""
+    rng = [(it[1], it[2]) for it, on in zip(items, live) if on and it[0] == j]
+    total = max([a + n for a, n in rng] + [0])
+    return _partitions(rng, total) and total > 0
+
+
+def _mlp_backward(run, dy: torch.Tensor, dx_out: Optional[torch.Tensor]) -> torch.Tensor:
+    """dX of an MLP runner (written into dx_out when given); parameter gradients accumulated in place."""
+    if isinstance(run, ChainRun):
+        dy = dy if dy.stride(1) == 1 and dy.stride(0) % 4 == 0 and dy.data_ptr() % 16 == 0 else _copy_aligned(dy)
+        return run.backward(dy, dx_out=dx_out)
+    dx, _ = run.backward(dy.contiguous(), need_dx=True, dx_out=dx_out)
+    return dx
+
+
+class GeoLossSegFunction(torch.autograd.Function):
+    """Eikonal MSE(||g||, 1) and curvature L1(sum h, 0) over every modality's rows of a batched hit set
+    (LossManager.compute_loss concatenates the modalities' gradients / hessians, losses.py:235-260).  ``counts``
+    (fixed-capacity batches): device hit counts [n_seg]; segment m owns rows [m rows_per_seg S, (m+1) rows_per_seg S)
+    of which the first counts[m] S are real.  None: every row is real."""
+
+    @staticmethod
+    def forward(ctx, S: int, counts, seg_rays: int, grads, hess):
+        ctx.set_materialize_grads(False)
+        dev = grads.device
+        g = grads.reshape(-1, 3).contiguous()
+        h = hess.reshape(-1, 3).contiguous() if hess is not None else None
+        M = g.shape[0]
+        eik, curv = torch.zeros(2, device=dev).unbind(0)   # outputs: not from the step arena
+        if counts is None:
+            _lib.call("mms_geo_loss_fwd", g.data_ptr(), _p(h), M, 1.0 / float(max(M, 1)), eik.data_ptr(),
+                      curv.data_ptr(), _s())
+        else:
+            n = counts.shape[0]
+            rows = seg_rays * S
+            for m in range(n):
+                _lib.call("mms_geo_loss_fwd_masked", g[m * rows:].data_ptr(),
+                          _p(None if h is None else h[m * rows:]), rows, S, counts[m:].data_ptr(), counts.data_ptr(),
+                          n, eik.data_ptr(), curv.data_ptr(), _s())
+        ctx.save_for_backward(g, h, counts)
+        ctx.S, ctx.seg_rays, ctx.shape = S, seg_rays, (tuple(grads.shape), None if hess is None else tuple(hess.shape))
+        return eik, curv
+
+    @staticmethod
+    def backward(ctx, deik, dcurv):
+        g, h, counts = ctx.saved_tensors
+        S = ctx.S
+        M = g.shape[0]
+        dg, dh = _zeroed_views([(M, 3), (M, 3) if h is not None else None], g.device)
+        de = _p(None if deik is None else deik.contiguous())
+        dc = _p(None if dcurv is None else dcurv.contiguous())
+        if counts is None:
+            _lib.call("mms_geo_loss_bwd", g.data_ptr(), _p(h), M, 1.0 / float(max(M, 1)), de, 1.0, dc, 1.0,
+                      dg.data_ptr(), _p(dh), _s())
+        else:
+            n = counts.shape[0]
+            rows = ctx.seg_rays * S
+            for m in range(n):
+                _lib.call("mms_geo_loss_bwd_masked", g[m * rows:].data_ptr(), _p(None if h is None else h[m * rows:]),
+                          rows, S, counts[m:].data_ptr(), counts.data_ptr(), n, de, 1.0, dc, 1.0,
+                          dg[m * rows:].data_ptr(), _p(None if dh is None else dh[m * rows:]), _s())
+        gs, hs = ctx.shape
+        return None, None, None, dg.view(gs), (dh.view(hs) if dh is not None else None)
 
 
 def HashGridApply(x, table, cfg: GridCfg, active: int):

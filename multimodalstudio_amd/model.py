@@ -7,6 +7,7 @@ base_model.py:82-161 stage by stage; every stage runs in libmms_hip.so through f
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
@@ -327,6 +328,23 @@ def _render_stats(w, normals, starts, ends, R: int, S: int, sidx, rows: int, dev
     return stats, rng
 
 
+def _render_stats_segments(w, normals, starts, ends, off: List[int], S: int, sidx, rows: int, dev):
+    """[n_seg rows, 5] = (accumulation, normals, depth) of every modality segment of a batched hit set: segment m's rays
+    [off[m], off[m+1]) scatter to rows m rows + sidx (zero elsewhere), the depth clipped to that segment's own sample
+    midpoint range (one DepthRenderer call per modality, renderers.py:205-214)."""
+    n = len(off) - 1
+    buf = torch.zeros(n * rows * 5 + 2 * n, device=dev)
+    stats = buf[:n * rows * 5].view(n * rows, 5)
+    rng = buf[n * rows * 5:]
+    rng.fill_(float("-inf"))
+    seg = (ctypes.c_int64 * (n + 1))(*off)
+    with torch.no_grad():
+        _lib.call("mms_render_stats_segments", w.data_ptr(), normals.detach().contiguous().data_ptr(),
+                  starts.data_ptr(), ends.data_ptr(), n, ctypes.cast(seg, ctypes.c_void_p), S, sidx.data_ptr(),
+                  stats.data_ptr(), 5, rows, rng.data_ptr(), fx._s())
+    return stats
+
+
 def nerf_encoding(x: torch.Tensor, F: int) -> torch.Tensor:
     """NeRFEncoding.forward (encodings.py:161-182), frequencies 2^0 .. 2^(F-1), input included, in torch operators
     (twice differentiable: the analytic-gradient fields differentiate through it again)."""
@@ -630,114 +648,196 @@ class BaseModel(nn.Module):
     def _forward(self, rays, rng, cap):
         """rays[mod] = {"origins", "directions", "up_directions"} ([N,3] device); returns per-modality outputs.
 
+        The reference loops over modalities (base_model.py:102-159), each with its own sampler and field calls; the
+        surface, radiance and background fields are shared, so here every modality's rays go through them as ONE
+        batch (one collider / compaction / sampler / field / hash-grid / weight-gradient launch per stage for all
+        modalities) and only the heads and the compositing stay per modality (HeadsCompositeFunction).  Each
+        modality's hit rays are a contiguous segment of the batch, in the reference's per-modality ray order, so every
+        per-ray result is the one the modality loop computes.  Modalities with different ray counts (an evaluation
+        chunk tail) form separate batches.
+
         ``cap``: fixed-capacity foreground batch for graph capture (graphs.py).  Each modality's hit rays are
         compacted into ``cap`` rows without reading the hit count on the host; rows past the count repeat the first
         hit ray, composite into a dummy output row N that is cut off, and are skipped by the geometric losses
         (outputs[mod]["count"] is the device hit count), so every gradient they produce is exactly zero and the
         results equal the dynamic path's.  Per-ray outputs ("gradients", "weights", ...) then have ``cap`` rows."""
         rng = rng or RNG()
+        groups: Dict[int, List[str]] = {}
+        for m in self.spec.modalities:
+            groups.setdefault(int(rays[m]["origins"].shape[0]), []).append(m)
+        outputs, drew = {}, False
+        for gi, (N, mods) in enumerate(groups.items()):
+            out, d = self._forward_batch(mods, rays, rng, cap, N, gi)
+            outputs.update(out)
+            drew = drew or d
+        if drew:
+            dev = next(iter(rays.values()))["origins"].device
+            _lib.call("mms_counter_advance", self._draw_counter(dev).data_ptr(), 1 << 32, fx._s())
+        return {m: outputs[m] for m in self.spec.modalities}
+
+    def _draws_for(self, mods, get, rows, shape_tail, dev):
+        """Injected per-modality draws concatenated in modality order (per-hit-ray draws cut / zero-padded to
+        ``rows[i]``); None when no modality has any and the model is not training (evaluation: no jitter); missing
+        ones drawn fresh."""
+        parts = [get(m) for m in mods]
+        if all(p is None for p in parts) and not self.training:
+            return None
+        out = []
+        for i, p in enumerate(parts):
+            if p is None:
+                p = torch.rand(rows[i], *shape_tail, device=dev)
+            elif tuple(shape_tail) == (1,):
+                p = _pad_rows(p[:rows[i]], rows[i])
+            out.append(p)
+        return out[0] if len(out) == 1 else torch.cat(out, 0)
+
+    def _forward_batch(self, mods, rays, rng, cap, N: int, gi: int):
         sp = self.spec
-        outputs = {}
+        nm = len(mods)
+        dev = rays[mods[0]]["origins"].device
         s_param = self.surface_model.volume_rendering.density_fn.variance_network.s
         inv_s = 1.0 / self.surface_model.volume_rendering.density_fn.variance_network.get_inv_variance()  # once
+        cat = (lambda ts: ts[0]) if nm == 1 else (lambda ts: torch.cat(ts, 0))
+        o = cat([rays[m]["origins"] for m in mods])
+        d = cat([rays[m]["directions"] for m in mods])
+        up = cat([rays[m]["up_directions"] for m in mods])
+        nears, fars, bnears, bfars, mask = fx.ColliderFunction.apply(o, d, 1.0)
+        seg = N if cap is None else min(int(cap), N)
+        gidx, sidx_all, counts = fx.compact_segments(mask, nm, N, seg)
+        if cap is None:
+            # dynamic shapes: the hit counts on the host (one read for every modality)
+            Rm = [int(c) for c in counts.tolist()]
+            sidx_m = [sidx_all[i * N:i * N + Rm[i]] for i in range(nm)]
+            idx = cat([gidx[i * N:i * N + Rm[i]] for i in range(nm)])
+            sidx_cat = cat(sidx_m)
+            count_of = [None] * nm
+        else:
+            Rm = [seg] * nm
+            sidx_m = [sidx_all[i * seg:(i + 1) * seg] for i in range(nm)]
+            idx, sidx_cat = gidx, sidx_all
+            count_of = [counts[i:i + 1] for i in range(nm)]
+        off = [0]
+        for r in Rm:
+            off.append(off[-1] + r)
+        R = off[-1]
+        o_h, d_h, up_h, n_h, f_h = fx.HitGatherFunction.apply(idx, o, d, up, nears, fars)
         drew = False
-        for mi, mod in enumerate(sp.modalities):
-            r = rays[mod]
-            o, d, up = r["origins"], r["directions"], r["up_directions"]
-            N = o.shape[0]
-            dev = o.device
-            nears, fars, bnears, bfars, mask = fx.ColliderFunction.apply(o, d, 1.0)
-            if cap is None:
-                idx = fx.compact(mask)
-                sidx, count = idx, None
-            else:
-                idx, sidx, count = fx.compact_padded(mask, min(int(cap), N))
-            R = idx.shape[0]
-            o_h, d_h, up_h, n_h, f_h = fx.HitGatherFunction.apply(idx, o, d, up, nears, fars)
-            fused = self.training and mod not in rng.uniform and mod not in rng.pdf and mod not in rng.background
-            if fused:
-                # this modality's jitter, PDF and background draws in one device launch (mms_uniform)
-                t_rand, pdf, bt_fused = self._device_draws(mi, R, N, dev)
-                drew = True
-            else:
-                t_rand = _pad_rows(rng.uniform.get(mod), R)
-                if t_rand is None and self.training:
-                    t_rand = torch.rand(R, 1, device=dev)
-                pdf = rng.pdf.get(mod)
-                if pdf is not None:
-                    pdf = [_pad_rows(p, R) for p in pdf]
-                elif self.training:
-                    pdf = [torch.rand(R, 1, device=dev) for _ in range(sp.upsample_steps)]
-            # background (background_model.py:73-111) on all N rays.  It depends on the foreground only through the
-            # final composite, so it runs on a second HIP stream (forward here, and -- autograd runs each node's
-            # backward on its forward's stream -- its backward too), overlapping the NeuS sampler and the surface /
-            # radiance work; the main stream joins it right before the composite, and every backward through it ends
-            # with a join (_JoinBackground)
-            bt = bt_fused if fused else rng.background.get(mod)
-            if bt is None and self.training:
-                bt = torch.rand(N, sp.bg_samples + 1, device=dev)
-            cur = torch.cuda.current_stream(dev)
-            bgs = background_stream(dev) if self.concurrent_background else cur
-            if bgs is not cur:
-                bgs.wait_stream(cur)
-            # every head on every modality's rays (radiance_model.py:143-149) -- or, with own_heads_only (training:
-            # only the ray's own modality's output reaches the loss, raw_pipeline.py:112-122), just its own
-            heads_for = [mod] if (self.own_heads_only and torch.is_grad_enabled()) else None
-            with torch.cuda.stream(bgs):
-                blin = self._lin_dev(sp.bg_samples + 1, 1.0, dev)
-                bbins = torch.empty(N, sp.bg_samples + 1, device=dev)
-                _lib.call("mms_stratified_bins", blin.data_ptr(), sp.bg_samples + 1, fx._p(bt), sp.bg_samples + 1, N,
-                          bbins.data_ptr(), fx._s())
-                bpos, bdeltas, _, _ = fx.SamplesFunction.apply(bbins, bnears, bfars, o, d, 1)
-                density, bfeat = self.background_model.field(bpos, d, sp.bg_samples)
-                bw = fx.DensityWeightsFunction.apply(density, bdeltas, sp.bg_samples)
-                bg_out = {}
-                for m, head in self.background_model.modality_heads.items():
-                    if heads_for is not None and m not in heads_for:
-                        continue
-                    vals = head(bfeat, d, up, sp.bg_samples)
-                    bg_out[m] = fx.CompositeFunction.apply(bw, vals, None, None, sp.bg_samples)
-            # NeuS sampling (ray_samplers.py:448-514) -- latency-bound launches the background work overlaps
-            bins = self.neus_bins(n_h.detach(), f_h.detach(), o_h.detach(), d_h.detach(), t_rand, pdf)
-            S = bins.shape[1] - 1
-            pos, deltas, starts, ends = fx.SamplesFunction.apply(bins, n_h, f_h, o_h, d_h, 0)
-            # surface + radiance
-            sdf, geo, grads, hess, normals = self.surface_model(pos)
-            vr = self.surface_model.volume_rendering
-            w = fx.NeusWeightsFunction.apply(sdf, grads, d_h, deltas, s_param, vr._cos_anneal_ratio, S)
-            feat = self.radiance_model.features(pos, d_h, normals.detach(), geo, S)
-            out = {}
-            rows = N if cap is None else N + 1     # padded batches scatter into a dummy row N, cut off below
-            if bgs is not cur:
-                cur.wait_stream(bgs)
-                for m in list(bg_out):
-                    bg_out[m].record_stream(cur)    # made on the background stream, read (and freed) on this one
-                    if torch.is_grad_enabled() and bg_out[m].requires_grad:
-                        bg_out[m] = _JoinBackground.apply(bg_out[m], torch.device(dev).index or 0)
-            for m, head in self.radiance_model.modality_heads.items():
-                if heads_for is not None and m not in heads_for:
-                    continue
-                vals = head(feat, d_h, up_h, S)
-                bg = bg_out[m]
-                if cap is not None:
-                    bg = torch.cat([bg, bg.new_zeros(1, bg.shape[1])])
-                out[m] = fx.CompositeFunction.apply(w, vals, bg, sidx, S)[:N]
-            # accumulation / normals / depth renderers (renderers.py:176-242, no grad): one launch pair
-            stats, rng_buf = _render_stats(w, normals, starts, ends, R, S, sidx, rows, dev)
-            out["normals"] = stats[:N, 1:4]
-            out["depth"] = stats[:N, 4:5]
-            out["accumulation"] = stats[:N, 0:1]
-            out["count"] = count
-            out["gradients"] = grads.view(R, S, 3)
-            out["hessians"] = hess.view(R, S, 3) if hess is not None else None
+        if self.training and not any(m in rng.uniform or m in rng.pdf or m in rng.background for m in mods):
+            # every modality's jitter, PDF and background draws in one device launch (mms_uniform)
+            t_rand, pdf, bt = self._device_draws(gi, R, nm * N, dev)
+            drew = True
+        else:
+            t_rand = self._draws_for(mods, rng.uniform.get, Rm, (1,), dev)
+            pdf = None
+            if any(m in rng.pdf for m in mods) or self.training:
+                pdf = [self._draws_for(mods, lambda m, j=j: (rng.pdf[m][j] if m in rng.pdf else None), Rm, (1,), dev)
+                       for j in range(sp.upsample_steps)]
+            bt = self._draws_for(mods, rng.background.get, [N] * nm, (sp.bg_samples + 1,), dev)
+        # background (background_model.py:73-111) on all rays.  It depends on the foreground only through the final
+        # composite, so it runs on a second HIP stream (forward here, and -- autograd runs each node's backward on its
+        # forward's stream -- its backward too), overlapping the NeuS sampler and the surface / radiance work; the
+        # main stream joins it right before the composite, and every backward through it ends with a join
+        cur = torch.cuda.current_stream(dev)
+        bgs = background_stream(dev) if self.concurrent_background else cur
+        if bgs is not cur:
+            bgs.wait_stream(cur)
+        # every head on every modality's rays (radiance_model.py:143-149) -- or, with own_heads_only (training: only
+        # the ray's own modality's output reaches the loss, raw_pipeline.py:112-122), just its own
+        own = self.own_heads_only and torch.is_grad_enabled()
+        with torch.cuda.stream(bgs):
+            nb = sp.bg_samples + 1
+            blin = self._lin_dev(nb, 1.0, dev)
+            bbins = torch.empty(nm * N, nb, device=dev)
+            _lib.call("mms_stratified_bins", blin.data_ptr(), nb, fx._p(bt), nb, nm * N, bbins.data_ptr(), fx._s())
+            bpos, bdeltas, _, _ = fx.SamplesFunction.apply(bbins, bnears, bfars, o, d, 1)
+            density, bfeat = self.background_model.field(bpos, d, sp.bg_samples)
+            bw = fx.DensityWeightsFunction.apply(density, bdeltas, sp.bg_samples)
+            bg_out = self._heads_composite(self.background_model.modality_heads, mods, own, bfeat, bw, d, up,
+                                           sp.bg_samples, [i * N for i in range(nm)], [N] * nm)
+        # NeuS sampling (ray_samplers.py:448-514) -- latency-bound launches the background work overlaps
+        bins = self.neus_bins(n_h.detach(), f_h.detach(), o_h.detach(), d_h.detach(), t_rand, pdf)
+        S = bins.shape[1] - 1
+        pos, deltas, starts, ends = fx.SamplesFunction.apply(bins, n_h, f_h, o_h, d_h, 0)
+        # surface + radiance
+        sdf, geo, grads, hess, normals = self.surface_model(pos)
+        vr = self.surface_model.volume_rendering
+        w = fx.NeusWeightsFunction.apply(sdf, grads, d_h, deltas, s_param, vr._cos_anneal_ratio, S)
+        feat = self.radiance_model.features(pos, d_h, normals.detach(), geo, S)
+        rows = N if cap is None else N + 1     # padded batches scatter into a dummy row N, cut off below
+        if bgs is not cur:
+            cur.wait_stream(bgs)
+            for k in list(bg_out):
+                bg_out[k].record_stream(cur)    # made on the background stream, read (and freed) on this one
+                if torch.is_grad_enabled() and bg_out[k].requires_grad:
+                    bg_out[k] = _JoinBackground.apply(bg_out[k], torch.device(dev).index or 0)
+        bg_in = {}
+        for k, b in bg_out.items():
+            bg_in[k] = b if cap is None else torch.cat([b, b.new_zeros(1, b.shape[1])])
+        fg = self._heads_composite(self.radiance_model.modality_heads, mods, own, feat, w, d_h, up_h, S, off[:-1], Rm,
+                                   sidx=sidx_m, bgs=bg_in, rows=rows)
+        # accumulation / normals / depth renderers (renderers.py:176-242, no grad): one launch pair for all modalities
+        stats = _render_stats_segments(w, normals, starts, ends, off, S, sidx_cat, rows, dev)
+        geo_batch = {"grads": grads, "hess": hess, "counts": None if cap is None else counts, "seg_rays": seg, "S": S,
+                     "mods": tuple(mods)}
+        outputs = {}
+        for i, mod in enumerate(mods):
+            a, b = off[i], off[i + 1]
+            out = {h: v[:N] for (k, h), v in fg.items() if k == i}
+            st = stats[i * rows:i * rows + N]
+            out["normals"] = st[:, 1:4]
+            out["depth"] = st[:, 4:5]
+            out["accumulation"] = st[:, 0:1]
+            out["count"] = count_of[i]
+            out["gradients"] = grads[a * S:b * S].view(b - a, S, 3)
+            out["hessians"] = hess[a * S:b * S].view(b - a, S, 3) if hess is not None else None
             out["inv_s"] = inv_s
-            out["weights"] = w
-            out["bins"] = bins
-            out["mask"] = mask
+            out["weights"] = w[a:b]
+            out["bins"] = bins[a:b]
+            out["mask"] = mask[i * N:(i + 1) * N]
+            out["_geo"] = geo_batch
             outputs[mod] = out
-        if drew:
-            _lib.call("mms_counter_advance", self._draw_counter(dev).data_ptr(), 1 << 32, fx._s())
-        return outputs
+        return outputs, drew
+
+    def _heads_composite(self, heads: nn.ModuleDict, mods, own: bool, feat, w, dirs, ups, S: int, seg_off, seg_rays,
+                         sidx=None, bgs=None, rows=None):
+        """Every (modality segment, head) output of one branch through HeadsCompositeFunction: {(segment, head name):
+        [rows, C]}.  With gradients each pair is a job of its own (its head's backward covers exactly its rows);
+        without (evaluation) each head runs once over the whole batch and the pairs composite slices of it."""
+        names = list(heads)
+        specs, params = [], []
+        for h in names:
+            mod = heads[h]
+            ps = mod.field.params()
+            specs.append(fx.HeadSpec(mod.kind, mod.field.acts, mod.field.precision_key, len(ps)))
+            params += ps
+        pairs = [(i, mods[i]) for i in range(len(mods)) if mods[i] in heads] if own else \
+            [(i, h) for i in range(len(mods)) for h in names]
+        grad = torch.is_grad_enabled()
+        jobs, items, bg_list, keys, out = [], [], [], [], {}
+        job_of_head = {}
+        for i, h in pairs:
+            bg = None if bgs is None else bgs[(i, h)]
+            if seg_rays[i] == 0:
+                out[(i, h)] = bg        # no hit ray: the modality's output is its background
+                continue
+            hid = names.index(h)
+            if grad:
+                jobs.append((hid, seg_off[i], seg_rays[i]))
+                j, sub = len(jobs) - 1, 0
+            else:
+                if hid not in job_of_head:
+                    jobs.append((hid, 0, sum(seg_rays)))
+                    job_of_head[hid] = len(jobs) - 1
+                j, sub = job_of_head[hid], seg_off[i]
+            items.append((j, sub, seg_rays[i], seg_off[i], None if sidx is None else sidx[i], rows))
+            bg_list.append(bg)
+            keys.append((i, h))
+        if items:
+            res = fx.HeadsCompositeFunction.apply(feat, w, dirs, ups, S, specs, jobs, items, *bg_list, *params)
+            if not isinstance(res, tuple):
+                res = (res,)
+            out.update(zip(keys, res))
+        return out
 
     # -- training-mode uniform draws on the device ----------------------------------------------------
     def seed_draws(self, seed: int, dev) -> None:
@@ -755,15 +855,15 @@ class BaseModel(nn.Module):
             self._draw_ctr = c
         return c
 
-    def _device_draws(self, mi: int, R: int, N: int, dev):
-        """(jitter [R,1], PDF draws 4 x [R,1], background [N, bg+1]) ~ U[0,1) from one mms_uniform launch, the
-        stream keyed by (draw_seed, modality index); the reference draws these with torch.rand in the same shapes
-        (SURVEY §8(d) 'RNG')."""
+    def _device_draws(self, gi: int, R: int, N: int, dev):
+        """(jitter [R,1], PDF draws 4 x [R,1], background [N, bg+1]) ~ U[0,1) of a whole modality batch from one
+        mms_uniform launch, the stream keyed by (draw_seed, batch index); the reference draws these with torch.rand in
+        the same shapes per modality (SURVEY §8(d) 'RNG')."""
         sp = self.spec
         nb = sp.bg_samples + 1
         k = sp.upsample_steps
         buf = torch.empty(R * (1 + k) + N * nb, device=dev)
-        _lib.call("mms_uniform", int(getattr(self, "draw_seed", 0)) & ((1 << 64) - 1), mi,
+        _lib.call("mms_uniform", int(getattr(self, "draw_seed", 0)) & ((1 << 64) - 1), gi,
                   self._draw_counter(dev).data_ptr(), 0, buf.numel(), buf.data_ptr(), fx._s())
         t_rand = buf[:R].view(R, 1)
         pdf = [buf[R * (1 + j):R * (2 + j)].view(R, 1) for j in range(k)]

@@ -229,9 +229,16 @@ def compute_loss(outputs, targets: Dict[str, torch.Tensor], modalities: List[str
         l = fx.L1LossFunction.apply(outputs[mod][mod], targets[mod], thr)
         losses[mod] = l
         total = l if total is None else total + l
-    grads = [outputs[m]["gradients"].reshape(-1, 3) for m in modalities]
     # mlp methods: no hessian and no curvature loss (method_configs.py:350-352: geometry losses = eikonal only)
     analytic = outputs[modalities[0]]["hessians"] is None
+    geo = outputs[modalities[0]].get("_geo")
+    if geo is not None and tuple(geo["mods"]) == tuple(modalities) and \
+            all(outputs[m].get("_geo") is geo for m in modalities):
+        # the model's batched geometry (every modality's rows of one tensor): the concatenation the reference
+        # builds (losses.py:235-248), read in place
+        eik, curv = fx.GeoLossSegFunction.apply(geo["S"], geo["counts"], geo["seg_rays"], geo["grads"], geo["hess"])
+        return _finish_loss(losses, total, eik, curv, analytic, step, max_iters)
+    grads = [outputs[m]["gradients"].reshape(-1, 3) for m in modalities]
     hess = [torch.zeros_like(g) if analytic else outputs[m]["hessians"].reshape(-1, 3)
             for m, g in zip(modalities, grads)]
     counts = [outputs[m].get("count") for m in modalities]
@@ -241,6 +248,11 @@ def compute_loss(outputs, targets: Dict[str, torch.Tensor], modalities: List[str
         eik, curv = fx.GeoLossMaskedFunction.apply(S, counts, *grads, *hess)
     else:
         eik, curv = fx.GeoLossFunction.apply(*grads, *hess)
+    return _finish_loss(losses, total, eik, curv, analytic, step, max_iters)
+
+
+def _finish_loss(losses, total, eik, curv, analytic: bool, step: int, max_iters: int):
+    """Weighted eikonal (0.1) and curvature (5e-4 x warm-up / level factor) terms (method_configs.py:252-253)."""
     losses["eikonal_loss"] = eik
     total = total + 0.1 * eik
     if not analytic:

@@ -117,11 +117,45 @@ def analytic_radiance(origins: np.ndarray, dirs: np.ndarray, channels: int) -> n
     return np.clip(out, 0.0, 1.0).astype(np.float32)
 
 
+POL_LIGHT = (0.48, -0.36, 0.8)    # unit light direction of the polarization frames' specular highlight
+
+
+def polarization_intensities(n: torch.Tensor, hit: torch.Tensor, d: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+    """Four polarizer-filtered intensities [..., 4] (0, 45, 90, 135 deg) of a Stokes field that the reference's
+    PolarizationHead can represent exactly: world-frame Stokes S = s0 (1, p cos 2psi, p sin 2psi) that depend on
+    the hit normal n (the direction d for misses), rotated into the camera frame by align_polarization_filters'
+    angle theta = acos(clamp(normalize(d x z) . up, +-(1 - 1e-4))) - pi/2 and split by stokes_to_intensity
+    (/root/reference/src/model_components/polarizer.py:54-101), so I0 + I2 = I1 + I3 = s0 as a real polarization
+    camera measures (Malus).  A specular highlight pushes s0 past 1 on a small patch: those pixels clip at 1.0 and
+    are what SkipSaturationLoss (losses.py:152-164) exists for."""
+    L = torch.tensor(POL_LIGHT, device=d.device, dtype=d.dtype)
+    L = L / L.norm()
+    ndl = (n * L).sum(-1)
+    s0_fg = 0.15 + 0.55 * (0.5 + 0.5 * ndl) + 1.1 * torch.clamp(ndl, min=0.0) ** 6
+    p_fg = 0.1 + 0.4 * (1.0 - (n * -d).sum(-1).abs())
+    psi_fg = torch.atan2(n[..., 1], n[..., 0])
+    s0_bg = 0.45 + 0.35 * d[..., 2]
+    psi_bg = torch.atan2(d[..., 1], d[..., 0])
+    s0 = torch.where(hit, s0_fg, s0_bg)
+    p = torch.where(hit, p_fg, torch.full_like(s0_bg, 0.2))
+    psi = torch.where(hit, psi_fg, psi_bg)
+    s1, s2 = s0 * p * torch.cos(2 * psi), s0 * p * torch.sin(2 * psi)
+    zaxis = torch.zeros_like(d)
+    zaxis[..., 2] = 1.0
+    plane = torch.nn.functional.normalize(torch.linalg.cross(d, zaxis), dim=-1)
+    cos_t = torch.clamp((plane * up).sum(-1), min=-1 + 1e-4, max=1 - 1e-4)
+    theta = torch.acos(cos_t) - np.pi / 2
+    c, s = torch.cos(2 * theta), torch.sin(2 * theta)
+    a1, a2 = c * s1 + s * s2, -s * s1 + c * s2
+    return 0.5 * torch.stack([s0 + a1, s0 + a2, s0 - a1, s0 - a2], -1)
+
+
 def render_frames(cams: ModalityCameras, channels: int, device, raw_mod: Optional[str] = None) -> torch.Tensor:
     """Analytic frames [C, H, W, channels] (or mosaicked [C, H, W, 1] when raw_mod is given) on `device`.
 
     Data preparation only (the reference loads frames from disk into RAM, dataloaders.py:135-162); uses
-    plain tensor math on the chosen device.
+    plain tensor math on the chosen device.  Four-channel (polarization) frames are polarizer intensities of a
+    Stokes field (polarization_intensities); every other modality is a normal-shaded sphere with per-band gains.
     """
     H, W = cams.height, cams.width
     ys, xs = torch.meshgrid(torch.arange(H, device=device, dtype=torch.float32),
@@ -143,8 +177,12 @@ def render_frames(cams: ModalityCameras, channels: int, device, raw_mod: Optiona
         n = (o + d * t[..., None]) / 0.5
         base = 0.5 + 0.5 * n
         bgc = 0.5 + 0.4 * torch.stack([d[..., 2], d[..., 0], d[..., 1]], -1)
-        col3 = torch.where(hit[..., None], base, bgc)
-        img = torch.clamp(col3[..., k % 3] * wk, 0.0, 1.0)
+        if channels == CHANNELS["polarization"]:
+            up = c2w[:, 1].expand_as(d)     # R (0, 1, 0) (cameras.py:680-682)
+            img = torch.clamp(polarization_intensities(n, hit, d, up), 0.0, 1.0)
+        else:
+            col3 = torch.where(hit[..., None], base, bgc)
+            img = torch.clamp(col3[..., k % 3] * wk, 0.0, 1.0)
         if mm is not None:
             img = torch.gather(img, -1, mm[..., None])
         frames.append(img)

@@ -92,8 +92,8 @@ def test_compute_loss_uses_the_runs_max_iters():
     100k default.  Checked on the host through the factor compute_loss passes to the weight."""
     import inspect
     from multimodalstudio_amd import pipeline
-    src = inspect.getsource(pipeline.compute_loss)
-    assert "curvature_factor(step, max_iters)" in src
+    assert "curvature_factor(step, max_iters)" in inspect.getsource(pipeline._finish_loss)
+    assert inspect.getsource(pipeline.compute_loss).count("step, max_iters)") == 2   # both geometry-loss paths
     assert "max_iters=self.cfg.max_iters" in inspect.getsource(pipeline.Trainer._compute_grads)
     from multimodalstudio_amd import graphs
     assert "max_iters=t.cfg.max_iters" in inspect.getsource(graphs.GraphTrainer._forward_backward_body)

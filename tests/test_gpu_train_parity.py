@@ -29,14 +29,17 @@ sys.path.insert(0, os.path.join(HERE, "golden"))
 TRAJ_STEPS = 5
 
 
-def run_parity(dev, precision: str, gold: str = GOLD):
+def run_parity(dev, precision: str, gold: str = GOLD, eps=None, cfg=None):
+    """The fixture's training run through the HIP path: (fixture, cfg, per-step losses, held-out PSNR per modality).
+    ``cfg`` replaces the fixture (a make_train_parity.CONFIGS entry: run without an oracle to compare against)."""
     from make_train_parity import draws, eval_inputs, step_inputs
     from multimodalstudio_amd import functions as fx
     from multimodalstudio_amd import model as mm
     from multimodalstudio_amd import pipeline as pl
     from multimodalstudio_amd import scene as ms
-    f = np.load(gold)
-    cfg = ast.literal_eval(f["cfg_json"].tobytes().decode())
+    f = np.load(gold) if cfg is None else None
+    if cfg is None:
+        cfg = ast.literal_eval(f["cfg_json"].tobytes().decode())
     raw = cfg["method"] == "grid_raw"
     mods = list(cfg["modalities"])
     channels = {m: ms.CHANNELS[m] for m in mods}
@@ -46,9 +49,12 @@ def run_parity(dev, precision: str, gold: str = GOLD):
                             log2T=cfg["log2T"], width=cfg["width"], height=cfg["height"], n_views=cfg["n_views"])
         tr = pl.Trainer(tc, dev)
         ck = float(sum(float(v.detach().double().abs().sum()) for v in tr.model.state_dict().values()))
-        assert ck == pytest.approx(float(f["init_checksum"]), rel=1e-9), "model init drifted from the fixture"
+        if f is not None:
+            assert ck == pytest.approx(float(f["init_checksum"]), rel=1e-9), "model init drifted from the fixture"
         tr.set_step(cfg["start_step"])
         tr.fields.step_count = 0          # fresh optimizer state, as the oracle run
+        # AdamW eps of the fixture's run (the reference's 1e-15 unless the fixture records another)
+        tr.fields.eps = float(cfg.get("eps", 1e-15) if eps is None else eps)
         if tr.poses is not None:
             tr.poses.step_count = 0
         # inputs: same host sampler, CPU-rendered targets, same draw stream as the fixture generator
