@@ -170,26 +170,44 @@ def kernel_records(summ, timing_steps: int, precision: str):
     return kernels
 
 
-def cpu_baseline(trainer, cfg, seconds: float):
-    """The fixture-pinned CPU restatement (oracle/) of the same workload, bounded sample, on host cores."""
+CPU_CONFIGS = {
+    # BASELINE.md §2 configurations the CPU restatement is timed on: (method, modalities)
+    "grid_rgb": ("grid", ("rgb",)),
+    "grid_raw5": ("grid_raw", ("rgb", "infrared", "mono", "polarization", "multispectral")),
+    "mlp_raw": ("mlp_raw", ("rgb",)),
+}
+
+
+def cpu_baseline(config: str, log2T: int, step: int, seconds: float, n_rays: int = 256):
+    """The fixture-pinned CPU restatement (oracle/) of one BASELINE configuration, bounded sample, on host cores:
+    the reference's own pure-PyTorch path restated (tests/test_oracle_golden.py pins it to the reference's outputs),
+    random-init weights of that method, model state at ``step``."""
     from oracle.train import OracleTrainer
     from multimodalstudio_amd import scene as ms
-    mods = list(cfg.modalities)
+    from multimodalstudio_amd.model import BaseModel, ModelSpec
+    from multimodalstudio_amd.pipeline import METHODS
+    method, mods = CPU_CONFIGS[config]
+    raw, bg_kind, fields = METHODS[method]
+    mods = list(mods)
     channels = {m: ms.CHANNELS[m] for m in mods}
-    sd = {k: v.detach().cpu() for k, v in trainer.model.state_dict().items()}
-    ot = OracleTrainer(sd, channels, trainer.host_cams, cfg.log2T, trainer.step, raw=False)
-    n_rays = 256
+    torch.manual_seed(654824)
+    model = BaseModel(ModelSpec(channels, log2T=log2T, bg_kind=bg_kind, fields=fields))
+    sd = {k: v.detach() for k, v in model.state_dict().items()}
+    del model
+    W, H = 640, 512
+    cams = ms.make_cameras(mods, 50, W, H, seed=0, train=True)
+    masks = {m: ms.mosaick_mask(m, W, H) for m in mods} if raw else None
+    ot = OracleTrainer(sd, channels, cams, log2T, step, raw=raw, mosaick=masks, fields=fields)
     g = torch.Generator().manual_seed(1)
 
     def batch():
         coords, targets = {}, {}
         for m in mods:
-            cams = trainer.host_cams[m]
-            C = cams.c2w.shape[0]
-            c = torch.stack([torch.randint(0, C, (n_rays,), generator=g), torch.randint(0, cfg.height, (n_rays,),
-                            generator=g), torch.randint(0, cfg.width, (n_rays,), generator=g)], -1).to(torch.int32)
+            C = cams[m].c2w.shape[0]
+            c = torch.stack([torch.randint(0, C, (n_rays,), generator=g), torch.randint(0, H, (n_rays,), generator=g),
+                             torch.randint(0, W, (n_rays,), generator=g)], -1).to(torch.int32)
             coords[m] = c
-            targets[m] = torch.rand(n_rays, channels[m], generator=g)
+            targets[m] = torch.rand(n_rays, 1 if raw else channels[m], generator=g)
         return coords, targets
 
     ot.train_step(*batch())   # warmup
@@ -206,8 +224,9 @@ def cpu_baseline(trainer, cfg, seconds: float):
         "unit": "rays/s",
         "cores": torch.get_num_threads(),
         "kind": "port",
-        "sample": f"{len(times)} timed steps (median) of the CPU restatement (oracle/, bit-exact to the reference "
-                  f"torch path) at {n_rays} rays/modality, same config, log2T={cfg.log2T}, fwd+bwd+AdamW; "
+        "sample": f"{len(times)} timed steps (median) of the CPU restatement (oracle/, pinned to the reference torch "
+                  f"path) of {config} ({method}, {len(mods)} modalit{'y' if len(mods) == 1 else 'ies'}) at {n_rays} "
+                  f"rays/modality, log2T={log2T}, model step {step}, fwd+bwd+AdamW; "
                   f"host {platform.processor() or platform.machine()}",
     }
 
@@ -340,9 +359,13 @@ def main():
                                   ("bwd", "mms_hashgrid_bwd_grouped:sdf_taps"),
                                   ("bwd_radiance", "mms_hashgrid_bwd_grouped:radiance_or_bg")] if n in by_name}
 
-    cpu = None
+    cpu, cpu_all = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(trainer, cfg, args.cpu_seconds)
+        # the headline config's CPU baseline, then the other BASELINE.md §2 configurations beside it
+        cpu = cpu_baseline(args.config, args.log2T, args.start_step, args.cpu_seconds) if args.config in CPU_CONFIGS \
+            else None
+        cpu_all = {c: cpu_baseline(c, args.log2T, args.start_step, args.cpu_seconds / 2)
+                   for c in CPU_CONFIGS if c != args.config}
 
     secondary = None
     if args.secondary and args.secondary != args.config:
@@ -353,7 +376,8 @@ def main():
         secondary = {"config": {"workload": CONFIGS[args.secondary][2], "modalities": list(CONFIGS[args.secondary][1]),
                                 "num_rays_per_modality": args.rays, "rays_per_step": r2["rays_per_step"]},
                      "value": round(r2["value"], 1), "unit": "rays/s", "steps": r2["steps"], "warmup": r2["warmup"],
-                     "ms_per_step": round(r2["ms_per_step"], 3), "step_mode": r2["step_mode"]}
+                     "ms_per_step": round(r2["ms_per_step"], 3), "step_mode": r2["step_mode"],
+                     "cpu_baseline": (cpu_all or {}).get(args.secondary)}
         del r2
 
     if rank == 0:
@@ -382,6 +406,7 @@ def main():
             "roofline_hash_grid": hash_roof,
             "roofline_kernels": kernels,
             "cpu_baseline": cpu,
+            "cpu_baseline_configs": cpu_all,
             "secondary": secondary,
         }
         print(json.dumps(line))

@@ -392,7 +392,7 @@ MMS_EXPORT int mms_render_stats_segments(const float* w, const float* normals, c
   MMS_REQUIRE(S >= 1 && S <= 64, fn, "samples per ray must be in [1, 64]");
   MMS_REQUIRE(ldo >= 5, fn, "output rows hold (acc, n0, n1, n2, depth)");
   MMS_REQUIRE(n_seg >= 1 && n_seg <= kMaxSeg, fn, "segment count must be in [1, 8]");
-  MMS_REQUIRE(seg_off && sidx && out && range, fn, "null pointer");
+  MMS_REQUIRE(seg_off, fn, "null pointer");
   SegOff so{};
   int64_t most = 0;
   for (int m = 0; m <= n_seg; ++m) so.off[m] = seg_off[m];
@@ -400,7 +400,8 @@ MMS_EXPORT int mms_render_stats_segments(const float* w, const float* normals, c
     MMS_REQUIRE(so.off[m + 1] >= so.off[m], fn, "segment offsets must be non-decreasing");
     most = so.off[m + 1] - so.off[m] > most ? so.off[m + 1] - so.off[m] : most;
   }
-  if (most == 0) return 0;
+  if (most == 0) return 0;   // no hit ray in any segment
+  MMS_REQUIRE(sidx && out && range, fn, "null pointer");
   hipStream_t s = mms::as_stream(stream);
   hipLaunchKernelGGL(render_stats_seg_kernel, dim3(mms::grid_for(most * 64, 256, 256), n_seg), dim3(256), 0, s, w,
                      normals, starts, ends, so, S, sidx, out, ldo, seg_rows, range);

@@ -142,9 +142,12 @@ def build_mosaick_mask(pattern: torch.Tensor, width: int, height: int) -> torch.
 # synthetic scene writer
 # ------------------------------------------------------------------------------------------------
 def write_synthetic_scene(path: str, modalities: Sequence[str], n_views: int = 50, width: int = 640,
-                          height: int = 512, raw: bool = True, seed: int = 0) -> str:
+                          height: int = 512, raw: bool = True, seed: int = 0,
+                          formats: Optional[Dict[str, str]] = None) -> str:
     """scene.py's analytic scene in the MMS-DATA on-disk format: 1- and 3-channel frames as 16- / 8-bit pngs,
-    others as npy (float32); raw scenes store the mosaicked single-band frames and each modality's pattern."""
+    others as npy (float32); raw scenes store the mosaicked single-band frames and each modality's pattern.
+    ``formats[mod]``: 'png' / 'npy' (float32) / 'npy_u16' (uint16 counts, normalised by the loader) overrides the
+    default per modality (an all-npy scene is what the reference's loader reads without OpenCV)."""
     os.makedirs(os.path.join(path, "modalities"), exist_ok=True)
     cams = mscene.make_cameras(list(modalities), n_views, width, height, seed=seed, train=None)
     md = {"undistorted": False, "raw": bool(raw), "pixel_offset": 0.0,
@@ -157,10 +160,13 @@ def write_synthetic_scene(path: str, modalities: Sequence[str], n_views: int = 5
         os.makedirs(os.path.join(path, "modalities", mod), exist_ok=True)
         entries = []
         nc = frames.shape[-1]
+        fmt = (formats or {}).get(mod, "png" if nc in CHANNEL_FORMAT else "npy")
         for i, v in enumerate(c.view_ids):
-            ext = CHANNEL_FORMAT.get(nc, ".npy")
+            ext = ".png" if fmt == "png" else ".npy"
             name = f"{v:04}{ext}"
             f = frames[i]
+            if fmt == "npy_u16":
+                f = np.round(f * 65535.0).astype(np.uint16)
             if ext == ".png":
                 f = np.round(f * (65535.0 if nc == 1 else 255.0)).astype(np.uint16 if nc == 1 else np.uint8)
                 if nc == 3:

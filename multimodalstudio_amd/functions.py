@@ -110,8 +110,22 @@ class WeightPrep:
         self.done = set()          # entries computed individually in the current forward
         self.dev = None
 
+    def _stale(self) -> bool:
+        """True when a registered parameter's storage moved since it was registered (e.g. FlatGroup re-pointing
+        p.data into its flat buffer after a first forward): the device tables would read freed memory."""
+        for g, v, W, nrm, idx in self.norm.values():
+            if idx is not None and (self.norm_items[idx].g != g.data_ptr() or self.norm_items[idx].v != v.data_ptr()):
+                return True
+        return False
+
+    def reset(self) -> None:
+        """Forget every entry (they re-register on their next use)."""
+        self.__init__()
+
     def run(self, dev) -> None:
         """Recompute every registered entry (start of a model forward)."""
+        if self.norm_items and self._stale() and not torch.cuda.is_current_stream_capturing():
+            self.reset()
         self.fresh = False
         self.done.clear()
         self.dev = dev
@@ -714,6 +728,8 @@ def zero_arena_end() -> None:
 def _zeroed_views(shapes, dev) -> List[Optional[torch.Tensor]]:
     """Zero-filled f32 accumulation buffers (None for a None shape) carved from the step's zero arena, or from one
     fresh zeroed allocation outside a training step / past the arena."""
+    if all(sh is None for sh in shapes):
+        return [None] * len(shapes)        # nothing carved: the arena offset keeps its 256-B alignment
     sizes = [0 if sh is None else math.prod(sh) for sh in shapes]
     padded = [(n + _ALIGN - 1) // _ALIGN * _ALIGN for n in sizes]
     total = max(sum(padded), 1)
@@ -800,7 +816,9 @@ class SurfaceFunction(torch.autograd.Function):
         dout = _alloc(5 * M, G + 1, dev)
         c = lambda t: None if t is None else (t if t.stride(-1) == 1 else t.contiguous())
         dsdf, dgeo = c(dsdf), c(dgeo)
-        _lib.call("mms_taps_combine_bwd", grads.data_ptr(), _p(c(dgrads)), _p(c(dhess)), _p(c(dnormals)), M,
+        # taps_combine_bwd reads these [M, 3] with a fixed row stride of 3: dense copies unless already dense
+        cc = lambda t: None if t is None else t.contiguous()
+        _lib.call("mms_taps_combine_bwd", grads.data_ptr(), _p(cc(dgrads)), _p(cc(dhess)), _p(cc(dnormals)), M,
                   ctx.four_delta, ctx.delta_sq, dout.data_ptr(), dout.stride(0), _p(dsdf),
                   0 if dsdf is None else dsdf.stride(0), _p(dgeo), 0 if dgeo is None else dgeo.stride(0), G, _s())
         need_table = ctx.needs_input_grad[1]
@@ -1182,7 +1200,11 @@ class BackgroundFunction(torch.autograd.Function):
         M, S, Fb = pos.shape[0], ctx.S, ctx.Fb
         R = M // S
         dev = pos.device
-        dH = _run_backward(ctx.head, dfeat)                                          # [M, Fb+27]
+        if dfeat is not None:
+            dH = _run_backward(ctx.head, dfeat)                                      # [M, Fb+27]
+        else:
+            # only the density reached the loss: the head panel's gradient is the density head's alone
+            dH = _zeroed_views([(M, ctx.H.stride(0))], dev)[0][:, :Fb + 27]
         if ddensity is None:
             ddensity = torch.zeros(M, 1, device=dev)
         # the density head's input gradient accumulates straight into the head panel's base columns

@@ -151,6 +151,22 @@ def radiance_field(pos, sh, additional, P, grid: GridSpec, active_levels: int,
     return feature_grid_and_mlp(inp, P, prefix, grid, active_levels, RAD_MLP)
 
 
+# the mlp / mlp_raw methods' fields (method_configs.py:303-353): 8-layer, 256-wide MLPs with a skip into layer 4
+SDF_MLP8 = dict(num_layers=8, act="Softplus", act_params={"beta": 100}, out_act=None, skips=(4,))
+RAD_MLP8 = dict(num_layers=8, act="ReLU", act_params=None, out_act="ReLU", skips=(4,))
+
+
+def sdf_field_mlp(x: torch.Tensor, P, prefix="surface_model.surface_field"):
+    """SDFField.forward (surface_field.py:99-116) with an MLP field: PE(6 freqs, input included) -> MLP -> [1, 256]."""
+    out = mlp_forward(nerf_encoding(x, 6, 0.0, 5.0, True), P, prefix + ".field", **SDF_MLP8)
+    return out[..., :1], out[..., 1:]
+
+
+def radiance_field_mlp(pos, sh, additional, P, prefix="radiance_model.radiance_field.base_field"):
+    """RadianceField.forward (radiance_field.py:72-77) with an MLP base field on [x, SH, geo, n.v] (285 -> 256)."""
+    return mlp_forward(torch.cat([pos, sh, additional], -1), P, prefix, **RAD_MLP8)
+
+
 # ------------------------------------------------------------------------------------------------
 # heads and polarizer
 # ------------------------------------------------------------------------------------------------

@@ -2,7 +2,7 @@
 
 Restates (paths under /root/reference/src):
   BaseModel.forward                    models/base_model.py:82-161
-  SurfaceModel.forward / gradient      model_components/surface_model.py:66-206, get_sdf :213-226
+  SurfaceModel.forward / gradient      model_components/surface_model.py:66-206 (4-tap and autograd), get_sdf :213-226
   set_delta callback                   model_components/surface_model.py:248-279
   NeuSVolumeRendering                  model_components/volume_rendering.py:171-239
   SingleVarianceNetwork                field_components/single_variance.py:34-36
@@ -107,12 +107,21 @@ class ModelSpec:
     upsample_steps: int = 4
     bg_samples: int = 16
     raw: bool = False
+    fields: str = "grid"      # "grid" (hash grid + 3-layer MLPs, 4-tap gradients) | "mlp" (8-layer MLPs, autograd)
 
 
 def spec_grid(modalities: Dict[str, int], log2T: int = 19, raw: bool = False) -> ModelSpec:
     s = ModelSpec(modalities=dict(modalities), grid=of.GridSpec(16, 16, 1024, log2T, 1.0), raw=raw)
     s.head_layers = {m: 3 for m in modalities}
     s.bg_head_layers = {m: 1 for m in modalities}
+    return s
+
+
+def spec_mlp(modalities: Dict[str, int], raw: bool = False) -> ModelSpec:
+    """The mlp / mlp_raw methods (method_configs.py:303-353): MLP fields, analytic SDF gradient, no hessian, the
+    grid methods' heads and NeRF background."""
+    s = spec_grid(modalities, raw=raw)
+    s.fields = "mlp"
     return s
 
 
@@ -125,6 +134,14 @@ def inv_variance(P) -> torch.Tensor:
 
 def surface_forward(pos: torch.Tensor, P, spec: ModelSpec, st: StepState):
     """SurfaceModel.forward (surface_model.py:66-127) on flattened start positions [M, 3]."""
+    if spec.fields == "mlp":
+        # use_numerical_gradients False: d sdf / d x by autograd, kept in the graph (surface_model.py:192-198);
+        # compute_hessian False for these methods
+        with torch.enable_grad():
+            x = pos if pos.requires_grad else pos.detach().requires_grad_(True)
+            sdf, geo = of.sdf_field_mlp(x, P)
+            grads = torch.autograd.grad(sdf, x, torch.ones_like(sdf), create_graph=True, retain_graph=True)[0]
+        return sdf, geo, grads, None
     sdf, geo = of.sdf_field(pos, P, spec.grid, st.active_levels)
     delta = st.delta / np.sqrt(3)
     taps = [of.sdf_field(pos + TAPS[i] * delta, P, spec.grid, st.active_levels)[0] for i in range(4)]
@@ -174,6 +191,8 @@ def model_forward(rays: Dict[str, orr.Rays], P, spec: ModelSpec, st: StepState, 
 
         def sdf_fn(pts):
             R, n = pts.shape[:2]
+            if spec.fields == "mlp":
+                return of.sdf_field_mlp(pts.reshape(-1, 3), P)[0].view(R, n)
             return of.sdf_field(pts.reshape(-1, 3), P, spec.grid, st.active_levels)[0].view(R, n)
 
         smp, hist = orr.neus_sample(n_h, f_h, o_h, d_h, sdf_fn, rng.uniform[mod], rng.pdf[mod],
@@ -190,7 +209,7 @@ def model_forward(rays: Dict[str, orr.Rays], P, spec: ModelSpec, st: StepState, 
         sdf, geo, grads, hess = surface_forward(pos, P, spec, st)
         sdf = sdf.view(R, S, 1)
         grads = grads.view(R, S, 3)
-        hess = hess.view(R, S, 3)
+        hess = hess.view(R, S, 3) if hess is not None else None
         normals = F.normalize(grads, p=2, dim=-1)
         s = inv_variance(P)
         alpha = neus_alpha(sdf, grads, d_h, smp.deltas, s, st.cos_anneal)
@@ -214,7 +233,10 @@ def radiance_forward(pos, d_h, up_h, normals, geo, P, spec: ModelSpec, st: StepS
     ups = up_h[:, None, :].expand(R, S, 3).reshape(-1, 3)
     ndv = torch.sum(normals * -dirs, dim=-1, keepdim=True)
     sh = of.sh_encoding(dirs.clone(), 5)
-    feat = of.radiance_field(pos, sh, torch.cat([geo, ndv], -1), P, spec.grid, st.active_levels)
+    if spec.fields == "mlp":
+        feat = of.radiance_field_mlp(pos, sh, torch.cat([geo, ndv], -1), P)
+    else:
+        feat = of.radiance_field(pos, sh, torch.cat([geo, ndv], -1), P, spec.grid, st.active_levels)
     out = {}
     for mod in spec.modalities:
         kind = "polarization" if mod == "polarization" else "plain"
@@ -297,14 +319,17 @@ def compute_loss(outputs, targets: Dict[str, torch.Tensor], spec: ModelSpec, st:
         losses[mod] = l
         total = total + l
     grads = torch.cat([outputs[m]["gradients"] for m in spec.modalities], 0)
-    hess = torch.cat([outputs[m]["hessians"] for m in spec.modalities], 0)
     gn = torch.norm(grads, 2, dim=-1)
     eik = F.mse_loss(gn, torch.ones_like(gn))
+    losses["eikonal_loss"] = eik
+    total = total + 0.1 * eik
+    if spec.fields == "mlp":
+        return losses, total        # geometry losses of the mlp methods: eikonal only (method_configs.py:350-352)
+    hess = torch.cat([outputs[m]["hessians"] for m in spec.modalities], 0)
     lap = hess.sum(dim=-1)
     curv = F.l1_loss(lap, torch.zeros_like(lap))
-    losses["eikonal_loss"] = eik
     losses["curvature_loss"] = curv
-    total = total + 0.1 * eik + 5e-4 * st.curvature_factor * curv
+    total = total + 5e-4 * st.curvature_factor * curv
     return losses, total
 
 

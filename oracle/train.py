@@ -18,9 +18,10 @@ from . import rays as orr
 class OracleTrainer:
     def __init__(self, state_dict: Dict[str, torch.Tensor], modalities: Dict[str, int], cams: dict, log2T: int,
                  step: int, raw: bool = False, pose: Dict[str, torch.Tensor] = None,
-                 mosaick: Dict[str, torch.Tensor] = None):
+                 mosaick: Dict[str, torch.Tensor] = None, fields: str = "grid"):
         self.P = {k: v.detach().clone().float().cpu().requires_grad_(True) for k, v in state_dict.items()}
-        self.spec = om.spec_grid(modalities, log2T=log2T, raw=raw)
+        self.spec = om.spec_mlp(modalities, raw=raw) if fields == "mlp" else om.spec_grid(modalities, log2T=log2T,
+                                                                                              raw=raw)
         self.cams = cams
         self.mods = list(modalities)
         self.pose = {m: (pose[m].detach().clone() if pose else torch.zeros(1, 6)).requires_grad_(True)

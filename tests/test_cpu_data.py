@@ -67,3 +67,37 @@ def test_frame_io_channel_order(tmp_path):
     md.write_frame(str(tmp_path / "g.png"), g16)
     assert np.array_equal(md.read_frame(str(tmp_path / "g.png")), g16)
     assert md.normalize_frame(g16).max() == pytest.approx(57000 / 65535)
+
+
+@pytest.mark.parametrize("tag", ["raw", "demosaicked"])
+def test_loader_matches_reference_dataset(tmp_path, tag):
+    """MMSDataset against the reference's own loader (tests/golden/loader.npz: RawMultimodalAlignedDataset /
+    MultimodalAlignedDataset, datasets.py:229-301, 303-360, 444-529, 608-633, run by tests/golden/make_golden.py
+    loader on the same writer's all-npy scenes, float32 and uint16 frames): frames, cameras, split, mosaick masks and
+    channel counts exactly equal."""
+    gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "loader.npz"))
+    # the scene table of the fixture generator, restated (make_golden imports the reference at module level)
+    scenes = {
+        "raw": (True, ("rgb", "infrared", "mono", "polarization", "multispectral"),
+                {"rgb": "npy", "infrared": "npy_u16", "mono": "npy", "polarization": "npy", "multispectral": "npy_u16"},
+                (1, 4)),
+        "demosaicked": (False, ("rgb", "mono", "multispectral"),
+                        {"rgb": "npy", "mono": "npy_u16", "multispectral": "npy"}, (2,)),
+    }
+    raw, mods, fmts, excl = scenes[tag]
+    d = md.write_synthetic_scene(str(tmp_path / tag), mods, raw=raw, formats=fmts, n_views=7, width=40, height=26,
+                                 seed=3)
+    ds = md.MMSDataset(d, mods, indexes_to_exclude={m: list(excl) for m in mods})
+    chans = ds.get_channels_per_modality()
+    for m in mods:
+        cam = ds.cameras[m]
+        assert cam.view_ids == [int(i) for i in gold[f"{tag}:indexes"]], m
+        np.testing.assert_array_equal(ds.images[m].numpy(), gold[f"{tag}:{m}:images"], err_msg=m)
+        np.testing.assert_array_equal(cam.c2w.numpy(), gold[f"{tag}:{m}:c2w"], err_msg=m)
+        for k in ("fx", "fy", "cx", "cy"):
+            np.testing.assert_array_equal(getattr(cam, k).numpy(), gold[f"{tag}:{m}:{k}"].reshape(-1), err_msg=k)
+        np.testing.assert_array_equal(cam.distortion.numpy(), gold[f"{tag}:{m}:distortion"], err_msg=m)
+        assert chans[m] == int(gold[f"{tag}:{m}:channels"]), m
+        if raw:
+            np.testing.assert_array_equal(ds.mosaick_masks[m].numpy(), gold[f"{tag}:{m}:mosaick_mask"], err_msg=m)
+    assert float(ds.scene_box["radius"]) == float(gold[f"{tag}:radius"])

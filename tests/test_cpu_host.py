@@ -203,6 +203,12 @@ def test_zero_arena_is_sized_by_the_first_step_and_carved_after():
         fx.zero_arena_begin(dev)           # the next step's fill zeroes what the last one wrote
         w1, = fx._zeroed_views([(5, 3)], dev)
         assert w1.data_ptr() == v1.data_ptr() and float(w1.abs().sum()) == 0.0
+        # an all-None request carves nothing (it used to advance the offset by one float, misaligning
+        # every later view of the step)
+        off = a.off
+        assert fx._zeroed_views([None, None], dev) == [None, None] and a.off == off
+        w2, = fx._zeroed_views([(3,)], dev)
+        assert (w2.data_ptr() - a.buf.data_ptr()) % 256 == 0
         fx.zero_arena_end()
     finally:
         a.buf, a.keep, a.need, a.off, a.in_step, a.active, a.dev = saved

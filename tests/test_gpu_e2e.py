@@ -87,8 +87,18 @@ def run_hip_e2e(f, dev, cap=None, concurrent_background=True):
     return mods, model, pose, outs, losses, total
 
 
+# fp32 parity-mode bounds, about 10x the measured worst case of each fixture (bounds 25-250x loose let
+# regressions pass).  Parameter gradients: scale-relative max error over every parameter tensor; the mlp_raw field's
+# analytic SDF gradient is differentiated twice (autograd through the HIP GEMM), so its parameter gradients carry
+# more reordering noise than the grid fields'.
+E2E_PARAM_TOL = {"e2e_mlp_raw_rgb_s95000": 1.5e-2}
+E2E_PARAM_TOL_DEFAULT = 2e-3
+E2E_DPOSE_TOL = 5e-3
+
+
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_rgb_s30000", "e2e_grid_raw_5mod_s95000",
-                                  "e2e_grid_raw_gridbg_s95000", "e2e_mlp_raw_rgb_s95000"])
+                                  "e2e_grid_raw_5mod_sat_s95000", "e2e_grid_raw_gridbg_s95000",
+                                  "e2e_mlp_raw_rgb_s95000"])
 def test_e2e_train_step(dev, name):
     f = load(name)
     mods, model, pose, outs, losses, total = run_hip_e2e(f, dev)
@@ -117,6 +127,8 @@ def test_e2e_train_step(dev, name):
         report[f"{m}:bins_exact_frac"] = float((bins == ref_bins).mean())
     for k in sorted(report, key=lambda k: -report[k])[:12]:
         print(f"{k:90s} {report[k]:.3e}")
+    print(f"{name}: worst parameter gradient {worst_param:.3e}; worst dpose "
+          f"{max(report[f'{m}:dpose'] for m in mods):.3e}")
     assert report["loss"] < 1e-4
     for m in mods:
         assert report[f"{m}:{m}"] < 1e-4, m
@@ -129,11 +141,11 @@ def test_e2e_train_step(dev, name):
         # SDF GEMM sums (a few ulp of |sdf| ~ 0.5, i.e. ~1e-7) moves it by ~0.1 absolute; the reference's own
         # CPU-vs-GPU runs differ the same way.  Bound: 4 ulp-scale errors amplified by 1/delta^2.
         assert report.get(f"{m}:hessians", 0.0) < 0.15
-        assert report[f"{m}:dpose"] < 5e-2
-    assert worst_param < 5e-2
+        assert report[f"{m}:dpose"] < E2E_DPOSE_TOL, (m, report[f"{m}:dpose"])
+    assert worst_param < E2E_PARAM_TOL.get(name, E2E_PARAM_TOL_DEFAULT), worst_param
 
 
-@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000"])
+@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000", "e2e_grid_raw_5mod_sat_s95000"])
 def test_e2e_fast_preset_deviation(dev, name):
     """The benchmarked `fast` preset (SDF MLP split-bf16x3, everything else bf16 MFMA) on the reference's fixture:
     per-modality rendered-radiance deviation, reported and bounded (bf16 is judged by PSNR parity,
@@ -153,8 +165,9 @@ def test_e2e_fast_preset_deviation(dev, name):
         ref = f[f"{m}:out:{m}"].astype(np.float64)
         rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-2)
         print(f"  {m:14s} radiance rel dev: mean {rel.mean():.3e}  max {rel.max():.3e}")
-        assert rel.mean() < 2.5e-2, (m, rel.mean())
-        assert rel.max() < 0.25, (m, rel.max())
+        # about 10x the measured deviation: polarization intensities are differences of Stokes terms
+        assert rel.mean() < (1e-2 if m == "polarization" else 2e-3), (m, rel.mean())
+        assert rel.max() < 0.1, (m, rel.max())
         # the geometry the eikonal / curvature losses see: 4-tap SDF gradients and hessians (second differences over
         # delta^2 ~ 1.3e-6, so any activation rounding that differs between the centre and the tap rows shows here)
         for k in ("gradients", "hessians"):

@@ -120,6 +120,70 @@ def test_weight_prep_batched_matches_single(dev):
         fx.set_precision("fp32")
 
 
+def test_weight_prep_follows_moved_parameters(dev):
+    """A forward run BEFORE the trainer's FlatGroup re-points every p.data into its flat buffer: the
+    batched preparation must not keep reading the old storage -- the next forward's weights are the current
+    parameters' W = g v / ||v||."""
+    from multimodalstudio_amd import functions as fx
+    from multimodalstudio_amd import model as mm
+    from multimodalstudio_amd import pipeline as pl
+    fx.set_precision("fast")
+    try:
+        torch.manual_seed(3)
+        model = mm.BaseModel(mm.ModelSpec({"rgb": 3}, log2T=12)).to(dev)
+        model.set_step(95000)
+        cams = pl.DeviceCameras(mm_cams(), dev)
+        gen = pl.RayGenerator({"rgb": cams}, pl.CameraOptimizer(["rgb"], {"rgb": cams.num}, mode="off"), 0.0)
+        coords = {"rgb": torch.tensor([[0, 20, 30], [1, 24, 32], [2, 10, 40]], dtype=torch.int32, device=dev)}
+        with torch.no_grad():
+            model(gen(coords))                 # registers the entries against the original storages
+            model(gen(coords))                 # batched tables now in use
+        pl.FlatGroup(list(model.parameters()), lr=1e-3, weight_decay=0.01, eps=1e-15)   # moves every p.data
+        torch.cuda.empty_cache()
+        with torch.no_grad():
+            for p in model.parameters():
+                p.mul_(1.5)                    # the new storages hold different values than the freed ones
+            model(gen(coords))
+            model(gen(coords))
+            fx.begin_forward(model._prep, dev)
+            fx.end_forward()
+            torch.cuda.synchronize()
+            assert model._prep.norm and all(idx is not None for *_, idx in model._prep.norm.values())
+            for g, v, W, nrm, idx in model._prep.norm.values():
+                ref = g.reshape(-1, 1) * v / torch.linalg.vector_norm(v, dim=1, keepdim=True)
+                assert torch.allclose(W, ref, rtol=1e-5, atol=1e-6)
+    finally:
+        fx.set_precision("fp32")
+
+
+def mm_cams():
+    from multimodalstudio_amd import scene as ms
+    return ms.make_cameras(["rgb"], 6, 64, 48, seed=0)["rgb"]
+
+
+def test_background_density_only_backward(dev):
+    """BackgroundFunction's backward with only the density reaching the loss (the feature gradient
+    arrives as None): equals the backward with an explicit zero feature gradient."""
+    from multimodalstudio_amd import functions as fx
+    from multimodalstudio_amd import model as mm
+    torch.manual_seed(5)
+    model = mm.BaseModel(mm.ModelSpec({"rgb": 3}, log2T=12)).to(dev)
+    pos = (torch.rand(64 * 16, 3, device=dev) - 0.5) * 6
+    dirs = torch.nn.functional.normalize(torch.randn(64, 3, device=dev), dim=-1)
+    grads = []
+    for explicit in (False, True):
+        for p in model.parameters():
+            p.grad = None
+        dens, feat = model.background_model.field(pos, dirs, 16)
+        loss = dens.sum() + (0.0 * feat.sum() if explicit else 0.0)
+        loss.backward()
+        torch.cuda.synchronize()
+        grads.append({k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None})
+    assert grads[0].keys() == grads[1].keys() and grads[0]
+    for k in grads[0]:
+        assert torch.allclose(grads[0][k], grads[1][k], rtol=1e-5, atol=1e-7), k
+
+
 def test_weight_norm_bwd_batched_matches_immediate(dev):
     """The training backward's deferred, batched weight-norm gradients (mms_weight_norm_bwd_batched) equal the
     immediate per-layer mms_weight_norm_bwd on the same forward (to float-atomic summation order)."""

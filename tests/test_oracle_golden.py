@@ -130,9 +130,12 @@ def e2e_inputs(name):
 def run_oracle_e2e(f):
     mods = [str(m) for m in f["mods"]]
     from multimodalstudio_amd.scene import CHANNELS, mosaick_mask
-    log2T = int(np.log2(f["p:surface_model.surface_field.field.feature_grid.encoding.hash_table"].shape[0] // 16))
     raw = bool(f["raw"])
-    spec = om.spec_grid({m: CHANNELS[m] for m in mods}, log2T=log2T, raw=raw)
+    key = "p:surface_model.surface_field.field.feature_grid.encoding.hash_table"
+    if key in f:
+        spec = om.spec_grid({m: CHANNELS[m] for m in mods}, log2T=int(np.log2(f[key].shape[0] // 16)), raw=raw)
+    else:
+        spec = om.spec_mlp({m: CHANNELS[m] for m in mods}, raw=raw)
     st = om.StepState(step=int(f["step"]))
     P = {k[2:]: T(v).clone().requires_grad_(True) for k, v in f.items() if k.startswith("p:")}
     poses = {m: T(f[f"{m}:pose"]).clone().requires_grad_(True) for m in mods}
@@ -155,14 +158,15 @@ def run_oracle_e2e(f):
     return mods, outs, losses, total, P, poses
 
 
-@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_rgb_s30000", "e2e_grid_raw_5mod_s95000"])
+@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_rgb_s30000", "e2e_grid_raw_5mod_s95000",
+                                  "e2e_grid_raw_5mod_sat_s95000", "e2e_mlp_raw_rgb_s95000"])
 def test_end_to_end(name):
     f = e2e_inputs(name)
     mods, outs, losses, total, P, poses = run_oracle_e2e(f)
     np.testing.assert_allclose(total.item(), float(f["loss"]), rtol=1e-5)
     for m in mods:
         o = outs[m]
-        for k in ["normals", "depth", "accumulation", "gradients", "hessians"]:
+        for k in ["normals", "depth", "accumulation", "gradients"] + (["hessians"] if f"{m}:out:hessians" in f else []):
             np.testing.assert_allclose(o[k].detach().numpy(), f[f"{m}:out:{k}"], rtol=1e-4, atol=1e-5,
                                        err_msg=f"{m}:{k}")
         np.testing.assert_allclose(o[m].detach().numpy(), f[f"{m}:out:{m}"], rtol=1e-4, atol=1e-6)
