@@ -31,25 +31,28 @@ const char* mms_last_error(void);
  * scales [L] host array (floor(min_res*g^l)), out [M, ldo] cols 0..2L-1.  Levels >= active_levels are
  * zero (coarse-to-fine mask).  bwd: dtable += (atomic), dpos[:, 0:3] += (either may be NULL).
  * radius r > 0: pos is the FeatureGrid input, x_hat = (x + r) / (2 r); r = 0: pos is already x_hat (a bare
- * HashEncoding.forward, encodings.py:263-304). */
+ * HashEncoding.forward, encodings.py:263-304).
+ * interp: 0 = "Linear" (trilinear weights frac / 1 - frac: the reference torch path, parity-pinned); 1 = "Smoothstep"
+ * (HashEncodingConfig.interpolation, encodings.py:64-67, the tcnn default: weights S(frac) = frac^2 (3 - 2 frac),
+ * position gradient through S'(frac) = 6 frac (1 - frac); tcnn is absent here, so this mode is parity-unpinned). */
 int mms_hashgrid_fwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L, int log2T, int F,
-                     const float* scales, float radius, int active_levels, float* out, int64_t ldo, void* stream);
+                     int interp, const float* scales, float radius, int active_levels, float* out, int64_t ldo, void* stream);
 /* Forward over Mg groups of `group` rows (row = g + j * gstride, j < group; group 1 or 5): the SDF batch
  * [centre | 4 taps] (surface_model.py:138-160) gathered in (sample, tap) order, so a sample's centre and taps --
  * which share cells at the coarse levels -- hit one L2.  Same values as mms_hashgrid_fwd on every row. */
 int mms_hashgrid_fwd_grouped(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx,
-                             const float* table, int L, int log2T, int F, const float* scales, float radius,
-                             int active_levels, float* out, int64_t ldo, void* stream);
+                             const float* table, int L, int log2T, int F, int interp, const float* scales,
+                             float radius, int active_levels, float* out, int64_t ldo, void* stream);
 int mms_hashgrid_bwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L, int log2T, int F,
-                     const float* scales, float radius, int active_levels, const float* dout, int64_t ldd,
+                     int interp, const float* scales, float radius, int active_levels, const float* dout, int64_t ldd,
                      float* dtable, float* dpos, int64_t lddx, void* stream);
 /* Same, for Mg groups of `group` rows (row = g + j * gstride, j < group; group 1 or 5): the SDF batch
  * [centre | 4 taps] (surface_model.py:138-160) -- the taps' shared-cell corner gradients are merged
  * in-thread before the table atomics. */
 int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx,
-                             const float* table, int L, int log2T, int F, const float* scales, float radius,
-                             int active_levels, const float* dout, int64_t ldd, float* dtable, float* dpos,
-                             int64_t lddx, void* stream);
+                             const float* table, int L, int log2T, int F, int interp, const float* scales,
+                             float radius, int active_levels, const float* dout, int64_t ldd, float* dtable,
+                             float* dpos, int64_t lddx, void* stream);
 
 /* ---- MLP GEMM engine (field_components/mlp.py:152-171): C = epilogue(op(A) op(B)^T).
  * trans_a = 0: A is [M, K] (lda); 1: A is stored [K, M].  trans_b = 0: B is [N, K]; 1: B is stored [K, N].

@@ -32,7 +32,11 @@ struct GridParams {
   int log2T;
   float inv_2r;       // 1 / (2 r)
   float radius;       // r
+  int smooth;         // interpolation "Smoothstep" (tcnn): weights S(t) = t^2 (3 - 2 t) of the fraction t
 };
+
+__device__ __forceinline__ float smoothstep(float t) { return t * t * (3.0f - 2.0f * t); }
+__device__ __forceinline__ float smoothstep_grad(float t) { return 6.0f * t * (1.0f - t); }
 
 __device__ __forceinline__ uint32_t hash3(int cx, int cy, int cz, uint32_t mask) {
   return (((uint32_t)cx) ^ ((uint32_t)cy * kP1) ^ ((uint32_t)cz * kP2)) & mask;
@@ -46,7 +50,7 @@ struct Corners {
 // Corner order (encodings.py:274-281): 0:(c,c,c) 1:(c,f,c) 2:(f,f,c) 3:(f,c,c)
 //                                      4:(c,c,f) 5:(c,f,f) 6:(f,f,f) 7:(f,c,f)
 __device__ __forceinline__ Corners make_corners(float x, float y, float z, float radius, float inv_2r,
-                                                float s, int level, int log2T) {
+                                                float s, int level, int log2T, bool smooth) {
   Corners c;
   // (x + r) / (2r): reference computes a true division by (2r); for r in {1, 2} the reciprocal
   // multiply is exact, but keep the division for bit-exact corner indices in general.
@@ -64,6 +68,11 @@ __device__ __forceinline__ Corners make_corners(float x, float y, float z, float
   c.ox = sx - fx;
   c.oy = sy - fy;
   c.oz = sz - fz;
+  if (smooth) {  // the ceil corner's weight S(frac), the floor corner's 1 - S(frac)
+    c.ox = smoothstep(c.ox);
+    c.oy = smoothstep(c.oy);
+    c.oz = smoothstep(c.oz);
+  }
   const uint32_t mask = (1u << log2T) - 1u;
   const uint32_t base = (uint32_t)level << log2T;
   c.idx[0] = base + hash3(cxc, cyc, czc, mask);
@@ -95,7 +104,7 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(const float* __restri
   float2 r = make_float2(0.f, 0.f);
   if (level < p.active_levels) {
     const float* xp = pos + pt * ldx;
-    Corners c = make_corners(xp[0], xp[1], xp[2], p.radius, p.inv_2r, p.scale[level], level, p.log2T);
+    Corners c = make_corners(xp[0], xp[1], xp[2], p.radius, p.inv_2r, p.scale[level], level, p.log2T, p.smooth != 0);
     float2 f[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) f[i] = table[c.idx[i]];
@@ -178,7 +187,9 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
         const float sy = (norm ? (py[j] + p.radius) / two_r : py[j]) * s;
         const float sz = (norm ? (pz[j] + p.radius) / two_r : pz[j]) * s;
         const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
-        const float ox = sx - fx, oy = sy - fy, oz = sz - fz;
+        const float tx = sx - fx, ty = sy - fy, tz = sz - fz;
+        const bool sm = p.smooth != 0;
+        const float ox = sm ? smoothstep(tx) : tx, oy = sm ? smoothstep(ty) : ty, oz = sm ? smoothstep(tz) : tz;
         const int cx = xc ? (int)ceilf(sx) : (int)fx;
         const int cy = yc ? (int)ceilf(sy) : (int)fy;
         const int cz = zc ? (int)ceilf(sz) : (int)fz;
@@ -201,6 +212,11 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
           float gx = (xc ? e : -e) * (wz * wy);
           float gy = (yc ? e : -e) * (wz * wx);
           float gz = (zc ? e : -e) * (wy * wx);
+          if (sm) {  // d weight / d frac = +-S'(frac)
+            gx *= smoothstep_grad(tx);
+            gy *= smoothstep_grad(ty);
+            gz *= smoothstep_grad(tz);
+          }
 #pragma unroll
           for (int off = 8; off >= 1; off >>= 1) {
             gx += __shfl_xor(gx, off, 16);
@@ -232,9 +248,11 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
   }
 }
 
-int fill_params(const char* fn, GridParams& p, int L, int log2T, const float* scales, float radius,
+int fill_params(const char* fn, GridParams& p, int L, int log2T, int interp, const float* scales, float radius,
                 int active_levels) {
   if (L < 1 || L > kMaxLevels) return mms::set_error(fn, "num_levels must be in [1, 16]");
+  if (interp != 0 && interp != 1) return mms::set_error(fn, "interp must be 0 (Linear) or 1 (Smoothstep)");
+  p.smooth = interp;
   if (log2T < 1 || log2T > 24) return mms::set_error(fn, "log2_hashmap_size must be in [1, 24]");
   if (!(radius >= 0.f)) return mms::set_error(fn, "radius must be >= 0 (0: inputs already in [0, 1])");
   p.levels = L;
@@ -249,15 +267,15 @@ int fill_params(const char* fn, GridParams& p, int L, int log2T, const float* sc
 }  // namespace
 
 MMS_EXPORT int mms_hashgrid_fwd_grouped(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx,
-                                        const float* table, int L, int log2T, int F, const float* scales, float radius,
-                                        int active_levels, float* out, int64_t ldo, void* stream) {
+                                        const float* table, int L, int log2T, int F, int interp, const float* scales,
+                                        float radius, int active_levels, float* out, int64_t ldo, void* stream) {
   const char* fn = "mms_hashgrid_fwd_grouped";
   MMS_REQUIRE(F == 2, fn, "features_per_level must be 2");
   MMS_REQUIRE(Mg >= 0 && ldx >= 3 && ldo >= 2 * L, fn, "bad shapes");
   MMS_REQUIRE(group == 1 || group == 5, fn, "group must be 1 (plain) or 5 (centre + 4 taps)");
   MMS_REQUIRE(group == 1 || gstride >= Mg, fn, "group rows overlap (gstride < groups)");
   GridParams p;
-  int rc = fill_params(fn, p, L, log2T, scales, radius, active_levels);
+  int rc = fill_params(fn, p, L, log2T, interp, scales, radius, active_levels);
   if (rc) return rc;
   if (Mg == 0) return 0;
   MMS_REQUIRE(pos && table && out, fn, "null pointer");
@@ -286,16 +304,16 @@ MMS_EXPORT int mms_hashgrid_fwd_grouped(const float* pos, int64_t Mg, int group,
 }
 
 MMS_EXPORT int mms_hashgrid_fwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L,
-                                int log2T, int F, const float* scales, float radius, int active_levels,
+                                int log2T, int F, int interp, const float* scales, float radius, int active_levels,
                                 float* out, int64_t ldo, void* stream) {
-  return mms_hashgrid_fwd_grouped(pos, M, 1, M, ldx, table, L, log2T, F, scales, radius, active_levels, out, ldo,
-                                  stream);
+  return mms_hashgrid_fwd_grouped(pos, M, 1, M, ldx, table, L, log2T, F, interp, scales, radius, active_levels, out,
+                                  ldo, stream);
 }
 
 MMS_EXPORT int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx,
-                                        const float* table, int L, int log2T, int F, const float* scales,
-                                        float radius, int active_levels, const float* dout, int64_t ldd,
-                                        float* dtable, float* dpos, int64_t lddx, void* stream) {
+                                        const float* table, int L, int log2T, int F, int interp,
+                                        const float* scales, float radius, int active_levels, const float* dout,
+                                        int64_t ldd, float* dtable, float* dpos, int64_t lddx, void* stream) {
   const char* fn = "mms_hashgrid_bwd_grouped";
   MMS_REQUIRE(F == 2, fn, "features_per_level must be 2");
   MMS_REQUIRE(Mg >= 0 && ldx >= 3 && ldd >= 2 * L, fn, "bad shapes");
@@ -303,7 +321,7 @@ MMS_EXPORT int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group,
   MMS_REQUIRE(group == 1 || gstride >= Mg, fn, "group rows overlap (gstride < groups)");
   MMS_REQUIRE(dpos == nullptr || lddx >= 3, fn, "bad dpos stride");
   GridParams p;
-  int rc = fill_params(fn, p, L, log2T, scales, radius, active_levels);
+  int rc = fill_params(fn, p, L, log2T, interp, scales, radius, active_levels);
   if (rc) return rc;
   if (Mg == 0 || (dtable == nullptr && dpos == nullptr)) return 0;
   MMS_REQUIRE(pos && table && dout, fn, "null pointer");
@@ -320,9 +338,9 @@ MMS_EXPORT int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group,
 }
 
 MMS_EXPORT int mms_hashgrid_bwd(const float* pos, int64_t M, int64_t ldx, const float* table, int L,
-                                int log2T, int F, const float* scales, float radius, int active_levels,
+                                int log2T, int F, int interp, const float* scales, float radius, int active_levels,
                                 const float* dout, int64_t ldd, float* dtable, float* dpos, int64_t lddx,
                                 void* stream) {
-  return mms_hashgrid_bwd_grouped(pos, M, 1, M, ldx, table, L, log2T, F, scales, radius, active_levels, dout, ldd,
-                                  dtable, dpos, lddx, stream);
+  return mms_hashgrid_bwd_grouped(pos, M, 1, M, ldx, table, L, log2T, F, interp, scales, radius, active_levels, dout,
+                                  ldd, dtable, dpos, lddx, stream);
 }

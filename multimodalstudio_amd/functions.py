@@ -290,12 +290,13 @@ def _f32arr(vals):
 class GridCfg:
     """Static description of one FeatureGrid(HashEncoding) (encodings.py:48-67, feature_structures.py:28-45)."""
 
-    def __init__(self, scales: Sequence[float], log2T: int, radius: float, features: int = 2):
+    def __init__(self, scales: Sequence[float], log2T: int, radius: float, features: int = 2, interp: int = 0):
         self.scales = [float(s) for s in scales]
         self.L = len(self.scales)
         self.log2T = int(log2T)
         self.radius = float(radius)
         self.F = int(features)
+        self.interp = int(interp)     # 0 "Linear" (the parity mode), 1 "Smoothstep" (tcnn's default, unpinned)
         self._arr = (ctypes.c_float * self.L)(*self.scales)
 
     @property
@@ -313,14 +314,14 @@ def grid_fwd(g: GridCfg, pos: torch.Tensor, ldx: int, M: int, table, active: int
     in (sample, tap) order, same values)."""
     Mg = M // group
     _lib.call("mms_hashgrid_fwd_grouped", pos.data_ptr(), Mg, group, Mg, ldx, table.data_ptr(), g.L, g.log2T, g.F,
-              g.scales_ptr, g.radius, active, out.data_ptr() + 4 * col, out.stride(0), _s())
+              g.interp, g.scales_ptr, g.radius, active, out.data_ptr() + 4 * col, out.stride(0), _s())
 
 
 def grid_bwd(g: GridCfg, pos, ldx, M, table, active, dout: torch.Tensor, col: int, dtable, dpos, group: int = 1):
     """Table / position gradients; group=5 for the [centre | 4 taps] SDF batch (M = 5 x centres)."""
     Mg = M // group
     _lib.call("mms_hashgrid_bwd_grouped", pos.data_ptr(), Mg, group, Mg, ldx, table.data_ptr(), g.L, g.log2T, g.F,
-              g.scales_ptr, g.radius, active, dout.data_ptr() + 4 * col, dout.stride(0), _p(dtable), _p(dpos),
+              g.interp, g.scales_ptr, g.radius, active, dout.data_ptr() + 4 * col, dout.stride(0), _p(dtable), _p(dpos),
               0 if dpos is None else dpos.stride(0), _s())
 
 
@@ -1903,4 +1904,4 @@ class GeoLossSegFunction(torch.autograd.Function):
 def HashGridApply(x, table, cfg: GridCfg, active: int):
     """Standalone FeatureGrid forward (feature_structures.py:78-83) with autograd to x and table."""
     from .hip_ops import HashGridFunction
-    return HashGridFunction.apply(x, table, cfg.scales, cfg.log2T, cfg.radius, active)
+    return HashGridFunction.apply(x, table, cfg.scales, cfg.log2T, cfg.radius, active, cfg.interp)

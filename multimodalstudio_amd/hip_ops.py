@@ -39,9 +39,12 @@ def _f32_array(vals):
     return arr
 
 
+INTERP = {None: 0, "Linear": 0, "Smoothstep": 1}   # HashEncodingConfig.interpolation (encodings.py:64-67)
+
+
 def hashgrid_forward(pos: torch.Tensor, table: torch.Tensor, scales, log2T: int, radius: float,
-                     active_levels: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Raw forward launch; pos [M, >=3] (row stride pos.stride(0)), out [M, >=2L]."""
+                     active_levels: int, out: Optional[torch.Tensor] = None, interp: int = 0) -> torch.Tensor:
+    """Raw forward launch; pos [M, >=3] (row stride pos.stride(0)), out [M, >=2L]; interp 0 Linear, 1 Smoothstep."""
     _check_dev(pos, table)
     L = len(scales)
     M = pos.shape[0]
@@ -50,18 +53,18 @@ def hashgrid_forward(pos: torch.Tensor, table: torch.Tensor, scales, log2T: int,
     assert pos.stride(1) == 1 and out.stride(1) == 1 and table.is_contiguous()
     sc = _f32_array(scales)
     _lib.call("mms_hashgrid_fwd", pos.data_ptr(), M, pos.stride(0), table.data_ptr(), L, log2T, table.shape[1],
-              ctypes.cast(sc, ctypes.c_void_p), float(radius), int(active_levels), out.data_ptr(), out.stride(0),
+              int(interp), ctypes.cast(sc, ctypes.c_void_p), float(radius), int(active_levels), out.data_ptr(), out.stride(0),
               _stream())
     return out
 
 
-def hashgrid_backward(pos, table, scales, log2T, radius, active_levels, dout, dtable=None, dpos=None):
+def hashgrid_backward(pos, table, scales, log2T, radius, active_levels, dout, dtable=None, dpos=None, interp: int = 0):
     _check_dev(pos, table, dout)
     L = len(scales)
     sc = _f32_array(scales)
     assert dout.stride(1) == 1
     _lib.call("mms_hashgrid_bwd", pos.data_ptr(), pos.shape[0], pos.stride(0), table.data_ptr(), L, log2T,
-              table.shape[1], ctypes.cast(sc, ctypes.c_void_p), float(radius), int(active_levels),
+              table.shape[1], int(interp), ctypes.cast(sc, ctypes.c_void_p), float(radius), int(active_levels),
               dout.data_ptr(), dout.stride(0), _ptr(dtable), _ptr(dpos), 0 if dpos is None else dpos.stride(0),
               _stream())
 
@@ -70,21 +73,22 @@ class HashGridFunction(torch.autograd.Function):
     """FeatureGrid(HashEncoding) forward/backward on the HIP kernels."""
 
     @staticmethod
-    def forward(ctx, pos, table, scales, log2T, radius, active_levels):
+    def forward(ctx, pos, table, scales, log2T, radius, active_levels, interp: int = 0):
         pos_c = pos.contiguous()
-        out = hashgrid_forward(pos_c, table, scales, log2T, radius, active_levels)
+        out = hashgrid_forward(pos_c, table, scales, log2T, radius, active_levels, interp=interp)
         ctx.save_for_backward(pos_c, table)
-        ctx.cfg = (scales, log2T, radius, active_levels)
+        ctx.cfg = (scales, log2T, radius, active_levels, interp)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         pos, table = ctx.saved_tensors
-        scales, log2T, radius, active_levels = ctx.cfg
+        scales, log2T, radius, active_levels, interp = ctx.cfg
         dtable = torch.zeros_like(table) if ctx.needs_input_grad[1] else None
         dpos = torch.zeros_like(pos) if ctx.needs_input_grad[0] else None
-        hashgrid_backward(pos, table, scales, log2T, radius, active_levels, dout.contiguous(), dtable, dpos)
-        return dpos, dtable, None, None, None, None
+        hashgrid_backward(pos, table, scales, log2T, radius, active_levels, dout.contiguous(), dtable, dpos,
+                          interp=interp)
+        return dpos, dtable, None, None, None, None, None
 
 
 # ----------------------------------------------------------------------------------------------

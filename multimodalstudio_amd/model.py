@@ -165,9 +165,13 @@ class HashEncoding(nn.Module):
     """HashEncoding (encodings.py:184-310) with implementation 'hip' (parameter hash_table [L*T, F])."""
 
     def __init__(self, num_levels=16, features_per_level=2, min_res=16, max_res=2048, log2_hashmap_size=19,
-                 hash_init_scale=0.001):
+                 hash_init_scale=0.001, interpolation: str = "Linear"):
         super().__init__()
         self.num_levels, self.features, self.log2T = num_levels, features_per_level, log2_hashmap_size
+        from .hip_ops import INTERP
+        if interpolation not in INTERP:
+            raise ValueError(f"interpolation '{interpolation}': Linear or Smoothstep (encodings.py:64-67)")
+        self.interp = INTERP[interpolation]
         self.growth_factor = float(np.exp((np.log(max_res) - np.log(min_res)) / (num_levels - 1)))
         levels = torch.arange(num_levels)
         self.scalings = torch.floor(min_res * self.growth_factor ** levels)
@@ -187,7 +191,8 @@ class FeatureGrid(nn.Module):
         self.encoding = encoding
         self.radius = float(radius)
         self.active_levels = encoding.num_levels
-        self.cfg = GridCfg(encoding.scalings.tolist(), encoding.log2T, self.radius, encoding.features)
+        self.cfg = GridCfg(encoding.scalings.tolist(), encoding.log2T, self.radius, encoding.features,
+                           getattr(encoding, "interp", 0))
 
     def update_mask(self, level: int):
         """feature_structures.py:85-88 (levels >= `level` contribute zero)."""
@@ -436,6 +441,9 @@ class ModelSpec:
     # "grid" (config 5 'grid_raw_grid_bg_unbalanced', method_configs.py:428-444: hash grid r = 2 + 71-128-128-256 MLP,
     # head 283-256x3-256, the radiance model's 3-layer heads)
     bg_kind: str = "nerf"
+    # HashEncodingConfig.interpolation of every grid: "Linear" (the reference torch path; parity-pinned) or
+    # "Smoothstep" (the reference config default, which only its tcnn backend implements; parity-unpinned)
+    interpolation: str = "Linear"
 
 
 @dataclass
@@ -556,7 +564,8 @@ class BaseModel(nn.Module):
         mods = spec.modalities
 
         def grid(radius=1.0):
-            enc = HashEncoding(spec.num_levels, 2, spec.min_res, spec.max_res, spec.log2T)
+            enc = HashEncoding(spec.num_levels, 2, spec.min_res, spec.max_res, spec.log2T,
+                               interpolation=spec.interpolation)
             return FeatureGrid(enc, radius)
 
         if spec.fields == "mlp":

@@ -44,7 +44,8 @@ class _Setup:
 
 @dataclass
 class HashEncodingConfig(_Setup):
-    """encodings.py:48-67 (implementation 'hip' added; tcnn's Smoothstep interpolation is not implemented)."""
+    """encodings.py:48-67 (implementation 'hip' added; interpolation "Linear" is the parity-pinned torch mode,
+    "Smoothstep" -- the reference default, tcnn's -- runs too, parity-unpinned)."""
     num_levels: int = 16
     features_per_level: int = 2
     min_res: int = 16
@@ -212,11 +213,13 @@ class RaySamples:
 # ------------------------------------------------------------------------------------------------
 # field components
 # ------------------------------------------------------------------------------------------------
-def _check_interp(cfg):
+def _check_interp(cfg) -> str:
+    """HashEncodingConfig.interpolation (encodings.py:64-67): "Linear" (the torch backend's only mode, :235-238; the
+    parity-pinned one) or "Smoothstep" (tcnn's, parity-unpinned: tcnn is not available to pin it)."""
     interp = getattr(cfg, "interpolation", None)
-    if interp not in (None, "Linear"):
-        raise ValueError(f"interpolation '{interp}' is not supported by the hip hash grid (Linear only, the torch "
-                         "backend's mode, encodings.py:235-238)")
+    if interp not in (None, "Linear", "Smoothstep"):
+        raise ValueError(f"interpolation '{interp}' is not supported by the hip hash grid (Linear or Smoothstep)")
+    return interp or "Linear"
 
 
 class HashEncoding(mm.HashEncoding):
@@ -226,16 +229,16 @@ class HashEncoding(mm.HashEncoding):
     def __init__(self, config, in_dim: int = 3):
         if in_dim != 3:
             raise ValueError("HashEncoding takes 3-D inputs")
-        _check_interp(config)
+        interp = _check_interp(config)
         super().__init__(config.num_levels, config.features_per_level, config.min_res, config.max_res,
-                         config.log2_hashmap_size, config.hash_init_scale)
+                         config.log2_hashmap_size, config.hash_init_scale, interpolation=interp)
         self.config = config
         self.input_dim = in_dim
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         shp = x.shape[:-1]
         out = HashGridFunction.apply(x.reshape(-1, 3), self.hash_table, self.scalings.tolist(), self.log2T, 0.0,
-                                     self.num_levels)
+                                     self.num_levels, self.interp)
         return out.reshape(*shp, self.get_out_dim())
 
 

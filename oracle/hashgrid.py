@@ -59,12 +59,19 @@ def corner_indices(scaled_c: torch.Tensor, scaled_f: torch.Tensor, log2T: int) -
     ]
 
 
-def hash_encode(x_hat: torch.Tensor, table: torch.Tensor, scales: torch.Tensor, log2T: int) -> torch.Tensor:
-    """HashEncoding.pytorch_fwd on normalised inputs x_hat [..., 3] -> [..., L * F] (differentiable)."""
+def hash_encode(x_hat: torch.Tensor, table: torch.Tensor, scales: torch.Tensor, log2T: int,
+                interpolation: str = "Linear") -> torch.Tensor:
+    """HashEncoding.pytorch_fwd on normalised inputs x_hat [..., 3] -> [..., L * F] (differentiable).
+
+    interpolation "Smoothstep": the tcnn mode of HashEncodingConfig.interpolation (encodings.py:64-67,207-221), which
+    the reference's torch path rejects (:235-238): the trilinear weights of the fractions t become S(t) =
+    t^2 (3 - 2 t) (tiny-cuda-nn's published grid encoding; tcnn is absent here, so this restatement is unpinned)."""
     xs = x_hat[..., None, :] * scales.view(-1, 1)                  # [..., L, 3]
     sc = torch.ceil(xs).to(torch.int32)
     sf = torch.floor(xs).to(torch.int32)
     off = xs - sf                                                  # int promoted; grad flows via xs
+    if interpolation == "Smoothstep":
+        off = off * off * (3.0 - 2.0 * off)
     idx = corner_indices(sc, sf, log2T)
     f = [table[i] for i in idx]                                    # each [..., L, F]
     ox, oy, oz = off[..., 0:1], off[..., 1:2], off[..., 2:3]
@@ -86,10 +93,10 @@ def level_mask(num_levels: int, features: int, active_levels: int) -> torch.Tens
 
 
 def feature_grid(x: torch.Tensor, table: torch.Tensor, scales: torch.Tensor, log2T: int, radius: float,
-                 active_levels: int) -> torch.Tensor:
+                 active_levels: int, interpolation: str = "Linear") -> torch.Tensor:
     """FeatureGrid.forward: rescale to [0, 1], encode, multiply by coarse-to-fine mask."""
     x_hat = (x + radius) / (2 * radius)
-    feats = hash_encode(x_hat, table, scales, log2T)
+    feats = hash_encode(x_hat, table, scales, log2T, interpolation)
     L = scales.shape[0]
     F = table.shape[-1]
     return feats * level_mask(L, F, active_levels)

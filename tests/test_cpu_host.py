@@ -58,12 +58,14 @@ def test_gemm_rejects_bad_arguments_before_touching_the_device(L):
 def test_hashgrid_rejects_bad_config(L):
     import ctypes
     sc = (ctypes.c_float * 16)(*([16.0] * 16))
-    rc = L.mms_hashgrid_fwd(1, 10, 3, 1, 16, 19, 3, ctypes.cast(sc, ctypes.c_void_p), 1.0, 16, 1, 32, None)
+    rc = L.mms_hashgrid_fwd(1, 10, 3, 1, 16, 19, 3, 0, ctypes.cast(sc, ctypes.c_void_p), 1.0, 16, 1, 32, None)
     assert rc != 0 and "features_per_level" in _err(L)
-    rc = L.mms_hashgrid_fwd(1, 10, 3, 1, 17, 19, 2, ctypes.cast(sc, ctypes.c_void_p), 1.0, 16, 1, 40, None)
+    rc = L.mms_hashgrid_fwd(1, 10, 3, 1, 17, 19, 2, 0, ctypes.cast(sc, ctypes.c_void_p), 1.0, 16, 1, 40, None)
     assert rc != 0 and "num_levels" in _err(L)
-    rc = L.mms_hashgrid_bwd_grouped(1, 10, 3, 10, 3, 1, 16, 19, 2, ctypes.cast(sc, ctypes.c_void_p), 1.0, 16, 1, 32,
-                                    1, None, 0, None)
+    rc = L.mms_hashgrid_fwd(1, 10, 3, 1, 16, 19, 2, 2, ctypes.cast(sc, ctypes.c_void_p), 1.0, 16, 1, 40, None)
+    assert rc != 0 and "interp" in _err(L)
+    rc = L.mms_hashgrid_bwd_grouped(1, 10, 3, 10, 3, 1, 16, 19, 2, 0, ctypes.cast(sc, ctypes.c_void_p), 1.0, 16, 1,
+                                    32, 1, None, 0, None)
     assert rc != 0 and "group" in _err(L)
 
 

@@ -38,6 +38,40 @@ def test_hashgrid_fwd_bwd(dev, log2T, active, radius):
     np.testing.assert_allclose(xd.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("group", [1, 5])
+def test_hashgrid_smoothstep(dev, group):
+    """interpolation "Smoothstep" (HashEncodingConfig, encodings.py:64-67; tcnn's mode, parity-unpinned): forward,
+    table and position gradients of the plain and the [centre | 4 taps] kernels vs the oracle's restatement of the
+    smoothstep weights, whose position gradient autograd derives (d S / dt = 6 t (1 - t))."""
+    from multimodalstudio_amd import functions as F
+    L, Mc, log2T = 16, 1500, 14
+    scales = ohg.level_scales(16, 1024, L)
+    g = torch.Generator().manual_seed(11)
+    table = (torch.rand(L << log2T, 2, generator=g) * 2 - 1) * 1e-1
+    c = _pts(Mc, seed=5)
+    dirs = torch.tensor([[1., -1., -1.], [-1., -1., 1.], [-1., 1., -1.], [1., 1., 1.]])
+    x = torch.cat([c] + [c + 1e-3 * d for d in dirs], 0).contiguous() if group == 5 else c
+    M = x.shape[0]
+    xr = x.clone().requires_grad_(True)
+    tr = table.clone().requires_grad_(True)
+    ref = ohg.feature_grid(xr, tr, scales, log2T, 1.0, L, "Smoothstep")
+    lin = ohg.feature_grid(x, table, scales, log2T, 1.0, L)
+    assert (ref.detach() - lin).abs().max() > 1e-3          # the modes differ
+    dout = torch.randn(ref.shape, generator=g)
+    ref.backward(dout)
+    cfg = F.GridCfg(scales.tolist(), log2T, 1.0, interp=1)
+    xd, td, dd = x.to(dev), table.to(dev), dout.to(dev).contiguous()
+    out = torch.zeros(M, 2 * L, device=dev)
+    F.grid_fwd(cfg, xd, 3, M, td, L, out, 0, group=group)
+    dtable = torch.zeros_like(td)
+    dpos = torch.zeros_like(xd)
+    F.grid_bwd(cfg, xd, 3, M, td, L, dd, 0, dtable, dpos, group=group)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out.cpu().numpy(), ref.detach().numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(dtable.cpu().numpy(), tr.grad.numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(dpos.cpu().numpy(), xr.grad.numpy(), rtol=1e-3, atol=1e-3)
+
+
 @pytest.mark.parametrize("log2T", [12, 19])
 def test_hashgrid_bwd_grouped_taps(dev, log2T):
     """[centre | 4 taps] batch: the grouped backward (in-thread merge of shared-cell corners) vs the oracle."""
