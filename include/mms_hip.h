@@ -338,14 +338,16 @@ int mms_uniform(uint64_t seed, uint32_t stream_id, const uint64_t* counter, int6
                 void* stream);
 int mms_counter_advance(uint64_t* counter, int64_t n, void* stream);
 
-/* ---- iso-surface of a dense SDF grid (mesh export: MeshExtractor.extract, evaluator_components/mesh_extractors.py:63;
- * utils/marching_cubes.py:35).  values [nx * ny * nz] x-major; cells split into 6 tetrahedra (marching tetrahedra).
- * count: counts[cell] = triangles of the cell ((nx-1)(ny-1)(nz-1) cells); emit: with offsets = exclusive scan of
- * counts (int64), verts [T * 3, 3] f32 (outward-oriented triangles) and keys [T * 3] int64 (grid-edge id of each
- * vertex, for welding).  origin / spacing: HOST arrays of 3 floats (point (i,j,k) = origin + spacing * (i,j,k)). */
-int mms_iso_count(const float* vals, int nx, int ny, int nz, float level, int32_t* counts, void* stream);
-int mms_iso_emit(const float* vals, int nx, int ny, int nz, float level, const float* origin, const float* spacing,
-                 const int64_t* offsets, float* verts, int64_t* keys, void* stream);
+/* ---- marching cubes over a dense SDF crop (mesh export: MeshExtractor.extract, evaluator_components/
+ * mesh_extractors.py:63 -> utils/marching_cubes.py:97-188, skimage.measure.marching_cubes per 256^3 crop).
+ * values [nx * ny * nz] x-major (numpy meshgrid(indexing="ij").ravel()).  Per cube the sign changes on its 12 edges
+ * are joined face by face (ambiguous faces by the asymptotic decider) into loops, fanned into triangles facing
+ * increasing SDF.  count: counts[cube] = triangles ((nx-1)(ny-1)(nz-1) cubes); emit: with offsets = exclusive scan of
+ * counts (int64), verts [T * 3, 3] f32 and keys [T * 3] int64 (3 * grid index of the vertex edge's lower end + axis,
+ * for welding).  origin / spacing: HOST arrays of 3 floats (point (i,j,k) = origin + spacing * (i,j,k)). */
+int mms_mc_count(const float* vals, int nx, int ny, int nz, float level, int32_t* counts, void* stream);
+int mms_mc_emit(const float* vals, int nx, int ny, int nz, float level, const float* origin, const float* spacing,
+                const int64_t* offsets, float* verts, int64_t* keys, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,141 +1,215 @@
-// Iso-surface extraction from a dense SDF grid (mesh export, /root/reference/src/evaluator_components/
-// mesh_extractors.py:63 -> utils/marching_cubes.py:35 get_surface_sliding).  The reference triangulates with
-// skimage's marching cubes, which is not available offline; here every grid cell is split into the 6 tetrahedra
-// around its main diagonal (corner 0 -> corner 6) and each tetrahedron is triangulated (marching tetrahedra): the
-// same zero level set, watertight across cells (neighbouring cells share face diagonals), with more triangles than
-// marching cubes.  Triangles are oriented with their normal towards increasing SDF (outward).
+// Marching cubes over a dense SDF crop (mesh export: /root/reference/src/evaluator_components/mesh_extractors.py:63
+// -> utils/marching_cubes.py:97-188 get_surface_sliding, which calls skimage.measure.marching_cubes per 256^3 crop).
 //
-// Grid: values [nx * ny * nz] f32, x-major (index (i * ny + j) * nz + k, point origin + spacing * (i, j, k)).
-// Two passes: count triangles per cell, exclusive scan (caller), emit.  Every vertex lies on a grid edge between a
-// point and a neighbour at a non-negative offset (1..7 = the offset's xyz bits), recorded as an edge key
-// base_index * 8 + offset for vertex welding by the caller.
+// skimage is absent offline, so the surface is built here from the cube's own corner values instead of a case table:
+// on each of the cube's 6 faces the sign changes along its 4 edges are joined into segments (2 crossings: one
+// segment; 4 crossings -- the ambiguous face -- two segments, paired by the asymptotic decider: the bilinear saddle
+// value (w0 w2 - w1 w3) / (w0 + w2 - w1 - w3) says whether the diagonal corners 0, 2 connect through the face, the
+// test Lewiner's marching cubes (skimage's) applies to faces).  Every crossed edge lies on exactly two faces, so the
+// segments close into loops; each loop is fanned into triangles.  A face is shared by two cubes that see its corners
+// in the same order (the face tables below list both sides alike), so both make the same decision: the surface is
+// watertight.  Triangles face increasing SDF (outward): each is flipped if its normal opposes the trilinear
+// interpolant's gradient at its centroid.
+//
+// Grid: values [nx * ny * nz] f32, x-major (index (i * ny + j) * nz + k: numpy meshgrid(indexing="ij").ravel(), the
+// reference's order), point = origin + spacing * (i, j, k).  Two passes: triangles per cube (count), exclusive scan
+// (caller), emit.  A vertex lies on a grid edge and is keyed 3 * (grid index of the edge's lower end) + axis, so the
+// caller welds vertices shared between cubes (the reference's trimesh merge_vertices) by key.
 #include "common.h"
 
 namespace {
 
-// corner c of a cell: (c & 1 ^ (c >> 1 & 1), c >> 1 & 1, c >> 2 & 1) in the order 0:(0,0,0) 1:(1,0,0) 2:(1,1,0)
-// 3:(0,1,0) 4:(0,0,1) 5:(1,0,1) 6:(1,1,1) 7:(0,1,1)
-__constant__ int kCx[8] = {0, 1, 1, 0, 0, 1, 1, 0};
-__constant__ int kCy[8] = {0, 0, 1, 1, 0, 0, 1, 1};
-__constant__ int kCz[8] = {0, 0, 0, 0, 1, 1, 1, 1};
-__constant__ int kTet[6][4] = {{0, 5, 1, 6}, {0, 1, 2, 6}, {0, 2, 3, 6}, {0, 3, 7, 6}, {0, 7, 4, 6}, {0, 4, 5, 6}};
+// corner c = dx + 2 dy + 4 dz
+// edges: 0-3 along x ((dy, dz) = (e & 1, e >> 1)), 4-7 along y ((dx, dz)), 8-11 along z ((dx, dy)); lower end first
+__constant__ int kEdgeA[12] = {0, 2, 4, 6, 0, 1, 4, 5, 0, 1, 2, 3};
+__constant__ int kEdgeB[12] = {1, 3, 5, 7, 2, 3, 6, 7, 4, 5, 6, 7};
+__constant__ int kEdgeAxis[12] = {0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2};
+// faces x=0, x=1, y=0, y=1, z=0, z=1: corners in cycle (the two cubes sharing a face list it in the same order) and
+// the edge between consecutive cycle corners (edge q joins corner q and q + 1)
+__constant__ int kFaceCorner[6][4] = {{0, 2, 6, 4}, {1, 3, 7, 5}, {0, 1, 5, 4}, {2, 3, 7, 6}, {0, 1, 3, 2}, {4, 5, 7, 6}};
+__constant__ int kFaceEdge[6][4] = {{4, 10, 6, 8}, {5, 11, 7, 9}, {0, 9, 2, 8}, {1, 11, 3, 10}, {0, 5, 1, 4}, {2, 7, 3, 6}};
 
-struct Cell {
-  float v[8];
-  int64_t g[8];  // grid index of each corner
+constexpr int kMaxTris = 12;  // per cube: at most 12 crossed edges, fanned loops of >= 3 give <= 10 triangles
+
+struct CubeSurface {
+  int n_loops;
+  int loop_len[4];
+  int loop[4][12];  // crossed edges of each loop, in order
 };
 
-__device__ __forceinline__ Cell load_cell(const float* vals, int ny, int nz, int i, int j, int k) {
-  Cell c;
+__device__ __forceinline__ void link(int (&nb)[12][2], int a, int b) {
+  nb[a][nb[a][0] < 0 ? 0 : 1] = b;
+  nb[b][nb[b][0] < 0 ? 0 : 1] = a;
+}
+
+// the loops of one cube (w = corner values - level; inside = w < 0)
+__device__ CubeSurface cube_loops(const float (&w)[8]) {
+  CubeSurface cs;
+  cs.n_loops = 0;
+  int nb[12][2];
+  bool cross[12];
+#pragma unroll
+  for (int e = 0; e < 12; ++e) {
+    nb[e][0] = nb[e][1] = -1;
+    cross[e] = (w[kEdgeA[e]] < 0.f) != (w[kEdgeB[e]] < 0.f);
+  }
+#pragma unroll
+  for (int f = 0; f < 6; ++f) {
+    int ce[4], cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ce[q] = kFaceEdge[f][q];
+      cnt += cross[ce[q]];
+    }
+    if (cnt == 2) {
+      int a = -1, b = -1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (cross[ce[q]]) { if (a < 0) a = ce[q]; else b = ce[q]; }
+      link(nb, a, b);
+    } else if (cnt == 4) {
+      // ambiguous face: corners 0, 2 on one side, 1, 3 on the other; the bilinear saddle decides which pair connects
+      const float w0 = w[kFaceCorner[f][0]], w1 = w[kFaceCorner[f][1]], w2 = w[kFaceCorner[f][2]],
+                  w3 = w[kFaceCorner[f][3]];
+      const float den = w0 + w2 - w1 - w3;
+      const float saddle = den != 0.f ? (w0 * w2 - w1 * w3) / den : 0.f;
+      const bool c02 = den != 0.f && ((saddle < 0.f) == (w0 < 0.f));
+      if (c02) {  // corners 0 and 2 joined: cut off corners 1 and 3
+        link(nb, ce[0], ce[1]);
+        link(nb, ce[2], ce[3]);
+      } else {    // cut off corners 0 and 2
+        link(nb, ce[3], ce[0]);
+        link(nb, ce[1], ce[2]);
+      }
+    }
+  }
+  bool seen[12];
+#pragma unroll
+  for (int e = 0; e < 12; ++e) seen[e] = false;
+  for (int e = 0; e < 12; ++e) {
+    if (!cross[e] || seen[e] || cs.n_loops >= 4) continue;
+    int n = 0, prev = -1, cur = e;
+    while (cur >= 0 && !seen[cur] && n < 12) {
+      seen[cur] = true;
+      cs.loop[cs.n_loops][n++] = cur;
+      const int nxt = nb[cur][0] != prev ? nb[cur][0] : nb[cur][1];
+      prev = cur;
+      cur = nxt;
+    }
+    cs.loop_len[cs.n_loops++] = n;
+  }
+  return cs;
+}
+
+struct Cube {
+  float w[8];
+  int64_t g0;  // grid index of corner 0
+};
+
+__device__ __forceinline__ Cube load_cube(const float* vals, int ny, int nz, int i, int j, int k, float level) {
+  Cube c;
+  c.g0 = ((int64_t)i * ny + j) * nz + k;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const int64_t gi = ((int64_t)(i + kCx[q]) * ny + (j + kCy[q])) * nz + (k + kCz[q]);
-    c.g[q] = gi;
-    c.v[q] = vals[gi];
+    const int64_t gi = ((int64_t)(i + (q & 1)) * ny + (j + ((q >> 1) & 1))) * nz + (k + (q >> 2));
+    c.w[q] = vals[gi] - level;
   }
   return c;
 }
 
-__device__ __forceinline__ int tet_tris(const Cell& c, int t, float level) {
+__device__ __forceinline__ bool cube_empty(const Cube& c) {
   int n = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) n += c.v[kTet[t][q]] < level;
-  return (n == 0 || n == 4) ? 0 : (n == 2 ? 2 : 1);
+  for (int q = 0; q < 8; ++q) n += c.w[q] < 0.f;
+  return n == 0 || n == 8;
 }
 
-__global__ void count_kernel(const float* __restrict__ vals, int nx, int ny, int nz, float level,
-                             int32_t* __restrict__ counts) {
-  const int64_t cells = (int64_t)(nx - 1) * (ny - 1) * (nz - 1);
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cells; e += (int64_t)gridDim.x * blockDim.x) {
+__device__ __forceinline__ int n_tris(const CubeSurface& cs) {
+  int t = 0;
+  for (int l = 0; l < cs.n_loops; ++l) t += cs.loop_len[l] >= 3 ? cs.loop_len[l] - 2 : 0;
+  return t < kMaxTris ? t : kMaxTris;
+}
+
+__global__ void mc_count_kernel(const float* __restrict__ vals, int nx, int ny, int nz, float level,
+                                int32_t* __restrict__ counts) {
+  const int64_t cubes = (int64_t)(nx - 1) * (ny - 1) * (nz - 1);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cubes; e += (int64_t)gridDim.x * blockDim.x) {
     const int k = (int)(e % (nz - 1));
     const int j = (int)((e / (nz - 1)) % (ny - 1));
     const int i = (int)(e / ((int64_t)(nz - 1) * (ny - 1)));
-    const Cell c = load_cell(vals, ny, nz, i, j, k);
-    int n = 0;
-#pragma unroll
-    for (int t = 0; t < 6; ++t) n += tet_tris(c, t, level);
-    counts[e] = n;
+    const Cube c = load_cube(vals, ny, nz, i, j, k, level);
+    counts[e] = cube_empty(c) ? 0 : n_tris(cube_loops(c.w));
   }
 }
 
-struct Vtx {
-  float p[3];
-  int64_t key;
-};
-
-__device__ __forceinline__ Vtx edge_vertex(const Cell& c, int a, int b, float level, const float* origin,
-                                           const float* spacing, int i, int j, int k) {
-  // order the edge from the lower to the upper grid point (non-negative offset)
-  if (c.g[a] > c.g[b]) { const int t = a; a = b; b = t; }
-  const float va = c.v[a], vb = c.v[b];
-  const float den = vb - va;
-  const float w = den != 0.f ? (level - va) / den : 0.5f;
-  Vtx v;
-  const float pa[3] = {(float)(i + kCx[a]), (float)(j + kCy[a]), (float)(k + kCz[a])};
-  const float pb[3] = {(float)(i + kCx[b]), (float)(j + kCy[b]), (float)(k + kCz[b])};
-#pragma unroll
-  for (int d = 0; d < 3; ++d) v.p[d] = origin[d] + spacing[d] * (pa[d] + w * (pb[d] - pa[d]));
-  const int off = (kCx[b] - kCx[a]) | ((kCy[b] - kCy[a]) << 1) | ((kCz[b] - kCz[a]) << 2);
-  v.key = c.g[a] * 8 + off;
-  return v;
+// local position (in cube units) of the crossing on edge e: lower end + t along the axis, t = -w_a / (w_b - w_a)
+__device__ __forceinline__ void edge_point(const Cube& c, int e, float (&p)[3]) {
+  const int a = kEdgeA[e], ax = kEdgeAxis[e];
+  const float wa = c.w[a], wb = c.w[kEdgeB[e]];
+  const float t = wa / (wa - wb);
+  p[0] = (float)(a & 1);
+  p[1] = (float)((a >> 1) & 1);
+  p[2] = (float)(a >> 2);
+  p[ax] += t;
 }
 
-__device__ __forceinline__ void put_tri(Vtx v0, Vtx v1, Vtx v2, const float* out_dir, float* verts, int64_t* keys,
-                                        int64_t slot) {
-  // orient the normal towards increasing SDF (out_dir: inside centroid -> outside centroid)
-  const float e1[3] = {v1.p[0] - v0.p[0], v1.p[1] - v0.p[1], v1.p[2] - v0.p[2]};
-  const float e2[3] = {v2.p[0] - v0.p[0], v2.p[1] - v0.p[1], v2.p[2] - v0.p[2]};
-  const float nrm[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
-  if (nrm[0] * out_dir[0] + nrm[1] * out_dir[1] + nrm[2] * out_dir[2] < 0.f) { const Vtx t = v1; v1 = v2; v2 = t; }
-  const Vtx vv[3] = {v0, v1, v2};
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-#pragma unroll
-    for (int d = 0; d < 3; ++d) verts[(slot * 3 + q) * 3 + d] = vv[q].p[d];
-    keys[slot * 3 + q] = vv[q].key;
-  }
-}
-
-__global__ void emit_kernel(const float* __restrict__ vals, int nx, int ny, int nz, float level, float ox, float oy,
-                            float oz, float sx, float sy, float sz, const int64_t* __restrict__ offsets,
-                            float* __restrict__ verts, int64_t* __restrict__ keys) {
-  const int64_t cells = (int64_t)(nx - 1) * (ny - 1) * (nz - 1);
-  const float origin[3] = {ox, oy, oz}, spacing[3] = {sx, sy, sz};
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cells; e += (int64_t)gridDim.x * blockDim.x) {
+__global__ void mc_emit_kernel(const float* __restrict__ vals, int nx, int ny, int nz, float level, float ox, float oy,
+                               float oz, float hx, float hy, float hz, const int64_t* __restrict__ offsets,
+                               float* __restrict__ verts, int64_t* __restrict__ keys) {
+  const int64_t cubes = (int64_t)(nx - 1) * (ny - 1) * (nz - 1);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cubes; e += (int64_t)gridDim.x * blockDim.x) {
     const int k = (int)(e % (nz - 1));
     const int j = (int)((e / (nz - 1)) % (ny - 1));
     const int i = (int)(e / ((int64_t)(nz - 1) * (ny - 1)));
-    const Cell c = load_cell(vals, ny, nz, i, j, k);
-    int64_t slot = offsets[e];
+    const Cube c = load_cube(vals, ny, nz, i, j, k, level);
+    if (cube_empty(c)) continue;
+    const CubeSurface cs = cube_loops(c.w);
+    int64_t t = offsets[e];
+    int emitted = 0;
+    for (int l = 0; l < cs.n_loops; ++l) {
+      const int n = cs.loop_len[l];
+      for (int q = 1; q + 1 < n && emitted < kMaxTris; ++q, ++emitted) {
+        int ed[3] = {cs.loop[l][0], cs.loop[l][q], cs.loop[l][q + 1]};
+        float p[3][3];
 #pragma unroll
-    for (int t = 0; t < 6; ++t) {
-      int in[4], out[4], ni = 0, no = 0;
+        for (int v = 0; v < 3; ++v) edge_point(c, ed[v], p[v]);
+        // orientation: normal (world units) against the trilinear interpolant's gradient at the centroid
+        const float u = (p[0][0] + p[1][0] + p[2][0]) / 3.f, vv = (p[0][1] + p[1][1] + p[2][1]) / 3.f,
+                    ww = (p[0][2] + p[1][2] + p[2][2]) / 3.f;
+        float g[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int cq = kTet[t][q];
-        if (c.v[cq] < level) in[ni++] = cq; else out[no++] = cq;
-      }
-      if (ni == 0 || no == 0) continue;
-      float dir[3] = {0.f, 0.f, 0.f};
-      for (int q = 0; q < no; ++q) { dir[0] += kCx[out[q]] / (float)no; dir[1] += kCy[out[q]] / (float)no; dir[2] += kCz[out[q]] / (float)no; }
-      for (int q = 0; q < ni; ++q) { dir[0] -= kCx[in[q]] / (float)ni; dir[1] -= kCy[in[q]] / (float)ni; dir[2] -= kCz[in[q]] / (float)ni; }
+        for (int q8 = 0; q8 < 8; ++q8) {
+          const float bx = (q8 & 1) ? u : 1.f - u, by = ((q8 >> 1) & 1) ? vv : 1.f - vv, bz = (q8 >> 2) ? ww : 1.f - ww;
+          g[0] += c.w[q8] * ((q8 & 1) ? 1.f : -1.f) * by * bz;
+          g[1] += c.w[q8] * (((q8 >> 1) & 1) ? 1.f : -1.f) * bx * bz;
+          g[2] += c.w[q8] * ((q8 >> 2) ? 1.f : -1.f) * bx * by;
+        }
+        const float h[3] = {hx, hy, hz};
+        float d1[3], d2[3];
 #pragma unroll
-      for (int d = 0; d < 3; ++d) dir[d] *= spacing[d];
-      if (ni == 1 || no == 1) {
-        const int apex = ni == 1 ? in[0] : out[0];
-        const int* rest = ni == 1 ? out : in;
-        const Vtx a = edge_vertex(c, apex, rest[0], level, origin, spacing, i, j, k);
-        const Vtx b = edge_vertex(c, apex, rest[1], level, origin, spacing, i, j, k);
-        const Vtx d = edge_vertex(c, apex, rest[2], level, origin, spacing, i, j, k);
-        put_tri(a, b, d, dir, verts, keys, slot++);
-      } else {
-        // quad across the 4 edges in0-out0, in0-out1, in1-out1, in1-out0 (a cycle)
-        const Vtx a = edge_vertex(c, in[0], out[0], level, origin, spacing, i, j, k);
-        const Vtx b = edge_vertex(c, in[0], out[1], level, origin, spacing, i, j, k);
-        const Vtx d = edge_vertex(c, in[1], out[1], level, origin, spacing, i, j, k);
-        const Vtx f = edge_vertex(c, in[1], out[0], level, origin, spacing, i, j, k);
-        put_tri(a, b, d, dir, verts, keys, slot++);
-        put_tri(a, d, f, dir, verts, keys, slot++);
+        for (int a = 0; a < 3; ++a) {
+          d1[a] = (p[1][a] - p[0][a]) * h[a];
+          d2[a] = (p[2][a] - p[0][a]) * h[a];
+        }
+        const float nrm[3] = {d1[1] * d2[2] - d1[2] * d2[1], d1[2] * d2[0] - d1[0] * d2[2], d1[0] * d2[1] - d1[1] * d2[0]};
+        if (nrm[0] * g[0] / h[0] + nrm[1] * g[1] / h[1] + nrm[2] * g[2] / h[2] < 0.f) {
+          const int te = ed[1]; ed[1] = ed[2]; ed[2] = te;
+        }
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+          // from the edge's lower grid point and its own t: bit-identical in every cube sharing the edge
+          const int a = kEdgeA[ed[v]], ax = kEdgeAxis[ed[v]];
+          const float wa = c.w[a], wb = c.w[kEdgeB[ed[v]]];
+          const float te = wa / (wa - wb);
+          const int I[3] = {i + (a & 1), j + ((a >> 1) & 1), k + (a >> 2)};
+          float* o = verts + (t * 3 + v) * 3;
+          o[0] = ox + hx * ((float)I[0] + (ax == 0 ? te : 0.f));
+          o[1] = oy + hy * ((float)I[1] + (ax == 1 ? te : 0.f));
+          o[2] = oz + hz * ((float)I[2] + (ax == 2 ? te : 0.f));
+          const int64_t ga = ((int64_t)I[0] * ny + I[1]) * nz + I[2];
+          keys[t * 3 + v] = 3 * ga + ax;
+        }
+        ++t;
       }
     }
   }
@@ -143,23 +217,23 @@ __global__ void emit_kernel(const float* __restrict__ vals, int nx, int ny, int 
 
 }  // namespace
 
-MMS_EXPORT int mms_iso_count(const float* vals, int nx, int ny, int nz, float level, int32_t* counts, void* stream) {
-  const char* fn = "mms_iso_count";
+MMS_EXPORT int mms_mc_count(const float* vals, int nx, int ny, int nz, float level, int32_t* counts, void* stream) {
+  const char* fn = "mms_mc_count";
   MMS_REQUIRE(nx >= 2 && ny >= 2 && nz >= 2, fn, "grid needs >= 2 points per axis");
   MMS_REQUIRE(vals && counts, fn, "null pointer");
-  const int64_t cells = (int64_t)(nx - 1) * (ny - 1) * (nz - 1);
-  hipLaunchKernelGGL(count_kernel, dim3(mms::grid_for(cells, 256, 65536)), dim3(256), 0, mms::as_stream(stream), vals,
+  const int64_t cubes = (int64_t)(nx - 1) * (ny - 1) * (nz - 1);
+  hipLaunchKernelGGL(mc_count_kernel, dim3(mms::grid_for(cubes, 256, 65536)), dim3(256), 0, mms::as_stream(stream), vals,
                      nx, ny, nz, level, counts);
   return mms::check_launch(fn);
 }
 
-MMS_EXPORT int mms_iso_emit(const float* vals, int nx, int ny, int nz, float level, const float* origin,
-                            const float* spacing, const int64_t* offsets, float* verts, int64_t* keys, void* stream) {
-  const char* fn = "mms_iso_emit";
+MMS_EXPORT int mms_mc_emit(const float* vals, int nx, int ny, int nz, float level, const float* origin,
+                           const float* spacing, const int64_t* offsets, float* verts, int64_t* keys, void* stream) {
+  const char* fn = "mms_mc_emit";
   MMS_REQUIRE(nx >= 2 && ny >= 2 && nz >= 2, fn, "grid needs >= 2 points per axis");
   MMS_REQUIRE(vals && origin && spacing && offsets && verts && keys, fn, "null pointer");
-  const int64_t cells = (int64_t)(nx - 1) * (ny - 1) * (nz - 1);
-  hipLaunchKernelGGL(emit_kernel, dim3(mms::grid_for(cells, 256, 65536)), dim3(256), 0, mms::as_stream(stream), vals,
+  const int64_t cubes = (int64_t)(nx - 1) * (ny - 1) * (nz - 1);
+  hipLaunchKernelGGL(mc_emit_kernel, dim3(mms::grid_for(cubes, 256, 65536)), dim3(256), 0, mms::as_stream(stream), vals,
                      nx, ny, nz, level, origin[0], origin[1], origin[2], spacing[0], spacing[1], spacing[2], offsets,
                      verts, keys);
   return mms::check_launch(fn);

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--config", default=None, help="a make_train_parity.CONFIGS name instead of --fixture")
     ap.add_argument("--start-step", type=int, default=None)
     ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--checkpoints", type=int, nargs="*", default=[25, 50, 100])
     a = ap.parse_args()
     from test_gpu_train_parity import run_parity
     dev = torch.device("cuda", 0)
@@ -41,19 +42,22 @@ def main():
             cfg["start_step"] = a.start_step
         if a.steps is not None:
             cfg["steps"] = a.steps
-        _, _, _, p0 = run_parity(dev, a.precision, gold, cfg=dict(cfg, steps=0))
-        print(f"{a.config} start {cfg['start_step']} steps {cfg['steps']}: PSNR at init " +
-              " ".join(f"{m}:{v:.4f}" for m, v in p0.items()), flush=True)
     for eps in a.eps:
-        rows = []
+        hists = []
         for r in range(a.runs):
-            _, cfg, losses, psnr = run_parity(dev, a.precision, gold, eps=eps, cfg=cfg)
-            rows.append(psnr)
+            hist = []
+            _, cfg, losses, psnr = run_parity(dev, a.precision, gold, eps=eps, cfg=cfg, history=hist,
+                                              checkpoints=tuple(a.checkpoints))
+            hists.append(dict(hist))
             print(f"eps {eps:g} run {r}: mean loss {losses.mean():.6f} PSNR " +
                   " ".join(f"{m}:{v:.4f}" for m, v in psnr.items()), flush=True)
-        mods = list(rows[0])
-        sd = {m: float(np.std([p[m] for p in rows], ddof=1)) for m in mods}
-        print(f"eps {eps:g}: run-to-run sd " + " ".join(f"{m}:{v:.4f}" for m, v in sd.items()), flush=True)
+        for step in sorted(hists[0]):
+            rows = [h[step] for h in hists]
+            mods = list(rows[0])
+            mean = {m: float(np.mean([p[m] for p in rows])) for m in mods}
+            sd = {m: float(np.std([p[m] for p in rows], ddof=1)) for m in mods}
+            print(f"eps {eps:g} step {step}: mean " + " ".join(f"{m}:{v:.3f}" for m, v in mean.items()) +
+                  " | run-to-run sd " + " ".join(f"{m}:{v:.4f}" for m, v in sd.items()), flush=True)
 
 
 if __name__ == "__main__":

@@ -88,12 +88,24 @@ def run_hip_e2e(f, dev, cap=None, concurrent_background=True):
 
 
 # fp32 parity-mode bounds, about 10x the measured worst case of each fixture (bounds 25-250x loose let
-# regressions pass).  Parameter gradients: scale-relative max error over every parameter tensor; the mlp_raw field's
-# analytic SDF gradient is differentiated twice (autograd through the HIP GEMM), so its parameter gradients carry
-# more reordering noise than the grid fields'.
-E2E_PARAM_TOL = {"e2e_mlp_raw_rgb_s95000": 1.5e-2}
+# regressions pass).  Parameter gradients, per tensor: the relative L2 error ||g - ref|| / ||ref|| (the bound that
+# catches a systematic difference) and the scale-relative max error max|g - ref| / max|ref|.  The max error has a
+# floor set by discrete flips: a ReLU pre-activation or an L1 residual within fp32 reordering of zero takes the other
+# branch for one sample, which moves one unit's row of weight gradients by ~5e-3 of the scale (measured on the
+# saturated 5-modality fixture: radiance layer-1 unit 17, scripts/e2e_diag.py) while every other element agrees to
+# ~1e-4.  The mlp_raw field's analytic SDF gradient is differentiated twice (autograd through the HIP GEMM), so its
+# gradients carry more reordering noise than the grid fields'.
+E2E_PARAM_L2_TOL = 2e-3
+E2E_PARAM_TOL = {"e2e_mlp_raw_rgb_s95000": 1.5e-2, "e2e_grid_raw_5mod_sat_s95000": 1e-2}
 E2E_PARAM_TOL_DEFAULT = 2e-3
 E2E_DPOSE_TOL = 5e-3
+
+
+def rel_l2(actual, ref):
+    a = np.asarray(actual, dtype=np.float64)
+    r = np.asarray(ref, dtype=np.float64)
+    n = np.linalg.norm(r)
+    return float(np.linalg.norm(a - r) / n) if n > 0 else float(np.linalg.norm(a - r))
 
 
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_rgb_s30000", "e2e_grid_raw_5mod_s95000",
@@ -111,12 +123,13 @@ def test_e2e_train_step(dev, name):
             if f"{m}:out:{k}" in f:
                 report[f"{m}:{k}"] = rel_err(o[k].detach().cpu(), f[f"{m}:out:{k}"])
         report[f"{m}:dpose"] = rel_err(pose.pose_adjustment[m].grad.cpu(), f[f"{m}:dpose"])
-    worst_param = 0.0
+    worst_param, worst_l2 = 0.0, 0.0
     for k, p in model.named_parameters():
         if "g:" + k in f:
             e = rel_err(p.grad.cpu(), f["g:" + k])
             report["g:" + k] = e
             worst_param = max(worst_param, e)
+            worst_l2 = max(worst_l2, rel_l2(p.grad.cpu(), f["g:" + k]))
     for m in mods:
         o = outs[m]
         assert np.array_equal(o["mask"].cpu().numpy().astype(bool), f[f"{m}:mask"]), m
@@ -127,7 +140,7 @@ def test_e2e_train_step(dev, name):
         report[f"{m}:bins_exact_frac"] = float((bins == ref_bins).mean())
     for k in sorted(report, key=lambda k: -report[k])[:12]:
         print(f"{k:90s} {report[k]:.3e}")
-    print(f"{name}: worst parameter gradient {worst_param:.3e}; worst dpose "
+    print(f"{name}: worst parameter gradient {worst_param:.3e} (relative L2 {worst_l2:.3e}); worst dpose "
           f"{max(report[f'{m}:dpose'] for m in mods):.3e}")
     assert report["loss"] < 1e-4
     for m in mods:
@@ -143,6 +156,7 @@ def test_e2e_train_step(dev, name):
         assert report.get(f"{m}:hessians", 0.0) < 0.15
         assert report[f"{m}:dpose"] < E2E_DPOSE_TOL, (m, report[f"{m}:dpose"])
     assert worst_param < E2E_PARAM_TOL.get(name, E2E_PARAM_TOL_DEFAULT), worst_param
+    assert worst_l2 < E2E_PARAM_L2_TOL, worst_l2
 
 
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000", "e2e_grid_raw_5mod_sat_s95000"])

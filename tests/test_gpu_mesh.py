@@ -1,10 +1,12 @@
-"""Mesh extraction (mesh.py: dense SDF grid + marching tetrahedra on the HIP kernels).
+"""Mesh extraction (mesh.py: the reference's coarse-to-fine SDF pyramid + marching cubes on the HIP kernels).
 
-The reference's mesh path (utils/marching_cubes.py, skimage + trimesh) is not importable offline, so the mesh is
-checked against geometry instead (parity unpinned): on an analytic sphere SDF the welded mesh is a closed
-2-manifold of genus 0 (every edge in exactly two faces, V - E + F = 2), its vertices lie on the sphere to the
-linear-interpolation error, every triangle faces outward, and its area is 4 pi r^2 within 1 %.  The model path
-exports a PLY from a geometric-init SDF field (a sphere of radius ~0.4 by construction, mlp.py:173-198).
+The reference's mesh path (utils/marching_cubes.py: skimage's marching cubes + trimesh) is not importable offline, so
+the mesh is checked against geometry (parity unpinned): on analytic sphere and torus SDFs the welded mesh
+is a closed 2-manifold (every edge in exactly two faces) of the right genus (V - E + F = 2 and 0), its vertices lie
+on the surface to the linear-interpolation error, every triangle faces outward, its area matches, and its triangle
+count is marching cubes' (about 2 triangles per surface cube, half of marching tetrahedra's).  The pyramid evaluates
+only the near-surface points at full resolution.  The model path exports a PLY from a geometric-init SDF field (a
+sphere of radius ~0.4 by construction, mlp.py:173-198).
 """
 import os
 
@@ -15,25 +17,65 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def test_sphere_iso_surface(dev):
-    from multimodalstudio_amd import mesh
-    n, r = 64, 0.5
-    vals = mesh.sdf_grid(lambda p: p.norm(dim=-1) - r, n, [-1, -1, -1], [1, 1, 1], dev)
-    h = 2.0 / (n - 1)
-    V, F = mesh.iso_surface(vals, (n, n, n), [-1, -1, -1], [h, h, h])
-    v = V.double().cpu().numpy()
-    f = F.cpu().numpy()
-    assert len(f) > 1000
-    assert np.abs(np.linalg.norm(v, axis=1) - r).max() < 0.5 * h * h / r + 1e-5
+def sphere(r):
+    return lambda p: p.norm(dim=-1) - r
+
+
+def torus(R, r):
+    return lambda p: torch.sqrt((torch.sqrt(p[:, 0] ** 2 + p[:, 1] ** 2) - R) ** 2 + p[:, 2] ** 2) - r
+
+
+def _check_closed(v, f, euler):
     e = np.sort(np.concatenate([f[:, [0, 1]], f[:, [1, 2]], f[:, [2, 0]]]), axis=1)
     _, cnt = np.unique(e, axis=0, return_counts=True)
-    assert (cnt == 2).all()
-    assert len(v) - len(cnt) + len(f) == 2
+    assert (cnt == 2).all(), np.bincount(cnt)
+    assert len(v) - len(cnt) + len(f) == euler
+
+
+@pytest.mark.parametrize("shape", ["sphere", "torus"])
+def test_marching_cubes_analytic(dev, shape):
+    from multimodalstudio_amd import mesh
+    n = 96
+    fn = sphere(0.5) if shape == "sphere" else torus(0.5, 0.2)
+    vals = mesh.sdf_grid(fn, n, [-1, -1, -1], [1, 1, 1], dev)
+    h = 2.0 / (n - 1)
+    V, F = mesh.marching_cubes(vals, (n, n, n), [-1, -1, -1], [h, h, h])
+    v = V.double().cpu().numpy()
+    f = F.cpu().numpy()
+    _check_closed(v, f, 2 if shape == "sphere" else 0)
+    sdf = fn(torch.from_numpy(v)).numpy()
+    assert np.abs(sdf).max() < 0.5 * h * h / 0.2 + 1e-5          # linear interpolation of a curved surface
     a, b, c = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
     nrm = np.cross(b - a, c - a)
-    assert ((nrm * (a + b + c)).sum(1) > 0).all()
+    cen = torch.from_numpy((a + b + c) / 3).requires_grad_(True)
+    fn(cen).sum().backward()
+    assert ((nrm * cen.grad.numpy()).sum(1) > 0).all()         # outward: along the SDF gradient
     area = 0.5 * np.linalg.norm(nrm, axis=1).sum()
-    assert abs(area / (4 * np.pi * r * r) - 1) < 0.01
+    ref = 4 * np.pi * 0.25 if shape == "sphere" else 4 * np.pi ** 2 * 0.5 * 0.2
+    assert abs(area / ref - 1) < 0.01
+    # marching cubes' triangle density: ~2 triangles per surface cube (tetrahedra gave 2-3x more)
+    cubes = int(((vals.view(n, n, n) < 0).float().unfold(0, 2, 1).unfold(1, 2, 1).unfold(2, 2, 1)
+                 .reshape(n - 1, n - 1, n - 1, 8).sum(-1).remainder(8) != 0).sum())
+    assert 1.5 * cubes <= len(f) <= 2.5 * cubes, (len(f), cubes)
+
+
+def test_pyramid_extraction_evaluates_near_surface_only(dev):
+    """get_surface_sliding at resolution 512 (8 crops of 256^3): far fewer SDF evaluations than 512^3, and the same
+    surface as the dense grid -- the merged mesh is closed and on the sphere."""
+    from multimodalstudio_amd import mesh
+    r = 0.6
+    stats = {}
+    V, F = mesh.get_surface_sliding(sphere(r), 512, (-1, -1, -1), (1, 1, 1), dev, merge=True, stats=stats)
+    assert stats["points"] == 512 ** 3
+    assert stats["evaluated"] < 0.1 * 512 ** 3, stats
+    v = V.double().cpu().numpy()
+    f = F.cpu().numpy()
+    h = 2.0 / 511
+    assert np.abs(np.linalg.norm(v, axis=1) - r).max() < 1e-3 + 0.5 * h * h / r
+    _check_closed(v, f, 2)
+    # without the merge (MeshExtractor.extract's return_mesh path) the crops' boundary vertices stay duplicated
+    V2, F2 = mesh.get_surface_sliding(sphere(r), 512, (-1, -1, -1), (1, 1, 1), dev)
+    assert F2.shape == F.shape and V2.shape[0] > V.shape[0]
 
 
 def test_model_mesh_export(dev, tmp_path):
@@ -41,7 +83,7 @@ def test_model_mesh_export(dev, tmp_path):
     from multimodalstudio_amd import model as mm
     torch.manual_seed(0)
     model = mm.BaseModel(mm.ModelSpec({"rgb": 3}, log2T=14)).to(dev)
-    ex = mesh.MeshExtractor(mesh.MeshExtractorConfig(resolution=64, gt_scale=True), [[-1, -1, -1], [1, 1, 1]],
+    ex = mesh.MeshExtractor(mesh.MeshExtractorConfig(resolution=256, gt_scale=True), [[-1, -1, -1], [1, 1, 1]],
                             np.diag([2.0, 2.0, 2.0, 1.0]), str(tmp_path))
     path = ex.extract(mesh.model_sdf_fn(model), step=1234)
     assert path.endswith(os.path.join("meshes", "00001234.ply"))
@@ -52,3 +94,4 @@ def test_model_mesh_export(dev, tmp_path):
     assert nv > 100 and nf > 100
     size = os.path.getsize(path)
     assert size == len(head) + len("end_header\n") + 12 * nv + 13 * nf
+    assert ex.last_stats["evaluated"] < 0.25 * 256 ** 3

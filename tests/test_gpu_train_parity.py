@@ -29,9 +29,10 @@ sys.path.insert(0, os.path.join(HERE, "golden"))
 TRAJ_STEPS = 5
 
 
-def run_parity(dev, precision: str, gold: str = GOLD, eps=None, cfg=None):
+def run_parity(dev, precision: str, gold: str = GOLD, eps=None, cfg=None, history=None, checkpoints=()):
     """The fixture's training run through the HIP path: (fixture, cfg, per-step losses, held-out PSNR per modality).
-    ``cfg`` replaces the fixture (a make_train_parity.CONFIGS entry: run without an oracle to compare against)."""
+    ``cfg`` replaces the fixture (a make_train_parity.CONFIGS entry: run without an oracle to compare against);
+    ``history`` (a list) receives (step, PSNR) at each of ``checkpoints`` and at the end."""
     from make_train_parity import draws, eval_inputs, step_inputs
     from multimodalstudio_amd import functions as fx
     from multimodalstudio_amd import model as mm
@@ -65,8 +66,34 @@ def run_parity(dev, precision: str, gold: str = GOLD, eps=None, cfg=None):
                       "indexes": torch.arange(cams[m].c2w.shape[0], dtype=torch.int32)} for m in mods}
         sampler = pl.UniformPixelSampler(cfg["rays"], cfg["sampler_seed"])
         gen = torch.Generator().manual_seed(cfg["rng_seed"])
+        # eval: held-out views, zero pose delta, no grad, the fixture's eval draws
+        ecams = ms.make_cameras(mods, cfg["n_views"], cfg["width"], cfg["height"], seed=0, train=False)
+        eimages = {m: ms.render_frames(ecams[m], channels[m], cpu, m if raw else None) for m in mods}
+        dcams = {m: pl.DeviceCameras(ecams[m], dev) for m in mods}
+        gen_rays = pl.RayGenerator(dcams, pl.CameraOptimizer(mods, {m: dcams[m].num for m in mods}, mode="off"), 0.0)
+
+        def evaluate():
+            tr.model.set_step(tr.step, tc.max_iters)
+            psnr = {}
+            with torch.no_grad():
+                rng, ecoords, tgts = mm.RNG({}, {}, {}), {}, {}
+                for m in mods:
+                    coords, tgt, (u, p, b) = eval_inputs(cfg, ecams, eimages, m)
+                    rng.uniform[m], rng.pdf[m], rng.background[m] = u.to(dev), [x.to(dev) for x in p], b.to(dev)
+                    ecoords[m], tgts[m] = coords.to(dev), tgt
+                outs = tr.model(gen_rays(ecoords), rng)
+                for m in mods:
+                    pred = outs[m][m]
+                    if raw:     # each pixel's own band (RawEvaluator, evaluator.py:721-745)
+                        c = ecoords[m]
+                        pred = pl.select_right_channel(pred, tr.masks[m][c[:, 1].long(), c[:, 2].long()].long()[:, None])
+                    psnr[m] = -10.0 * float(np.log10(float(((pred.float().cpu() - tgts[m]) ** 2).mean())))
+            return psnr
+
         losses = []
         for k in range(cfg["steps"]):
+            if history is not None and k in checkpoints:
+                history.append((k, evaluate()))
             coords, targets = step_inputs(cfg, sampler, frames, images, mods)
             rng = mm.RNG({}, {}, {})
             for m in mods:
@@ -74,26 +101,9 @@ def run_parity(dev, precision: str, gold: str = GOLD, eps=None, cfg=None):
                 rng.uniform[m], rng.pdf[m], rng.background[m] = u.to(dev), [x.to(dev) for x in p], b.to(dev)
             _, total, _ = tr.train_step(coords, targets, rng)
             losses.append(float(total))
-        # eval: held-out views, zero pose delta, no grad
-        ecams = ms.make_cameras(mods, cfg["n_views"], cfg["width"], cfg["height"], seed=0, train=False)
-        eimages = {m: ms.render_frames(ecams[m], channels[m], cpu, m if raw else None) for m in mods}
-        dcams = {m: pl.DeviceCameras(ecams[m], dev) for m in mods}
-        gen_rays = pl.RayGenerator(dcams, pl.CameraOptimizer(mods, {m: dcams[m].num for m in mods}, mode="off"), 0.0)
-        tr.model.set_step(tr.step, tc.max_iters)
-        psnr = {}
-        with torch.no_grad():
-            rng, ecoords, tgts = mm.RNG({}, {}, {}), {}, {}
-            for m in mods:
-                coords, tgt, (u, p, b) = eval_inputs(cfg, ecams, eimages, m)
-                rng.uniform[m], rng.pdf[m], rng.background[m] = u.to(dev), [x.to(dev) for x in p], b.to(dev)
-                ecoords[m], tgts[m] = coords.to(dev), tgt
-            outs = tr.model(gen_rays(ecoords), rng)
-            for m in mods:
-                pred = outs[m][m]
-                if raw:     # each pixel's own band (RawEvaluator, evaluator.py:721-745)
-                    c = ecoords[m]
-                    pred = pl.select_right_channel(pred, tr.masks[m][c[:, 1].long(), c[:, 2].long()].long()[:, None])
-                psnr[m] = -10.0 * float(np.log10(float(((pred.float().cpu() - tgts[m]) ** 2).mean())))
+        psnr = evaluate()
+        if history is not None:
+            history.append((cfg["steps"], psnr))
         return f, cfg, np.array(losses), psnr
     finally:
         fx.set_precision("fp32")
