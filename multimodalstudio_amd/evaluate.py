@@ -13,6 +13,7 @@ from __future__ import annotations
 import time
 from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 
 from . import scene as mscene
@@ -26,6 +27,46 @@ def psnr(rendering: torch.Tensor, gt: torch.Tensor) -> float:
     r = rendering.clip(0.0, 1.0).to(torch.float64)
     mse = torch.mean((r - gt.to(torch.float64)) ** 2)
     return float(10.0 * torch.log10(1.0 / mse))
+
+
+def ssim(rendering: torch.Tensor, gt: torch.Tensor, data_range: float = 1.0, kernel_size: int = 11,
+         sigma: float = 1.5, k1: float = 0.01, k2: float = 0.03) -> float:
+    """structural_similarity_index_measure(clip(rendering, 0, 1), gt, data_range=1.0) on [H, W, C] images, as
+    compute_metrics calls it for full views (eval_utils.py:325-394): an 11 x 11 Gaussian window (sigma 1.5) over
+    reflect-padded images, c1 = (k1 L)^2, c2 = (k2 L)^2, the map cropped to the unpadded interior and averaged.
+    torchmetrics' published formula restated (torchmetrics is absent here: parity unpinned)."""
+    x = rendering.clip(0.0, 1.0).to(torch.float64).permute(2, 0, 1)[None]
+    y = gt.to(torch.float64).permute(2, 0, 1)[None]
+    C = x.shape[1]
+    d = torch.arange((1 - kernel_size) / 2, (1 + kernel_size) / 2, 1.0, dtype=torch.float64, device=x.device)
+    g = torch.exp(-((d / sigma) ** 2) / 2)
+    g = g / g.sum()
+    kern = (g[:, None] * g[None, :]).expand(C, 1, kernel_size, kernel_size)
+    pad = (kernel_size - 1) // 2
+    xp = torch.nn.functional.pad(x, (pad, pad, pad, pad), mode="reflect")
+    yp = torch.nn.functional.pad(y, (pad, pad, pad, pad), mode="reflect")
+    stats = torch.nn.functional.conv2d(torch.cat([xp, yp, xp * xp, yp * yp, xp * yp]), kern, groups=C)
+    mx, my, xx, yy, xy = stats.split(1)
+    c1, c2 = (k1 * data_range) ** 2, (k2 * data_range) ** 2
+    vx, vy, cxy = xx - mx * mx, yy - my * my, xy - mx * my
+    full = ((2 * mx * my + c1) * (2 * cxy + c2)) / ((mx * mx + my * my + c1) * (vx + vy + c2))
+    return float(full[..., pad:-pad, pad:-pad].mean())
+
+
+def degree_of_polarization(data: torch.Tensor) -> torch.Tensor:
+    """to_dop (polarizer.py:103-116): Stokes (0.5 sum I, I0 - I90, I45 - I135) of the 4 intensities [..., 4], then
+    ||(s1, s2)|| / s0."""
+    s0 = 0.5 * data.sum(-1)
+    s1, s2 = data[..., 0] - data[..., 2], data[..., 1] - data[..., 3]
+    return torch.sqrt(s1 * s1 + s2 * s2) / s0
+
+
+def angle_of_polarization(data: torch.Tensor) -> torch.Tensor:
+    """to_aop (polarizer.py:118-134): 0.5 atan2(s2, s1 + 1e-7) wrapped into [0, pi]."""
+    s1, s2 = data[..., 0] - data[..., 2], data[..., 1] - data[..., 3]
+    aop = 0.5 * torch.atan2(s2, s1 + 1e-7)
+    aop = torch.where(aop < 0, aop + np.pi, aop)
+    return torch.clamp(aop, 0, np.pi)
 
 
 def full_view_coords(frame: int, H: int, W: int, device) -> torch.Tensor:
@@ -81,7 +122,11 @@ class FullViewEvaluator:
     @torch.no_grad()
     def render_view(self, frames: Dict[str, int]) -> Dict[str, Dict[str, torch.Tensor]]:
         """Evaluator.render_view (evaluator.py:100-178) for one frame per modality: images [H, W, C] per head plus
-        depth / accumulation / normals; raw methods add 'mosaicked' [H, W, 1] (the modality's own band per pixel)."""
+        depth / accumulation / normals; raw methods add 'mosaicked' [H, W, 1] (the modality's own band per pixel).
+        RawEvaluator.generate_eval_renderings' extras (evaluator.py:621-700, eval_utils.py:77-160) under the key
+        '_aligned': every head on the FIRST modality's view ('aligned' renderings), each raw head mosaicked with its
+        modality's pattern over that view ('<head>:mosaicked'), and for polarization the degree / angle of
+        polarization of the aligned rendering (polarizer.to_dop / to_aop, the angle divided by pi)."""
         dev = next(self.model.parameters()).device
         coords = {m: full_view_coords(f, self.H, self.W, dev) for m, f in frames.items()}
         flat = self.query(coords)
@@ -93,14 +138,29 @@ class FullViewEvaluator:
                 band = self.mosaick[m][c[:, 1].long(), c[:, 2].long()].long()[:, None]
                 img["mosaicked"] = select_right_channel(o[m], band).reshape(self.H, self.W, 1)
             out[m] = img
+        first = next(iter(flat))
+        heads = [h for h in self.model.spec.modalities if h in flat[first]]
+        aligned = {h: out[first][h] for h in heads}
+        if self.mosaick is not None:
+            c = coords[first]
+            for h in heads:
+                band = self.mosaick[h][c[:, 1].long(), c[:, 2].long()].long()[:, None]
+                aligned[f"{h}:mosaicked"] = select_right_channel(flat[first][h], band).reshape(self.H, self.W, 1)
+        if "polarization" in aligned:
+            aligned["degree_of_polarization"] = degree_of_polarization(aligned["polarization"])
+            aligned["angle_of_polarization"] = angle_of_polarization(aligned["polarization"]) / np.pi
+        out["_aligned"] = aligned
         return out
 
     def compute_metrics(self, renderings: Dict[str, Dict[str, torch.Tensor]], gt: Dict[str, torch.Tensor]):
-        """Evaluator.compute_metrics (evaluator.py:431-440): PSNR per modality (raw: mosaicked vs the raw frame)."""
+        """Evaluator.compute_metrics (evaluator.py:431-440, eval_utils.py:325-394): PSNR and SSIM per modality (raw:
+        mosaicked vs the raw frame)."""
         metrics = {}
         for m, r in renderings.items():
+            if m.startswith("_"):
+                continue
             img = r["mosaicked"] if "mosaicked" in r else r[m]
-            metrics[m] = {"PSNR": psnr(img, gt[m])}
+            metrics[m] = {"PSNR": psnr(img, gt[m]), "SSIM": ssim(img, gt[m])}
         return metrics
 
 

@@ -50,9 +50,29 @@ def main():
     tg = Trainer(cfg, dev, rank=rank)
     tg.set_step(95000)
     g = GraphTrainer(tg, ddp=ddp)
+    # the graph path's exchange: the local gradients the replayed forward/backward graph left, and what the
+    # all-reduce between the two graphs made of them
+    seen = {"local": [], "reduced": []}
+    orig = ddp.allreduce_grads
+
+    def spy(groups):
+        seen["local"].append([gr.grad.clone() for gr in groups])
+        orig(groups)
+        seen["reduced"].append([gr.grad.clone() for gr in groups])
+
+    ddp.allreduce_grads = spy
     for _ in range(5):
         g.step()
     torch.cuda.synchronize()
+    ddp.allreduce_grads = orig
+    if seen["local"]:
+        errs = []
+        for local, red in zip(seen["local"], seen["reduced"]):
+            for lg, rg in zip(local, red):
+                mean = sum(gather(lg)) / world
+                errs.append(float((rg.cpu() - mean).abs().max()) / max(float(mean.abs().max()), 1e-30))
+        res["graph_grad_err"] = max(errs)
+        res["graph_allreduces"] = len(seen["local"])
     p = gather(tg.fields.flat)
     q = gather(tg.poses.flat)
     res["graph_params_equal"] = bool(torch.equal(p[0], p[1]) and torch.equal(q[0], q[1]))

@@ -6,6 +6,7 @@ import os
 import sys
 
 import pytest
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -223,3 +224,47 @@ def test_benchmarked_preset_keeps_the_sdf_chain_split_bf16x3():
     fast = fx.PRESETS["fast"]
     assert fast["sdf"] == 2 and fast["sdf_chain"] in (0, 2) and fast["mlp"] == 0
     assert fx.PRESETS["fast_x2"]["sdf_chain"] == 3
+
+
+def test_ssim_matches_direct_window_sums():
+    """evaluate.ssim (torchmetrics' SSIM restated: 11x11 Gaussian, sigma 1.5, reflect padding, interior mean) against
+    direct per-window sums in numpy; identical images score 1, noise lowers it."""
+    from multimodalstudio_amd import evaluate as ev
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(21, 18, 2, generator=g)
+    y = (x + 0.1 * torch.randn(21, 18, 2, generator=g)).clip(0, 1)
+    assert abs(ev.ssim(x, x) - 1.0) < 1e-12
+    k, sig = 11, 1.5
+    d = np.arange(k) - (k - 1) / 2
+    w1 = np.exp(-(d / sig) ** 2 / 2)
+    w1 /= w1.sum()
+    w = np.outer(w1, w1)
+    p = (k - 1) // 2
+    xs = np.pad(x.numpy().astype(np.float64), ((p, p), (p, p), (0, 0)), mode="reflect")
+    ys = np.pad(y.numpy().astype(np.float64), ((p, p), (p, p), (0, 0)), mode="reflect")
+    H, W = xs.shape[0] - 2 * p, xs.shape[1] - 2 * p
+    c1, c2 = 0.01 ** 2, 0.03 ** 2
+    vals = []
+    for c in range(2):
+        for i in range(p, H - p):        # the map is cropped to the interior of the unpadded image
+            for j in range(p, W - p):
+                a = xs[i:i + k, j:j + k, c]
+                b = ys[i:i + k, j:j + k, c]
+                mx, my = (w * a).sum(), (w * b).sum()
+                vx = (w * a * a).sum() - mx * mx
+                vy = (w * b * b).sum() - my * my
+                cxy = (w * a * b).sum() - mx * my
+                vals.append(((2 * mx * my + c1) * (2 * cxy + c2)) / ((mx * mx + my * my + c1) * (vx + vy + c2)))
+    assert abs(ev.ssim(y, x) - float(np.mean(vals))) < 1e-10
+    assert ev.ssim(y, x) < 0.99
+
+
+def test_polarization_extras():
+    """evaluate.degree_of_polarization / angle_of_polarization (polarizer.py:103-134) on intensities of known Stokes
+    vectors: I = 0.5 [s0 + s1, s0 + s2, s0 - s1, s0 - s2]."""
+    from multimodalstudio_amd import evaluate as ev
+    s0, p, psi = 0.8, 0.3, 0.4
+    s1, s2 = s0 * p * np.cos(2 * psi), s0 * p * np.sin(2 * psi)
+    I = 0.5 * torch.tensor([[s0 + s1, s0 + s2, s0 - s1, s0 - s2]], dtype=torch.float64)
+    assert abs(float(ev.degree_of_polarization(I)[0]) - p) < 1e-12
+    assert abs(float(ev.angle_of_polarization(I)[0]) - psi) < 1e-6

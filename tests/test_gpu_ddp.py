@@ -35,3 +35,6 @@ def test_two_rank_training(tmp_path):
     assert res["graph_disabled"] is None
     assert res["graph_stats"]["replays"] >= 1, res
     assert res["graph_params_equal"]
+    # the graph path's all-reduce (between the captured forward/backward and optimizer graphs) averages the ranks'
+    # gradients, as the eager path does
+    assert res["graph_allreduces"] >= 1 and res["graph_grad_err"] < 1e-6, res

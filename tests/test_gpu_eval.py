@@ -81,3 +81,29 @@ def test_eval_split_smoke(dev):
     for m, s in scores.items():
         assert np.isfinite(s) and s > 0, (m, s)
     assert rate > 0
+
+
+def test_raw_eval_renderings(dev):
+    """RawEvaluator's extras (evaluator.py:621-700): every head aligned to the first modality's view and mosaicked with
+    each modality's pattern, degree / angle of polarization of the aligned polarization rendering, SSIM beside PSNR."""
+    from multimodalstudio_amd import evaluate as ev
+    from multimodalstudio_amd import scene as ms
+    from multimodalstudio_amd.pipeline import DeviceCameras, RayGenerator, TrainConfig, Trainer
+    t = Trainer(TrainConfig(method="grid_raw", modalities=("rgb", "polarization"), num_rays_per_modality=256,
+                            log2T=14, width=48, height=40), dev)
+    t.set_step(95000)
+    cams = ms.make_cameras(t.modalities, 50, 48, 40, seed=0, train=False)
+    dcams = {m: DeviceCameras(cams[m], dev) for m in t.modalities}
+    e = ev.FullViewEvaluator(t.model, RayGenerator(dcams, t.pose, 0.0), 40, 48, 512, t.masks)
+    rend = e.render_view({"rgb": 0, "polarization": 0})
+    al = rend["_aligned"]
+    assert al["rgb"].shape == (40, 48, 3) and al["polarization"].shape == (40, 48, 4)
+    assert al["rgb:mosaicked"].shape == (40, 48, 1) and al["polarization:mosaicked"].shape == (40, 48, 1)
+    # the aligned heads are the first modality's own renderings
+    assert torch.equal(al["rgb"], rend["rgb"]["rgb"])
+    dop, aop = al["degree_of_polarization"], al["angle_of_polarization"]
+    assert dop.shape == (40, 48) and torch.isfinite(aop).all() and (aop >= 0).all() and (aop <= 1).all()
+    gt = {m: ms.render_frames(ev._one_view(cams[m], 0), ms.CHANNELS[m], dev, m)[0] for m in t.modalities}
+    met = e.compute_metrics(rend, gt)
+    for m in t.modalities:
+        assert np.isfinite(met[m]["PSNR"]) and -1.0 <= met[m]["SSIM"] <= 1.0, met
