@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--eval-views", type=int, default=5)
     ap.add_argument("--seed", type=int, default=654824)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--override", nargs="*", default=[],
+                    help="PRECISION entries to change after the preset, e.g. heads=2 radiance=2 (functions.PRESETS)")
     a = ap.parse_args()
     from multimodalstudio_amd import evaluate as ev
     from multimodalstudio_amd import functions as fx
@@ -44,6 +46,9 @@ def main():
     from multimodalstudio_amd import pipeline as pl
     dev = torch.device("cuda", 0)
     fx.set_precision(a.precision)
+    for kv in a.override:
+        k, v = kv.split("=")
+        fx.PRECISION[k] = int(v)
     mods = tuple(a.modalities.split(","))
     tc = pl.TrainConfig(method=a.method, modalities=mods, num_rays_per_modality=a.rays, log2T=a.log2T,
                         max_iters=a.max_iters, gpu_sampler=True, seed=a.seed)
@@ -63,7 +68,7 @@ def main():
             hist.append({"step": k, "psnr": psnr, "test_rays_per_sec": rate, "wall_s": time.time() - t0})
             print(f"[{a.precision}] step {k}: " + " ".join(f"{m} {v:.3f}" for m, v in psnr.items()) +
                   f"  ({time.time() - t0:.0f}s, eval {rate / 1e6:.2f} Mrays/s)", flush=True)
-    res = {"precision": a.precision, "method": a.method, "modalities": mods, "rays": a.rays, "steps": a.steps,
+    res = {"precision": a.precision, "overrides": a.override, "method": a.method, "modalities": mods, "rays": a.rays, "steps": a.steps,
            "max_iters": a.max_iters, "log2T": a.log2T, "graph_stats": gt.stats, "history": hist}
     if a.out:
         with open(a.out, "w") as f:

@@ -95,7 +95,10 @@ def run_hip_e2e(f, dev, cap=None, concurrent_background=True):
 # saturated 5-modality fixture: radiance layer-1 unit 17, scripts/e2e_diag.py) while every other element agrees to
 # ~1e-4.  The mlp_raw field's analytic SDF gradient is differentiated twice (autograd through the HIP GEMM), so its
 # gradients carry more reordering noise than the grid fields'.
-E2E_PARAM_L2_TOL = 2e-3
+# (the flip floor is the reference algorithm's own: tests/test_oracle_golden.py::test_saturated_fixture_flip_floor
+# moves the same element by 5.05e-3 with the weights perturbed at fp32-reordering scale)
+E2E_PARAM_L2_TOL = {"e2e_grid_raw_5mod_sat_s95000": 5e-3}
+E2E_PARAM_L2_TOL_DEFAULT = 1e-3
 E2E_PARAM_TOL = {"e2e_mlp_raw_rgb_s95000": 1.5e-2, "e2e_grid_raw_5mod_sat_s95000": 1e-2}
 E2E_PARAM_TOL_DEFAULT = 2e-3
 E2E_DPOSE_TOL = 5e-3
@@ -156,7 +159,7 @@ def test_e2e_train_step(dev, name):
         assert report.get(f"{m}:hessians", 0.0) < 0.15
         assert report[f"{m}:dpose"] < E2E_DPOSE_TOL, (m, report[f"{m}:dpose"])
     assert worst_param < E2E_PARAM_TOL.get(name, E2E_PARAM_TOL_DEFAULT), worst_param
-    assert worst_l2 < E2E_PARAM_L2_TOL, worst_l2
+    assert worst_l2 < E2E_PARAM_L2_TOL.get(name, E2E_PARAM_L2_TOL_DEFAULT), worst_l2
 
 
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000", "e2e_grid_raw_5mod_sat_s95000"])
