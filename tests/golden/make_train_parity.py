@@ -9,7 +9,7 @@ and the uniform draws from a CPU generator in fixed-size blocks (independent of 
 fixture stores only the configuration, the oracle's per-step losses and its held-out PSNR before and
 after training.  tests/test_gpu_train_parity.py replays the same K steps through the HIP path.
 
-    python tests/golden/make_train_parity.py [rgb|raw5] [seed]   (CPU, ~3 / ~6 min on 8 threads)
+    python tests/golden/make_train_parity.py [rgb|raw5] [seed]   (CPU, ~3 / ~2.5 min on 8 threads)
 
 writes train_parity_<name>.npz (seed 0) or train_parity_<name>_s<seed>.npz: seed k > 0 shifts the pixel-sampler and
 draw seeds by k (same init), an independent trajectory of the same training problem.  One trajectory's held-out
@@ -34,9 +34,13 @@ CONFIGS = {
                 start_step=95000, steps=300, eval_rays=4096, init_seed=654824, sampler_seed=654824, rng_seed=11,
                 eval_seed=5, bg_samples=16),
     # BASELINE configs[2] shape: grid_raw, five mosaicked modalities (each pixel supervises its own band)
+    # (a short window at the step-95k learning rate: the first AdamW steps move the hash tables by ~lr per entry and the
+    # held-out PSNR by several dB per modality while independent runs of one implementation stay within ~0.05 dB --
+    # float-atomic reordering has not yet decorrelated them -- so the 0.1 dB criterion sits well above the noise
+    # floor; by step 200 one run's PSNR scatters by 0.1-0.4 dB, scripts/parity_scatter.py)
     "raw5": dict(method="grid_raw", modalities=("rgb", "infrared", "mono", "polarization", "multispectral"),
-                 rays=96, log2T=12, width=96, height=80, n_views=10, start_step=95000, steps=200, eval_rays=2048,
-                 init_seed=654824, sampler_seed=654824, rng_seed=11, eval_seed=5, bg_samples=16),
+                 rays=96, log2T=12, width=96, height=80, n_views=10, start_step=95000, steps=50, checkpoints=(25,),
+                 eval_rays=2048, init_seed=654824, sampler_seed=654824, rng_seed=11, eval_seed=5, bg_samples=16),
 }
 CFG = CONFIGS["rgb"]
 
@@ -142,6 +146,8 @@ def main(name: str = "rgb", seed: int = 0):
     evaluate("eval0")
     t0 = time.time()
     for k in range(cfg["steps"]):
+        if k in cfg.get("checkpoints", ()):
+            evaluate(f"eval{k}")
         coords, targets = step_inputs(cfg, sampler, frames, images, mods)
         out[f"s{k}:loss"] = np.float64(ot.train_step(coords, targets))
         if k % 25 == 0:

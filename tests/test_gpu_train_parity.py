@@ -134,66 +134,74 @@ def _fixtures(gold: str):
 
 
 def _repeated(dev, precision, gold=GOLD):
-    """Held-out PSNR differences HIP - oracle, paired seed by seed.  One trajectory's PSNR scatters by about +-0.07 dB
-    on either side (float-atomic hash-gradient sums are not reproducible and AdamW's eps 1e-15 turns last-bit
-    differences of near-zero gradients into full-size updates; the oracle's single CPU run is one draw of the same
-    scatter), so the criterion is on the mean difference over independent seeds (each oracle seed run once, the
-    HIP path once per seed); with fewer than 4 seeds the HIP path runs REPEATS times per seed."""
+    """Held-out PSNR differences HIP - oracle, paired seed by seed, at the fixture's checkpoints and at its end.
+    Independent trajectories of one implementation drift apart (float-atomic hash-gradient sums are not reproducible
+    and AdamW's eps 1e-15 turns last-bit differences of near-zero gradients into full-size updates), so the criterion
+    is on the mean difference over independent seeds (each oracle seed run once, the HIP path once per seed; with
+    fewer than 4 seeds the HIP path runs REPEATS times per seed).  Returns (cfg, runs, {tag: {mod: mean diff}})."""
     fixtures = _fixtures(gold)
     reps = 1 if len(fixtures) >= 4 else REPEATS
-    runs, diffs = [], []
+    runs, diffs = [], {}
     for fx_path in fixtures:
+        f0 = np.load(fx_path)
+        cps = tuple(ast.literal_eval(f0["cfg_json"].tobytes().decode()).get("checkpoints", ()))
         for _ in range(reps):
-            f, cfg, losses, psnr = run_parity(dev, precision, fx_path)
+            hist = []
+            f, cfg, losses, psnr = run_parity(dev, precision, fx_path, history=hist, checkpoints=cps)
             ref, rel, oracle = _report(f"{precision}[{os.path.basename(fx_path)}]", f, cfg, losses, psnr)
             runs.append((f, cfg, losses, psnr, ref, rel))
-            diffs.append({m: psnr[m] - oracle[m] for m in cfg["modalities"]})
+            for step, p in hist:
+                tag = "eval" if step == cfg["steps"] else f"eval{step}"
+                diffs.setdefault(tag, []).append({m: p[m] - float(f[f"{tag}:{m}:psnr"]) for m in cfg["modalities"]})
     cfg = runs[0][1]
     mods = cfg["modalities"]
-    mean = {m: float(np.mean([d[m] for d in diffs])) for m in mods}
-    sd = {m: float(np.std([d[m] for d in diffs], ddof=1)) for m in mods}
-    # tolerance: 0.1 dB, or 2.5 standard errors of the paired mean where one trajectory's scatter is larger than the
-    # seeds available can resolve (polarization: ~0.4 dB per pair)
-    tol = {m: max(PSNR_TOL, 2.5 * sd[m] / np.sqrt(len(diffs))) for m in mods}
-    print(f"{precision}: {len(fixtures)} seeds x {reps}: mean dPSNR {mean}; sd of one pair {sd}; tolerance {tol}; "
-          f"all-modality mean {float(np.mean(list(mean.values()))):+.4f}")
-    return cfg, runs, mean, tol
+    means = {}
+    for tag, ds in sorted(diffs.items()):
+        mean = {m: float(np.mean([d[m] for d in ds])) for m in mods}
+        sd = {m: float(np.std([d[m] for d in ds], ddof=1)) for m in mods}
+        print(f"{precision} {tag}: {len(fixtures)} seeds x {reps}: mean dPSNR " +
+              " ".join(f"{m} {v:+.4f}" for m, v in mean.items()) + " | sd of one pair " +
+              " ".join(f"{m} {v:.4f}" for m, v in sd.items()))
+        means[tag] = mean
+    return cfg, runs, means
 
 
 PSNR_TOL = 0.1
 
 
-def _check_psnr(cfg, mean, tol):
-    for m in cfg["modalities"]:
-        assert abs(mean[m]) <= tol[m], (m, mean[m], tol[m])
-    assert abs(float(np.mean(list(mean.values())))) <= PSNR_TOL
+def _check_psnr(cfg, means):
+    """|mean dPSNR| <= 0.1 dB for every modality at every checkpoint (no widening by the seeds' scatter)."""
+    for tag, mean in means.items():
+        for m in cfg["modalities"]:
+            assert abs(mean[m]) <= PSNR_TOL, (tag, m, mean[m])
 
 
 @pytest.mark.gpu
 def test_train_parity_fp32(dev):
-    cfg, runs, mean, tol = _repeated(dev, "fp32")
+    cfg, runs, means = _repeated(dev, "fp32")
     for _, _, losses, _, ref, rel in runs:
         assert rel[:TRAJ_STEPS].max() < 1e-3
         assert abs(losses.mean() - ref.mean()) / ref.mean() < 2e-2
-    _check_psnr(cfg, mean, tol)
+    _check_psnr(cfg, means)
 
 
 @pytest.mark.gpu
 def test_train_parity_fast_preset(dev):
-    cfg, runs, mean, tol = _repeated(dev, FAST)
+    cfg, runs, means = _repeated(dev, FAST)
     for _, _, losses, _, ref, rel in runs:
         assert abs(losses.mean() - ref.mean()) / ref.mean() < 2e-2
-    _check_psnr(cfg, mean, tol)
+    _check_psnr(cfg, means)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("precision", ["fp32", FAST])
 def test_train_parity_grid_raw_5mod(dev, precision):
-    """BASELINE configs[2] shape (grid_raw, five mosaicked modalities incl. polarization): mean dPSNR over the seeded
-    fixtures within 0.1 dB per modality (or 2.5 standard errors where one pair's scatter exceeds what the seeds
-    resolve) and within 0.1 dB averaged over the modalities, for the parity and the benchmarked preset."""
-    cfg, runs, mean, tol = _repeated(dev, precision, GOLD_RAW5)
+    """BASELINE configs[2] shape (grid_raw, five mosaicked modalities incl. polarization with saturated highlights):
+    mean dPSNR over the 16 seeded fixtures within 0.1 dB per modality at step 25 and at step 50 -- a window in which
+    the held-out PSNR moves by 2-6 dB per modality while one trajectory scatters by <= 0.05 dB (make_train_parity.py) --
+    for the parity and the benchmarked preset."""
+    cfg, runs, means = _repeated(dev, precision, GOLD_RAW5)
     for _, _, losses, _, ref, rel in runs:
         assert rel[:TRAJ_STEPS].max() < (1e-3 if precision == "fp32" else 1e-2)
         assert abs(losses.mean() - ref.mean()) / ref.mean() < 2e-2
-    _check_psnr(cfg, mean, tol)
+    _check_psnr(cfg, means)
