@@ -46,8 +46,11 @@ MFMA_PEAK_TF = {"fp32": F32_MFMA_PEAK_TF, "bf16": BF16_MFMA_PEAK_TF, "bf16x3": B
                 "bf16x2": BF16_MFMA_PEAK_TF / 2}
 PREC_NAMES = {0: "fp32", 1: "bf16", 2: "bf16x3", 3: "bf16x2"}
 DTYPES = {"fp32": "fp32",
-          "fast": "bf16 MFMA (fp32 accumulate; SDF MLP chain, its weight gradients and the polarization heads "
-                  "split-bf16x3), fp32 elsewhere",
+          "fast": "split-bf16x3 MFMA (bf16 hi + lo operands, fp32 accumulate) for every MLP, fp32 elsewhere",
+          "fast_bf16": "bf16 MFMA (fp32 accumulate; SDF MLP and polarization heads split-bf16x3) -- not a parity "
+                       "preset: -0.56 dB converged PSNR, fp32 elsewhere",
+          "fast_m4": "split-bf16x3 forward / bf16 backward for the radiance, head and background MLPs -- not a parity "
+                     "preset, fp32 elsewhere",
           "fast_x2": "bf16 MFMA (fp32 accumulate; SDF MLP chain bf16 weights x split-bf16 activations -- not a parity "
                      "preset: hessians off), fp32 elsewhere",
           "bf16x3": "split-bf16x3 MFMA (fp32-accurate), fp32 elsewhere"}

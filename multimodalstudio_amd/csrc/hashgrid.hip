@@ -21,6 +21,7 @@
 
 namespace {
 
+typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int kMaxLevels = 16;
 constexpr uint32_t kP1 = 2654435761u;
 constexpr uint32_t kP2 = 805459861u;
@@ -129,16 +130,68 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(const float* __restri
   }
 }
 
+// DPP lane moves (gfx9 encodings): quad_perm [1,0,3,2] / [2,3,0,1], row_ror:4 / :8 (rotation inside a 16-lane row),
+// row_bcast:15 / :31 (lane 15 / 31 of a row into the next row(s), masked by ROWS).  Rows not in ROWS read 0.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xf, false));
+}
+
+// sum over the wave's 64 lanes, complete in lane 63: each 16-lane row by rotations and quad swaps (VALU, no LDS
+// permutes), then row 0 + row 1 and row 2 + row 3 by row_bcast:15, the halves by row_bcast:31
+__device__ __forceinline__ float wave_sum_to_63(float v) {
+  v += dpp<0x128>(v);  // row_ror:8
+  v += dpp<0x124>(v);  // row_ror:4
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v += dpp<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+  return v;
+}
+
+// Table-gradient merge buffer of one workgroup: kLines 64-B table lines (8 entries x 2 features) in LDS, open
+// addressing on the line index.  Scattered float atomics cost one memory-side request per 64-B line an
+// instruction touches (~20 G requests/s chip-wide, MI355X_MICROARCH.md §Global float atomics), so the walk adds
+// every corner gradient into LDS and the block flushes each touched line once, its nonzero floats in one
+// 16-lane segment: the centre and taps of a sample share most corners at the fine levels (their cells are
+// neighbours -- shared corners sit in different corner slots of the two points) and consecutive samples of a ray
+// share cells at the coarse ones.  On the hash_bench geometry this is ~3.9 M line requests per SDF batch instead of
+// the per-lane pending merge's 9.3 M.  A line that finds no slot within kMaxProbe probes goes straight to memory.
+constexpr int kLines = 512;
+constexpr int kLogLines = 9;
+constexpr int kMaxProbe = 32;
+constexpr uint32_t kEmpty = 0xffffffffu;
+
+__device__ __forceinline__ void merge_add(uint32_t* keys, float* vals, float* __restrict__ dtable, uint32_t entry,
+                                          int feat, float v) {
+  const uint32_t line = entry >> 3;
+  uint32_t h = (line * 0x9E3779B1u) >> (32 - kLogLines);
+#pragma unroll 1
+  for (int probe = 0; probe < kMaxProbe; ++probe) {
+    // one LDS round trip per probe: the compare-and-swap claims an empty slot or returns its owner
+    const uint32_t k = atomicCAS(&keys[h], kEmpty, line);
+    if (k == kEmpty || k == line) {
+      atomicAdd(&vals[h * 16 + (entry & 7) * 2 + feat], v);
+      return;
+    }
+    h = (h + 1) & (kLines - 1);
+  }
+  atomicAdd(dtable + 2 * (int64_t)entry + feat, v);
+}
+
 // Backward ("walk"): one workgroup = 16 level groups x 16 lanes and owns CH consecutive point groups (rows
 // g0 .. g0+CH-1 and, for G = 5, their tap rows g + j * gstride).  A level group walks the CH * G points in order
 // (centre, then its 4 taps, then the next sample); lane q holds one (corner, feature) slot -- (y, z) corner pair
-// q >> 2, x side (q >> 1) & 1, feature q & 1 -- and keeps ONE pending (table entry, gradient) accumulator,
-// issuing its atomic only when its entry changes.  Consecutive samples of a ray and the 4 taps around a sample
-// share cells at all coarse levels, so most adds merge in registers.  The two x corners of a pair differ only in
-// the low hash bits (the x prime is 1): they usually share a 64-B line and sit in adjacent lanes, so an atomic
-// wave-instruction touches ~16 lines instead of 32 (scattered float atomics cost per 64-B request,
-// MI355X_MICROARCH.md §Global float atomics).  Position gradients are summed over the 16 lanes by shuffles and
-// over levels through LDS, then added to dpos once per point.
+// q >> 2, x side (q >> 1) & 1, feature q & 1 -- and keeps ONE pending (table entry, gradient) accumulator that goes
+// to the LDS merge buffer (merge_add) only when its entry changes; the buffer's lines are added to the table gradient
+// at the end, one 16-lane segment per line.  Measured on the SDF batch (scripts/hash_bench.py): 0.48 ms against
+// 0.53 ms for per-lane global atomics; the merge's LDS round trips (compare-and-swap, then add) now bound the walk --
+// issuing all of a lane's lookups together (unrolled two-pass form) measured slower (0.72 ms).
+// The block first stages its points' normalised positions x_hat = (x + r) / (2 r) (one exact division per
+// coordinate per point instead of one per lane and level) and their output-gradient rows (coalesced 128-B rows
+// instead of 4-B loads replicated over 8 lanes) in LDS.  Position gradients are summed over the wave's 4 levels x
+// 16 lanes by DPP moves (wave_sum_to_63) into a per-wave LDS slot -- plain stores, no LDS atomics -- and the 4 waves'
+// partials are added in wave order at the end: dpos is deterministic.
 template <int G, int CH>
 __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __restrict__ pos, int64_t Mg,
                                                                 int64_t gstride, int64_t ldx,
@@ -146,9 +199,16 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
                                                                 const float* __restrict__ dout, int64_t ldd,
                                                                 float* __restrict__ dtable, float* __restrict__ dpos,
                                                                 int64_t lddx) {
-  __shared__ float sdp[CH * G * 3];
+  constexpr int NP = CH * G;
+  __shared__ float shat[NP][3];
+  __shared__ float sde[NP][2 * kMaxLevels];
+  __shared__ float sdp[4][NP][3];
+  __shared__ uint32_t skeys[kLines];
+  __shared__ f4 svals[kLines * 4];
+  float* vals = reinterpret_cast<float*>(svals);
   const int t = threadIdx.x;
   const int level = t >> 4;
+  const int wave = t >> 6;
   const int q = t & 15;
   const int pr = q >> 2;                // 0: (y c, z c)  1: (y f, z c)  2: (y c, z f)  3: (y f, z f)
   const bool xc = ((q >> 1) & 1) == 0;  // x = ceil corner
@@ -156,95 +216,105 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
   const int feat = q & 1;
   const int64_t g0 = (int64_t)blockIdx.x * CH;
   const int nck = (int)((Mg - g0) < CH ? (Mg - g0) : CH);
-  if (dpos != nullptr) {
-    for (int i = t; i < CH * G * 3; i += 256) sdp[i] = 0.f;
-    __syncthreads();
-  }
-  if (level < p.levels && level < p.active_levels) {
-    const float s = p.scale[level];
-    const uint32_t hmask = (1u << p.log2T) - 1u;
-    const uint32_t base = (uint32_t)level << p.log2T;
+  const int np = nck * G;
+  const int nlv = p.levels < p.active_levels ? p.levels : p.active_levels;  // levels with a gradient
+  const int nc = 2 * p.levels;
+  // point i of the block: sample k = i / G, tap j = i % G (walk order)
+  auto row_of = [&](int i) {
+    const int k = i / G, j = i - k * G;
+    return g0 + k + (int64_t)j * gstride;
+  };
+  {
     const float two_r = 2.0f * p.radius;
     const bool norm = p.radius > 0.f;
+    if ((t & 3) < 3)
+      for (int pi = t >> 2; pi < np; pi += 64) {
+        const float x = pos[row_of(pi) * ldx + (t & 3)];
+        shat[pi][t & 3] = norm ? (x + p.radius) / two_r : x;  // make_corners' rounding (bit-exact corners)
+      }
+    if ((t & 31) < nc)
+      for (int pi = t >> 5; pi < np; pi += 8) sde[pi][t & 31] = dout[row_of(pi) * ldd + (t & 31)];
+    if (dpos != nullptr)
+      for (int i = t; i < 4 * NP * 3; i += 256) (&sdp[0][0][0])[i] = 0.f;
+    if (dtable != nullptr) {
+      for (int i = t; i < kLines; i += 256) skeys[i] = kEmpty;
+      for (int i = t; i < 4 * kLines; i += 256) svals[i] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __syncthreads();
+  // a wave runs if any of its 4 levels has a gradient (its inactive rows contribute zeros and read no table entry)
+  if (4 * wave < nlv) {
+    const bool live = level < nlv;
+    const float s = p.scale[level];
+    const uint32_t hmask = (1u << p.log2T) - 1u;
+    const uint32_t base = live ? (uint32_t)level << p.log2T : 0u;
+    const bool sm = p.smooth != 0;
     uint32_t pidx = 0u;
     float pacc = 0.f;
-    for (int k = 0; k < nck; ++k) {
-      // the G points' inputs first: independent loads in flight together
-      float px[G], py[G], pz[G], pe[G];
-#pragma unroll
-      for (int j = 0; j < G; ++j) {
-        const int64_t pt = g0 + k + (int64_t)j * gstride;
-        const float* xp = pos + pt * ldx;
-        px[j] = xp[0];
-        py[j] = xp[1];
-        pz[j] = xp[2];
-        pe[j] = dout[pt * ldd + 2 * level + feat];
-      }
-#pragma unroll
-      for (int j = 0; j < G; ++j) {
-        // same rounded values as make_corners (bit-exact corners)
-        const float sx = (norm ? (px[j] + p.radius) / two_r : px[j]) * s;
-        const float sy = (norm ? (py[j] + p.radius) / two_r : py[j]) * s;
-        const float sz = (norm ? (pz[j] + p.radius) / two_r : pz[j]) * s;
-        const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
-        const float tx = sx - fx, ty = sy - fy, tz = sz - fz;
-        const bool sm = p.smooth != 0;
-        const float ox = sm ? smoothstep(tx) : tx, oy = sm ? smoothstep(ty) : ty, oz = sm ? smoothstep(tz) : tz;
-        const int cx = xc ? (int)ceilf(sx) : (int)fx;
-        const int cy = yc ? (int)ceilf(sy) : (int)fy;
-        const int cz = zc ? (int)ceilf(sz) : (int)fz;
-        const uint32_t idx = base + hash3(cx, cy, cz, hmask);
-        const float wx = xc ? ox : 1.0f - ox, wy = yc ? oy : 1.0f - oy, wz = zc ? oz : 1.0f - oz;
-        const float dE = pe[j];
-        if (dtable != nullptr) {
-          // autograd order of encodings.py:292-302 reversed: ((dE * w_z) * w_y) * w_x
-          const float df = ((dE * wz) * wy) * wx;
-          if (idx == pidx) {
-            pacc += df;
-          } else {
-            if (pacc != 0.f) atomicAdd(dtable + 2 * (int64_t)pidx + feat, pacc);
-            pidx = idx;
-            pacc = df;
-          }
+    for (int i = 0; i < np; ++i) {
+      const float sx = shat[i][0] * s, sy = shat[i][1] * s, sz = shat[i][2] * s;
+      const float dE = live ? sde[i][2 * level + feat] : 0.f;
+      const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+      const float tx = sx - fx, ty = sy - fy, tz = sz - fz;
+      const float ox = sm ? smoothstep(tx) : tx, oy = sm ? smoothstep(ty) : ty, oz = sm ? smoothstep(tz) : tz;
+      const int cx = xc ? (int)ceilf(sx) : (int)fx;
+      const int cy = yc ? (int)ceilf(sy) : (int)fy;
+      const int cz = zc ? (int)ceilf(sz) : (int)fz;
+      const uint32_t idx = base + (live ? hash3(cx, cy, cz, hmask) : 0u);
+      const float wx = xc ? ox : 1.0f - ox, wy = yc ? oy : 1.0f - oy, wz = zc ? oz : 1.0f - oz;
+      // the position gradient's table value: issued before the merge work below, used after it
+      const float tv = (dpos != nullptr && live) ? table[2 * (int64_t)idx + feat] : 0.f;
+      if (dtable != nullptr) {
+        // autograd order of encodings.py:292-302 reversed: ((dE * w_z) * w_y) * w_x
+        const float df = ((dE * wz) * wy) * wx;
+        if (idx == pidx) {
+          pacc += df;
+        } else {
+          if (pacc != 0.f) merge_add(skeys, vals, dtable, pidx, feat, pacc);
+          pidx = idx;
+          pacc = df;
         }
-        if (dpos != nullptr) {
-          const float e = dE * table[2 * (int64_t)idx + feat];
-          float gx = (xc ? e : -e) * (wz * wy);
-          float gy = (yc ? e : -e) * (wz * wx);
-          float gz = (zc ? e : -e) * (wy * wx);
-          if (sm) {  // d weight / d frac = +-S'(frac)
-            gx *= smoothstep_grad(tx);
-            gy *= smoothstep_grad(ty);
-            gz *= smoothstep_grad(tz);
-          }
-#pragma unroll
-          for (int off = 8; off >= 1; off >>= 1) {
-            gx += __shfl_xor(gx, off, 16);
-            gy += __shfl_xor(gy, off, 16);
-            gz += __shfl_xor(gz, off, 16);
-          }
-          if (q == 0) {
-            float* d = sdp + (k * G + j) * 3;
-            atomicAdd(d, gx * s);
-            atomicAdd(d + 1, gy * s);
-            atomicAdd(d + 2, gz * s);
-          }
+      }
+      if (dpos != nullptr) {
+        const float e = dE * tv;
+        float gx = (xc ? e : -e) * (wz * wy);
+        float gy = (yc ? e : -e) * (wz * wx);
+        float gz = (zc ? e : -e) * (wy * wx);
+        if (sm) {  // d weight / d frac = +-S'(frac)
+          gx *= smoothstep_grad(tx);
+          gy *= smoothstep_grad(ty);
+          gz *= smoothstep_grad(tz);
+        }
+        // d x_hat * s per level; the wave's 4 levels summed in lane 63
+        gx = wave_sum_to_63(gx * s);
+        gy = wave_sum_to_63(gy * s);
+        gz = wave_sum_to_63(gz * s);
+        if ((t & 63) == 63) {
+          sdp[wave][i][0] = gx;
+          sdp[wave][i][1] = gy;
+          sdp[wave][i][2] = gz;
         }
       }
     }
-    if (dtable != nullptr && pacc != 0.f) atomicAdd(dtable + 2 * (int64_t)pidx + feat, pacc);
+    if (dtable != nullptr && pacc != 0.f) merge_add(skeys, vals, dtable, pidx, feat, pacc);
+  }
+  __syncthreads();
+  if (dtable != nullptr) {
+    // flush: 4 lines per wave-instruction, lane (t & 15) = float (entry (t & 15) / 2, feature t & 1) of the line
+    for (int sl = t >> 4; sl < kLines; sl += 16) {
+      const uint32_t k = skeys[sl];
+      const float v = vals[sl * 16 + (t & 15)];
+      if (k != kEmpty && v != 0.f) atomicAdd(dtable + (int64_t)k * 16 + (t & 15), v);
+    }
   }
   if (dpos != nullptr) {
-    __syncthreads();
     const float two_r = p.radius > 0.f ? 2.0f * p.radius : 1.0f;
-    for (int i = t; i < nck * G; i += 256) {
-      const int k = i / G, j = i - k * G;
-      const int64_t pt = g0 + k + (int64_t)j * gstride;
-      float* dp = dpos + pt * lddx;
-      dp[0] += sdp[3 * i] / two_r;
-      dp[1] += sdp[3 * i + 1] / two_r;
-      dp[2] += sdp[3 * i + 2] / two_r;
-    }
+    if ((t & 3) < 3)
+      for (int pi = t >> 2; pi < np; pi += 64) {
+        const int c = t & 3;
+        const float v = ((sdp[0][pi][c] + sdp[1][pi][c]) + sdp[2][pi][c]) + sdp[3][pi][c];
+        dpos[row_of(pi) * lddx + c] += v / two_r;
+      }
   }
 }
 
@@ -325,12 +395,13 @@ MMS_EXPORT int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group,
   if (rc) return rc;
   if (Mg == 0 || (dtable == nullptr && dpos == nullptr)) return 0;
   MMS_REQUIRE(pos && table && dout, fn, "null pointer");
+  // CH: about 260 touched lines per block on the SDF batch (kLines = 512 merge slots: 4 blocks per CU)
   if (group == 5) {
-    constexpr int CH = 16;
+    constexpr int CH = 4;
     hipLaunchKernelGGL((hashgrid_bwd_walk_kernel<5, CH>), dim3(mms::grid_for(Mg, CH, INT32_MAX)), dim3(256), 0,
                        mms::as_stream(stream), pos, Mg, gstride, ldx, table, p, dout, ldd, dtable, dpos, lddx);
   } else {
-    constexpr int CH = 32;
+    constexpr int CH = 8;
     hipLaunchKernelGGL((hashgrid_bwd_walk_kernel<1, CH>), dim3(mms::grid_for(Mg, CH, INT32_MAX)), dim3(256), 0,
                        mms::as_stream(stream), pos, Mg, Mg, ldx, table, p, dout, ldd, dtable, dpos, lddx);
   }

@@ -745,8 +745,8 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
       launch_chain<PREC, 17, 8, 8, 3, true, 2, 2, 0, 0>(a, s);
       return true;
     }
-    if constexpr (PREC == 1) {
-      // the plain modality heads 256-64-64-C (ReLU, ReLU, Sigmoid; field_heads.py:71-88), C <= 32, bf16
+    if constexpr (PREC == 1 || PREC == 2) {
+      // the plain modality heads 256-64-64-C (ReLU, ReLU, Sigmoid; field_heads.py:71-88), C <= 32, bf16 or split-bf16x3
       if (!bwd && ks0 == 16 && nt[0] == 2 && nt[1] == 2 && nt[2] == 1 && a0 == 1 && a1 == 1 && a2 == 3 && hidden64 &&
           keep) {
         launch_chain<PREC, 16, 2, 2, 1, false, 1, 1, 3, 0, true>(a, s);
@@ -760,8 +760,8 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
     }
     return false;
   }
-  // 4-layer chains: the background MLPs, bf16 operands only (the background's precision in every preset but bf16x3)
-  if constexpr (PREC == 1) {
+  // 4-layer chains: the background MLPs, bf16 or split-bf16x3
+  if constexpr (PREC == 1 || PREC == 2) {
     if (nl != 4 || nt[0] != 8 || nt[1] != 8 || nt[2] != 8 || a0 != 1 || a1 != 1 || a2 != 1) return false;
     if (!bwd && hidden_full && keep && a3 == 1) {
       // base 39-256x4 (NeRF background), head 283-256-256-256-128 (NeRF) / -256 (config-5 grid background)

@@ -34,29 +34,42 @@ ACT = {None: 0, "None": 0, "ReLU": 1, "Softplus": 2, "Sigmoid": 3}
 # GEMM operand precision per MLP family: 0 exact fp32 MFMA (parity mode), 1 bf16, 2 split bf16x3.
 PRESETS = {
     "fp32": {"sdf": 0, "radiance": 0, "heads": 0, "pol_head": 0, "background": 0, "mlp": 0},
-    # throughput mode: the SDF MLP keeps ~fp32 operand precision (its 4-tap finite differences divide
-    # sdf differences by 4 delta ~ 4.5e-3), everything else runs bf16 MFMA with fp32 accumulation; the analytic-
-    # gradient MLP fields (mlp methods, differentiated twice) stay on the exact fp32 MFMA
-    # (the polarization heads keep split-bf16x3 too: their Stokes outputs are combined into intensities by
-    # differences, and their PSNR after training moved by ~0.2 dB in bf16, tests/test_gpu_train_parity.py)
-    # "sdf_chain": the SDF chain kernel's operand mode (0: the "sdf" GEMM precision).  The benchmarked preset keeps the
-    # chain on split-bf16x3: the curvature loss sees hessians = second differences of the SDF over delta^2 ~ 1.3e-6,
-    # and with bf16-ROUNDED weights (mode 3, "fast_x2") they are the hessians of a different, rippled function --
-    # 56x the reference's hessian scale off on the e2e fixtures and a 24x larger curvature loss over the rgb training
-    # trajectory, although radiance and PSNR are unchanged (tests/test_gpu_e2e.py::test_e2e_fast_preset_deviation)
-    "fast": {"sdf": 2, "radiance": 1, "heads": 1, "pol_head": 2, "background": 1, "mlp": 0},
+    # throughput mode: every MLP of the grid methods on split-bf16x3 MFMA (x = hi + lo on both operands, ~17
+    # significant bits, fp32 accumulation), the analytic-gradient MLP fields (mlp methods, differentiated twice) on
+    # the exact fp32 MFMA.  The SDF needs the extra mantissa for its 4-tap finite differences (sdf differences over
+    # 4 delta ~ 4.5e-3, hessians over delta^2 ~ 1.3e-6); the radiance, head and background MLPs need it for converged
+    # quality: with their operands in plain bf16 the held-out PSNR of grid_raw5 after 3000 steps from scratch was
+    # 0.56 dB below fp32 (paired over 3 seeds), 0.27 dB with bf16 only in their backward (mode 4), and -0.12 +- 0.16 dB
+    # with split-bf16x3 throughout (profiles/round3_converged_psnr.json)
+    "fast": {"sdf": 2, "radiance": 2, "heads": 2, "pol_head": 2, "background": 2, "mlp": 0},
+    # NOT parity presets, kept to price the precision: "fast_bf16" = round 2's fast (bf16 radiance / heads /
+    # background), "fast_m4" = their forward split-bf16x3 and backward bf16 (PRECISION value 4)
+    "fast_bf16": {"sdf": 2, "radiance": 1, "heads": 1, "pol_head": 2, "background": 1, "mlp": 0},
+    "fast_m4": {"sdf": 2, "radiance": 4, "heads": 4, "pol_head": 2, "background": 4, "mlp": 0},
     "bf16x3": {"sdf": 2, "radiance": 2, "heads": 2, "pol_head": 2, "background": 2, "mlp": 2},
 }
 for _p in PRESETS.values():
     _p.setdefault("sdf_chain", 0)      # 0: the chain runs on the "sdf" GEMM precision
 # NOT a parity preset: the SDF chain on bf16 weights x split activations (mms_mlp_chain prec 3, two MFMAs per product;
-# its geometry fails the hessian bound above), kept to measure what the curvature parity costs
-PRESETS["fast_x2"] = dict(PRESETS["fast"], sdf_chain=3)
+# with bf16-ROUNDED weights the SDF is a different, rippled function: 56x the reference's hessian scale off on the
+# e2e fixtures and a 24x larger curvature loss over the rgb training trajectory), kept to measure what the curvature
+# parity costs
+PRESETS["fast_x2"] = dict(PRESETS["fast_bf16"], sdf_chain=3)
 PRECISION = dict(PRESETS["fp32"])
 
 
+def fwd_prec(p: int) -> int:
+    """GEMM / chain operand mode of a family's forward: PRECISION value 4 = split-bf16x3 forward, bf16 backward."""
+    return 2 if p == 4 else p
+
+
+def bwd_prec(p: int) -> int:
+    """... and of its backward (data and weight gradients)."""
+    return 1 if p == 4 else p
+
+
 def set_precision(mode: str) -> None:
-    """Select the MLP GEMM precision preset ('fp32' parity | 'fast' | 'bf16x3' | 'fast_x2')."""
+    """Select the MLP GEMM precision preset ('fp32' parity | 'fast' | 'bf16x3' | 'fast_bf16' | 'fast_m4' | 'fast_x2')."""
     PRECISION.update(PRESETS[mode])
 
 
@@ -333,6 +346,7 @@ class MLPRun:
 
     def __init__(self, params: Sequence[torch.Tensor], acts: Sequence[Tuple[int, float, float]], prec: int = 0):
         self.prec = int(prec)
+        self.fprec, self.bprec = fwd_prec(self.prec), bwd_prec(self.prec)   # forward / backward GEMM modes
         self.params = list(params)
         self.acts = list(acts)
         self.L = len(self.params) // 3
@@ -361,7 +375,7 @@ class MLPRun:
             # the backward takes ReLU' / Sigmoid' from the output: only Softplus keeps its pre-activation
             Z = _alloc(M, N, dev) if (keep and act == 2) else None
             gemm(NT, M, N, K, h, h.stride(0), W, W.stride(0), Y, Y.stride(0), bias=b, Z=Z,
-                 ldz=0 if Z is None else Z.stride(0), act=act, beta=beta, thr=thr, prec=self.prec)
+                 ldz=0 if Z is None else Z.stride(0), act=act, beta=beta, thr=thr, prec=self.fprec)
             if keep:
                 self.Ws.append(W)
                 self.norms.append(nrm)
@@ -405,7 +419,7 @@ class MLPRun:
                 db = bt if bt is not None else torch.zeros(N, device=dev)
                 tiles = ((N + 127) // 128) * ((K + 127) // 128)
                 gemm(TN, N, K, M, dZ, dZ.stride(0), Xin, Xin.stride(0), dW, K, accumulate=True,
-                     splits=_splits_for(M, tiles, self.prec), prec=self.prec, colsum=db)
+                     splits=_splits_for(M, tiles, self.bprec), prec=self.bprec, colsum=db)
                 dg = gt.reshape(-1) if gt is not None else torch.zeros(N, device=dev)
                 dv = vt if vt is not None else torch.zeros(N, K, device=dev)
                 _wn_bwd(g.reshape(-1), v, self.norms[l], dW, dg, dv)
@@ -415,12 +429,12 @@ class MLPRun:
                 zaux, did = self._grad_src(l - 1) if pa != 0 else (None, 0)
                 gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[l], self.Ws[l].stride(0), dprev, dprev.stride(0),
                      aux=zaux, ldaux=0 if zaux is None else zaux.stride(0), dact=did, beta=pbeta, thr=pthr,
-                     prec=self.prec)
+                     prec=self.bprec)
                 dZ = dprev
             elif need_dx:
                 dx = dx_out if dx_out is not None else _alloc(M, K, dev)
                 gemm(NN, M, K, N, dZ, dZ.stride(0), self.Ws[0], self.Ws[0].stride(0), dx, dx.stride(0),
-                     prec=self.prec)
+                     prec=self.bprec)
         return dx, grads
 
 
@@ -434,25 +448,29 @@ class ChainRun:
 
     def __init__(self, params: Sequence[torch.Tensor], acts: Sequence[Tuple[int, float, float]], prec: int,
                  chain_prec: int = 0):
-        if prec not in (1, 2):
-            raise ValueError("the fused chain runs the bf16 (1) and split-bf16x3 (2) modes")
-        self.params, self.acts, self.prec = list(params), list(acts), int(prec)
-        # the chain kernel's operand mode (prec, or 3: split activations x bf16 weights); weight gradients use prec
-        self.cprec = int(chain_prec) or self.prec
+        if prec not in (1, 2, 4):
+            raise ValueError("the fused chain runs the bf16 (1), split-bf16x3 (2) and x3-forward (4) modes")
+        self.params, self.acts = list(params), list(acts)
+        # the forward chain's operand mode (or chain_prec 3: split activations x bf16 weights); the backward chain and
+        # the weight gradients run bwd_prec (mode 4: split-bf16x3 forward, bf16 backward)
+        self.prec = bwd_prec(int(prec))
+        self.cprec = int(chain_prec) or fwd_prec(int(prec))
+        self.bcprec = self.prec if int(prec) == 4 else self.cprec
         self.L = len(self.params) // 3
         if self.L not in (3, 4):
             raise ValueError("chains of 3 or 4 layers")
         self.beta, self.thr = float(acts[0][1]), float(acts[0][2])
 
-    def _pack(self, W, rows: int, cols: int, transpose: bool, permute: bool):
+    def _pack(self, W, rows: int, cols: int, transpose: bool, permute: bool, prec: Optional[int] = None):
+        prec = self.cprec if prec is None else prec
         prep = _ACTIVE_PREP[0]
         if prep is not None:
-            return prep.packed(W, rows, cols, transpose, permute, self.cprec)
-        return self._pack_new(W, rows, cols, transpose, permute)
+            return prep.packed(W, rows, cols, transpose, permute, prec)
+        return self._pack_new(W, rows, cols, transpose, permute, prec)
 
-    def _pack_new(self, W, rows: int, cols: int, transpose: bool, permute: bool):
+    def _pack_new(self, W, rows: int, cols: int, transpose: bool, permute: bool, prec: int):
         hi = torch.empty(rows, cols, dtype=torch.bfloat16, device=W.device)
-        lo = torch.empty_like(hi) if self.cprec == 2 else None
+        lo = torch.empty_like(hi) if prec == 2 else None
         N, K = W.shape
         _lib.call("mms_mlp_pack", W.data_ptr(), N, K, W.stride(0), int(transpose), int(permute), rows, cols,
                   hi.data_ptr(), _p(lo), _s())
@@ -460,6 +478,7 @@ class ChainRun:
 
     def _chain(self, backward: bool, X, K0: int, rows_full: int, packs, bias, aux, outs, Ns, acts,
                xaux=None, xact: int = 0, xout=None, w2row0=None):
+        prec = self.bcprec if backward else self.cprec
         n = self.L
         VP = ctypes.c_void_p * n
         his = VP(*[p[0].data_ptr() for p in packs])
@@ -472,7 +491,7 @@ class ChainRun:
         ns = (ctypes.c_int * n)(*Ns)
         ac = (ctypes.c_int * n)(*acts)
         cast = lambda a: ctypes.cast(a, ctypes.c_void_p)
-        _lib.call("mms_mlp_chain", self.cprec, int(backward), n, X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
+        _lib.call("mms_mlp_chain", prec, int(backward), n, X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
                   _p(xaux), 0 if xaux is None else xaux.stride(0), int(xact), _p(xout),
                   0 if xout is None else xout.stride(0), cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux),
                   cast(os_), cast(ldo), cast(ns), cast(ac), self.beta, self.thr, _p(w2row0), _s())
@@ -518,8 +537,9 @@ class ChainRun:
         L = self.L
         Ns = [W.shape[0] for W in self.Ws]
         up = lambda n, k: k * ((n + k - 1) // k)
-        return [self._pack(self.Ws[L - 1], up(Ns[L - 2], 32), up(Ns[L - 1], 16), True, False)] + \
-               [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 32), up(Ns[l], 32), True, True)
+        p = self.bcprec
+        return [self._pack(self.Ws[L - 1], up(Ns[L - 2], 32), up(Ns[L - 1], 16), True, False, p)] + \
+               [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 32), up(Ns[l], 32), True, True, p)
                 for l in range(L - 2, -1, -1)]
 
     def backward(self, dy: torch.Tensor, dx_out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -911,16 +931,16 @@ def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> to
 
 def _chain_shape(params, acts, prec: int = 2) -> bool:
     """True when the fused chain kernel serves this MLP (mms_mlp_chain's dispatch table): the SDF (71-256-256-257,
-    Softplus, Softplus, none) and radiance (317-256-256-256, ReLU x 3) chains, and in bf16 (prec 1) the background
-    NeRF's 4-layer ReLU MLPs (base 39-256-256-256-256, head 283-256-256-256-128 / -256)."""
+    Softplus, Softplus, none) and radiance (317-256-256-256, ReLU x 3) chains, the background NeRF's 4-layer ReLU
+    MLPs (base 39-256-256-256-256, head 283-256-256-256-128 / -256) and the plain heads 256-64-64-C."""
     dims = [params[1].shape[1]] + [params[3 * l + 1].shape[0] for l in range(len(params) // 3)]
     a = tuple(x[0] for x in acts)
     if len(params) == 9:
         if (dims == [71, 256, 256, 257] and a == (2, 2, 0)) or (dims == [317, 256, 256, 256] and a == (1, 1, 1)):
             return True
-        # the plain modality heads 256-64-64-C, C <= 32 (bf16)
-        return prec == 1 and dims[:3] == [256, 64, 64] and dims[3] <= 32 and a == (1, 1, 3)
-    if len(params) == 12 and prec == 1 and a == (1, 1, 1, 1):
+        # the plain modality heads 256-64-64-C, C <= 32
+        return prec in (1, 2, 4) and dims[:3] == [256, 64, 64] and dims[3] <= 32 and a == (1, 1, 3)
+    if len(params) == 12 and prec in (1, 2, 4) and a == (1, 1, 1, 1):
         return dims in ([39, 256, 256, 256, 256], [283, 256, 256, 256, 128], [283, 256, 256, 256, 256])
     return False
 
@@ -1237,7 +1257,7 @@ def _mlp_strided(run: MLPRun, H: torch.Tensor, Fb: int) -> torch.Tensor:
     Y = torch.empty(M, N, device=dev)
     Z = _alloc(M, N, dev)
     gemm(NT, M, N, K, H, H.stride(0), W, W.stride(0), Y, Y.stride(0), bias=b, Z=Z, ldz=Z.stride(0), act=act,
-         beta=beta, thr=thr, prec=run.prec)
+         beta=beta, thr=thr, prec=run.fprec)
     run.Ws, run.norms, run.Zs, run.Ys = [W], [nrm], [Z], [Y]
     return Y
 
@@ -1255,17 +1275,17 @@ def _mlp_strided_bwd(run: MLPRun, dy: torch.Tensor, H: torch.Tensor, Fb: int, dx
     if gt is not None or vt is not None or bt is not None:
         dW = _dw_views([v], dev)[0]
         db = bt if bt is not None else torch.zeros(N, device=dev)
-        gemm(TN, N, K, M, dZ, dZ.stride(0), H, H.stride(0), dW, K, accumulate=True, splits=_splits_for(M, 1, run.prec),
-             prec=run.prec, colsum=db)
+        gemm(TN, N, K, M, dZ, dZ.stride(0), H, H.stride(0), dW, K, accumulate=True,
+             splits=_splits_for(M, 1, run.bprec), prec=run.bprec, colsum=db)
         dg = gt.reshape(-1) if gt is not None else torch.zeros(N, device=dev)
         dv = vt if vt is not None else torch.zeros(N, K, device=dev)
         _wn_bwd(g.reshape(-1), v, run.norms[0], dW, dg, dv)
     if dx_into is not None:
         gemm(NN, M, K, N, dZ, dZ.stride(0), run.Ws[0], run.Ws[0].stride(0), dx_into, dx_into.stride(0),
-             accumulate=True, prec=run.prec)
+             accumulate=True, prec=run.bprec)
         return dx_into, [None, None, None]
     dxin = _alloc(M, K, dev)
-    gemm(NN, M, K, N, dZ, dZ.stride(0), run.Ws[0], run.Ws[0].stride(0), dxin, dxin.stride(0), prec=run.prec)
+    gemm(NN, M, K, N, dZ, dZ.stride(0), run.Ws[0], run.Ws[0].stride(0), dxin, dxin.stride(0), prec=run.bprec)
     return dxin, [None, None, None]
 
 

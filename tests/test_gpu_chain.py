@@ -229,13 +229,15 @@ def _masked_ref_n(x, params, acts, Y, dy):
     return d, out
 
 
+@pytest.mark.parametrize("prec", [1, 4])
 @pytest.mark.parametrize("dims", [[39, 256, 256, 256, 256], [283, 256, 256, 256, 128], [283, 256, 256, 256, 256],
                                   [317, 256, 256, 256]])
-def test_chain_relu_layers(dev, dims):
-    """ReLU chains in bf16 -- the background NeRF's 4-layer MLPs and the radiance MLP -- at a row count that is not a
-    multiple of the 128-row block (the clamped rows past M must store exactly row M - 1's values): forward vs an fp64
-    restatement, backward (dx and every weight-norm / bias gradient, i.e. every stored dZ) vs the fp64 backward at
-    the kernel's own activations; the last layer writes into a caller-owned strided view (the background panel)."""
+def test_chain_relu_layers(dev, dims, prec):
+    """ReLU chains in bf16 (prec 1) and in mode 4 (split-bf16x3 forward, bf16 backward) -- the background NeRF's
+    4-layer MLPs and the radiance MLP -- at a row count that is not a multiple of the 128-row block (the clamped rows
+    past M must store exactly row M - 1's values): forward vs an fp64 restatement, backward (dx and every weight-norm /
+    bias gradient, i.e. every stored dZ) vs the fp64 backward at the kernel's own activations; the last layer writes
+    into a caller-owned strided view (the background panel)."""
     from multimodalstudio_amd import functions as fx
     g = torch.Generator().manual_seed(sum(dims))
     M = 1500
@@ -250,14 +252,15 @@ def test_chain_relu_layers(dev, dims):
     x = torch.randn(M, dims[0], generator=g)
     X = _panel(x, dev)
     panel = fx._alloc(M, dims[L] + 27, dev)
-    run = fx.ChainRun(params, acts, 1)
+    assert fx._chain_shape(params, acts, prec)
+    run = fx.ChainRun(params, acts, prec)
     y = run.forward(X, keep=True, last_out=panel[:, :dims[L]])
     assert y.data_ptr() == panel.data_ptr()
     h = x.double()
     for l in range(L):
         gg, v, b = [p.detach().double().cpu() for p in params[3 * l: 3 * l + 3]]
         h = torch.relu(h @ torch._weight_norm(v, gg, 0).T + b)
-    assert rel(y.detach().cpu(), h) < TOL[1]
+    assert rel(y.detach().cpu(), h) < (TOL[2] if prec == 4 else TOL[1])
     Y = [t.detach().clone() for t in run.Y]
     dy = torch.randn(M, dims[L], generator=g)
     dx = run.backward(_panel(dy, dev))
@@ -268,8 +271,9 @@ def test_chain_relu_layers(dev, dims):
         assert rel(p.grad.cpu(), ref_g[i]) < TOL[1], (i, rel(p.grad.cpu(), ref_g[i]))
 
 
+@pytest.mark.parametrize("prec", [1, 4])
 @pytest.mark.parametrize("C", [3, 1, 5])
-def test_chain_head(dev, C):
+def test_chain_head(dev, C, prec):
     """A modality head 256-64-64-C (ReLU, ReLU, Sigmoid; field_heads.py:71-88) on the bf16 chain kernel: forward vs
     fp64, backward (dx, every parameter gradient) vs the fp64 backward at the kernel's own activations (Sigmoid' from
     the output), at a row count that is not a multiple of the 128-row block."""
@@ -284,16 +288,16 @@ def test_chain_head(dev, C):
         params += [v.norm(dim=1, keepdim=True).clone(), v, torch.randn(n, generator=g) * 0.1]
     params = [p.to(dev).requires_grad_(True) for p in params]
     acts = [(1, 1.0, 20.0), (1, 1.0, 20.0), (3, 1.0, 20.0)]
-    assert fx._chain_shape(params, acts, 1)
+    assert fx._chain_shape(params, acts, prec)
     x = torch.randn(M, 256, generator=g)
-    run = fx.ChainRun(params, acts, 1)
+    run = fx.ChainRun(params, acts, prec)
     y = run.forward(_panel(x, dev), keep=True)
     h = x.double()
     for l in range(3):
         gg, v, b = [p.detach().double().cpu() for p in params[3 * l: 3 * l + 3]]
         h = h @ torch._weight_norm(v, gg, 0).T + b
         h = torch.relu(h) if l < 2 else torch.sigmoid(h)
-    assert rel(y.detach().cpu(), h) < TOL[1]
+    assert rel(y.detach().cpu(), h) < (TOL[2] if prec == 4 else TOL[1])
     Y = [t.detach().clone().double().cpu() for t in run.Y]
     dy = torch.randn(M, C, generator=g)
     dx = run.backward(_panel(dy, dev))
