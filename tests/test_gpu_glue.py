@@ -114,7 +114,7 @@ def test_weight_prep_batched_matches_single(dev):
         for key, (W, hi, lo, idx) in prep.pack.items():
             _, _, rows, cols, tr, pm, prec = key
             run = fx.ChainRun([torch.zeros(1)] * 9, [(1, 1.0, 20.0)] * 3, 2 if prec == 3 else prec, chain_prec=prec)
-            h1, l1 = run._pack_new(W, rows, cols, tr, pm)
+            h1, l1 = run._pack_new(W, rows, cols, tr, pm, prec)
             assert torch.equal(hi, h1) and (lo is None or torch.equal(lo, l1))
     finally:
         fx.set_precision("fp32")
