@@ -105,6 +105,8 @@ def chain_work(a):
     width = n[nl - 1] if bwd else K0
     if nl == 4:
         role = "bg_base" if width < 64 else "bg_head"
+    elif n[0] == 64:
+        role = "head"                      # the modality heads 256-64-64-C (bwd: 64-64-256 from C)
     else:
         role = ("sdf" if width < 128 else "radiance") + ("_infer" if (not bwd and rf == 0) else "")
     return f"{PREC_NAMES[prec]}:{role}{'_bwd' if bwd else '_fwd'}", (flops, nbytes)
@@ -123,6 +125,7 @@ def work_fns():
     return {
         "mms_gemm": gemm_work,
         "mms_gemm_tn_grouped": gemm_grouped_work,
+        "mms_gemm_tn_wide": gemm_grouped_work,
         "mms_mlp_chain": chain_work,
         "mms_hashgrid_fwd_grouped": hash_fwd_work,
         "mms_hashgrid_bwd_grouped": lambda a: ("sdf_taps" if a[2] == 5 else "radiance_or_bg",
@@ -140,7 +143,7 @@ def kernel_records(summ, timing_steps: int, precision: str):
         launches_per_step = n / timing_steps
         rec = {"kernel": name, "avg_ms": round(ms, 5), "launches_per_step": launches_per_step,
                "ms_per_step": round(ms * launches_per_step, 4), "traffic": None}
-        if name.startswith("mms_gemm") or name.startswith("mms_mlp_chain"):   # (incl. mms_gemm_tn_grouped)
+        if name.startswith("mms_gemm") or name.startswith("mms_mlp_chain"):   # (incl. the grouped weight gradients)
             flops, nbytes = work
             mode = name.split(":")[1]      # "mms_gemm:<precision>:<NT|NN|TN>", "mms_mlp_chain:<precision>:<role>"
             peak = F32_MFMA_PEAK_TF if mode == "fp32" else BF16_MFMA_PEAK_TF

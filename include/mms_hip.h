@@ -53,6 +53,13 @@ int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group, int64_t gs
                              const float* table, int L, int log2T, int F, int interp, const float* scales,
                              float radius, int active_levels, const float* dout, int64_t ldd, float* dtable,
                              float* dpos, int64_t lddx, void* stream);
+/* The position gradient alone (dpos[:, 0:3] +=), as a forward-style gather (thread per (point, level)): with
+ * mms_hashgrid_bwd_grouped(dtable, dpos = NULL) the same two gradients in two launches, the table walk then free of
+ * table loads.  Same arguments and grouping as mms_hashgrid_bwd_grouped. */
+int mms_hashgrid_dpos_grouped(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx,
+                              const float* table, int L, int log2T, int F, int interp, const float* scales,
+                              float radius, int active_levels, const float* dout, int64_t ldd, float* dpos,
+                              int64_t lddx, void* stream);
 
 /* ---- MLP GEMM engine (field_components/mlp.py:152-171): C = epilogue(op(A) op(B)^T).
  * trans_a = 0: A is [M, K] (lda); 1: A is stored [K, M].  trans_b = 0: B is [N, K]; 1: B is stored [K, N].
@@ -74,6 +81,13 @@ int mms_gemm_tn_grouped(int prec, int n, const int64_t* M, const int64_t* N, con
                         const float* const* A, const int64_t* lda, const float* const* B, const int64_t* ldb,
                         float* const* C, const int64_t* ldc, float* const* colsum, int target_blocks, void* stream);
 
+/* The same weight gradients with 256 x 256 output tiles (blocks of 8 waves, every operand row read once per K slice),
+ * bf16 (prec 1) or split bf16x3 (prec 2) operands, 16-B aligned operand rows; stage_rows = 16 or 32 rows per LDS
+ * stage (72 / 144 KB of LDS for split bf16x3).  Same reference interface as mms_gemm_tn_grouped. */
+int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const int64_t* K, const float* const* A,
+                     const int64_t* lda, const float* const* B, const int64_t* ldb, float* const* C,
+                     const int64_t* ldc, float* const* colsum, int target_blocks, int stage_rows, void* stream);
+
 /* ---- fused MLP chains (MLP.forward mlp.py:152-171 under weight norm :206-209, all layers in one launch) for the
  * SDF field (71-256-256-257, Softplus(100), surface_field.py:99-116), the radiance field (317-256-256-256, ReLU,
  * radiance_field.py:72-77) and the background NeRF (n_layers = 4: base 39-256-256-256-256 and head
@@ -87,13 +101,18 @@ int mms_gemm_tn_grouped(int prec, int n, const int64_t* M, const int64_t* N, con
  * Backward-data (backward = 1): X = dY of the last forward layer (rows >= rows_full: column 0 only), optionally
  *   scaled by act'(xaux) (stored to xout); out[l] = (prev . W^T) * act_l'(aux[l]) with act' evaluated from the
  *   forward output aux[l] (NULL: no scaling); the last out = dX.
+ * SDF backward only (3 layers, Softplus, rows_full < M): tap_part [ceil(M / 128) - rows_full / 128][ld_tap > N[0]]
+ *   receives one row per 128-row block holding rows >= rows_full: that block's share of the last forward layer's
+ *   weight-gradient row 0, sum over its rows >= rows_full of X[m, 0] * aux[0][m, :] (columns < N[0]), and of the bias
+ *   gradient, sum of X[m, 0] (column N[0]) -- the taps' sdf column, surface_model.py:137-153 (reduce with
+ *   mms_rowsum_add); NULL: not computed. 
  * a_hi / a_lo: per-layer packed weights from mms_mlp_pack (bf16, 32 ceil(N/32) x 16 ceil(K/16)); layers >= 1 are
  * register-fed and must be packed with permute = 1.  All row pitches multiples of 4 floats, 16-B aligned. */
 int mms_mlp_chain(int prec, int backward, int n_layers, const float* X, int64_t ldx, int K0, int64_t M,
                   int64_t rows_full, const float* xaux, int64_t ldxaux, int xact, float* xout, int64_t ldxout,
                   const void* const* a_hi, const void* const* a_lo, const float* const* bias, const float* const* aux,
                   const int64_t* ldaux, float* const* out, const int64_t* ldo, const int* N, const int* act,
-                  float beta, float thr, const float* w2row0, void* stream);
+                  float beta, float thr, const float* w2row0, float* tap_part, int64_t ld_tap, void* stream);
 /* bf16 (hi, and lo = residual if non-NULL) image of W [N, K] (ldw) as an MFMA A operand of rows x cols:
  * transpose = 0 -> A = W, 1 -> A = W^T; permute = 1 stores each 16-column step in register-fed order
  * (columns 0-3, 8-11, 4-7, 12-15).  Zero padded; rows % 32 == 0, cols % 16 == 0.  Fragment-major: the 32x16
@@ -220,6 +239,22 @@ int mms_render_stats(const float* w, const float* normals, const float* starts, 
 int mms_render_stats_segments(const float* w, const float* normals, const float* starts, const float* ends, int n_seg,
                               const int64_t* seg_off, int S, const int64_t* sidx, float* out, int64_t ldo,
                               int64_t seg_rows, float* range, void* stream);
+
+/* dst_a[c] += sum_r src[r][c] for c < na and dst_b[c - na] += sum_r src[r][c] for na <= c < cols (src [rows][ld]):
+ * the reduction of per-block partial rows (mms_mlp_chain's tap_part) into a weight-gradient row and its bias. */
+int mms_rowsum_add(const float* src, int64_t rows, int64_t cols, int64_t ld, float* dst_a, int64_t na, float* dst_b,
+                   void* stream);
+
+/* ---- narrow weight-normed linear layers (C <= 16 outputs, K = 128 / 256 / 512 inputs): the background density head
+ * (nerf_field.py:92-105, 256 -> 1 Softplus) and the 1-layer background modality heads (background_model.py:101-109,
+ * field_heads.py:71-88, 128 -> C).  fwd: Y[m, c] = act(X[m] . W[c] + b[c]) (W [C, K] row-major, the weight-normed
+ * weight; act 0 none, 1 ReLU, 2 Softplus(beta, thr), 3 Sigmoid).  bwd: dz = dY * act'(Y) (from the output);
+ * dX = (or += with accumulate) dz W; dW += dz^T X; db += sum dz (dW, db, dX may be NULL).  fp32 VALU. */
+int mms_small_linear_fwd(const float* X, int64_t ldx, int64_t M, int K, const float* W, const float* b, int C, int act,
+                         float beta, float thr, float* Y, int64_t ldy, void* stream);
+int mms_small_linear_bwd(const float* X, int64_t ldx, int64_t M, int K, const float* W, int C, int act, float beta,
+                         float thr, const float* Y, int64_t ldy, const float* dY, int64_t lddy, float* dX,
+                         int64_t lddx, int accumulate, float* dW, float* db, void* stream);
 
 /* ---- PolarizationHead Stokes alignment + intensities (field_heads.py:90-106; polarizer.py:54-101).
  * stokes [M,3] (MLP output), dirs/ups per ray [M/S, 3]; out [M,4]; bwd dstokes =, ddirs +=, dups += */

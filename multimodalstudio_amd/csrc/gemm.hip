@@ -437,6 +437,189 @@ __global__ __launch_bounds__(256) void gemm_tn_grouped_kernel(TnGroup g) {
   gemm_block<PREC, true, true, VEC>(mt, nt, slice, t.M, t.N, t.K, t.A, t.lda, t.B, t.ldb, t.C, t.ldc, ep, t.kps);
 }
 
+// ---------------------------------------------------------------------------- wide weight gradients
+// dW[Mo, Ni] += dZ^T X over the rows of a K slice with a 256 x 256 output tile per block (8 waves of 64 x 128, 2 x 4
+// MFMA tiles each): every operand row is read ONCE per slice -- the 128 x 128 tiles of gemm_tn_grouped_kernel read
+// each 256-wide operand twice (the tiles of one slice share rows; profiles/pmc_traffic_fast.json: 1.4x the
+// algorithmic bytes for the SDF MLP's 1.27 GB).  Both operands are T sources ([rows][units], 16-B rows); a stage of
+// 32 rows is loaded into registers one stage ahead, split into bf16 hi (+ lo) and stored into one of two LDS image
+// sets ([k][256 + 32] per image, ds_read_b64_tr_b16 fragments), so one barrier per stage.  LDS: 144 KB (split-bf16x3)
+// -> one block of 8 waves per CU.  Output tiles past Mo / Ni are skipped per wave-tile (the SDF input layer's 71
+// columns run 3 of 8 column tiles).  The slices' partial tiles are added with float atomics (one per element per
+// block), the bias gradients (column sums of dZ) reduced in LDS first.
+constexpr int kWT = 256;            // output tile edge
+constexpr int kWLD = kWT + 32;      // image row pitch (elements): 576-B rows, conflict-free transposing reads
+
+struct WideItem {
+  int64_t M, N, K;   // C[M, N] += A^T B: A [K rows, M] (lda), B [K rows, N] (ldb)
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  float* C;
+  int64_t ldc;
+  float* colsum;
+  int64_t kps;       // rows per slice
+  int mt, nt, zs;    // 256-tiles along M and N, K slices
+  int blocks;        // mt * nt * zs
+};
+struct WideGroup {
+  WideItem it[kMaxTnItems];
+  int n;
+};
+
+template <int PREC, int WK>
+__global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
+  constexpr int kWK = WK;             // rows per stage (16 or 32)
+  constexpr int NLD = WK / 8;         // float4 loads per thread per operand and stage
+  constexpr int NIMG = PREC == P_BF16X3 ? 2 : 1;
+  constexpr int IMG = kWK * kWLD;                        // elements per image
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2][2 * NIMG * IMG];   // [buffer][A hi, (A lo), B hi, (B lo)]
+  __shared__ float scs[8][kWT];                           // bias-gradient partials per wave
+  int id = blockIdx.x, ii = 0;
+  while (ii + 1 < g.n && id >= g.it[ii].blocks) {
+    id -= g.it[ii].blocks;
+    ++ii;
+  }
+  const WideItem& t = g.it[ii];
+  const int tiles = t.mt * t.nt;
+  const int tile = id % tiles, slice = id / tiles;
+  const int64_t m0 = (int64_t)(tile % t.mt) * kWT, n0 = (int64_t)(tile / t.mt) * kWT;
+  const int64_t kbeg = (int64_t)slice * t.kps;
+  const int64_t kend = kbeg + t.kps < t.K ? kbeg + t.kps : t.K;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 3, wn = w >> 2;
+  // staging: thread -> float4 column (lane) of rows (w + 8 i), i < WK / 8, for A and B
+  const int64_t ca = m0 + 4 * lane, cb = n0 + 4 * lane;
+  const int64_t ca_c = ca + 3 < t.M ? ca : ((t.M - 1) & ~(int64_t)3);   // clamped (always valid) 16-B column
+  const int64_t cb_c = cb + 3 < t.N ? cb : ((t.N - 1) & ~(int64_t)3);
+  const int va = (int)(t.M - ca < 0 ? 0 : (t.M - ca > 4 ? 4 : t.M - ca));   // valid elements of the float4
+  const int vb = (int)(t.N - cb < 0 ? 0 : (t.N - cb > 4 ? 4 : t.N - cb));
+  const bool do_cs = t.colsum != nullptr && n0 == 0;
+  float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 ra[NLD], rb[NLD];
+  int nrows = 0;
+  auto load = [&](int s) {
+    const int64_t r0 = kbeg + (int64_t)s * kWK;
+    nrows = (int)(kend - r0 < kWK ? kend - r0 : kWK);
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int64_t r = r0 + w + 8 * i;
+      const int64_t rc = r < kend ? r : kend - 1;
+      ra[i] = *reinterpret_cast<const float4*>(t.A + rc * t.lda + ca_c);
+      rb[i] = *reinterpret_cast<const float4*>(t.B + rc * t.ldb + cb_c);
+    }
+  };
+  auto mask4 = [](float4 v, int valid, bool row_ok) {
+    if (!row_ok) return make_float4(0.f, 0.f, 0.f, 0.f);
+    v.x = valid > 0 ? v.x : 0.f;
+    v.y = valid > 1 ? v.y : 0.f;
+    v.z = valid > 2 ? v.z : 0.f;
+    v.w = valid > 3 ? v.w : 0.f;
+    return v;
+  };
+  auto store = [&](int buf) {
+    __bf16* base = &lds[buf][0];
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const bool ok = w + 8 * i < nrows;
+      const float4 a = mask4(ra[i], va, ok), b = mask4(rb[i], vb, ok);
+      if (do_cs) { cs.x += a.x; cs.y += a.y; cs.z += a.z; cs.w += a.w; }
+      const int off = (w + 8 * i) * kWLD + 4 * lane;
+      const bf16x4 ah = cvt4(a), bh = cvt4(b);
+      *reinterpret_cast<bf16x4*>(base + off) = ah;
+      *reinterpret_cast<bf16x4*>(base + NIMG * IMG + off) = bh;
+      if constexpr (PREC == P_BF16X3) {
+        *reinterpret_cast<bf16x4*>(base + IMG + off) = cvt4(resid4(a, ah));
+        *reinterpret_cast<bf16x4*>(base + 3 * IMG + off) = cvt4(resid4(b, bh));
+      }
+    }
+  };
+  // wave-tile activity (wave-uniform): rows 64 wm + 32 i, columns 128 wn + 32 j of the block tile
+  bool act_i[2], act_j[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) act_i[i] = m0 + 64 * wm + 32 * i < t.M;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) act_j[j] = n0 + 128 * wn + 32 * j < t.N;
+  floatx16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx16{};
+  auto compute = [&](int buf) {
+    const __bf16* Ai = &lds[buf][0];
+    const __bf16* Bi = &lds[buf][NIMG * IMG];
+#pragma unroll
+    for (int ks = 0; ks < kWK; ks += 16) {
+      bf16x8 ah[2], al[2], bh[4], bl[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        ah[i] = frag_bf16<true, 8, kWLD>(Ai, 64 * wm + 32 * i, ks);
+        if constexpr (PREC == P_BF16X3) al[i] = frag_bf16<true, 8, kWLD>(Ai + IMG, 64 * wm + 32 * i, ks);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bh[j] = frag_bf16<true, 8, kWLD>(Bi, 128 * wn + 32 * j, ks);
+        if constexpr (PREC == P_BF16X3) bl[j] = frag_bf16<true, 8, kWLD>(Bi + IMG, 128 * wn + 32 * j, ks);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (!act_i[i]) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (!act_j[j]) continue;
+          if constexpr (PREC == P_BF16X3) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  };
+  const int S = (int)((kend - kbeg + kWK - 1) / kWK);
+  if (S > 0) {
+    load(0);
+    store(0);
+    if (S > 1) load(1);
+  }
+  __syncthreads();
+  for (int s = 0; s < S; ++s) {
+    compute(s & 1);
+    if (s + 1 < S) {
+      store((s + 1) & 1);
+      if (s + 2 < S) load(s + 2);
+    }
+    __syncthreads();
+  }
+  if (do_cs) {
+    *reinterpret_cast<float4*>(&scs[w][4 * lane]) = cs;
+    __syncthreads();
+    if (tid < kWT && m0 + tid < t.M) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v += scs[j][tid];
+      atomicAdd(t.colsum + m0 + tid, v);
+    }
+  }
+  // C/D map: column = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if (!act_i[i]) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!act_j[j]) continue;
+      const int64_t col = n0 + 128 * wn + 32 * j + (lane & 31);
+      const int64_t rb0 = m0 + 64 * wm + 32 * i + 4 * (lane >> 5);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t row = rb0 + (e & 3) + 8 * (e >> 2);
+        if (row < t.M && col < t.N) atomicAdd(t.C + row * t.ldc + col, acc[i][j][e]);
+      }
+    }
+  }
+}
+
 template <int PREC, bool TA, bool TB>
 int launch(bool vec, dim3 grid, hipStream_t s, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
            const float* B, int64_t ldb, float* C, int64_t ldc, Epi ep, int64_t kps, int mtp, int nt) {
@@ -564,6 +747,64 @@ MMS_EXPORT int mms_gemm_tn_grouped(int prec, int n, const int64_t* M, const int6
       if (vec) hipLaunchKernelGGL((gemm_tn_grouped_kernel<P_BF16X3, true>), grid, blk, 0, s, g);
       else hipLaunchKernelGGL((gemm_tn_grouped_kernel<P_BF16X3, false>), grid, blk, 0, s, g);
       break;
+  }
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const int64_t* K,
+                                const float* const* A, const int64_t* lda, const float* const* B, const int64_t* ldb,
+                                float* const* C, const int64_t* ldc, float* const* colsum, int target_blocks,
+                                int stage_rows, void* stream) {
+  const char* fn = "mms_gemm_tn_wide";
+  MMS_REQUIRE(stage_rows == 16 || stage_rows == 32, fn, "stage_rows must be 16 or 32");
+  MMS_REQUIRE(prec == 1 || prec == 2, fn, "prec must be 1 (bf16) or 2 (bf16x3)");
+  MMS_REQUIRE(n >= 1 && n <= kMaxTnItems, fn, "1 to 5 weight-gradient items per launch");
+  MMS_REQUIRE(M && N && K && A && lda && B && ldb && C && ldc, fn, "null argument array");
+  if (target_blocks < 1) target_blocks = 256;
+  double work = 0.0;
+  for (int i = 0; i < n; ++i) {
+    MMS_REQUIRE(M[i] >= 0 && N[i] >= 0 && K[i] >= 0, fn, "negative size");
+    if (M[i] == 0 || N[i] == 0 || K[i] == 0) continue;
+    MMS_REQUIRE(A[i] && B[i] && C[i], fn, "null operand");
+    MMS_REQUIRE(aligned16(A[i]) && aligned16(B[i]) && lda[i] % 4 == 0 && ldb[i] % 4 == 0, fn,
+                "operand rows must be 16-B aligned");
+    MMS_REQUIRE(lda[i] >= M[i] && ldb[i] >= N[i], fn, "leading dimension smaller than the row");
+    work += (double)((M[i] + kWT - 1) / kWT) * ((N[i] + kWT - 1) / kWT) * (double)K[i];
+  }
+  WideGroup g{};
+  int64_t total = 0;
+  int m = 0;
+  for (int i = 0; i < n; ++i) {
+    if (M[i] == 0 || N[i] == 0 || K[i] == 0) continue;   // nothing to add
+    WideItem& t = g.it[m++];
+    t.M = M[i]; t.N = N[i]; t.K = K[i];
+    t.A = A[i]; t.lda = lda[i]; t.B = B[i]; t.ldb = ldb[i]; t.C = C[i]; t.ldc = ldc[i];
+    t.colsum = colsum ? colsum[i] : nullptr;
+    t.mt = (int)((t.M + kWT - 1) / kWT);
+    t.nt = (int)((t.N + kWT - 1) / kWT);
+    // K slices in proportion to the item's share of the work (every block streams about the same rows), >= 1024 rows
+    const double share = (double)t.mt * t.nt * (double)t.K / work;
+    int64_t zs = (int64_t)(share * target_blocks / (t.mt * t.nt) + 0.5);
+    if (zs > t.K / 1024) zs = t.K / 1024;
+    if (zs < 1) zs = 1;
+    int64_t kps = (t.K + zs - 1) / zs;
+    kps = (kps + 31) / 32 * 32;
+    t.kps = kps;
+    t.zs = (int)((t.K + kps - 1) / kps);
+    t.blocks = t.mt * t.nt * t.zs;
+    total += t.blocks;
+  }
+  g.n = m;
+  if (m == 0) return 0;
+  MMS_REQUIRE(total <= INT32_MAX, fn, "grid too large");
+  hipStream_t s = mms::as_stream(stream);
+  const dim3 grid((unsigned)total), blk(512);
+  if (stage_rows == 32) {
+    if (prec == P_BF16) hipLaunchKernelGGL((gemm_tn_wide_kernel<P_BF16, 32>), grid, blk, 0, s, g);
+    else hipLaunchKernelGGL((gemm_tn_wide_kernel<P_BF16X3, 32>), grid, blk, 0, s, g);
+  } else {
+    if (prec == P_BF16) hipLaunchKernelGGL((gemm_tn_wide_kernel<P_BF16, 16>), grid, blk, 0, s, g);
+    else hipLaunchKernelGGL((gemm_tn_wide_kernel<P_BF16X3, 16>), grid, blk, 0, s, g);
   }
   return mms::check_launch(fn);
 }

@@ -318,6 +318,74 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
   }
 }
 
+// Position gradient alone, as a gather like the forward (thread per (point, level), 16 lanes per point, the SDF
+// batch in (sample, tap) order): every lane's 8 corner loads are independent, so they are all in flight at once --
+// the walk kernel's per-point table re-gather sat on one global-load latency per point, serially.  Per level:
+// d out_f / d x_axis = s / (2 r) sum_c T[c][f] dw_c / d o_axis (w_c the trilinear -- or smoothstep -- corner weight,
+// +-1 times the other two axes' weights, times S'(t) in Smoothstep mode); the 16 levels are summed by xor shuffles.
+template <int G>
+__global__ __launch_bounds__(256) void hashgrid_dpos_kernel(const float* __restrict__ pos, int64_t Mg, int64_t gstride,
+                                                            int64_t ldx, const float2* __restrict__ table, GridParams p,
+                                                            const float* __restrict__ dout, int64_t ldd,
+                                                            float* __restrict__ dpos, int64_t lddx) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t q = tid >> 4;
+  const int level = (int)(tid & 15);
+  const int64_t g = G == 1 ? q : q / G;
+  const int64_t pt = G == 1 ? q : g + (q - g * G) * gstride;
+  if (g >= Mg) return;   // whole 16-lane groups (one point) leave together
+  const int nlv = p.levels < p.active_levels ? p.levels : p.active_levels;
+  float gx = 0.f, gy = 0.f, gz = 0.f;
+  if (level < nlv) {
+    const float* xp = pos + pt * ldx;
+    const float s = p.scale[level];
+    const float two_r = 2.0f * p.radius;
+    const bool norm = p.radius > 0.f;
+    const float hx = norm ? (xp[0] + p.radius) / two_r : xp[0];   // make_corners' rounding (same corners)
+    const float hy = norm ? (xp[1] + p.radius) / two_r : xp[1];
+    const float hz = norm ? (xp[2] + p.radius) / two_r : xp[2];
+    Corners c = make_corners(xp[0], xp[1], xp[2], p.radius, p.inv_2r, s, level, p.log2T, p.smooth != 0);
+    float2 f[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = table[c.idx[i]];
+    const float dE0 = dout[pt * ldd + 2 * level], dE1 = dout[pt * ldd + 2 * level + 1];
+    float e[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = dE0 * f[i].x + dE1 * f[i].y;
+    const float ox = c.ox, oy = c.oy, oz = c.oz, nx = 1.0f - ox, ny = 1.0f - oy, nz = 1.0f - oz;
+    // corners (x, y, z sides; c = ceil, weight o; f = floor, weight 1 - o):
+    // 0 ccc, 1 cfc, 2 ffc, 3 fcc, 4 ccf, 5 cff, 6 fff, 7 fcf
+    gx = ((e[0] * oy + e[1] * ny) * oz + (e[4] * oy + e[5] * ny) * nz) -
+         ((e[3] * oy + e[2] * ny) * oz + (e[7] * oy + e[6] * ny) * nz);
+    gy = ((e[0] * ox + e[3] * nx) * oz + (e[4] * ox + e[7] * nx) * nz) -
+         ((e[1] * ox + e[2] * nx) * oz + (e[5] * ox + e[6] * nx) * nz);
+    gz = ((e[0] * ox + e[3] * nx) * oy + (e[1] * ox + e[2] * nx) * ny) -
+         ((e[4] * ox + e[7] * nx) * oy + (e[5] * ox + e[6] * nx) * ny);
+    if (p.smooth) {
+      const float sx = hx * s, sy = hy * s, sz = hz * s;
+      gx *= smoothstep_grad(sx - floorf(sx));
+      gy *= smoothstep_grad(sy - floorf(sy));
+      gz *= smoothstep_grad(sz - floorf(sz));
+    }
+    gx *= s;
+    gy *= s;
+    gz *= s;
+  }
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    gx += __shfl_xor(gx, o);
+    gy += __shfl_xor(gy, o);
+    gz += __shfl_xor(gz, o);
+  }
+  if (level == 0) {
+    const float two_r = p.radius > 0.f ? 2.0f * p.radius : 1.0f;
+    float* d = dpos + pt * lddx;
+    d[0] += gx / two_r;
+    d[1] += gy / two_r;
+    d[2] += gz / two_r;
+  }
+}
+
 int fill_params(const char* fn, GridParams& p, int L, int log2T, int interp, const float* scales, float radius,
                 int active_levels) {
   if (L < 1 || L > kMaxLevels) return mms::set_error(fn, "num_levels must be in [1, 16]");
@@ -414,4 +482,30 @@ MMS_EXPORT int mms_hashgrid_bwd(const float* pos, int64_t M, int64_t ldx, const 
                                 void* stream) {
   return mms_hashgrid_bwd_grouped(pos, M, 1, M, ldx, table, L, log2T, F, interp, scales, radius, active_levels, dout,
                                   ldd, dtable, dpos, lddx, stream);
+}
+
+MMS_EXPORT int mms_hashgrid_dpos_grouped(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx,
+                                         const float* table, int L, int log2T, int F, int interp, const float* scales,
+                                         float radius, int active_levels, const float* dout, int64_t ldd, float* dpos,
+                                         int64_t lddx, void* stream) {
+  const char* fn = "mms_hashgrid_dpos_grouped";
+  MMS_REQUIRE(F == 2, fn, "features_per_level must be 2");
+  MMS_REQUIRE(Mg >= 0 && ldx >= 3 && ldd >= 2 * L && lddx >= 3, fn, "bad shapes");
+  MMS_REQUIRE(group == 1 || group == 5, fn, "group must be 1 (plain) or 5 (centre + 4 taps)");
+  MMS_REQUIRE(group == 1 || gstride >= Mg, fn, "group rows overlap (gstride < groups)");
+  GridParams p;
+  int rc = fill_params(fn, p, L, log2T, interp, scales, radius, active_levels);
+  if (rc) return rc;
+  if (Mg == 0) return 0;
+  MMS_REQUIRE(pos && table && dout && dpos, fn, "null pointer");
+  const unsigned blocks = mms::grid_for(Mg * group * 16, 256, INT32_MAX);
+  const float2* t2 = reinterpret_cast<const float2*>(table);
+  hipStream_t s = mms::as_stream(stream);
+  if (group == 5)
+    hipLaunchKernelGGL((hashgrid_dpos_kernel<5>), dim3(blocks), dim3(256), 0, s, pos, Mg, gstride, ldx, t2, p, dout, ldd,
+                       dpos, lddx);
+  else
+    hipLaunchKernelGGL((hashgrid_dpos_kernel<1>), dim3(blocks), dim3(256), 0, s, pos, Mg, Mg, ldx, t2, p, dout, ldd,
+                       dpos, lddx);
+  return mms::check_launch(fn);
 }

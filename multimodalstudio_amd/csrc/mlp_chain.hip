@@ -66,6 +66,8 @@ struct ChainArgs {
   int64_t ldxout;
   float beta, thr;     // Softplus(beta, threshold)
   const float* w2row0; // forward: fp32 row 0 of the last layer's weight for the single-output row blocks
+  float* tap_part;     // backward, SDF taps: per-block partials [blocks from rows_full / 128][ld_tap] of
+  int64_t ld_tap;      //   sum over rows >= rows_full of X[m, 0] * aux0[m, :] (cols < N0) and of X[m, 0] (col N0)
   ChainLayer L[4];     // 3 or 4 layers (kernel template NL)
 };
 
@@ -325,15 +327,31 @@ __device__ __forceinline__ void epi_tile_full(floatx16& acc, int t, const float*
 // dZ = acc * act'(Y) with the forward output Y read row-contiguously (each load instruction 8 rows x 128 B, the next
 // tile's rows in flight while this tile is processed) and dZ stored the same way; both sides pass the accumulator
 // layout through the scratch.  Rows past M read / write row M - 1 (identical values).
-template <int NT, int ACT>
+// TAPW (the SDF backward's first layer, W_last^T): the single-output rows' (rows >= rows_full, the taps) share of the
+// last forward layer's weight-gradient row 0, dW[0, n] += sum_m X[m, 0] Y[m, n], accumulated from the Y rows this
+// epilogue loads anyway (the grouped weight-gradient launch would re-read 4 M rows x 1 KB of Y for that one row):
+// per lane 4 rows x 4 columns per tile, reduced over the wave's rows by xor shuffles into the wave's LDS row `sp`
+// (plain LDS stores: nothing here adds a vector-memory instruction the k-loops' exact vmcnt waits would count); the
+// block writes its partial row once, at the end of the kernel.
+template <int NT, int ACT, bool TAPW = false>
 __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const ChainLayer& Ly, int64_t m0, int64_t M,
-                                                    float* scr, int lane, float beta, float thr) {
+                                                    float* scr, int lane, float beta, float thr,
+                                                    const ChainArgs* ta = nullptr, float* sp = nullptr) {
   const int r = lane & 31, h = lane >> 5, q = lane & 7;
   int64_t rows[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t mr = m0 + 8 * j + (lane >> 3);
     rows[j] = mr < M ? mr : M - 1;
+  }
+  float x0[4] = {0.f, 0.f, 0.f, 0.f};   // TAPW: X[m, 0] of the lane's 4 rows (0 for centre rows and rows past M)
+  if constexpr (TAPW) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t mr = m0 + 8 * j + (lane >> 3);
+      const float v = ta->X[rows[j] * ta->ldx];
+      x0[j] = (mr < M && mr >= ta->rows_full) ? v : 0.f;
+    }
   }
   f32x4 y[2][4];
   auto load = [&](int t, f32x4* dst) {
@@ -344,6 +362,22 @@ __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const C
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     if (t + 1 < NT) load(t + 1, y[(t + 1) & 1]);
+    if constexpr (TAPW) {
+      f32x4 sw = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sw[c] = __builtin_fmaf(x0[j], y[t & 1][j][c], sw[c]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float v = sw[c];
+        v += __shfl_xor(v, 8);
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        sw[c] = v;
+      }
+      if (lane < 8) *reinterpret_cast<f32x4*>(sp + 32 * t + 4 * q) = sw;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(scr + (8 * j + (lane >> 3)) * kScr + 4 * q) = y[t & 1][j];
 #pragma unroll
@@ -362,6 +396,13 @@ __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const C
       const f32x4 v = *reinterpret_cast<const f32x4*>(scr + (8 * j + (lane >> 3)) * kScr + 4 * q);
       st_nt4(Ly.out + rows[j] * Ly.ldo + 32 * t + 4 * q, v);
     }
+  }
+  if constexpr (TAPW) {
+    float v = (q == 0) ? ((x0[0] + x0[1]) + (x0[2] + x0[3])) : 0.f;
+    v += __shfl_xor(v, 8);
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane == 0) sp[32 * NT] = v;
   }
 }
 
@@ -505,6 +546,9 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   constexpr bool kStage = BWD || KEEP;
   __shared__ __attribute__((aligned(16))) float sscr[kStage ? 4 : 1][32 * kScr];
   float* scr = &sscr[kStage ? wave : 0][0];
+  // the SDF backward (3 layers, Softplus, input = the last forward layer's dY): the taps' dW_last row-0 partials
+  constexpr bool kTapW = BWD && NL == 3 && A0 == 2 && XA == 0;
+  __shared__ __attribute__((aligned(16))) float stap[kTapW ? 4 : 1][32 * NT0 + 4];
   if constexpr (!BWD) {
 #pragma unroll
     for (int l = 0; l < NL; ++l)
@@ -584,7 +628,11 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   constexpr int kGE = (!BWD && KEEP) ? 4 : 0;
   bf16x8 b1h[2 * NT0], b1l[2 * NT0];
   if constexpr (BWD) {
-    epilogue_bwd_staged<NT0, A0>(acc0, a.L[0], m0, a.M, scr, lane, a.beta, a.thr);
+    // the SDF backward (3 layers, Softplus, input = the last forward layer's dY): the taps' dW_last row 0 on the way
+    if (kTapW && a.tap_part != nullptr && mb + 128 > a.rows_full)
+      epilogue_bwd_staged<NT0, A0, kTapW>(acc0, a.L[0], m0, a.M, scr, lane, a.beta, a.thr, &a, &stap[wave][0]);
+    else
+      epilogue_bwd_staged<NT0, A0>(acc0, a.L[0], m0, a.M, scr, lane, a.beta, a.thr);
     to_b<PREC, NT0>(acc0, b1h, b1l);
   }
 
@@ -661,6 +709,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     }
   };
 
+  // (the block's taps partial row is written after the last layer, below)
   if constexpr (NL == 4) {
     // ---- middle layer 2: B operand from layer 1's registers (same width and activation as layer 1)
     bf16x8 bmh[2 * NT1], bml[2 * NT1];
@@ -685,6 +734,13 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     last_layer(accm, std::integral_constant<int, 2>{});
   } else {
     last_layer(acc1, std::integral_constant<int, 1>{});
+  }
+  if constexpr (kTapW) {
+    if (a.tap_part != nullptr && mb + 128 > a.rows_full) {
+      __syncthreads();
+      float* row = a.tap_part + (int64_t)(blockIdx.x - a.rows_full / 128) * a.ld_tap;
+      for (int i = threadIdx.x; i <= 32 * NT0; i += 256) row[i] = ((stap[0][i] + stap[1][i]) + stap[2][i]) + stap[3][i];
+    }
   }
 }
 
@@ -755,6 +811,17 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
       if (bwd && ks0 == 1 && nt[0] == 2 && nt[1] == 2 && nt[2] == 8 && a0 == 1 && a1 == 1 && a2 == 0 && xio3 &&
           bwd_stored && hidden64) {
         launch_chain<PREC, 1, 2, 2, 8, true, 1, 1, 0, 3>(a, s);
+        return true;
+      }
+      // the polarization heads 256-64-64-3 (Stokes, no output activation; field_heads.py:90-106)
+      if (!bwd && ks0 == 16 && nt[0] == 2 && nt[1] == 2 && nt[2] == 1 && a0 == 1 && a1 == 1 && a2 == 0 && hidden64 &&
+          keep) {
+        launch_chain<PREC, 16, 2, 2, 1, false, 1, 1, 0, 0, true>(a, s);
+        return true;
+      }
+      if (bwd && ks0 == 1 && nt[0] == 2 && nt[1] == 2 && nt[2] == 8 && a0 == 1 && a1 == 1 && a2 == 0 && noxa &&
+          a.xout == nullptr && bwd_stored && hidden64) {
+        launch_chain<PREC, 1, 2, 2, 8, true, 1, 1, 0, 0>(a, s);
         return true;
       }
     }
@@ -850,7 +917,7 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
                              int64_t ldxout, const void* const* a_hi, const void* const* a_lo,
                              const float* const* bias, const float* const* aux, const int64_t* ldaux,
                              float* const* out, const int64_t* ldo, const int* N, const int* act, float beta,
-                             float thr, const float* w2row0, void* stream) {
+                             float thr, const float* w2row0, float* tap_part, int64_t ld_tap, void* stream) {
   const char* fn = "mms_mlp_chain";
   MMS_REQUIRE(prec >= 1 && prec <= 3, fn, "prec must be 1 (bf16), 2 (split bf16x3) or 3 (split activations)");
   MMS_REQUIRE(n_layers == 3 || n_layers == 4, fn, "chains of 3 or 4 layers");
@@ -865,6 +932,11 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
   a.xout = backward ? xout : nullptr; a.ldxout = ldxout;
   a.beta = beta; a.thr = thr;
   a.w2row0 = backward ? nullptr : w2row0;
+  a.tap_part = backward ? tap_part : nullptr;
+  a.ld_tap = ld_tap;
+  MMS_REQUIRE(tap_part == nullptr || !backward || (n_layers == 3 && act[0] == 2 && xaux == nullptr && N[0] <= 256 &&
+                                                   ld_tap > N[0] && rows_full >= 0 && rows_full < M), fn,
+              "the taps' weight-gradient partials (tap_part) are a feature of the SDF backward chain");
   MMS_REQUIRE(backward || rows_full >= M || w2row0 != nullptr, fn,
               "forward with single-output rows (rows_full < M) needs the last layer's fp32 weight row 0");
   MMS_REQUIRE(n_layers == 3 || rows_full < 0 || rows_full >= M, fn, "single-output rows are a 3-layer (SDF) feature");

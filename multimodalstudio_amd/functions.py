@@ -330,12 +330,24 @@ def grid_fwd(g: GridCfg, pos: torch.Tensor, ldx: int, M: int, table, active: int
               g.interp, g.scales_ptr, g.radius, active, out.data_ptr() + 4 * col, out.stride(0), _s())
 
 
+# hash-grid backward with both gradients: MMS_HASH_SPLIT=1 runs the table walk without position gradients + the
+# gather-style position-gradient kernel (scripts/hash_bench.py: the same 0.52 ms as the walk computing both, whose
+# time is the LDS merge, not its table re-gather), so the walk computes both by default
+HASH_SPLIT = os.environ.get("MMS_HASH_SPLIT", "0") == "1"
+
+
 def grid_bwd(g: GridCfg, pos, ldx, M, table, active, dout: torch.Tensor, col: int, dtable, dpos, group: int = 1):
     """Table / position gradients; group=5 for the [centre | 4 taps] SDF batch (M = 5 x centres)."""
     Mg = M // group
+    split = HASH_SPLIT and dtable is not None and dpos is not None
+    wpos = None if split else dpos
     _lib.call("mms_hashgrid_bwd_grouped", pos.data_ptr(), Mg, group, Mg, ldx, table.data_ptr(), g.L, g.log2T, g.F,
-              g.interp, g.scales_ptr, g.radius, active, dout.data_ptr() + 4 * col, dout.stride(0), _p(dtable), _p(dpos),
-              0 if dpos is None else dpos.stride(0), _s())
+              g.interp, g.scales_ptr, g.radius, active, dout.data_ptr() + 4 * col, dout.stride(0), _p(dtable), _p(wpos),
+              0 if wpos is None else wpos.stride(0), _s())
+    if split:
+        _lib.call("mms_hashgrid_dpos_grouped", pos.data_ptr(), Mg, group, Mg, ldx, table.data_ptr(), g.L, g.log2T,
+                  g.F, g.interp, g.scales_ptr, g.radius, active, dout.data_ptr() + 4 * col, dout.stride(0),
+                  dpos.data_ptr(), dpos.stride(0), _s())
 
 
 # ------------------------------------------------------------------------------------------------
@@ -438,6 +450,70 @@ class MLPRun:
         return dx, grads
 
 
+class SmallRun:
+    """A single weight-normed linear layer with C <= 16 outputs on the narrow-layer kernels (mms_small_linear_fwd/bwd,
+    fp32 VALU): the background density head (256 -> 1) and the 1-layer background modality heads (128 -> C).  Same
+    interface as MLPRun; the bf16 precision modes only (the fp32 parity mode keeps the f32-MFMA GEMMs)."""
+
+    def __init__(self, params: Sequence[torch.Tensor], acts: Sequence[Tuple[int, float, float]], prec: int = 1):
+        self.params = list(params)
+        self.acts = list(acts)
+        self.prec = int(prec)
+        self.x = self.W = self.norm = self.Y = None
+
+    @staticmethod
+    def serves(params, acts, prec: int) -> bool:
+        if prec == 0 or len(params) != 3:
+            return False
+        N, K = params[1].shape
+        return N <= 16 and K in (128, 256, 512) and acts[0][0] in (0, 1, 2, 3) and (K == 128 or N <= 4096 // K)
+
+    def forward(self, x: torch.Tensor, keep: bool, last_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x [M, K] with unit column stride and 16-B aligned rows (a column view of a wider panel is fine)."""
+        M = x.shape[0]
+        g, v, b = self.params
+        N, K = v.shape
+        W, nrm = normed_weight(g, v)
+        act, beta, thr = self.acts[0]
+        Y = last_out if last_out is not None else torch.empty(M, N, device=x.device)
+        _lib.call("mms_small_linear_fwd", x.data_ptr(), x.stride(0), M, K, W.data_ptr(), _p(b), N, act, beta, thr,
+                  Y.data_ptr(), Y.stride(0), _s())
+        if keep:
+            self.x, self.W, self.norm, self.Y = x, W, nrm, Y
+        return Y
+
+    def backward(self, dy: torch.Tensor, need_dx: bool, pre_activated: bool = False,
+                 dx_out: Optional[torch.Tensor] = None, accumulate: bool = False):
+        """dx written into (or, accumulate, added to) ``dx_out`` when given; parameter gradients accumulated in place."""
+        x, Y = self.x, self.Y
+        M = x.shape[0]
+        dev = x.device
+        g, v, b = self.params
+        N, K = v.shape
+        act, beta, thr = self.acts[0]
+        gt, vt, bt = grad_target(g), grad_target(v), grad_target(b)
+        need_w = gt is not None or vt is not None or bt is not None
+        dW = _dw_views([v], dev)[0] if need_w else None
+        db = (bt if bt is not None else torch.zeros(N, device=dev)) if need_w else None
+        dx = None
+        if need_dx:
+            dx = dx_out if dx_out is not None else _alloc(M, K, dev)
+        dy = dy if dy.stride(1) == 1 else dy.contiguous()
+        _lib.call("mms_small_linear_bwd", x.data_ptr(), x.stride(0), M, K, self.W.data_ptr(), N,
+                  0 if pre_activated else act, beta, thr, Y.data_ptr(), Y.stride(0), dy.data_ptr(), dy.stride(0),
+                  _p(dx), 0 if dx is None else dx.stride(0), int(accumulate and dx_out is not None), _p(dW), _p(db),
+                  _s())
+        if need_w:
+            _wn_bwd(g.reshape(-1), v, self.norm, dW, gt.reshape(-1) if gt is not None else
+                    torch.zeros(N, device=dev), vt if vt is not None else torch.zeros(N, K, device=dev))
+        self.x = self.Y = None
+        return dx, [None, None, None]
+
+
+# the SDF taps' weight-gradient row inside the backward chain (MMS_TAP_WGRAD=0: a grouped weight-gradient item)
+TAP_WGRAD_IN_CHAIN = os.environ.get("MMS_TAP_WGRAD", "1") != "0"
+
+
 class ChainRun:
     """A weight-normed 3- or 4-layer MLP on the fused chain kernel (mms_mlp_chain: all layers in one launch, bf16 or
     split-bf16x3 operands) plus the weight-gradient GEMMs.  Serves the SDF (71-256-256-257), radiance
@@ -477,7 +553,7 @@ class ChainRun:
         return hi, lo
 
     def _chain(self, backward: bool, X, K0: int, rows_full: int, packs, bias, aux, outs, Ns, acts,
-               xaux=None, xact: int = 0, xout=None, w2row0=None):
+               xaux=None, xact: int = 0, xout=None, w2row0=None, tap_part=None):
         prec = self.bcprec if backward else self.cprec
         n = self.L
         VP = ctypes.c_void_p * n
@@ -494,7 +570,8 @@ class ChainRun:
         _lib.call("mms_mlp_chain", prec, int(backward), n, X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
                   _p(xaux), 0 if xaux is None else xaux.stride(0), int(xact), _p(xout),
                   0 if xout is None else xout.stride(0), cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux),
-                  cast(os_), cast(ldo), cast(ns), cast(ac), self.beta, self.thr, _p(w2row0), _s())
+                  cast(os_), cast(ldo), cast(ns), cast(ac), self.beta, self.thr, _p(w2row0), _p(tap_part),
+                  0 if tap_part is None else tap_part.stride(0), _s())
 
     def forward(self, x: torch.Tensor, keep: bool, rows_full: Optional[int] = None,
                 dense_col0: bool = False, last_out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -558,28 +635,46 @@ class ChainRun:
         dx = dx_out if dx_out is not None else _alloc(M, K0, dev)
         dy = dy if dy.stride(1) == 1 and dy.stride(0) % 4 == 0 else _copy_aligned(dy)
         order = list(range(L - 2, -1, -1))           # hidden layers, last first
-        self._chain(True, dy, Ns[L - 1], self.rows_full, packs, [None] * L, [Y[l] for l in order] + [None],
-                    [dZ[l] for l in order] + [dx], [Ns[l] for l in order] + [K0], [acts[l] for l in order] + [0],
-                    xaux=Y[L - 1] if acts[L - 1] != 0 else None, xact=acts[L - 1], xout=dZl)
-        dZ = dZ + [dZl if dZl is not None else dy]
-        Xin = [x] + Y[:L - 1]
         rf = self.rows_full
         dWs = _dw_views([self.params[3 * l + 1] for l in range(L)], dev)
+        dbs = []
+        for l in range(L):
+            N = self.params[3 * l + 1].shape[0]
+            bt = grad_target(self.params[3 * l + 2])
+            dbs.append(bt if bt is not None else torch.zeros(N, device=dev))
+        needs = [any(grad_target(p) is not None for p in self.params[3 * l: 3 * l + 3]) for l in range(L)]
+        # the SDF chain: the taps' (rows >= rows_full: sdf column only) share of the last layer's weight-gradient row 0
+        # is summed inside the backward chain from the Y rows it loads anyway (per-block partial rows, mms_mlp_chain
+        # tap_part), then reduced into dW[0] / db[0] (mms_rowsum_add)
+        tapw = TAP_WGRAD_IN_CHAIN and rf < M and needs[L - 1] and L == 3 and acts[0] == 2 and acts[L - 1] == 0
+        tap_part = None
+        if tapw:
+            n0 = Ns[L - 2]
+            tap_part = torch.empty(-(-M // 128) - rf // 128, n0 + 4, device=dev)
+        self._chain(True, dy, Ns[L - 1], rf, packs, [None] * L, [Y[l] for l in order] + [None],
+                    [dZ[l] for l in order] + [dx], [Ns[l] for l in order] + [K0], [acts[l] for l in order] + [0],
+                    xaux=Y[L - 1] if acts[L - 1] != 0 else None, xact=acts[L - 1], xout=dZl, tap_part=tap_part)
+        if tapw:
+            _lib.call("mms_rowsum_add", tap_part.data_ptr(), tap_part.shape[0], n0 + 1, tap_part.stride(0),
+                      dWs[L - 1].data_ptr(), n0, dbs[L - 1].data_ptr(), _s())
+        dZ = dZ + [dZl if dZl is not None else dy]
+        Xin = [x] + Y[:L - 1]
         # every layer's weight gradient dW_l += dZ_l^T X_l (+ bias column sums) in ONE grouped launch
         items, wn = [], []
         for l in range(L):
             g, v, b = self.params[3 * l: 3 * l + 3]
             N, K = v.shape
-            gt, vt, bt = grad_target(g), grad_target(v), grad_target(b)
-            if gt is None and vt is None and bt is None:
+            gt, vt = grad_target(g), grad_target(v)
+            if not needs[l]:
                 continue
             dW = dWs[l]
-            db = bt if bt is not None else torch.zeros(N, device=dev)
+            db = dbs[l]
             A, B = dZ[l], Xin[l]
             if l == L - 1 and rf < M:
-                # rows past rows_full carry only the output column 0
+                # rows past rows_full carry only the output column 0 (summed by the chain above when tapw)
                 items.append((N, K, rf, A, B, dW, db))
-                items.append((1, K, M - rf, A[rf:], B[rf:], dW, db))
+                if not tapw:
+                    items.append((1, K, M - rf, A[rf:], B[rf:], dW, db))
             else:
                 items.append((N, K, M, A, B, dW, db))
             wn.append((g, v, l, dW, gt, vt, N, K))
@@ -595,13 +690,14 @@ class ChainRun:
         return dx
 
 
-# Weight gradients off the critical path.  Inside a training backward (deferred weight norm: nothing reads dW before
-# the flush) an MLP's grouped weight-gradient launch goes to a side stream forked from the caller's: the SDF MLP's
-# 0.46 ms split-K launch then runs beside the hash-grid backward it used to delay (the grid needs only the chain's dx),
-# and the radiance MLP's beside the radiance grid's (side-streaming only the SDF MLP's measured 5 % slower than
-# all).  A final autograd callback joins the side stream back into the caller's stream, so the weight-norm flush and
-# the optimizer see every gradient.  MMS_SYNC_WGRAD=1 keeps them inline.
-ASYNC_WGRAD = os.environ.get("MMS_SYNC_WGRAD", "0") != "1"
+# Weight gradients on a side stream (MMS_SYNC_WGRAD=0).  Inside a training backward (deferred weight norm: nothing
+# reads dW before the flush) an MLP's grouped weight-gradient launch can go to a side stream forked from the caller's,
+# beside the hash-grid backward (the grid needs only the chain's dx); a final autograd callback joins the side stream
+# back into the caller's stream, so the weight-norm flush and the optimizer see every gradient.  With the 128 x 128
+# tiled engine that overlap paid (521k -> 545-556k rays/s in round 2); the wide engine's 8-wave, 152 KB-LDS blocks
+# fill whole CUs, so beside the hash walk they only contend: inline, wide 540.6k vs side stream, tiled 514-522k,
+# wide 506.8k (round-3 A/B, profiles/round3b_wgrad_ab.txt).  Inline by default.
+ASYNC_WGRAD = os.environ.get("MMS_SYNC_WGRAD", "1") != "1"
 _WGRAD_STREAMS: dict = {}
 
 
@@ -938,8 +1034,8 @@ def _chain_shape(params, acts, prec: int = 2) -> bool:
     if len(params) == 9:
         if (dims == [71, 256, 256, 257] and a == (2, 2, 0)) or (dims == [317, 256, 256, 256] and a == (1, 1, 1)):
             return True
-        # the plain modality heads 256-64-64-C, C <= 32
-        return prec in (1, 2, 4) and dims[:3] == [256, 64, 64] and dims[3] <= 32 and a == (1, 1, 3)
+        # the modality heads 256-64-64-C, C <= 32: plain (Sigmoid out) and polarization (Stokes, no out activation)
+        return prec in (1, 2, 4) and dims[:3] == [256, 64, 64] and dims[3] <= 32 and a in ((1, 1, 3), (1, 1, 0))
     if len(params) == 12 and prec in (1, 2, 4) and a == (1, 1, 1, 1):
         return dims in ([39, 256, 256, 256, 256], [283, 256, 256, 256, 128], [283, 256, 256, 256, 256])
     return False
@@ -947,9 +1043,12 @@ def _chain_shape(params, acts, prec: int = 2) -> bool:
 
 def mlp_runner(params, acts, prec: int):
     """The MLP engine for a weight-normed MLP: the fused 3-layer chain kernel in the bf16 modes where its shape is
-    served, else the per-layer GEMM engine (every shape, every precision)."""
+    served, the narrow-layer kernels for a single layer of <= 16 outputs, else the per-layer GEMM engine (every shape,
+    every precision)."""
     if prec != 0 and _chain_shape(params, acts, prec):
         return ChainRun(params, acts, prec)
+    if SmallRun.serves(params, acts, prec):
+        return SmallRun(params, acts, prec)
     return MLPRun(params, acts, prec)
 
 
@@ -1206,7 +1305,7 @@ class BackgroundFunction(torch.autograd.Function):
         # base and head MLPs: 4-layer chain kernels in bf16 (mlp_runner), per-layer GEMMs otherwise
         base = mlp_runner(base_p, BG_BASE_ACTS[:nb], PRECISION["background"])
         base.forward(X, keep=True, last_out=H[:, :Fb])  # writes cols [0, Fb) of the head panel
-        dens = MLPRun(dens_p, BG_DENS_ACTS, PRECISION["background"])
+        dens = mlp_runner(dens_p, BG_DENS_ACTS, PRECISION["background"])
         density = _mlp_strided(dens, H, Fb)             # density head reads the base features in place
         head = mlp_runner(head_p, BG_HEAD_ACTS[:len(head_p) // 3], PRECISION["background"])
         feat = head.forward(H, keep=True)
@@ -1246,8 +1345,10 @@ class BackgroundFunction(torch.autograd.Function):
         return (dpos, ddirs, None, None, None, None, None, None, *([None] * len(params)))
 
 
-def _mlp_strided(run: MLPRun, H: torch.Tensor, Fb: int) -> torch.Tensor:
+def _mlp_strided(run, H: torch.Tensor, Fb: int) -> torch.Tensor:
     """Run a 1-layer MLP on the first Fb columns of panel H (row stride H.stride(0))."""
+    if isinstance(run, SmallRun):
+        return run.forward(H[:, :Fb], keep=True)
     g, v, b = run.params
     N, K = v.shape
     M = H.shape[0]
@@ -1262,8 +1363,11 @@ def _mlp_strided(run: MLPRun, H: torch.Tensor, Fb: int) -> torch.Tensor:
     return Y
 
 
-def _mlp_strided_bwd(run: MLPRun, dy: torch.Tensor, H: torch.Tensor, Fb: int, dx_into: Optional[torch.Tensor] = None):
+def _mlp_strided_bwd(run, dy: torch.Tensor, H: torch.Tensor, Fb: int, dx_into: Optional[torch.Tensor] = None):
     """Backward of _mlp_strided; the input gradient is returned, or (dx_into) added into that [M, K] view."""
+    if isinstance(run, SmallRun):
+        dx, _ = run.backward(dy, need_dx=True, dx_out=dx_into, accumulate=dx_into is not None)
+        return dx, [None, None, None]
     g, v, b = run.params
     N, K = v.shape
     M = H.shape[0]

@@ -151,16 +151,38 @@ def _splits_for(M_rows: int, tiles: int, prec: int = 0) -> int:
 _GROUP_BLOCKS = {0: 1024, 1: 256, 2: 512}
 
 
-def gemm_tn_grouped(items, prec: int, target_blocks: Optional[int] = None):
+# weight-gradient engine of the bf16 modes: "wide" (mms_gemm_tn_wide: 256 x 256 tiles, operand rows read once per
+# slice; SDF MLP 0.52 -> 0.36 ms alone, scripts/tn_wide_bench.py) or "tiled" (mms_gemm_tn_grouped: 128 x 128 tiles);
+# MMS_TN_ENGINE overrides (A/B measurement)
+TN_ENGINE = os.environ.get("MMS_TN_ENGINE", "wide")
+_WIDE_BLOCKS = 256
+TN_STAGE_ROWS = int(os.environ.get("MMS_TN_STAGE", "16"))
+
+
+def _aligned_item(it) -> bool:
+    A, B = it[3], it[4]
+    return all(t.data_ptr() % 16 == 0 and t.stride(0) % 4 == 0 and t.stride(1) == 1 for t in (A, B))
+
+
+def gemm_tn_grouped(items, prec: int, target_blocks: Optional[int] = None, engine: Optional[str] = None,
+                    stage_rows: Optional[int] = None):
     """items = [(N_out, K_in, rows, dZ [rows, >=N_out], X [rows, >=K_in], dW [N_out, K_in], db [N_out] or None)]:
     dW += dZ^T X and db += colsum(dZ) for every item in one launch (<= 5 items)."""
     n = len(items)
     I64 = ctypes.c_int64 * n
     VP = ctypes.c_void_p * n
-    target = int(os.environ.get("MMS_TN_BLOCKS", "0")) or target_blocks or _GROUP_BLOCKS.get(int(prec), 512)
-    _lib.call("mms_gemm_tn_grouped", int(prec), n, I64(*[it[0] for it in items]), I64(*[it[1] for it in items]),
+    engine = engine or TN_ENGINE
+    wide = engine == "wide" and int(prec) in (1, 2) and all(_aligned_item(it) for it in items)
+    if wide:
+        entry = "mms_gemm_tn_wide"
+        target = int(os.environ.get("MMS_TN_BLOCKS", "0")) or target_blocks or _WIDE_BLOCKS
+    else:
+        entry = "mms_gemm_tn_grouped"
+        target = int(os.environ.get("MMS_TN_BLOCKS", "0")) or target_blocks or _GROUP_BLOCKS.get(int(prec), 512)
+    _lib.call(entry, int(prec), n, I64(*[it[0] for it in items]), I64(*[it[1] for it in items]),
               I64(*[it[2] for it in items]), VP(*[it[3].data_ptr() for it in items]),
               I64(*[it[3].stride(0) for it in items]), VP(*[it[4].data_ptr() for it in items]),
               I64(*[it[4].stride(0) for it in items]), VP(*[it[5].data_ptr() for it in items]),
               I64(*[it[5].stride(0) for it in items]),
-              VP(*[(it[6].data_ptr() if it[6] is not None else None) for it in items]), target, _stream())
+              VP(*[(it[6].data_ptr() if it[6] is not None else None) for it in items]), target,
+              *((int(stage_rows or TN_STAGE_ROWS),) if wide else ()), _stream())

@@ -70,6 +70,14 @@ def main():
                                                                group=5)), 2188)
     rep("bwd G=5    (dtable only)", timeit(lambda: F.grid_bwd(cfg, x, 3, 5 * M, table, L, dout, 0, dtable, None,
                                                              group=5)), 2188)
+    rep("dpos gather G=5", timeit(lambda: F._lib.call(
+        "mms_hashgrid_dpos_grouped", x.data_ptr(), M, 5, M, 3, table.data_ptr(), cfg.L, cfg.log2T, cfg.F, cfg.interp,
+        cfg.scales_ptr, cfg.radius, L, dout.data_ptr(), dout.stride(0), dpos.data_ptr(), 3, F._s())), 1164)
+    rep("dpos gather plain (radiance-like, 1/5 rows)", timeit(lambda: F._lib.call(
+        "mms_hashgrid_dpos_grouped", x.data_ptr(), M, 1, M, 3, table.data_ptr(), cfg.L, cfg.log2T, cfg.F, cfg.interp,
+        cfg.scales_ptr, cfg.radius, L, dout.data_ptr(), dout.stride(0), dpos.data_ptr(), 3, F._s())) * 5, 1164)
+    rep("bwd plain 1/5 rows (dtable + dpos) x5", timeit(lambda: F.grid_bwd(cfg, x, 3, M, table, L, dout, 0, dtable,
+                                                                           dpos)) * 5, 2188)
     rep("zero dtable (64 MiB memset)", timeit(lambda: dtable.zero_()), 0)
 
 

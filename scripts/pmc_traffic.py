@@ -25,6 +25,7 @@ CHAIN_ROLES = {  # (bwd, KS0, NT2, NL, KEEP) -> the role label bench.py's chain_
     (False, 20, 8, 3, True): "radiance_fwd", (True, 17, 3, 3, False): "sdf_bwd", (True, 16, 10, 3, False): "radiance_bwd",
     (False, 3, 8, 4, True): "bg_base_fwd", (False, 18, 4, 4, True): "bg_head_fwd", (False, 18, 8, 4, True): "bg_head_fwd",
     (True, 16, 2, 4, False): "bg_base_bwd", (True, 8, 9, 4, False): "bg_head_bwd", (True, 16, 9, 4, False): "bg_head_bwd",
+    (False, 16, 1, 3, True): "head_fwd", (True, 1, 8, 3, False): "head_bwd",
 }
 
 
@@ -32,6 +33,9 @@ def label(name, grid=0):
     m = re.search(r"gemm_tn_grouped_kernel<(\d), (true|false)>", name)
     if m:
         return f"mms_gemm_tn_grouped:{PREC[m.group(1)]}:TN_grouped"
+    m = re.search(r"gemm_tn_wide_kernel<(\d), \d+>", name)
+    if m:
+        return f"mms_gemm_tn_wide:{PREC[m.group(1)]}:TN_grouped"
     m = re.search(r"gemm_kernel<(\d), (true|false), (true|false), (true|false)>", name)
     if m:
         return f"mms_gemm:{PREC[m.group(1)]}:{MODE.get((m.group(2), m.group(3)), '??')}"

@@ -139,10 +139,12 @@ def test_sdf_chain_split_activations(dev):
         assert v < 1e-4, f"prec=3 {k}: {v:.2e}"
 
 
-def _ref_mlp(x, params, acts):
+def _ref_mlp(x, params, acts, leaves=None):
+    """fp64 forward; ``leaves``: fp64 CPU copies of params to differentiate through (else detached copies)."""
     h = x
     for l in range(3):
-        g, v, b = [p.detach().double().cpu() for p in params[3 * l: 3 * l + 3]]
+        g, v, b = leaves[3 * l: 3 * l + 3] if leaves is not None else \
+            [p.detach().double().cpu() for p in params[3 * l: 3 * l + 3]]
         w = torch._weight_norm(v, g, 0)
         h = h @ w.T + b
         act, beta, thr = acts[l]
@@ -156,7 +158,8 @@ def _ref_mlp(x, params, acts):
 @pytest.mark.parametrize("M,rows_full", [(1000, 200), (777, 777), (640, 0)])
 def test_chain_sdf_tap_rows(dev, M, rows_full):
     """SDF chain with tap rows (>= rows_full): column 0 for every row, all 257 columns for the rows below; the
-    backward reads only column 0 of the tap rows (the rest of those rows is garbage on purpose)."""
+    backward reads only column 0 of the tap rows (the rest of those rows is garbage on purpose).  Parameter gradients
+    too: the taps' share of the last layer's row 0 is summed inside the backward chain (dw_row0 / db_row0)."""
     from multimodalstudio_amd import functions as fx
     g = torch.Generator().manual_seed(M + rows_full)
     f = dict(np.load(os.path.join(GOLD, "mlp_geo.npz")))
@@ -167,7 +170,8 @@ def test_chain_sdf_tap_rows(dev, M, rows_full):
     keep = rows_full > 0
     y = run.forward(X, keep=keep, rows_full=rows_full)
     xr = x.double().requires_grad_(True)
-    ref = _ref_mlp(xr, params, CASES["geo"])
+    leaves = [p.detach().double().cpu().requires_grad_(True) for p in params]
+    ref = _ref_mlp(xr, params, CASES["geo"], leaves)
     yc = y.detach().cpu().double()
     assert rel(yc[:, 0], ref[:, 0].detach()) < TOL[2]
     if rows_full > 0:
@@ -186,6 +190,8 @@ def test_chain_sdf_tap_rows(dev, M, rows_full):
     ref.backward(dyr)
     assert rel(dx.cpu(), xr.grad) < TOL[2]
     assert torch.isfinite(dx).all()
+    for i, (p, q) in enumerate(zip(params, leaves)):
+        assert rel(p.grad.cpu(), q.grad) < TOL[2], (i, rel(p.grad.cpu(), q.grad))
 
 
 def test_sdf_only_fast_matches_fp32(dev):
@@ -271,12 +277,13 @@ def test_chain_relu_layers(dev, dims, prec):
         assert rel(p.grad.cpu(), ref_g[i]) < TOL[1], (i, rel(p.grad.cpu(), ref_g[i]))
 
 
-@pytest.mark.parametrize("prec", [1, 4])
-@pytest.mark.parametrize("C", [3, 1, 5])
-def test_chain_head(dev, C, prec):
-    """A modality head 256-64-64-C (ReLU, ReLU, Sigmoid; field_heads.py:71-88) on the bf16 chain kernel: forward vs
-    fp64, backward (dx, every parameter gradient) vs the fp64 backward at the kernel's own activations (Sigmoid' from
-    the output), at a row count that is not a multiple of the 128-row block."""
+@pytest.mark.parametrize("prec,C,out", [(1, 3, 3), (1, 1, 3), (1, 5, 3), (4, 3, 3), (4, 1, 3), (4, 5, 3), (2, 3, 0),
+                                        (1, 3, 0)])
+def test_chain_head(dev, C, prec, out):
+    """A modality head 256-64-64-C (ReLU, ReLU, Sigmoid: field_heads.py:71-88; or no output activation: the
+    polarization heads' Stokes, :90-106) on the chain kernel: forward vs fp64, backward (dx, every parameter gradient)
+    vs the fp64 backward at the kernel's own activations (Sigmoid' from the output), at a row count that is not a
+    multiple of the 128-row block."""
     from multimodalstudio_amd import functions as fx
     dims = [256, 64, 64, C]
     g = torch.Generator().manual_seed(C)
@@ -287,7 +294,7 @@ def test_chain_head(dev, C, prec):
         v = torch.randn(n, k, generator=g) / np.sqrt(k)
         params += [v.norm(dim=1, keepdim=True).clone(), v, torch.randn(n, generator=g) * 0.1]
     params = [p.to(dev).requires_grad_(True) for p in params]
-    acts = [(1, 1.0, 20.0), (1, 1.0, 20.0), (3, 1.0, 20.0)]
+    acts = [(1, 1.0, 20.0), (1, 1.0, 20.0), (out, 1.0, 20.0)]
     assert fx._chain_shape(params, acts, prec)
     x = torch.randn(M, 256, generator=g)
     run = fx.ChainRun(params, acts, prec)
@@ -296,13 +303,13 @@ def test_chain_head(dev, C, prec):
     for l in range(3):
         gg, v, b = [p.detach().double().cpu() for p in params[3 * l: 3 * l + 3]]
         h = h @ torch._weight_norm(v, gg, 0).T + b
-        h = torch.relu(h) if l < 2 else torch.sigmoid(h)
-    assert rel(y.detach().cpu(), h) < (TOL[2] if prec == 4 else TOL[1])
+        h = torch.relu(h) if l < 2 else (torch.sigmoid(h) if out == 3 else h)
+    assert rel(y.detach().cpu(), h) < (TOL[2] if prec in (2, 4) else TOL[1])
     Y = [t.detach().clone().double().cpu() for t in run.Y]
     dy = torch.randn(M, C, generator=g)
     dx = run.backward(_panel(dy, dev))
     torch.cuda.synchronize()
-    d = dy.double() * Y[2] * (1 - Y[2])
+    d = dy.double() * Y[2] * (1 - Y[2]) if out == 3 else dy.double()
     ins = [x.double(), Y[0], Y[1]]
     ref = [None] * 9
     for l in (2, 1, 0):

@@ -38,12 +38,14 @@ def test_hashgrid_fwd_bwd(dev, log2T, active, radius):
     np.testing.assert_allclose(xd.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("group", [1, 5])
-def test_hashgrid_smoothstep(dev, group):
+def test_hashgrid_smoothstep(dev, group, split, monkeypatch):
     """interpolation "Smoothstep" (HashEncodingConfig, encodings.py:64-67; tcnn's mode, parity-unpinned): forward,
     table and position gradients of the plain and the [centre | 4 taps] kernels vs the oracle's restatement of the
     smoothstep weights, whose position gradient autograd derives (d S / dt = 6 t (1 - t))."""
     from multimodalstudio_amd import functions as F
+    monkeypatch.setattr(F, "HASH_SPLIT", split)    # position gradient by the gather kernel / by the table walk
     L, Mc, log2T = 16, 1500, 14
     scales = ohg.level_scales(16, 1024, L)
     g = torch.Generator().manual_seed(11)
@@ -72,10 +74,13 @@ def test_hashgrid_smoothstep(dev, group):
     np.testing.assert_allclose(dpos.cpu().numpy(), xr.grad.numpy(), rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("log2T", [12, 19])
-def test_hashgrid_bwd_grouped_taps(dev, log2T):
-    """[centre | 4 taps] batch: the grouped backward (in-thread merge of shared-cell corners) vs the oracle."""
+def test_hashgrid_bwd_grouped_taps(dev, log2T, split, monkeypatch):
+    """[centre | 4 taps] batch: the grouped backward (LDS merge of shared-cell corners; position gradient by the
+    gather kernel or by the walk) vs the oracle."""
     from multimodalstudio_amd import functions as F
+    monkeypatch.setattr(F, "HASH_SPLIT", split)
     L, Mc, delta = 16, 2000, 2.0 / 1024 / 3 ** 0.5
     scales = ohg.level_scales(16, 2048, L)
     g = torch.Generator().manual_seed(7)
@@ -258,11 +263,13 @@ def test_gemm_tall_skinny_epilogues(dev, prec, tol, M, N, K):
     assert e < tol, e
 
 
-@pytest.mark.parametrize("prec,tol", [(0, 2e-6), (2, 2e-5), (1, 2e-2)])
-def test_gemm_tn_grouped(dev, prec, tol):
-    """mms_gemm_tn_grouped: several layers' weight gradients (+ bias column sums) in one launch vs fp64 -- ragged
-    widths, a single-column item sharing its dW with a full item (the SDF taps), unaligned rows (scalar staging),
-    and slices long enough for the asm-prefetched k-loop to wrap several times."""
+@pytest.mark.parametrize("prec,tol,engine", [(0, 2e-6, "tiled"), (2, 2e-5, "tiled"), (1, 2e-2, "tiled"),
+                                             (2, 2e-5, "wide"), (1, 2e-2, "wide")])
+def test_gemm_tn_grouped(dev, prec, tol, engine):
+    """mms_gemm_tn_grouped / mms_gemm_tn_wide: several layers' weight gradients (+ bias column sums) in one launch vs
+    fp64 -- ragged widths (257 outputs: two 256-row tiles; 317 inputs: two column tiles), a single-column item sharing
+    its dW with a full item (the SDF taps), unaligned rows (the tiled engine's scalar staging; the wide engine's
+    caller falls back to it), and slices long enough for the k-loop to wrap several times."""
     from multimodalstudio_amd import hip_ops
     from multimodalstudio_amd.functions import _alloc
     g = torch.Generator().manual_seed(11 + prec)
@@ -296,8 +303,8 @@ def test_gemm_tn_grouped(dev, prec, tol):
     dZu, Xu = wd[:, 1:33], wd[:, 3:20]
     dWu = torch.zeros(32, 17, device=dev)
     items_u = [(32, 17, 5000, dZu, Xu, dWu, None)]
-    hip_ops.gemm_tn_grouped(items, prec)
-    hip_ops.gemm_tn_grouped(items_u, prec)
+    hip_ops.gemm_tn_grouped(items, prec, engine=engine)
+    hip_ops.gemm_tn_grouped(items_u, prec, engine=engine)
     torch.cuda.synchronize()
     for (N, K, M, _, _, dW, db), (rw, rb) in zip(items[:4], refs):
         err = np.abs(dW.cpu().double().numpy() - rw.numpy()).max() / np.abs(rw.numpy()).max()
@@ -307,3 +314,46 @@ def test_gemm_tn_grouped(dev, prec, tol):
     ru = wide.double()[:, 1:33].T @ wide.double()[:, 3:20]
     err = np.abs(dWu.cpu().double().numpy() - ru.numpy()).max() / np.abs(ru.numpy()).max()
     assert err < tol, f"unaligned item prec={prec}: rel err {err:.2e}"
+
+
+@pytest.mark.parametrize("C,K,act", [(1, 256, 2), (9, 128, 3), (3, 128, 0), (4, 512, 1)])
+def test_small_linear(dev, C, K, act):
+    """mms_small_linear_fwd / _bwd (the background density head and 1-layer modality heads) vs fp64: a column view of
+    a wider panel as input (row stride > K), accumulate into an existing dX, dW / db accumulation over ragged rows."""
+    from multimodalstudio_amd.functions import _alloc
+    from multimodalstudio_amd import _lib
+    g = torch.Generator().manual_seed(C * 1000 + K)
+    M = 70001
+    beta, thr = (1.0, 20.0)
+    panel = _alloc(M, K + 27, dev)
+    panel.copy_(torch.randn(M, K + 27, generator=g).to(dev))
+    X = panel[:, :K]
+    W = (torch.randn(C, K, generator=g) / K ** 0.5).to(dev)
+    b = torch.randn(C, generator=g).to(dev)
+    Y = torch.empty(M, C, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.call("mms_small_linear_fwd", X.data_ptr(), X.stride(0), M, K, W.data_ptr(), b.data_ptr(), C, act, beta, thr,
+              Y.data_ptr(), Y.stride(0), s)
+    Xd, Wd, bd = X.double().cpu(), W.double().cpu(), b.double().cpu()
+    Z = Xd @ Wd.T + bd
+    ref = {0: Z, 1: Z.clamp_min(0), 2: torch.nn.functional.softplus(Z, beta, thr), 3: torch.sigmoid(Z)}[act]
+    torch.cuda.synchronize()
+    assert ((Y.double().cpu() - ref).abs().max() / ref.abs().max()).item() < 1e-5
+    dY = torch.randn(M, C, generator=g).to(dev)
+    dX0 = torch.randn(M, K, generator=g)
+    dX = _alloc(M, K, dev)
+    dX.copy_(dX0.to(dev))
+    dW = torch.ones(C, K, device=dev)
+    db = torch.ones(C, device=dev)
+    _lib.call("mms_small_linear_bwd", X.data_ptr(), X.stride(0), M, K, W.data_ptr(), C, act, beta, thr, Y.data_ptr(),
+              Y.stride(0), dY.data_ptr(), dY.stride(0), dX.data_ptr(), dX.stride(0), 1, dW.data_ptr(), db.data_ptr(), s)
+    torch.cuda.synchronize()
+    y = ref
+    dact = {0: torch.ones_like(y), 1: (y > 0).double(), 2: 1 - torch.exp(-beta * y), 3: y * (1 - y)}[act]
+    dz = dY.double().cpu() * dact
+    rdx = dX0.double() + dz @ Wd
+    rdw = 1 + dz.T @ Xd
+    rdb = 1 + dz.sum(0)
+    for got, want, name in ((dX, rdx, "dX"), (dW, rdw, "dW"), (db, rdb, "db")):
+        e = ((got.double().cpu() - want).abs().max() / want.abs().max()).item()
+        assert e < 1e-5, f"{name}: rel err {e:.2e}"
