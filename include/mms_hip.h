@@ -342,6 +342,11 @@ int mms_geo_loss_bwd_masked(const float* grads, const float* hess, int64_t M, in
                             const int64_t* counts_all, int n_counts, const float* deik, float eik_scale,
                             const float* dcurv, float curv_scale, float* dgrads, float* dhess, void* stream);
 
+/* out[0] = sum_i x[i] * w[i] in index order (device x[n], host weights w[n], n <= 16): the total training loss from
+ * its terms, LossManager.compute_loss's weighted sum (losses.py:224-265; weights 1 per L1 term, 0.1 eikonal,
+ * 5e-4 x schedule curvature, method_configs.py:252-253). */
+int mms_weighted_sum(const float* x, int n, const float* w, float* out, void* stream);
+
 /* ---- optimizer (pipelines/base_pipeline.py:232-248 clip_gradients, torch.optim.AdamW single-tensor step,
  * method_configs.py:260-269): acc += sum x^2 ; AdamW with clip coefficient min(1, max_norm / (sqrt(*sumsq) + 1e-6))
  * read on device.  lr / wd / betas / eps are torch.optim.AdamW's hyper-parameters, step the optimizer's step count

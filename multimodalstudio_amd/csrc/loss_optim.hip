@@ -320,3 +320,26 @@ MMS_EXPORT int mms_adamw_dev(float* p, const float* g, float* m, float* v, int64
                      v, n, sumsq, max_norm, hyper);
   return mms::check_launch(fn);
 }
+
+namespace {
+struct WSumArgs {
+  float w[16];
+};
+// total = ((x0 w0 + x1 w1) + x2 w2) + ...: the reference's left-to-right sum of the weighted loss terms
+// (LossManager.compute_loss, losses.py:224-265), one lane
+__global__ void weighted_sum_kernel(const float* __restrict__ x, int n, WSumArgs a, float* __restrict__ out) {
+  float t = x[0] * a.w[0];
+  for (int i = 1; i < n; ++i) t += x[i] * a.w[i];
+  out[0] = t;
+}
+}  // namespace
+
+MMS_EXPORT int mms_weighted_sum(const float* x, int n, const float* w, float* out, void* stream) {
+  const char* fn = "mms_weighted_sum";
+  MMS_REQUIRE(n >= 1 && n <= 16, fn, "1 to 16 terms");
+  MMS_REQUIRE(x && w && out, fn, "null pointer");
+  WSumArgs a{};
+  for (int i = 0; i < n; ++i) a.w[i] = w[i];
+  hipLaunchKernelGGL(weighted_sum_kernel, dim3(1), dim3(1), 0, mms::as_stream(stream), x, n, a, out);
+  return mms::check_launch(fn);
+}

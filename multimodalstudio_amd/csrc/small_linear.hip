@@ -100,6 +100,8 @@ __global__ __launch_bounds__(256) void small_linear_bwd_kernel(const float* __re
 #pragma unroll
     for (int j = 0; j < KC; ++j) acc[c][j] = 0.f;
   }
+  // the block's rows are interleaved with the other blocks' (stride gridDim.x * 16); blocks_for_bwd sizes the grid so
+  // each lane walks only a few rows and many rows' loads are in flight at once
   for (int64_t m = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; m < M; m += (int64_t)gridDim.x * 16) {
     float dz[CM];
 #pragma unroll
@@ -190,6 +192,21 @@ unsigned blocks_for(int64_t M) {
   return (unsigned)(b < 1 ? 1 : b);
 }
 
+// backward: about two rows per lane group (each block reduces its dW partials once, C K atomics per block)
+unsigned blocks_for_bwd(int64_t M) {
+  int64_t b = (M + 31) / 32;
+  if (b > 2048) b = 2048;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+template <int KC, int CM>
+void launch_bwd(unsigned g, hipStream_t s, const float* X, int64_t ldx, int64_t M, const float* W, int C, int act,
+                float beta, float thr, const float* Y, int64_t ldy, const float* dY, int64_t lddy, float* dX,
+                int64_t lddx, int accumulate, float* dW, float* db) {
+  hipLaunchKernelGGL((small_linear_bwd_kernel<KC, CM>), dim3(g), dim3(256), 0, s, X, ldx, M, W, C, act, beta, thr, Y,
+                     ldy, dY, lddy, dX, lddx, accumulate, dW, db);
+}
+
 }  // namespace
 
 MMS_EXPORT int mms_small_linear_fwd(const float* X, int64_t ldx, int64_t M, int K, const float* W, const float* b,
@@ -225,16 +242,18 @@ MMS_EXPORT int mms_small_linear_bwd(const float* X, int64_t ldx, int64_t M, int 
   MMS_REQUIRE(dW == nullptr || (X && aligned16(X) && ldx % 4 == 0 && ldx >= K), fn, "input rows must be 16-B aligned");
   MMS_REQUIRE(dX == nullptr || (aligned16(dX) && lddx % 4 == 0 && lddx >= K), fn, "dX rows must be 16-B aligned");
   hipStream_t s = mms::as_stream(stream);
-  const unsigned g = blocks_for(M);
-  if (K == 128)
-    hipLaunchKernelGGL((small_linear_bwd_kernel<8, 16>), dim3(g), dim3(256), 0, s, X, ldx, M, W, C, act, beta, thr, Y,
-                       ldy, dY, lddy, dX, lddx, accumulate, dW, db);
-  else if (K == 256)
-    hipLaunchKernelGGL((small_linear_bwd_kernel<16, 8>), dim3(g), dim3(256), 0, s, X, ldx, M, W, C, act, beta, thr, Y,
-                       ldy, dY, lddy, dX, lddx, accumulate, dW, db);
-  else
-    hipLaunchKernelGGL((small_linear_bwd_kernel<32, 4>), dim3(g), dim3(256), 0, s, X, ldx, M, W, C, act, beta, thr, Y,
-                       ldy, dY, lddy, dX, lddx, accumulate, dW, db);
+  const unsigned g = blocks_for_bwd(M);
+  // the per-lane partials are CM x KC registers: CM = the smallest of 1 / 4 / (8, 16) that holds C
+#define MMS_SL_BWD(KC, CM) launch_bwd<KC, CM>(g, s, X, ldx, M, W, C, act, beta, thr, Y, ldy, dY, lddy, dX, lddx, \
+                                              accumulate, dW, db)
+  if (K == 128) {
+    if (C == 1) MMS_SL_BWD(8, 1); else if (C <= 4) MMS_SL_BWD(8, 4); else MMS_SL_BWD(8, 16);
+  } else if (K == 256) {
+    if (C == 1) MMS_SL_BWD(16, 1); else if (C <= 4) MMS_SL_BWD(16, 4); else MMS_SL_BWD(16, 8);
+  } else {
+    if (C == 1) MMS_SL_BWD(32, 1); else MMS_SL_BWD(32, 4);
+  }
+#undef MMS_SL_BWD
   return mms::check_launch(fn);
 }
 

@@ -2025,6 +2025,91 @@ class GeoLossSegFunction(torch.autograd.Function):
         return None, None, None, dg.view(gs), (dh.view(hs) if dh is not None else None)
 
 
+class StepLossFunction(torch.autograd.Function):
+    """The whole training loss of a batched hit set in one autograd node (LossManager.compute_loss, losses.py:213-265):
+    per modality nn.L1Loss(mean) with the polarization SkipSaturation fill (:152-164), the eikonal MSE and curvature L1
+    over every modality's rows (:107-150, GeoLossSegFunction's kernels), total = sum of L1 terms + 0.1 eik + w_curv
+    curv (method_configs.py:252-253) -- the terms land in one device buffer and one launch forms the total; the
+    backward hands each term's kernel the total's gradient with its weight as the scale, so none of the scalar
+    add / mul nodes (and their backward launches) exist.  Returns (total, terms [n_mod + 2], not differentiable)."""
+
+    @staticmethod
+    def forward(ctx, n_mod: int, sat_thrs, w_curv: float, S: int, counts, seg_rays: int, grads, hess, *outs_targets):
+        ctx.set_materialize_grads(False)
+        outs, targets = outs_targets[:n_mod], outs_targets[n_mod:]
+        dev = grads.device
+        terms = torch.zeros(n_mod + 2, device=dev)
+        saved, scr = [], []
+        for i in range(n_mod):
+            o, t = outs[i], targets[i].contiguous()
+            o = o if o.stride(1) == 1 else o.contiguous()
+            N, C = t.shape
+            thr = sat_thrs[i]
+            sc = torch.empty(1, dtype=torch.int64, device=dev) if thr is not None else None
+            _lib.call("mms_l1_loss_fwd", o.data_ptr(), o.stride(0), t.data_ptr(), N, C, 0.0 if thr is None else thr,
+                      _p(sc), terms[i:].data_ptr(), _s())
+            saved += [o, t]
+            scr.append(sc)
+        g = grads.reshape(-1, 3).contiguous()
+        h = hess.reshape(-1, 3).contiguous() if hess is not None else None
+        M = g.shape[0]
+        eik, curv = terms[n_mod:], terms[n_mod + 1:]
+        if counts is None:
+            _lib.call("mms_geo_loss_fwd", g.data_ptr(), _p(h), M, 1.0 / float(max(M, 1)), eik.data_ptr(),
+                      curv.data_ptr(), _s())
+        else:
+            n = counts.shape[0]
+            rows = seg_rays * S
+            for m in range(n):
+                _lib.call("mms_geo_loss_fwd_masked", g[m * rows:].data_ptr(),
+                          _p(None if h is None else h[m * rows:]), rows, S, counts[m:].data_ptr(), counts.data_ptr(),
+                          n, eik.data_ptr(), curv.data_ptr(), _s())
+        w = [1.0] * n_mod + [0.1] + ([float(w_curv)] if h is not None else [])
+        total = torch.empty((), device=dev)
+        _lib.call("mms_weighted_sum", terms.data_ptr(), len(w), _f32arr(w), total.data_ptr(), _s())
+        ctx.mark_non_differentiable(terms)
+        ctx.save_for_backward(g, h, counts, *saved)
+        ctx.n_mod, ctx.sat, ctx.scr, ctx.w_curv, ctx.S, ctx.seg_rays = n_mod, sat_thrs, scr, float(w_curv), S, seg_rays
+        ctx.shape = (tuple(grads.shape), None if hess is None else tuple(hess.shape))
+        ctx.out_shapes = [tuple(o.shape) for o in outs]
+        return total, terms
+
+    @staticmethod
+    def backward(ctx, dtotal, dterms):
+        g, h, counts, *saved = ctx.saved_tensors
+        n_mod = ctx.n_mod
+        dev = g.device
+        if dtotal is None:
+            return (None,) * (8 + 2 * n_mod)
+        dl = dtotal.contiguous()
+        douts = []
+        for i in range(n_mod):
+            o, t = saved[2 * i], saved[2 * i + 1]
+            N, C = t.shape
+            thr = ctx.sat[i]
+            d = _zeroed_views([ctx.out_shapes[i]], dev)[0]
+            _lib.call("mms_l1_loss_bwd", o.data_ptr(), o.stride(0), t.data_ptr(), N, C, 0.0 if thr is None else thr,
+                      _p(ctx.scr[i]), dl.data_ptr(), 1.0, d.data_ptr(), d.stride(0), _s())
+            douts.append(d)
+        M = g.shape[0]
+        dg, dh = _zeroed_views([(M, 3), (M, 3) if h is not None else None], dev)
+        S = ctx.S
+        if counts is None:
+            _lib.call("mms_geo_loss_bwd", g.data_ptr(), _p(h), M, 1.0 / float(max(M, 1)), dl.data_ptr(), 0.1,
+                      dl.data_ptr(), ctx.w_curv, dg.data_ptr(), _p(dh), _s())
+        else:
+            n = counts.shape[0]
+            rows = ctx.seg_rays * S
+            for m in range(n):
+                _lib.call("mms_geo_loss_bwd_masked", g[m * rows:].data_ptr(), _p(None if h is None else h[m * rows:]),
+                          rows, S, counts[m:].data_ptr(), counts.data_ptr(), n, dl.data_ptr(), 0.1, dl.data_ptr(),
+                          ctx.w_curv, dg[m * rows:].data_ptr(), _p(None if dh is None else dh[m * rows:]), _s())
+        gs, hs = ctx.shape
+        ctx.scr = None
+        return (None, None, None, None, None, None, dg.view(gs), (dh.view(hs) if dh is not None else None),
+                *douts, *([None] * n_mod))
+
+
 def HashGridApply(x, table, cfg: GridCfg, active: int):
     """Standalone FeatureGrid forward (feature_structures.py:78-83) with autograd to x and table."""
     from .hip_ops import HashGridFunction

@@ -172,7 +172,9 @@ def gemm_tn_grouped(items, prec: int, target_blocks: Optional[int] = None, engin
     I64 = ctypes.c_int64 * n
     VP = ctypes.c_void_p * n
     engine = engine or TN_ENGINE
-    wide = engine == "wide" and int(prec) in (1, 2) and all(_aligned_item(it) for it in items)
+    # the wide engine's 256-row tiles pay for MLPs with 256-wide layers; the 64-wide modality heads stay on 128 tiles
+    wide = engine == "wide" and int(prec) in (1, 2) and all(_aligned_item(it) for it in items) and \
+        max(it[0] for it in items) >= 128
     if wide:
         entry = "mms_gemm_tn_wide"
         target = int(os.environ.get("MMS_TN_BLOCKS", "0")) or target_blocks or _WIDE_BLOCKS

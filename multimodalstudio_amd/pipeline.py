@@ -9,6 +9,7 @@ gradient all-reduce (ddp.py) is a handful of large RCCL calls instead of one per
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -218,10 +219,31 @@ def curvature_factor(step: int, max_iters: int = 100000, num_levels=16, min_res=
 # ------------------------------------------------------------------------------------------------
 # losses
 # ------------------------------------------------------------------------------------------------
+# one autograd node for the whole loss of the batched model (MMS_FUSED_LOSS=0: per-term nodes + Python arithmetic)
+FUSED_LOSS = os.environ.get("MMS_FUSED_LOSS", "1") != "0"
+
+
 def compute_loss(outputs, targets: Dict[str, torch.Tensor], modalities: List[str], step: int,
                  sat_threshold: float = 0.9980, max_iters: int = 100000):
     """LossManager.compute_loss (losses.py:224-265) for the grid / grid_raw configs.  ``max_iters`` is the run's
     num_iterations: the curvature weight's warm-up / level schedule follows it (schedulers.py:320-343)."""
+    geo = outputs[modalities[0]].get("_geo")
+    analytic = outputs[modalities[0]]["hessians"] is None
+    if FUSED_LOSS and geo is not None and tuple(geo["mods"]) == tuple(modalities) and \
+            all(outputs[m].get("_geo") is geo for m in modalities):
+        # the model's batched geometry: every term and the total in one autograd node (functions.StepLossFunction)
+        n = len(modalities)
+        sat = [sat_threshold if m == "polarization" else None for m in modalities]
+        w_curv = 0.0 if analytic else 5e-4 * curvature_factor(step, max_iters)
+        total, terms = fx.StepLossFunction.apply(n, sat, w_curv, geo["S"], geo["counts"], geo["seg_rays"],
+                                                 geo["grads"], None if analytic else geo["hess"],
+                                                 *[outputs[m][m] for m in modalities],
+                                                 *[targets[m] for m in modalities])
+        losses = {m: terms[i] for i, m in enumerate(modalities)}
+        losses["eikonal_loss"] = terms[n]
+        if not analytic:
+            losses["curvature_loss"] = terms[n + 1]
+        return losses, total
     losses = {}
     total = None
     for mod in modalities:

@@ -1,0 +1,13 @@
+#!/bin/bash
+# converged PSNR runs (grid_raw5, 3000 steps = the whole schedule, FullViewEvaluator on 5 held-out views)
+# usage: bash scripts/gpu_conv.sh "fast:1 fast:2 fp32:4 ..."
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+set -e
+for job in $1; do
+  p=${job%%:*}; s=${job##*:}
+  timeout -k 10 300 python -u scripts/converge_psnr.py --precision $p --steps 3000 --max-iters 3000 --eval-every 3000 \
+    --seed $s --out gpurun_out/conv3k_${p}_s$s.json > gpurun_out/conv3k_${p}_s$s.log 2>&1
+done

@@ -39,7 +39,8 @@ def label(name, grid=0):
     m = re.search(r"gemm_kernel<(\d), (true|false), (true|false), (true|false)>", name)
     if m:
         return f"mms_gemm:{PREC[m.group(1)]}:{MODE.get((m.group(2), m.group(3)), '??')}"
-    m = re.search(r"chain_kernel<(\d), (\d+), \d+, \d+, (\d+), (true|false), \d, \d, \d, \d, (true|false), (\d)>", name)
+    m = re.search(r"chain_kernel<(\d), (\d+), \d+, \d+, (\d+), (true|false), \d, \d, \d, \d, (true|false), (\d)(?:, \d)?>",
+                  name)
     if m:
         key = (m.group(4) == "true", int(m.group(2)), int(m.group(3)), int(m.group(6)), m.group(5) == "true")
         return f"mms_mlp_chain:{PREC[m.group(1)]}:{CHAIN_ROLES.get(key, 'other')}"

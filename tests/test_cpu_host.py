@@ -96,7 +96,8 @@ def test_compute_loss_uses_the_runs_max_iters():
     import inspect
     from multimodalstudio_amd import pipeline
     assert "curvature_factor(step, max_iters)" in inspect.getsource(pipeline._finish_loss)
-    assert inspect.getsource(pipeline.compute_loss).count("step, max_iters)") == 2   # both geometry-loss paths
+    # the fused step-loss node and both per-term geometry-loss paths
+    assert inspect.getsource(pipeline.compute_loss).count("step, max_iters)") == 3
     assert "max_iters=self.cfg.max_iters" in inspect.getsource(pipeline.Trainer._compute_grads)
     from multimodalstudio_amd import graphs
     assert "max_iters=t.cfg.max_iters" in inspect.getsource(graphs.GraphTrainer._forward_backward_body)

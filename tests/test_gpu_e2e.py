@@ -164,7 +164,8 @@ def test_e2e_train_step(dev, name):
 
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000", "e2e_grid_raw_5mod_sat_s95000"])
 def test_e2e_fast_preset_deviation(dev, name):
-    """The benchmarked `fast` preset (SDF MLP split-bf16x3, everything else bf16 MFMA) on the reference's fixture:
+    """The benchmarked `fast` preset (every MLP on split-bf16x3 MFMA operands, the narrow background layers fp32 VALU)
+    on the reference's fixture:
     per-modality rendered-radiance deviation, reported and bounded (bf16 is judged by PSNR parity,
     tests/test_gpu_train_parity.py, plus this measured deviation; the reference's own fp16 autocast is ~1e-3 mean rel
     and bf16 5e-3 .. 2.5e-2).  Relative to max(|ref|, 1e-2) per element (polarization channels sit near 0)."""
@@ -182,16 +183,17 @@ def test_e2e_fast_preset_deviation(dev, name):
         ref = f[f"{m}:out:{m}"].astype(np.float64)
         rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-2)
         print(f"  {m:14s} radiance rel dev: mean {rel.mean():.3e}  max {rel.max():.3e}")
-        # about 10x the measured deviation: polarization intensities are differences of Stokes terms
-        assert rel.mean() < (1e-2 if m == "polarization" else 2e-3), (m, rel.mean())
-        assert rel.max() < 0.1, (m, rel.max())
+        # about 10x the measured deviation (round 3, every MLP split-bf16x3: mean <= 2.4e-5, polarization 3.8e-4 --
+        # its intensities are differences of Stokes terms --, max 2.4e-3)
+        assert rel.mean() < (4e-3 if m == "polarization" else 3e-4), (m, rel.mean())
+        assert rel.max() < 2.5e-2, (m, rel.max())
         # the geometry the eikonal / curvature losses see: 4-tap SDF gradients and hessians (second differences over
         # delta^2 ~ 1.3e-6, so any activation rounding that differs between the centre and the tap rows shows here)
         for k in ("gradients", "hessians"):
             e = rel_err(outs[m][k].detach().cpu(), f[f"{m}:out:{k}"])
             print(f"  {m:14s} {k} rel err {e:.3e}")
             assert e < GEO_TOL_FAST[k], (m, k, e)
-    assert loss_rel < 2e-2
+    assert loss_rel < 2e-4   # measured <= 1.6e-5
 
 
 # fast preset geometry bounds (fp32 mode: gradients 2e-3, hessians 0.15)

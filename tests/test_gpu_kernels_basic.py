@@ -316,7 +316,7 @@ def test_gemm_tn_grouped(dev, prec, tol, engine):
     assert err < tol, f"unaligned item prec={prec}: rel err {err:.2e}"
 
 
-@pytest.mark.parametrize("C,K,act", [(1, 256, 2), (9, 128, 3), (3, 128, 0), (4, 512, 1)])
+@pytest.mark.parametrize("C,K,act", [(1, 256, 2), (9, 128, 3), (3, 128, 0), (4, 512, 1), (1, 128, 3), (5, 256, 0)])
 def test_small_linear(dev, C, K, act):
     """mms_small_linear_fwd / _bwd (the background density head and 1-layer modality heads) vs fp64: a column view of
     a wider panel as input (row stride > K), accumulate into an existing dX, dW / db accumulation over ragged rows."""
