@@ -83,10 +83,13 @@ int mms_gemm_tn_grouped(int prec, int n, const int64_t* M, const int64_t* N, con
 
 /* The same weight gradients with 256 x 256 output tiles (blocks of 8 waves, every operand row read once per K slice),
  * bf16 (prec 1) or split bf16x3 (prec 2) operands, 16-B aligned operand rows; stage_rows = 16 or 32 rows per LDS
- * stage (72 / 144 KB of LDS for split bf16x3).  Same reference interface as mms_gemm_tn_grouped. */
+ * stage (72 / 144 KB of LDS for split bf16x3).  workspace (scratch, >= blocks x 65536 floats, blocks <= target_blocks
+ * + 16): the K slices' partial tiles are stored there and summed by a second launch in slice order instead of being
+ * added with float atomics; NULL (or too small): atomics.  Same reference interface as mms_gemm_tn_grouped. */
 int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const int64_t* K, const float* const* A,
                      const int64_t* lda, const float* const* B, const int64_t* ldb, float* const* C,
-                     const int64_t* ldc, float* const* colsum, int target_blocks, int stage_rows, void* stream);
+                     const int64_t* ldc, float* const* colsum, int target_blocks, int stage_rows, float* workspace,
+                     int64_t workspace_floats, void* stream);
 
 /* ---- fused MLP chains (MLP.forward mlp.py:152-171 under weight norm :206-209, all layers in one launch) for the
  * SDF field (71-256-256-257, Softplus(100), surface_field.py:99-116), the radiance field (317-256-256-256, ReLU,

@@ -466,6 +466,8 @@ struct WideItem {
 struct WideGroup {
   WideItem it[kMaxTnItems];
   int n;
+  float* ws;         // non-null: each block stores its partial tile here ([block][256][256]) for the reduce kernel,
+                     // instead of adding it to C with float atomics
 };
 
 template <int PREC, int WK>
@@ -603,21 +605,52 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
     }
   }
   // C/D map: column = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+  float* part = g.ws != nullptr ? g.ws + (int64_t)blockIdx.x * (kWT * kWT) : nullptr;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     if (!act_i[i]) continue;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (!act_j[j]) continue;
-      const int64_t col = n0 + 128 * wn + 32 * j + (lane & 31);
-      const int64_t rb0 = m0 + 64 * wm + 32 * i + 4 * (lane >> 5);
+      const int tc = 128 * wn + 32 * j + (lane & 31);
+      const int tr0 = 64 * wm + 32 * i + 4 * (lane >> 5);
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int64_t row = rb0 + (e & 3) + 8 * (e >> 2);
-        if (row < t.M && col < t.N) atomicAdd(t.C + row * t.ldc + col, acc[i][j][e]);
+        const int tr = tr0 + (e & 3) + 8 * (e >> 2);
+        if (part != nullptr) {
+          part[tr * kWT + tc] = acc[i][j][e];    // 128-B row segments per instruction: plain, coalesced stores
+        } else if (m0 + tr < t.M && n0 + tc < t.N) {
+          atomicAdd(t.C + (m0 + tr) * t.ldc + n0 + tc, acc[i][j][e]);
+        }
       }
     }
   }
+}
+
+// The slices' partial tiles summed per output element in slice order and added to C: one thread per element of a tile,
+// blockIdx.y = the tile (over every item of the group), reads coalesced across the block; one float atomic per output
+// element and item (instead of one per element and slice).
+// Only the wave-tiles the wide kernel computed are read (the others it did not write).
+__global__ __launch_bounds__(256) void gemm_tn_wide_reduce_kernel(WideGroup g) {
+  int tile = blockIdx.y, ii = 0, base = 0;
+  while (ii + 1 < g.n && tile >= g.it[ii].mt * g.it[ii].nt) {
+    tile -= g.it[ii].mt * g.it[ii].nt;
+    base += g.it[ii].blocks;
+    ++ii;
+  }
+  const WideItem& t = g.it[ii];
+  const int tiles = t.mt * t.nt;
+  const int64_t m0 = (int64_t)(tile % t.mt) * kWT, n0 = (int64_t)(tile / t.mt) * kWT;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int tr = e / kWT, tc = e % kWT;
+  // the kernel above skips whole 32 x 32 wave-tiles past M / N: only elements inside the written tiles are read
+  const bool in_tile = m0 + (tr & ~31) < t.M && n0 + (tc & ~31) < t.N;
+  if (!in_tile || m0 + tr >= t.M || n0 + tc >= t.N) return;
+  const float* p = g.ws + (int64_t)(base + tile) * (kWT * kWT) + e;
+  float v = 0.f;
+  for (int sl = 0; sl < t.zs; ++sl) v += p[(int64_t)sl * tiles * (kWT * kWT)];
+  // an atomic add: items of one launch may share an output (the SDF taps item adds into the last layer's dW row 0)
+  atomicAdd(t.C + (m0 + tr) * t.ldc + n0 + tc, v);
 }
 
 template <int PREC, bool TA, bool TB>
@@ -754,7 +787,7 @@ MMS_EXPORT int mms_gemm_tn_grouped(int prec, int n, const int64_t* M, const int6
 MMS_EXPORT int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const int64_t* K,
                                 const float* const* A, const int64_t* lda, const float* const* B, const int64_t* ldb,
                                 float* const* C, const int64_t* ldc, float* const* colsum, int target_blocks,
-                                int stage_rows, void* stream) {
+                                int stage_rows, float* workspace, int64_t workspace_floats, void* stream) {
   const char* fn = "mms_gemm_tn_wide";
   MMS_REQUIRE(stage_rows == 16 || stage_rows == 32, fn, "stage_rows must be 16 or 32");
   MMS_REQUIRE(prec == 1 || prec == 2, fn, "prec must be 1 (bf16) or 2 (bf16x3)");
@@ -798,6 +831,10 @@ MMS_EXPORT int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t
   if (m == 0) return 0;
   MMS_REQUIRE(total <= INT32_MAX, fn, "grid too large");
   hipStream_t s = mms::as_stream(stream);
+  // partial tiles through the workspace when it holds them all (else float atomics into C)
+  g.ws = (workspace != nullptr && workspace_floats >= total * (int64_t)(kWT * kWT)) ? workspace : nullptr;
+  int all_tiles = 0;
+  for (int i = 0; i < m; ++i) all_tiles += g.it[i].mt * g.it[i].nt;
   const dim3 grid((unsigned)total), blk(512);
   if (stage_rows == 32) {
     if (prec == P_BF16) hipLaunchKernelGGL((gemm_tn_wide_kernel<P_BF16, 32>), grid, blk, 0, s, g);
@@ -806,5 +843,7 @@ MMS_EXPORT int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t
     if (prec == P_BF16) hipLaunchKernelGGL((gemm_tn_wide_kernel<P_BF16, 16>), grid, blk, 0, s, g);
     else hipLaunchKernelGGL((gemm_tn_wide_kernel<P_BF16X3, 16>), grid, blk, 0, s, g);
   }
+  if (g.ws != nullptr)
+    hipLaunchKernelGGL(gemm_tn_wide_reduce_kernel, dim3(kWT * kWT / 256, all_tiles), dim3(256), 0, s, g);
   return mms::check_launch(fn);
 }

@@ -157,8 +157,20 @@ __device__ __forceinline__ float wave_sum_to_63(float v) {
 // neighbours -- shared corners sit in different corner slots of the two points) and consecutive samples of a ray
 // share cells at the coarse ones.  On the hash_bench geometry this is ~3.9 M line requests per SDF batch instead of
 // the per-lane pending merge's 9.3 M.  A line that finds no slot within kMaxProbe probes goes straight to memory.
-constexpr int kLines = 512;
-constexpr int kLogLines = 9;
+// Diagnostic variant builds (scripts/hash_variants.py compiles them separately; the product library uses the
+// defaults): MMS_HASH_LOG_LINES = log2 of the merge-table lines, MMS_HASH_CH5 = samples per block of the SDF batch,
+// MMS_HASH_FINE = first level whose pending gradients go straight to memory instead of through the LDS merge.
+#ifndef MMS_HASH_LOG_LINES
+#define MMS_HASH_LOG_LINES 9
+#endif
+#ifndef MMS_HASH_CH5
+#define MMS_HASH_CH5 4
+#endif
+#ifndef MMS_HASH_FINE
+#define MMS_HASH_FINE 12
+#endif
+constexpr int kLogLines = MMS_HASH_LOG_LINES;
+constexpr int kLines = 1 << kLogLines;
 constexpr int kMaxProbe = 32;
 constexpr uint32_t kEmpty = 0xffffffffu;
 
@@ -270,7 +282,10 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
         if (idx == pidx) {
           pacc += df;
         } else {
-          if (pacc != 0.f) merge_add(skeys, vals, dtable, pidx, feat, pacc);
+          if (pacc != 0.f) {
+            if (level >= MMS_HASH_FINE) atomicAdd(dtable + 2 * (int64_t)pidx + feat, pacc);
+            else merge_add(skeys, vals, dtable, pidx, feat, pacc);
+          }
           pidx = idx;
           pacc = df;
         }
@@ -296,7 +311,10 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
         }
       }
     }
-    if (dtable != nullptr && pacc != 0.f) merge_add(skeys, vals, dtable, pidx, feat, pacc);
+    if (dtable != nullptr && pacc != 0.f) {
+      if (level >= MMS_HASH_FINE) atomicAdd(dtable + 2 * (int64_t)pidx + feat, pacc);
+      else merge_add(skeys, vals, dtable, pidx, feat, pacc);
+    }
   }
   __syncthreads();
   if (dtable != nullptr) {
@@ -465,7 +483,7 @@ MMS_EXPORT int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group,
   MMS_REQUIRE(pos && table && dout, fn, "null pointer");
   // CH: about 260 touched lines per block on the SDF batch (kLines = 512 merge slots: 4 blocks per CU)
   if (group == 5) {
-    constexpr int CH = 4;
+    constexpr int CH = MMS_HASH_CH5;
     hipLaunchKernelGGL((hashgrid_bwd_walk_kernel<5, CH>), dim3(mms::grid_for(Mg, CH, INT32_MAX)), dim3(256), 0,
                        mms::as_stream(stream), pos, Mg, gstride, ldx, table, p, dout, ldd, dtable, dpos, lddx);
   } else {

@@ -157,6 +157,7 @@ _GROUP_BLOCKS = {0: 1024, 1: 256, 2: 512}
 TN_ENGINE = os.environ.get("MMS_TN_ENGINE", "wide")
 _WIDE_BLOCKS = 256
 TN_STAGE_ROWS = int(os.environ.get("MMS_TN_STAGE", "16"))
+TN_WORKSPACE = os.environ.get("MMS_TN_WS", "0") == "1"
 
 
 def _aligned_item(it) -> bool:
@@ -181,10 +182,16 @@ def gemm_tn_grouped(items, prec: int, target_blocks: Optional[int] = None, engin
     else:
         entry = "mms_gemm_tn_grouped"
         target = int(os.environ.get("MMS_TN_BLOCKS", "0")) or target_blocks or _GROUP_BLOCKS.get(int(prec), 512)
+    extra = ()
+    if wide:
+        # the slices' partial tiles go through a scratch buffer and a deterministic reduce launch (plain stores instead
+        # of 256 KB of float atomics per block); MMS_TN_WS=0 keeps the atomics
+        ws = torch.empty((target + 16) * 65536, device=items[0][3].device) if TN_WORKSPACE else None
+        extra = (int(stage_rows or TN_STAGE_ROWS), None if ws is None else ws.data_ptr(),
+                 0 if ws is None else ws.numel())
     _lib.call(entry, int(prec), n, I64(*[it[0] for it in items]), I64(*[it[1] for it in items]),
               I64(*[it[2] for it in items]), VP(*[it[3].data_ptr() for it in items]),
               I64(*[it[3].stride(0) for it in items]), VP(*[it[4].data_ptr() for it in items]),
               I64(*[it[4].stride(0) for it in items]), VP(*[it[5].data_ptr() for it in items]),
               I64(*[it[5].stride(0) for it in items]),
-              VP(*[(it[6].data_ptr() if it[6] is not None else None) for it in items]), target,
-              *((int(stage_rows or TN_STAGE_ROWS),) if wide else ()), _stream())
+              VP(*[(it[6].data_ptr() if it[6] is not None else None) for it in items]), target, *extra, _stream())

@@ -48,20 +48,24 @@ def main():
             db = torch.zeros(N, device=dev)
             items.append((N, K, R, dZ, X, dW, db))
             nbytes += R * 4 * (N + K)
-        for prec in (2, 1):
+        for prec in (2,):
             outs = {}
-            for engine, sr, targets in (("tiled", None, (None,)), ("wide", 32, (256, 512)), ("wide", 16, (256, 384, 512))):
+            for engine, sr, targets in (("tiled", None, (None,)), ("wide", 16, (256, 512)), ("wide-ws", 16, (256, 512))):
+                hip_ops.TN_WORKSPACE = engine == "wide-ws"
+                engine = "wide" if engine == "wide-ws" else engine
                 for tb in targets:
                     for it in items:
                         it[5].zero_()
                     run = lambda: hip_ops.gemm_tn_grouped(items, prec, target_blocks=tb, engine=engine, stage_rows=sr)
                     run()
                     torch.cuda.synchronize()
-                    outs[(engine, sr, tb)] = [it[5].clone() for it in items]
+                    outs[(engine, sr, tb, hip_ops.TN_WORKSPACE)] = [it[5].clone() for it in items]
                     us = timeit(run)
-                    ref = outs[("tiled", None, None)]
-                    err = max(((a - b).abs().max() / b.abs().max()).item() for a, b in zip(outs[(engine, sr, tb)], ref))
-                    print(f"{name:9s} prec {prec} {engine:5s}/{str(sr):4s} blocks {str(tb):5s} {us:8.1f} us "
+                    ref = outs[("tiled", None, None, False)]
+                    err = max(((a - b).abs().max() / b.abs().max()).item()
+                              for a, b in zip(outs[(engine, sr, tb, hip_ops.TN_WORKSPACE)], ref))
+                    tag = engine + ("+ws" if engine == "wide" and hip_ops.TN_WORKSPACE else "")
+                    print(f"{name:9s} prec {prec} {tag:8s}/{str(sr):4s} blocks {str(tb):5s} {us:8.1f} us "
                           f"{nbytes / us / 1e3:7.1f} GB/s algorithmic  (vs tiled: {err:.1e})", flush=True)
 
 

@@ -263,15 +263,17 @@ def test_gemm_tall_skinny_epilogues(dev, prec, tol, M, N, K):
     assert e < tol, e
 
 
-@pytest.mark.parametrize("prec,tol,engine", [(0, 2e-6, "tiled"), (2, 2e-5, "tiled"), (1, 2e-2, "tiled"),
-                                             (2, 2e-5, "wide"), (1, 2e-2, "wide")])
-def test_gemm_tn_grouped(dev, prec, tol, engine):
+@pytest.mark.parametrize("prec,tol,engine,ws", [(0, 2e-6, "tiled", True), (2, 2e-5, "tiled", True),
+                                                (1, 2e-2, "tiled", True), (2, 2e-5, "wide", True),
+                                                (1, 2e-2, "wide", True), (2, 2e-5, "wide", False)])
+def test_gemm_tn_grouped(dev, prec, tol, engine, ws, monkeypatch):
     """mms_gemm_tn_grouped / mms_gemm_tn_wide: several layers' weight gradients (+ bias column sums) in one launch vs
     fp64 -- ragged widths (257 outputs: two 256-row tiles; 317 inputs: two column tiles), a single-column item sharing
     its dW with a full item (the SDF taps), unaligned rows (the tiled engine's scalar staging; the wide engine's
     caller falls back to it), and slices long enough for the k-loop to wrap several times."""
     from multimodalstudio_amd import hip_ops
     from multimodalstudio_amd.functions import _alloc
+    monkeypatch.setattr(hip_ops, "TN_WORKSPACE", ws)   # wide engine: partial tiles via the workspace, or atomics
     g = torch.Generator().manual_seed(11 + prec)
     specs = [(256, 71, 30000), (256, 256, 30000), (257, 256, 9000), (130, 317, 20000)]
     items, refs = [], []
