@@ -159,7 +159,8 @@ __device__ __forceinline__ float wave_sum_to_63(float v) {
 // the per-lane pending merge's 9.3 M.  A line that finds no slot within kMaxProbe probes goes straight to memory.
 // Diagnostic variant builds (scripts/hash_variants.py compiles them separately; the product library uses the
 // defaults): MMS_HASH_LOG_LINES = log2 of the merge-table lines, MMS_HASH_CH5 = samples per block of the SDF batch,
-// MMS_HASH_FINE = first level whose pending gradients go straight to memory instead of through the LDS merge.
+// MMS_HASH_FINE = first level whose pending gradients go straight to memory instead of through the LDS merge
+// (MMS_HASH_FINE1 / MMS_HASH_CH1: the same for the plain, one-row-per-point walk).
 #ifndef MMS_HASH_LOG_LINES
 #define MMS_HASH_LOG_LINES 9
 #endif
@@ -168,6 +169,12 @@ __device__ __forceinline__ float wave_sum_to_63(float v) {
 #endif
 #ifndef MMS_HASH_FINE
 #define MMS_HASH_FINE 12
+#endif
+#ifndef MMS_HASH_FINE1
+#define MMS_HASH_FINE1 MMS_HASH_FINE
+#endif
+#ifndef MMS_HASH_CH1
+#define MMS_HASH_CH1 8
 #endif
 constexpr int kLogLines = MMS_HASH_LOG_LINES;
 constexpr int kLines = 1 << kLogLines;
@@ -204,7 +211,7 @@ __device__ __forceinline__ void merge_add(uint32_t* keys, float* vals, float* __
 // instead of 4-B loads replicated over 8 lanes) in LDS.  Position gradients are summed over the wave's 4 levels x
 // 16 lanes by DPP moves (wave_sum_to_63) into a per-wave LDS slot -- plain stores, no LDS atomics -- and the 4 waves'
 // partials are added in wave order at the end: dpos is deterministic.
-template <int G, int CH>
+template <int G, int CH, int FINE>
 __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __restrict__ pos, int64_t Mg,
                                                                 int64_t gstride, int64_t ldx,
                                                                 const float* __restrict__ table, GridParams p,
@@ -283,7 +290,7 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
           pacc += df;
         } else {
           if (pacc != 0.f) {
-            if (level >= MMS_HASH_FINE) atomicAdd(dtable + 2 * (int64_t)pidx + feat, pacc);
+            if (level >= FINE) atomicAdd(dtable + 2 * (int64_t)pidx + feat, pacc);
             else merge_add(skeys, vals, dtable, pidx, feat, pacc);
           }
           pidx = idx;
@@ -312,7 +319,7 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
       }
     }
     if (dtable != nullptr && pacc != 0.f) {
-      if (level >= MMS_HASH_FINE) atomicAdd(dtable + 2 * (int64_t)pidx + feat, pacc);
+      if (level >= FINE) atomicAdd(dtable + 2 * (int64_t)pidx + feat, pacc);
       else merge_add(skeys, vals, dtable, pidx, feat, pacc);
     }
   }
@@ -484,11 +491,11 @@ MMS_EXPORT int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group,
   // CH: about 260 touched lines per block on the SDF batch (kLines = 512 merge slots: 4 blocks per CU)
   if (group == 5) {
     constexpr int CH = MMS_HASH_CH5;
-    hipLaunchKernelGGL((hashgrid_bwd_walk_kernel<5, CH>), dim3(mms::grid_for(Mg, CH, INT32_MAX)), dim3(256), 0,
+    hipLaunchKernelGGL((hashgrid_bwd_walk_kernel<5, CH, MMS_HASH_FINE>), dim3(mms::grid_for(Mg, CH, INT32_MAX)), dim3(256), 0,
                        mms::as_stream(stream), pos, Mg, gstride, ldx, table, p, dout, ldd, dtable, dpos, lddx);
   } else {
-    constexpr int CH = 8;
-    hipLaunchKernelGGL((hashgrid_bwd_walk_kernel<1, CH>), dim3(mms::grid_for(Mg, CH, INT32_MAX)), dim3(256), 0,
+    constexpr int CH = MMS_HASH_CH1;
+    hipLaunchKernelGGL((hashgrid_bwd_walk_kernel<1, CH, MMS_HASH_FINE1>), dim3(mms::grid_for(Mg, CH, INT32_MAX)), dim3(256), 0,
                        mms::as_stream(stream), pos, Mg, Mg, ldx, table, p, dout, ldd, dtable, dpos, lddx);
   }
   return mms::check_launch(fn);

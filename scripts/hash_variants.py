@@ -15,9 +15,13 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 OUT = ROOT / "multimodalstudio_amd" / "_variants"   # travels to the GPU box (scratch/ does not)
-VARIANTS = {  # name: (log2 lines, samples per block, first direct level)
+VARIANTS = {  # name: (log2 lines, samples per block, first direct level) of the SDF batch's [centre | 4 taps] walk
     "merge_all": (9, 4, 16), "fine14": (9, 4, 14), "fine13": (9, 4, 13), "fine12": (9, 4, 12), "fine11": (9, 4, 11),
     "ch2_fine12": (9, 2, 12), "ch8_fine12": (9, 8, 12), "l8_fine12": (8, 4, 12),
+}
+PLAIN = {  # name: (points per block, first direct level) of the plain walk (the radiance grid)
+    "p_ch8_f16": (8, 16), "p_ch8_f12": (8, 12), "p_ch8_f8": (8, 8), "p_ch8_f4": (8, 4), "p_ch8_f0": (8, 0),
+    "p_ch16_f8": (16, 8), "p_ch16_f4": (16, 4), "p_ch32_f4": (32, 4),
 }
 
 
@@ -28,6 +32,11 @@ def build():
     for name, (ll, ch, fine) in VARIANTS.items():
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-shared",
                "-munsafe-fp-atomics", f"-DMMS_HASH_LOG_LINES={ll}", f"-DMMS_HASH_CH5={ch}", f"-DMMS_HASH_FINE={fine}",
+               "-I", str(ROOT / "include"), str(src), "-o", str(OUT / f"hash_{name}.so")]
+        procs.append(subprocess.Popen(cmd))
+    for name, (ch, fine) in PLAIN.items():
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-shared",
+               "-munsafe-fp-atomics", f"-DMMS_HASH_CH1={ch}", f"-DMMS_HASH_FINE1={fine}",
                "-I", str(ROOT / "include"), str(src), "-o", str(OUT / f"hash_{name}.so")]
         procs.append(subprocess.Popen(cmd))
     for p in procs:
@@ -57,7 +66,9 @@ def run():
     dout = torch.randn(5 * M, 32, generator=g).to(dev)
     restype, argtypes = _lib.SIGNATURES["mms_hashgrid_bwd_grouped"]
     ref = None
-    for name in VARIANTS:
+    for name in list(VARIANTS) + list(PLAIN):
+        plain = name in PLAIN
+        G = 1 if plain else 5   # the plain walk runs the centre rows alone: the radiance grid's batch
         lib = ctypes.CDLL(str(OUT / f"hash_{name}.so"), mode=os.RTLD_LOCAL)
         fn = lib.mms_hashgrid_bwd_grouped
         fn.restype, fn.argtypes = restype, argtypes
@@ -65,14 +76,14 @@ def run():
         dpos = torch.zeros_like(x)
 
         def call():
-            rc = fn(x.data_ptr(), M, 5, M, 3, table.data_ptr(), L, log2T, 2, 0, cfg.scales_ptr, 1.0, L,
+            rc = fn(x.data_ptr(), M, G, M, 3, table.data_ptr(), L, log2T, 2, 0, cfg.scales_ptr, 1.0, L,
                     dout.data_ptr(), dout.stride(0), dtable.data_ptr(), dpos.data_ptr(), 3,
                     torch.cuda.current_stream().cuda_stream)
             assert rc == 0
         call()
         torch.cuda.synchronize()
         got = (dtable.clone(), dpos.clone())
-        if ref is None:
+        if ref is None or name == next(iter(PLAIN)):
             ref = got
         err = max(((a - b).abs().max() / b.abs().max()).item() for a, b in zip(got, ref))
         for _ in range(2):
@@ -84,7 +95,8 @@ def run():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 100.0
-        print(f"{name:12s} {VARIANTS[name]}  {us:8.1f} us  (vs {next(iter(VARIANTS))} {err:.1e})", flush=True)
+        first = next(iter(PLAIN if plain else VARIANTS))
+        print(f"{name:12s} {(PLAIN if plain else VARIANTS)[name]}  {us:8.1f} us  (vs {first} {err:.1e})", flush=True)
 
 
 if __name__ == "__main__":
