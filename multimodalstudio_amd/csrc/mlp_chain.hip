@@ -294,6 +294,14 @@ __device__ __forceinline__ void epi_tile(floatx16& acc, int t, const ChainLayer&
 // of the 4 store instructions writes 8 whole 128-B row segments.  Rows past M store row M - 1's values there again
 // (identical bits).  Still exactly 4 vector-memory instructions per lane (run_layer's counted waits).
 constexpr int kScr = 36;  // scratch row pitch (floats)
+#ifndef MMS_CHAIN_YAHEAD
+// backward epilogue: Y tiles loaded ahead (1 = one tile ahead, the round-3c kernel; scripts/chain_variants.py, step
+// A/B: SDF backward 370 -> 345 us at 2 or 4, radiance 165 at 1-4 but 177 at 8, where the 4-layer chains spill)
+#define MMS_CHAIN_YAHEAD 4
+#endif
+#ifndef MMS_CHAIN_YAHEAD4
+#define MMS_CHAIN_YAHEAD4 4  // the same for the 4-layer chains
+#endif
 
 template <int ACT, bool KEEP>
 __device__ __forceinline__ void epi_tile_full(floatx16& acc, int t, const float* sb, float* obase, int64_t ldo,
@@ -333,7 +341,7 @@ __device__ __forceinline__ void epi_tile_full(floatx16& acc, int t, const float*
 // per lane 4 rows x 4 columns per tile, reduced over the wave's rows by xor shuffles into the wave's LDS row `sp`
 // (plain LDS stores: nothing here adds a vector-memory instruction the k-loops' exact vmcnt waits would count); the
 // block writes its partial row once, at the end of the kernel.
-template <int NT, int ACT, bool TAPW = false>
+template <int NT, int ACT, bool TAPW = false, int YMAX = MMS_CHAIN_YAHEAD>
 __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const ChainLayer& Ly, int64_t m0, int64_t M,
                                                     float* scr, int lane, float beta, float thr,
                                                     const ChainArgs* ta = nullptr, float* sp = nullptr) {
@@ -353,21 +361,26 @@ __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const C
       x0[j] = (mr < M && mr >= ta->rows_full) ? v : 0.f;
     }
   }
-  f32x4 y[2][4];
+  // Y tiles in flight: YA tiles are loaded before the first is used and tile t + YA is issued once tile t's registers
+  // are free, so the layer's epilogue waits out the HBM latency about once instead of once per tile (one wave per
+  // SIMD: no other wave hides it)
+  constexpr int YA = NT < YMAX ? NT : YMAX;
+  f32x4 y[YA][4];
   auto load = [&](int t, f32x4* dst) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) dst[j] = ld_nt4(Ly.aux + rows[j] * Ly.ldaux + 32 * t + 4 * q);
   };
-  load(0, y[0]);
+#pragma unroll
+  for (int t = 0; t < YA; ++t) load(t, y[t]);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    if (t + 1 < NT) load(t + 1, y[(t + 1) & 1]);
+    f32x4 (&yt)[4] = y[t % YA];
     if constexpr (TAPW) {
       f32x4 sw = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) sw[c] = __builtin_fmaf(x0[j], y[t & 1][j][c], sw[c]);
+        for (int c = 0; c < 4; ++c) sw[c] = __builtin_fmaf(x0[j], yt[j][c], sw[c]);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         float v = sw[c];
@@ -379,7 +392,8 @@ __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const C
       if (lane < 8) *reinterpret_cast<f32x4*>(sp + 32 * t + 4 * q) = sw;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(scr + (8 * j + (lane >> 3)) * kScr + 4 * q) = y[t & 1][j];
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(scr + (8 * j + (lane >> 3)) * kScr + 4 * q) = yt[j];
+    if (t + YA < NT) load(t + YA, yt);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const f32x4 yv = *reinterpret_cast<const f32x4*>(scr + r * kScr + 8 * g + 4 * h);
@@ -632,7 +646,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     if (kTapW && a.tap_part != nullptr && mb + 128 > a.rows_full)
       epilogue_bwd_staged<NT0, A0, kTapW>(acc0, a.L[0], m0, a.M, scr, lane, a.beta, a.thr, &a, &stap[wave][0]);
     else
-      epilogue_bwd_staged<NT0, A0>(acc0, a.L[0], m0, a.M, scr, lane, a.beta, a.thr);
+      epilogue_bwd_staged<NT0, A0, false, NL == 4 ? MMS_CHAIN_YAHEAD4 : MMS_CHAIN_YAHEAD>(acc0, a.L[0], m0, a.M, scr,
+                                                                                        lane, a.beta, a.thr);
     to_b<PREC, NT0>(acc0, b1h, b1l);
   }
 
@@ -659,7 +674,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     constexpr int LP = decltype(lpc)::value, LL = LP + 1;
     bf16x8 b2h[2 * NT1], b2l[2 * NT1];
     if constexpr (BWD) {
-      epilogue_bwd_staged<NT1, A1>(accp, a.L[LP], m0, a.M, scr, lane, a.beta, a.thr);
+      epilogue_bwd_staged<NT1, A1, false, NL == 4 ? MMS_CHAIN_YAHEAD4 : MMS_CHAIN_YAHEAD>(accp, a.L[LP], m0, a.M, scr,
+                                                                                        lane, a.beta, a.thr);
       to_b<PREC, NT1>(accp, b2h, b2l);
     }
     floatx16 acc2[NT2];
@@ -714,7 +730,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     // ---- middle layer 2: B operand from layer 1's registers (same width and activation as layer 1)
     bf16x8 bmh[2 * NT1], bml[2 * NT1];
     if constexpr (BWD) {
-      epilogue_bwd_staged<NT1, A1>(acc1, a.L[1], m0, a.M, scr, lane, a.beta, a.thr);
+      epilogue_bwd_staged<NT1, A1, false, MMS_CHAIN_YAHEAD4>(acc1, a.L[1], m0, a.M, scr, lane, a.beta, a.thr);
       to_b<PREC, NT1>(acc1, bmh, bml);
     }
     floatx16 accm[NT1];
