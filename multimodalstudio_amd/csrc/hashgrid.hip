@@ -87,6 +87,23 @@ __device__ __forceinline__ Corners make_corners(float x, float y, float z, float
   return c;
 }
 
+// Block order in XCD-contiguous chunks: the dispatcher sends block b to XCD b % 8, so consecutive blocks -- whose
+// points are consecutive samples of the same rays, sharing their coarse cells -- would fetch the same table lines
+// into eight different L2s; block b instead takes position k = b / 8 of XCD (b % 8)'s contiguous chunk of the grid.
+// MMS_HASH_XCD=0 restores the plain order (diagnostic builds).
+#ifndef MMS_HASH_XCD
+#define MMS_HASH_XCD 1
+#endif
+__device__ __forceinline__ int64_t xcd_block() {
+#if MMS_HASH_XCD
+  const int64_t nb = gridDim.x, b = blockIdx.x;
+  const int64_t q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
+  return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+#else
+  return blockIdx.x;
+#endif
+}
+
 // G > 1 (the SDF panel: centre rows g, tap rows g + j * gstride, j < G): the lanes walk the points in (g, j) order, so
 // the centre and the 4 taps of one sample -- which share their cells at every level coarser than the tap offset --
 // and the next samples of the same ray are gathered by the same wave: their corner lines are fetched from MALL / HBM
@@ -96,7 +113,7 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(const float* __restri
                                                            int64_t gstride, int64_t ldx,
                                                            const float2* __restrict__ table, GridParams p,
                                                            float* __restrict__ out, int64_t ldo) {
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tid = xcd_block() * blockDim.x + threadIdx.x;
   const int64_t q = tid >> 4;
   const int level = (int)(tid & 15);
   const int64_t g = G == 1 ? q : q / G;
@@ -233,7 +250,7 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_walk_kernel(const float* __r
   const bool xc = ((q >> 1) & 1) == 0;  // x = ceil corner
   const bool yc = (pr & 1) == 0, zc = pr < 2;
   const int feat = q & 1;
-  const int64_t g0 = (int64_t)blockIdx.x * CH;
+  const int64_t g0 = xcd_block() * CH;
   const int nck = (int)((Mg - g0) < CH ? (Mg - g0) : CH);
   const int np = nck * G;
   const int nlv = p.levels < p.active_levels ? p.levels : p.active_levels;  // levels with a gradient
@@ -353,7 +370,7 @@ __global__ __launch_bounds__(256) void hashgrid_dpos_kernel(const float* __restr
                                                             int64_t ldx, const float2* __restrict__ table, GridParams p,
                                                             const float* __restrict__ dout, int64_t ldd,
                                                             float* __restrict__ dpos, int64_t lddx) {
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tid = xcd_block() * blockDim.x + threadIdx.x;
   const int64_t q = tid >> 4;
   const int level = (int)(tid & 15);
   const int64_t g = G == 1 ? q : q / G;

@@ -295,7 +295,7 @@ __device__ __forceinline__ void epi_tile(floatx16& acc, int t, const ChainLayer&
 // (identical bits).  Still exactly 4 vector-memory instructions per lane (run_layer's counted waits).
 constexpr int kScr = 36;  // scratch row pitch (floats)
 #ifndef MMS_CHAIN_YAHEAD
-// backward epilogue: Y tiles loaded ahead (1 = one tile ahead, the round-3c kernel; scripts/chain_variants.py, step
+// backward epilogue: Y tiles loaded ahead (1 = one tile ahead, the round-3c kernel; scripts/lib_variants.py, step
 // A/B: SDF backward 370 -> 345 us at 2 or 4, radiance 165 at 1-4 but 177 at 8, where the 4-layer chains spill)
 #define MMS_CHAIN_YAHEAD 4
 #endif

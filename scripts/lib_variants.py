@@ -1,0 +1,52 @@
+#!/usr/bin/env python
+"""Product-library build variants for step A/B runs (diagnostics): one translation unit rebuilt under macros -- the
+backward chain epilogue's Y-tile prefetch depth (csrc/mlp_chain.hip MMS_CHAIN_YAHEAD / MMS_CHAIN_YAHEAD4), the
+hash-grid kernels' block order (csrc/hashgrid.hip MMS_HASH_XCD) -- linked with the other objects and selected at run
+time with MMS_HIP_LIB.
+
+    python scripts/lib_variants.py [name ...]   # CPU container: build multimodalstudio_amd/_variants/libmms_<name>.so
+    MMS_HIP_LIB=multimodalstudio_amd/_variants/libmms_y1_1.so python bench.py ...   # GPU box
+"""
+from __future__ import annotations
+
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+from multimodalstudio_amd import build as b   # noqa: E402
+
+OUT = ROOT / "multimodalstudio_amd" / "_variants"
+VARIANTS = {  # name: (translation unit, macro definitions)
+    "y1_1": ("mlp_chain", {"MMS_CHAIN_YAHEAD": 1, "MMS_CHAIN_YAHEAD4": 1}),
+    "y2_2": ("mlp_chain", {"MMS_CHAIN_YAHEAD": 2, "MMS_CHAIN_YAHEAD4": 2}),
+    "y8_4": ("mlp_chain", {"MMS_CHAIN_YAHEAD": 8, "MMS_CHAIN_YAHEAD4": 4}),
+    "hx0": ("hashgrid", {"MMS_HASH_XCD": 0}),
+}
+
+
+def main():
+    names = sys.argv[1:] or list(VARIANTS)
+    b.build()
+    OUT.mkdir(parents=True, exist_ok=True)
+    procs = {}
+    for name in names:
+        unit, macros = VARIANTS[name]
+        obj = OUT / f"{unit}_{name}.o"
+        cmd = [b.HIPCC, *b.CFLAGS, *[f"-D{k}={v}" for k, v in macros.items()], "-c", str(b.CSRC / f"{unit}.hip"),
+               "-o", str(obj)]
+        procs[name] = (subprocess.Popen(cmd, stderr=subprocess.DEVNULL), obj, unit)
+    for name, (p, obj, unit) in procs.items():
+        if p.wait() != 0:
+            raise SystemExit(f"variant {name} failed")
+        others = [o for o in sorted(b.BUILD.glob("*.o")) if o.stem != unit]
+        lib = OUT / f"libmms_{name}.so"
+        subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", str(lib), str(obj),
+                        *map(str, others)], check=True)
+        obj.unlink()
+        print("built", lib)
+
+
+if __name__ == "__main__":
+    main()
