@@ -48,15 +48,18 @@ __device__ __forceinline__ float pe_bwd(const float* drow, int i, float xi, int 
 // columns, so a wave stores ~1.6 contiguous 156-B row heads (a thread per row wrote its 39 columns with a 288-B lane
 // stride: 64 lines per store instruction, 58 us for the 278k-row SDF batch).  Column c < 3: x_c; 3 <= c < 3 + 3F:
 // sin(x_i 2^k); then sin(x_i 2^k + pi/2), i = coordinate, k = frequency (pe_write's layout, same rounded arguments).
+// IDX: the index type of the (row, column) decomposition -- uint32_t whenever the panel head has < 2^32 elements
+// (the 64-bit divisions by the run-time width and row count cost more than the element's own work)
+template <typename IDX>
 __global__ __launch_bounds__(256) void geo_input_fwd_kernel(const float* __restrict__ pos, int64_t ldp, int64_t M,
                                                             int ntaps, float delta, int F, float* __restrict__ X,
                                                             int64_t ldx) {
   const int W = 3 + 6 * F;
-  const int64_t total = M * (1 + ntaps) * W;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = q / W;
-    const int c = (int)(q - r * W);
-    const int64_t t = r / M, i = r - t * M;
+  const IDX total = (IDX)(M * (1 + ntaps) * W);
+  for (IDX q = (IDX)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (IDX)gridDim.x * blockDim.x) {
+    const IDX r = q / (IDX)W;
+    const int c = (int)(q - r * (IDX)W);
+    const IDX t = r / (IDX)M, i = r - t * (IDX)M;
     int coord, k = 0;
     bool cosine = false;
     if (c < 3) {
@@ -69,14 +72,14 @@ __global__ __launch_bounds__(256) void geo_input_fwd_kernel(const float* __restr
       k = (c - 3 - 3 * F) - coord * F;
       cosine = true;
     }
-    float x = pos[i * ldp + coord];
+    float x = pos[(int64_t)i * ldp + coord];
     if (t > 0) x = x + kTap[t - 1][coord] * delta;
     float v = x;
     if (c >= 3) {
       const float s = x * (float)(1 << k);   // 2^k exactly, as pe_write's running f *= 2
       v = cosine ? sinf(s + kHalfPi) : sinf(s);
     }
-    X[r * ldx + c] = v;
+    X[(int64_t)r * ldx + c] = v;
   }
 }
 
@@ -164,21 +167,38 @@ __global__ void taps_combine_fwd_kernel(const float* __restrict__ out, int64_t l
   }
 }
 
+// dst[r, c] = src[r, c] (zeros when src is null), r < M, c < G: one element per thread of the blocks
+// [b0, gridDim.x), consecutive threads on consecutive columns (coalesced on both sides; a wave per row measured
+// slower: 36 -> 52 us in the radiance panel).  The (row, column) split of the element index in 32 bits when the
+// copy has < 2^32 elements (measured the same as the 64-bit split: profiles/round3d_ab.txt).
+template <typename IDX>
+__device__ __forceinline__ void copy_cols(const float* __restrict__ src, int64_t lds, float* __restrict__ dst,
+                                          int64_t ldd, int64_t M, int G, unsigned b0) {
+  const IDX n = (IDX)(M * G);
+  for (IDX e = (IDX)(blockIdx.x - b0) * blockDim.x + threadIdx.x; e < n; e += (IDX)(gridDim.x - b0) * blockDim.x) {
+    const IDX r = e / (IDX)G, c = e - r * (IDX)G;
+    dst[(int64_t)r * ldd + c] = src ? src[(int64_t)r * lds + c] : 0.f;
+  }
+}
+__device__ __forceinline__ void copy_cols_any(const float* __restrict__ src, int64_t lds, float* __restrict__ dst,
+                                              int64_t ldd, int64_t M, int G, unsigned b0) {
+  const int64_t span = (int64_t)(gridDim.x - b0) * blockDim.x;
+  if (M * G < ((int64_t)1 << 32) - span)
+    copy_cols<uint32_t>(src, lds, dst, ldd, M, G, b0);
+  else
+    copy_cols<int64_t>(src, lds, dst, ldd, M, G, b0);
+}
+
 // backward: writes d sdf into column 0 of dOut rows (centre + taps) (overwrite), plus the centre rows' own sdf
 // gradient (dsdf) and, in the blocks past tap_blocks, the geo-feature gradient into columns 1..G of the centre rows
-// (one element per thread, coalesced along the row)
+// (copy_cols)
 __global__ void taps_combine_bwd_kernel(const float* __restrict__ grads, const float* __restrict__ dgrads,
                                         const float* __restrict__ dhess, const float* __restrict__ dnormals,
                                         int64_t M, float four_delta, float delta_sq, float* __restrict__ dout,
                                         int64_t lddo, const float* __restrict__ dsdf, int64_t ldds,
                                         const float* __restrict__ dgeo, int64_t ldg, int G, unsigned tap_blocks) {
   if (blockIdx.x >= tap_blocks) {
-    const int64_t n = M * G;
-    for (int64_t e = (int64_t)(blockIdx.x - tap_blocks) * blockDim.x + threadIdx.x; e < n;
-         e += (int64_t)(gridDim.x - tap_blocks) * blockDim.x) {
-      const int64_t r = e / G, c = e - r * G;
-      dout[r * lddo + 1 + c] = dgeo ? dgeo[r * ldg + c] : 0.f;
-    }
+    copy_cols_any(dgeo, ldg, dout + 1, lddo, M, G, tap_blocks);
     return;
   }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)tap_blocks * blockDim.x) {
@@ -281,19 +301,14 @@ __device__ __forceinline__ void sh25_bwd(float x, float y, float z, const float*
 // Radiance panel [M, ld]: [pos 3 | SH 25 | geo 256 | ndv 1 | grid 32 (hashgrid kernel)]
 // pos rows i; direction per ray = dirs[i / S]; normals [M, 3]; geo from geometry-MLP output rows i, cols 1..256.
 // Blocks [0, row_blocks): one thread per row writes x, SH(d) and n.v; the blocks after them copy the geo feature
-// columns one element per thread (consecutive threads on consecutive columns: coalesced on both sides -- a thread
-// per row copying its own 256 columns touched 64 rows per instruction).
+// columns one element per thread (copy_cols: consecutive threads on consecutive columns, coalesced on both sides --
+// a thread per row copying its own 256 columns touched 64 rows per instruction).
 __global__ void rad_input_fwd_kernel(const float* __restrict__ pos, int64_t ldp, const float* __restrict__ dirs,
                                      const float* __restrict__ normals, const float* __restrict__ geo, int64_t ldg,
                                      int64_t M, int S, int G, float* __restrict__ X, int64_t ldx,
                                      unsigned row_blocks) {
   if (blockIdx.x >= row_blocks) {
-    const int64_t n = M * G;
-    for (int64_t e = (int64_t)(blockIdx.x - row_blocks) * blockDim.x + threadIdx.x; e < n;
-         e += (int64_t)(gridDim.x - row_blocks) * blockDim.x) {
-      const int64_t r = e / G, c = e - r * G;
-      X[r * ldx + 28 + c] = geo[r * ldg + c];
-    }
+    copy_cols_any(geo, ldg, X + 28, ldx, M, G, row_blocks);
     return;
   }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)row_blocks * blockDim.x) {
@@ -464,8 +479,14 @@ MMS_EXPORT int mms_geo_input_fwd(const float* pos, int64_t ldp, int64_t M, int n
   MMS_REQUIRE(ldx >= 3 + 6 * F, fn, "panel too narrow");
   MMS_REQUIRE(F >= 0 && F <= 24, fn, "PE frequencies must be in [0, 24]");
   if (M == 0) return 0;
-  hipLaunchKernelGGL(geo_input_fwd_kernel, dim3(mms::grid_for(M * (1 + ntaps) * (3 + 6 * F), 256, 65536)), dim3(256), 0,
-                     mms::as_stream(stream), pos, ldp, M, ntaps, delta, F, X, ldx);
+  const int64_t total = M * (1 + ntaps) * (3 + 6 * F);
+  const dim3 grid(mms::grid_for(total, 256, 65536));
+  if (total < ((int64_t)1 << 32) - (int64_t)grid.x * 256)   // (the grid-stride index stays below 2^32 too)
+    hipLaunchKernelGGL(geo_input_fwd_kernel<uint32_t>, grid, dim3(256), 0, mms::as_stream(stream), pos, ldp, M, ntaps,
+                       delta, F, X, ldx);
+  else
+    hipLaunchKernelGGL(geo_input_fwd_kernel<int64_t>, grid, dim3(256), 0, mms::as_stream(stream), pos, ldp, M, ntaps,
+                       delta, F, X, ldx);
   return mms::check_launch(fn);
 }
 
