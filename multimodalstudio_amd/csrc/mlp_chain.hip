@@ -131,6 +131,37 @@ constexpr int kMaxTiles = 10;  // widest chain layer: 10 column tiles (320 units
 constexpr int kSlot = 21;  // 1 KiB chunks per ring slot: hi + lo images of up to 10 tiles, + 1 spare (dummy loads)
 typedef __attribute__((address_space(3))) void lds_void;
 
+// Diagnostic build only (MMS_CHAIN_STAMPS=1, scripts/lib_variants.py "stamps"; the product library has none): each
+// wave accumulates s_memtime deltas per layer l -- [4 l] the k-steps' wait + barrier, [4 l + 1] ring / input issue and
+// get_b (the lazy epilogue, the backward's dZ stores), [4 l + 2] fragment reads + MFMA issue, [4 l + 3] the layer's
+// entry (the previous layer's last MFMAs and the work between layers) -- and [16] the tail, written per (block, wave)
+// to g_chain_stamps at the end.  Read their shares, not their sums: every stamp drains the wave's LDS reads.
+#ifndef MMS_CHAIN_STAMPS
+#define MMS_CHAIN_STAMPS 0
+#endif
+constexpr int kStamps = 17;
+#if MMS_CHAIN_STAMPS
+__device__ unsigned long long g_chain_stamps[1 << 20];
+__device__ __forceinline__ unsigned long long chain_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#endif
+__device__ __forceinline__ void stamp_seg(unsigned long long* st, unsigned long long* last, int k) {
+#if MMS_CHAIN_STAMPS
+  if (st != nullptr) {
+    const unsigned long long n = chain_stamp();
+    st[k] += n - *last;
+    *last = n;
+  }
+#else
+  (void)st; (void)last; (void)k;
+#endif
+}
+
 template <int PREC>
 constexpr int nimg() { return PREC == 2 ? 2 : 1; }
 
@@ -198,8 +229,10 @@ constexpr int gops(int s) { return s < 0 ? 0 : ((s & 1) ? GO : GE); }
 // branches), so the counts are exact for every wave.
 template <int PREC, int NT, int NTL, int KS, int PRE, int GE, int GO, typename Pre, typename GetB>
 __device__ __forceinline__ void run_layer(const ChainLayer& Ly, int ks, int nt, floatx16 (&acc)[NT], int wave,
-                                          int lane, bf16x8 (*ring)[kSlot][64], Pre&& pre, GetB&& get_b) {
+                                          int lane, bf16x8 (*ring)[kSlot][64], Pre&& pre, GetB&& get_b,
+                                          unsigned long long* st = nullptr, unsigned long long* st_last = nullptr) {
   constexpr int PER = stage_per<PREC, NTL>();
+  stamp_seg(st, st_last, 3);
   wait_vm_barrier<63>();  // every wave is done with the ring (previous layer / launch prologue)
 #pragma unroll
   for (int j = 0; j < kDepth; ++j) {
@@ -217,15 +250,18 @@ __device__ __forceinline__ void run_layer(const ChainLayer& Ly, int ks, int nt, 
       constexpr int kG = (kDepth >= 3 ? gops<GE, GO>(s - 3) : 0) + (kDepth >= 2 ? gops<GE, GO>(s - 2) : 0) +
                          gops<GE, GO>(s - 1);
       const int f = ks - 1 - s;
+      stamp_seg(st, st_last, 2);
       if (kDepth >= 3 && f >= 2) wait_vm_barrier<kG + (kDepth - 1) * (PRE + PER)>();
       else if (kDepth >= 2 && f >= 1) wait_vm_barrier<kG + (kDepth >= 3 ? 1 : kDepth - 1) * (PRE + PER)>();
       else wait_vm_barrier<kG>();
+      stamp_seg(st, st_last, 0);
       if (s + kDepth < ks) {
         pre(s + kDepth);
         stage<PREC, NT, NTL>(Ly, s + kDepth, wave, lane, ring);
       }
       bf16x8 bh, bl;
       get_b(s, bh, bl);
+      stamp_seg(st, st_last, 1);
       const bf16x8* slot = &ring[s % kRing][0][0];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -321,6 +357,37 @@ __device__ __forceinline__ void epi_tile_full(floatx16& acc, int t, const float*
   }
   if constexpr (KEEP) {
     const int q = lane & 7;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = 8 * j + (lane >> 3);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(scr + row * kScr + 4 * q);
+      const int64_t mr = m0 + row < M ? m0 + row : M - 1;
+      st_nt4(obase + mr * ldo + 32 * t + 4 * q, v);
+    }
+  }
+}
+
+// epi_tile_full in two parts, for the one-tile-ahead forward (MMS_CHAIN_AHEAD): bias + activation in place ...
+template <int ACT>
+__device__ __forceinline__ void epi_tile_act(floatx16& acc, int t, const float* sb, int lane, float beta, float thr) {
+  const int h = lane >> 5;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 bq = *reinterpret_cast<const f32x4*>(sb + 32 * t + 8 * g + 4 * h);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[4 * g + i] = act_fwd<ACT>(acc[4 * g + i] + bq[i], beta, thr);
+  }
+}
+// ... and (KEEP) the staged row-contiguous store of the activated tile (4 vector-memory instructions per lane)
+template <bool KEEP>
+__device__ __forceinline__ void epi_tile_store(const floatx16& acc, int t, float* obase, int64_t ldo, int64_t m0,
+                                               int64_t M, float* scr, int lane) {
+  if constexpr (KEEP) {
+    const int r = lane & 31, h = lane >> 5, q = lane & 7;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(scr + r * kScr + 8 * g + 4 * h) =
+          f32x4{acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = 8 * j + (lane >> 3);
@@ -527,6 +594,36 @@ __device__ __forceinline__ void to_b(const floatx16 (&acc)[NT], bf16x8 (&bh)[2 *
   for (int t = 0; t < NT; ++t) tile_to_b<PREC>(acc[t], &bh[2 * t], &bl[2 * t]);
 }
 
+// The forward's lazy epilogue of register-fed layer l + 1's B operand, at k-step s (compile-time after unrolling):
+// tile t = s / 2 of layer l is consumed by steps 2 t and 2 t + 1.  MMS_CHAIN_AHEAD (default): tile t + 1's bias,
+// activation and bf16 split run at step 2 t -- independent of that step's MFMAs, so the scheduler can issue them
+// between the MFMAs (one wave per SIMD: the stamp build measured the in-step epilogue as long as the MFMA issue, not
+// overlapped) -- and tile t's store stays at step 2 t (4 stores per even step: run_layer's exact vmcnt counts).
+#ifndef MMS_CHAIN_AHEAD
+#define MMS_CHAIN_AHEAD 1
+#endif
+template <int PREC, int ACT, bool KEEP, int NT>
+__device__ __forceinline__ void lazy_fwd_b(int s, floatx16 (&accp)[NT], bf16x8* bh, bf16x8* bl, const float* sb,
+                                           float* obase, int64_t ldo, int64_t m0, int64_t M, float* scr, int lane,
+                                           float beta, float thr) {
+  if ((s & 1) != 0) return;
+  const int t = s >> 1;
+#if MMS_CHAIN_AHEAD
+  if (t == 0) {
+    epi_tile_act<ACT>(accp[0], 0, sb, lane, beta, thr);
+    tile_to_b<PREC>(accp[0], &bh[0], &bl[0]);
+  }
+  epi_tile_store<KEEP>(accp[t], t, obase, ldo, m0, M, scr, lane);
+  if (t + 1 < NT) {
+    epi_tile_act<ACT>(accp[t + 1], t + 1, sb, lane, beta, thr);
+    tile_to_b<PREC>(accp[t + 1], &bh[2 * t + 2], &bl[2 * t + 2]);
+  }
+#else
+  epi_tile_full<ACT, KEEP>(accp[t], t, sb, obase, ldo, m0, M, scr, lane, beta, thr);
+  tile_to_b<PREC>(accp[t], &bh[s], &bl[s]);
+#endif
+}
+
 // Activations are template arguments (A0..A2: layer activations, forward ids or backward derivative ids; XA: the
 // backward's input scaling).  The forward's epilogue of layer l is LAZY: tile t is finished (bias, activation,
 // store, bf16 split) inside layer l + 1's k-step 2 t, right before the MFMAs that consume it, so its VALU and
@@ -555,6 +652,13 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   const bool anyfull = m0 < a.rows_full;   // wave-uniform
   const bool blockfull = mb < a.rows_full;  // block-uniform
   const floatx16 zero = {};
+#if MMS_CHAIN_STAMPS
+  unsigned long long st[kStamps] = {};
+  unsigned long long st_last = chain_stamp();
+#define MMS_ST(l) , st + 4 * (l), &st_last
+#else
+#define MMS_ST(l)
+#endif
   __shared__ __attribute__((aligned(16))) float sw0[BWD ? 1 : 32 * NT1];  // forward: last layer's weight row 0 (fp32)
   // per-wave staging of the row-contiguous stores (forward KEEP) and of the backward's Y loads / dZ stores
   constexpr bool kStage = BWD || KEEP;
@@ -634,7 +738,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
       split8<PREC>(v, bh, bl);
     };
     run_layer<PREC, NT0, NT0, KS0, XIO ? 4 : 2, XIO ? 2 : 0, XIO ? 2 : 0>(a.L[0], ks0, NT0, acc0, wave, lane, ring,
-                                                                         pre, get_b);
+                                                                         pre, get_b MMS_ST(0));
   }
   auto nopre = [](int) {};
   // forward layers 1 and 2: get_b(s) of an even step finishes (and with KEEP stores, 4 x 16 B per lane) one tile of the
@@ -658,15 +762,11 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   {
     run_layer<PREC, NT1, NT1, 2 * NT0, 0, kGE, 0>(a.L[1], 2 * NT0, NT1, acc1, wave, lane, ring, nopre,
                                        [&](int s, bf16x8& bh, bf16x8& bl) {
-      if constexpr (!BWD) {
-        if ((s & 1) == 0) {
-          epi_tile_full<A0, KEEP>(acc0[s >> 1], s >> 1, sbias[0], a.L[0].out, a.L[0].ldo, m0, a.M, scr, lane, a.beta,
-                                  a.thr);
-          tile_to_b<PREC>(acc0[s >> 1], &b1h[s], &b1l[s]);
-        }
-      }
+      if constexpr (!BWD)
+        lazy_fwd_b<PREC, A0, KEEP, NT0>(s, acc0, b1h, b1l, sbias[0], a.L[0].out, a.L[0].ldo, m0, a.M, scr, lane, a.beta,
+                                        a.thr);
       bh = b1h[s]; bl = b1l[s];
-    });
+    } MMS_ST(1));
   }
   // ---- the last layer (index LL = NL - 1), fed by the registers of layer LP = LL - 1 (NT1 tiles, activation A1).
   // Forward: SDF tap rows need only the sdf column tile; a block of tap rows stages only that tile.
@@ -683,17 +783,14 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     for (int t = 0; t < NT2; ++t) acc2[t] = zero;
     const int nt2 = (!BWD && !anyfull) ? 1 : NT2;
     auto get_b2 = [&](int s, bf16x8& bh, bf16x8& bl) {
-      if constexpr (!BWD) {
-        if ((s & 1) == 0) {
-          epi_tile_full<A1, KEEP>(accp[s >> 1], s >> 1, sbias[LP], a.L[LP].out, a.L[LP].ldo, m0, a.M, scr, lane,
-                                  a.beta, a.thr);
-          tile_to_b<PREC>(accp[s >> 1], &b2h[s], &b2l[s]);
-        }
-      }
+      if constexpr (!BWD)
+        lazy_fwd_b<PREC, A1, KEEP, NT1>(s, accp, b2h, b2l, sbias[LP], a.L[LP].out, a.L[LP].ldo, m0, a.M, scr, lane,
+                                        a.beta, a.thr);
       bh = b2h[s]; bl = b2l[s];
     };
     if (BWD || blockfull) {
-      run_layer<PREC, NT2, NT2, 2 * NT1, 0, kGE, 0>(a.L[LL], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2);
+      run_layer<PREC, NT2, NT2, 2 * NT1, 0, kGE, 0>(a.L[LL], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2
+                                                    MMS_ST(LL));
     } else {
       // a block of SDF tap rows (or the sampler's inference rows) needs only output 0 of the last layer: a 256-long
       // dot product per row, done in fp32 on the VALU (W row 0 from LDS) instead of 2 NT1 ring k-steps of one
@@ -738,19 +835,24 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     for (int t = 0; t < NT1; ++t) accm[t] = zero;
     run_layer<PREC, NT1, NT1, 2 * NT1, 0, kGE, 0>(a.L[2], 2 * NT1, NT1, accm, wave, lane, ring, nopre,
                                                   [&](int s, bf16x8& bh, bf16x8& bl) {
-      if constexpr (!BWD) {
-        if ((s & 1) == 0) {
-          epi_tile_full<A1, KEEP>(acc1[s >> 1], s >> 1, sbias[1], a.L[1].out, a.L[1].ldo, m0, a.M, scr, lane, a.beta,
-                                  a.thr);
-          tile_to_b<PREC>(acc1[s >> 1], &bmh[s], &bml[s]);
-        }
-      }
+      if constexpr (!BWD)
+        lazy_fwd_b<PREC, A1, KEEP, NT1>(s, acc1, bmh, bml, sbias[1], a.L[1].out, a.L[1].ldo, m0, a.M, scr, lane, a.beta,
+                                        a.thr);
       bh = bmh[s]; bl = bml[s];
-    });
+    } MMS_ST(2));
     last_layer(accm, std::integral_constant<int, 2>{});
   } else {
     last_layer(acc1, std::integral_constant<int, 1>{});
   }
+#if MMS_CHAIN_STAMPS
+  stamp_seg(st, &st_last, 16);
+  if (lane == 0) {
+    unsigned long long* o = g_chain_stamps + ((int64_t)blockIdx.x * 4 + wave) * kStamps;
+    if (((int64_t)blockIdx.x * 4 + wave + 1) * kStamps <= (1 << 20))
+      for (int i = 0; i < kStamps; ++i) o[i] = st[i];
+  }
+#endif
+#undef MMS_ST
   if constexpr (kTapW) {
     if (a.tap_part != nullptr && mb + 128 > a.rows_full) {
       __syncthreads();
@@ -906,6 +1008,19 @@ __global__ void pack_batched_kernel(const MmsPackItem* __restrict__ items, int n
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
+
+#if MMS_CHAIN_STAMPS
+// diagnostic build only: copy / clear the per-(block, wave) stamp sums (kStamps each)
+MMS_EXPORT int mms_chain_stamps(unsigned long long* host, int64_t n, int clear) {
+  if (n > (1 << 20)) n = 1 << 20;
+  if (clear) {
+    void* addr = nullptr;
+    if (hipGetSymbolAddress(&addr, HIP_SYMBOL(g_chain_stamps)) != hipSuccess) return 1;
+    return hipMemset(addr, 0, sizeof(unsigned long long) << 20) == hipSuccess ? 0 : 1;
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_chain_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 MMS_EXPORT int mms_mlp_pack_batched(const void* items, int n_items, int64_t total, void* stream) {
   const char* fn = "mms_mlp_pack_batched";

@@ -23,6 +23,8 @@ VARIANTS = {  # name: (translation unit, macro definitions)
     "y2_2": ("mlp_chain", {"MMS_CHAIN_YAHEAD": 2, "MMS_CHAIN_YAHEAD4": 2}),
     "y8_4": ("mlp_chain", {"MMS_CHAIN_YAHEAD": 8, "MMS_CHAIN_YAHEAD4": 4}),
     "hx0": ("hashgrid", {"MMS_HASH_XCD": 0}),
+    "stamps": ("mlp_chain", {"MMS_CHAIN_STAMPS": 1}),   # scripts/chain_stamps.py
+    "ahead0": ("mlp_chain", {"MMS_CHAIN_AHEAD": 0}),
 }
 
 
