@@ -139,27 +139,41 @@ __global__ void geo_loss_bwd_kernel(const float* __restrict__ grads, const float
 }
 
 // ------------------------------------------------------------------ optimizer
+// Launch shape measured on the bench step (scripts/gpu_iter20.sh / gpu_iter21.sh, rocprofv3 per-step tables,
+// profiles/round3d_ab.txt): the blocks' partial sums meet in ONE float atomic, which serializes at the memory side,
+// so fewer, fuller blocks win -- 2048 blocks x 4 loads 22.3 us per launch (avg of the two groups), 8192: 57.6,
+// 1024: 18.5, 512: 15.6, 256 x 8 loads: 14.3.
+#ifndef MMS_SUMSQ_UNROLL
+#define MMS_SUMSQ_UNROLL 8   // independent 16-B loads in flight per lane per iteration
+#endif
+#ifndef MMS_SUMSQ_GRID
+#define MMS_SUMSQ_GRID 256   // blocks (grid-stride): one per CU
+#endif
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ acc) {
-  float s = 0.f;
+  constexpr int U = MMS_SUMSQ_UNROLL;
   const int64_t n4 = n / 4;
   const float4* x4 = reinterpret_cast<const float4*>(x);
-  // four independent 16-B loads in flight per lane per iteration (one dependent load per iteration left the
-  // 138 MB gradient read at 3.1 TB/s), then the remainder one at a time
+  // U independent 16-B loads in flight per lane per iteration (one dependent load per iteration left the 138 MB
+  // gradient read at 3.1 TB/s), then the remainder one at a time
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  float s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  for (; i + 3 * stride < n4; i += 4 * stride) {
-    const float4 a = x4[i], b = x4[i + stride], c = x4[i + 2 * stride], d = x4[i + 3 * stride];
-    s += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
-    s1 += b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w;
-    s2 += c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w;
-    s3 += d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
+  float ps[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) ps[u] = 0.f;
+  for (; i + (U - 1) * stride < n4; i += U * stride) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = x4[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ps[u] += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
   }
   for (; i < n4; i += stride) {
     const float4 v = x4[i];
-    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    ps[0] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
   }
-  s = (s + s1) + (s2 + s3);
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) s += ps[u];
   for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     s += x[i] * x[i];
   s = block_reduce_sum(s);
@@ -289,7 +303,7 @@ MMS_EXPORT int mms_sumsq(const float* x, int64_t n, float* acc, void* stream) {
   const char* fn = "mms_sumsq";
   if (n == 0) return 0;
   MMS_REQUIRE(((uintptr_t)x & 15) == 0, fn, "buffer must be 16-byte aligned");
-  hipLaunchKernelGGL(sumsq_kernel, dim3(mms::grid_for(n / 4 + 1, 256, 2048)), dim3(256), 0, mms::as_stream(stream), x,
+  hipLaunchKernelGGL(sumsq_kernel, dim3(mms::grid_for(n / 4 + 1, 256, MMS_SUMSQ_GRID)), dim3(256), 0, mms::as_stream(stream), x,
                      n, acc);
   return mms::check_launch(fn);
 }
