@@ -181,7 +181,26 @@ CPU_CONFIGS = {
     "grid_rgb": ("grid", ("rgb",)),
     "grid_raw5": ("grid_raw", ("rgb", "infrared", "mono", "polarization", "multispectral")),
     "mlp_raw": ("mlp_raw", ("rgb",)),
+    "grid_bg5": ("grid_raw_grid_bg_unbalanced", ("rgb", "polarization")),
 }
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_threads() -> tuple:
+    """(threads used, CPUs in this process's affinity mask): BASELINE.md §2 asks for len(os.sched_getaffinity(0));
+    on a shared GPU box the job's CPU share is OMP_NUM_THREADS (set by the pool), so the smaller of the two."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return (min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff), aff
 
 
 def cpu_baseline(config: str, log2T: int, step: int, seconds: float, n_rays: int = 256):
@@ -192,18 +211,24 @@ def cpu_baseline(config: str, log2T: int, step: int, seconds: float, n_rays: int
     from multimodalstudio_amd import scene as ms
     from multimodalstudio_amd.model import BaseModel, ModelSpec
     from multimodalstudio_amd.pipeline import METHODS
+    from multimodalstudio_amd.pipeline import skip_views_for
     method, mods = CPU_CONFIGS[config]
     raw, bg_kind, fields = METHODS[method]
     mods = list(mods)
     channels = {m: ms.CHANNELS[m] for m in mods}
+    threads, affinity = cpu_threads()
+    torch.set_num_threads(threads)
     torch.manual_seed(654824)
     model = BaseModel(ModelSpec(channels, log2T=log2T, bg_kind=bg_kind, fields=fields))
     sd = {k: v.detach() for k, v in model.state_dict().items()}
     del model
     W, H = 640, 512
     cams = ms.make_cameras(mods, 50, W, H, seed=0, train=True)
+    for m, skip in (skip_views_for(method) or {}).items():
+        if m in cams:
+            cams[m] = ms.select_views(cams[m], [v for v in cams[m].view_ids if v not in set(skip)])
     masks = {m: ms.mosaick_mask(m, W, H) for m in mods} if raw else None
-    ot = OracleTrainer(sd, channels, cams, log2T, step, raw=raw, mosaick=masks, fields=fields)
+    ot = OracleTrainer(sd, channels, cams, log2T, step, raw=raw, mosaick=masks, fields=fields, bg_kind=bg_kind)
     g = torch.Generator().manual_seed(1)
 
     def batch():
@@ -229,11 +254,13 @@ def cpu_baseline(config: str, log2T: int, step: int, seconds: float, n_rays: int
         "value": round(n_rays * len(mods) / med, 2),
         "unit": "rays/s",
         "cores": torch.get_num_threads(),
+        "affinity_cpus": affinity,
+        "cpu_model": cpu_model(),
         "kind": "port",
         "sample": f"{len(times)} timed steps (median) of the CPU restatement (oracle/, pinned to the reference torch "
                   f"path) of {config} ({method}, {len(mods)} modalit{'y' if len(mods) == 1 else 'ies'}) at {n_rays} "
-                  f"rays/modality, log2T={log2T}, model step {step}, fwd+bwd+AdamW; "
-                  f"host {platform.processor() or platform.machine()}",
+                  f"rays/modality, log2T={log2T}, model step {step}, fwd+bwd+AdamW; {torch.get_num_threads()} threads "
+                  f"on {cpu_model()} ({affinity} CPUs in the affinity mask)",
     }
 
 
@@ -243,10 +270,9 @@ def timed_run(config: str, args, dev, rank: int, ddp, steps: int, warmup: int) -
     from multimodalstudio_amd.pipeline import Trainer, TrainConfig
     method, mods, _ = CONFIGS[config]
     world = ddp.world if ddp is not None else 1
-    from multimodalstudio_amd.pipeline import POL_10_VIEWS_SKIP
-    skip = {"polarization": POL_10_VIEWS_SKIP} if config == "grid_bg5" else None
+    from multimodalstudio_amd.pipeline import skip_views_for
     cfg = TrainConfig(method=method, modalities=mods, num_rays_per_modality=args.rays, log2T=args.log2T,
-                      skip_views=skip, gpu_sampler=args.sampler == "device")
+                      skip_views=skip_views_for(method), gpu_sampler=args.sampler == "device")
     trainer = Trainer(cfg, dev, rank=rank)
     trainer.model.concurrent_background = not args.serial_background
     trainer.set_step(args.start_step)
@@ -284,6 +310,22 @@ def timed_run(config: str, args, dev, rank: int, ddp, steps: int, warmup: int) -
             "steps": steps, "warmup": warmup}
 
 
+def spawn_ranks(n: int) -> int:
+    """``python bench.py --gpus N`` without a torch.distributed environment: one process per GPU, as the reference's
+    Fabric launch does (/root/reference/src/engine/trainer.py:57-63), through torch.distributed.run with the same
+    arguments; this process touches no GPU and exits with the launcher's status (rank 0 prints the JSON line)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -305,11 +347,14 @@ def main():
                     help="run the background branch on the main stream (default: its own stream, overlapped)")
     ap.add_argument("--mode", default="graph", choices=["graph", "eager"],
                     help="graph: hipGraph-captured steps (multimodalstudio_amd/graphs.py); eager: Python-launched")
-    ap.add_argument("--secondary", default="grid_raw5", help="also time this config (nested 'secondary' record); "
-                    "'' to skip")
+    ap.add_argument("--secondary", default="grid_raw5,grid_bg5",
+                    help="also time these configs (comma-separated; nested records: the first as 'secondary', BASELINE "
+                         "configs[4] as 'config5'); '' to skip")
     ap.add_argument("--timing-steps", type=int, default=5,
                     help="eager steps after the timed region whose watched launches are timed with HIP events")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
 
     from multimodalstudio_amd import _lib
     from multimodalstudio_amd import ddp as mddp
@@ -318,6 +363,8 @@ def main():
     mfn.set_precision(args.precision)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE {world}: measuring {world} rank(s)", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -373,18 +420,24 @@ def main():
         cpu_all = {c: cpu_baseline(c, args.log2T, args.start_step, args.cpu_seconds / 2)
                    for c in CPU_CONFIGS if c != args.config}
 
-    secondary = None
-    if args.secondary and args.secondary != args.config:
-        # a second driver-timed line for the 5-modality workload (BASELINE configs[2] per GPU), same process
+    extra = {}
+    names = [c for c in (args.secondary or "").split(",") if c and c != args.config]
+    if names:
         del trainer, runner, run
+    for name in names:
+        # further driver-timed lines in the same process: the 5-modality workload (BASELINE configs[2] per GPU) and
+        # config 5 (configs[4] per GPU: rgb + 10-view polarization, hash-grid background, pose refinement)
         torch.cuda.empty_cache()
-        r2 = timed_run(args.secondary, args, dev, rank, ddp, max(1, min(args.steps, 20)), max(1, min(args.warmup, 5)))
-        secondary = {"config": {"workload": CONFIGS[args.secondary][2], "modalities": list(CONFIGS[args.secondary][1]),
-                                "num_rays_per_modality": args.rays, "rays_per_step": r2["rays_per_step"]},
-                     "value": round(r2["value"], 1), "unit": "rays/s", "steps": r2["steps"], "warmup": r2["warmup"],
-                     "ms_per_step": round(r2["ms_per_step"], 3), "step_mode": r2["step_mode"],
-                     "cpu_baseline": (cpu_all or {}).get(args.secondary)}
+        r2 = timed_run(name, args, dev, rank, ddp, max(1, min(args.steps, 20)), max(1, min(args.warmup, 5)))
+        extra[name] = {"config": {"workload": CONFIGS[name][2], "modalities": list(CONFIGS[name][1]),
+                                  "num_rays_per_modality": args.rays, "rays_per_step": r2["rays_per_step"],
+                                  "parallelism": f"dp{world}"},
+                       "value": round(r2["value"], 1), "per_rank_value": round(r2["value"] / world, 1),
+                       "unit": "rays/s", "steps": r2["steps"], "warmup": r2["warmup"],
+                       "ms_per_step": round(r2["ms_per_step"], 3), "step_mode": r2["step_mode"],
+                       "cpu_baseline": (cpu_all or {}).get(name)}
         del r2
+    secondary = extra.pop(names[0]) if names else None
 
     if rank == 0:
         line = {
@@ -395,6 +448,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
+            # the reference's own TRAIN_RAYS_PER_SEC is per rank (trainer.py:107-114); value is the whole job's
+            "per_rank_value": round(value / world, 1),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -414,6 +469,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_configs": cpu_all,
             "secondary": secondary,
+            "config5": extra.get("grid_bg5"),
         }
         print(json.dumps(line))
     if ddp:

@@ -470,88 +470,6 @@ __global__ __launch_bounds__(256) void bg_input_bwd_kernel(const float* __restri
   }
 }
 
-// The same with each ray's rows staged through LDS first (MMS_BG_BWD_STAGED, default): a lane reading its own row's 39
-// dX and 27 dD columns touched 64 rows per load instruction (58 us for the 131k background rows); here the wave copies
-// its rows' column runs with consecutive lanes on consecutive columns, then each lane reads its row from LDS (odd
-// pitches: conflict-free).  4 rays (waves) per block, no early return (block barrier).
-#ifndef MMS_BG_BWD_STAGED
-#define MMS_BG_BWD_STAGED 0   // off until measured on the GPU (scripts/lib_variants.py bg1)
-#endif
-constexpr int kBgX = 39, kBgXP = 41, kBgD = 27, kBgDP = 27;
-__global__ __launch_bounds__(256) void bg_input_bwd_staged_kernel(const float* __restrict__ pos,
-                                                                  const float* __restrict__ X, int64_t ldx,
-                                                                  const float* __restrict__ dX, int64_t lddx,
-                                                                  const float* __restrict__ dirs,
-                                                                  const float* __restrict__ dD, int64_t lddd,
-                                                                  int64_t dcol, int64_t R, int S,
-                                                                  float* __restrict__ dpos, float* __restrict__ ddirs) {
-  __shared__ float sdx[4][64 * kBgXP];
-  __shared__ float sdd[4][64 * kBgDP];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t ray = (int64_t)blockIdx.x * 4 + w;
-  const bool live = ray < R;
-  const int64_t i0 = ray * S;
-  if (live) {
-    for (int e = lane; e < S * kBgX; e += 64) {
-      const int r = e / kBgX, c = e - r * kBgX;
-      sdx[w][r * kBgXP + c] = dX[(i0 + r) * lddx + c];
-    }
-    if (ddirs && dD)
-      for (int e = lane; e < S * kBgD; e += 64) {
-        const int r = e / kBgD, c = e - r * kBgD;
-        sdd[w][r * kBgDP + c] = dD[(i0 + r) * lddd + dcol + c];
-      }
-  }
-  __syncthreads();
-  if (!live) return;
-  float gd[3] = {0.f, 0.f, 0.f};
-  if (lane < S) {
-    const int64_t i = i0 + lane;
-    const float* xr = X + i * ldx;
-    const float* dr = &sdx[w][lane * kBgXP];
-    float gc[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) gc[c] = dr[c] + pe_bwd(dr, c, xr[c], 6);
-    if (dpos) {
-      const float p[3] = {pos[i * 3], pos[i * 3 + 1], pos[i * 3 + 2]};
-      const float ax = fabsf(p[0]), ay = fabsf(p[1]), az = fabsf(p[2]);
-      const float mag = fmaxf(fmaxf(ax, ay), az);
-      float gp[3];
-      if (mag >= 1.0f) {
-        const int ks = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
-        const float s = 2.0f - 1.0f / mag;
-        float dot = 0.f;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) { gp[c] = gc[c] * s / mag; dot += gc[c] * p[c]; }
-        const float dm = dot * (2.0f / (mag * mag * mag) - 2.0f / (mag * mag));
-        gp[ks] += dm * (p[ks] >= 0.f ? 1.f : -1.f);
-      } else {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) gp[c] = gc[c];
-      }
-#pragma unroll
-      for (int c = 0; c < 3; ++c) dpos[i * 3 + c] = gp[c];
-    }
-    if (ddirs && dD) {
-      const float* dd = &sdd[w][lane * kBgDP];
-      const float* d = dirs + ray * 3;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) gd[c] = dd[c] + pe_bwd(dd, c, d[c], 4);
-    }
-  }
-  if (ddirs && dD) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-#pragma unroll
-      for (int c = 0; c < 3; ++c) gd[c] += __shfl_xor(gd[c], o);
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int c = 0; c < 3; ++c) ddirs[ray * 3 + c] += gd[c];
-    }
-  }
-}
-
 }  // namespace
 
 MMS_EXPORT int mms_geo_input_fwd(const float* pos, int64_t ldp, int64_t M, int ntaps, float delta, int F, float* X,
@@ -649,11 +567,9 @@ MMS_EXPORT int mms_bg_input_bwd(const float* pos, const float* X, int64_t ldx, c
   const char* fn = "mms_bg_input_bwd";
   MMS_REQUIRE(S >= 1 && S <= 64, fn, "samples per ray must be in [1, 64]");
   if (R == 0) return 0;
-  if (MMS_BG_BWD_STAGED && ldx >= 3)
-    hipLaunchKernelGGL(bg_input_bwd_staged_kernel, dim3(mms::grid_for(R, 4, INT32_MAX)), dim3(256), 0,
-                       mms::as_stream(stream), pos, X, ldx, dX, lddx, dirs, dD, lddd, dcol, R, S, dpos, ddirs);
-  else
-    hipLaunchKernelGGL(bg_input_bwd_kernel, dim3(mms::grid_for(R * 64, 256, INT32_MAX)), dim3(256), 0,
-                       mms::as_stream(stream), pos, X, ldx, dX, lddx, dirs, dD, lddd, dcol, R, S, dpos, ddirs);
+  // (an LDS-staged variant of this kernel -- each ray's rows copied column-contiguously first -- measured no faster on
+  // the config-5 step, 545.2k vs 546.7k rays/s, gpurun_out r4a, and was removed)
+  hipLaunchKernelGGL(bg_input_bwd_kernel, dim3(mms::grid_for(R * 64, 256, INT32_MAX)), dim3(256), 0,
+                     mms::as_stream(stream), pos, X, ldx, dX, lddx, dirs, dD, lddd, dcol, R, S, dpos, ddirs);
   return mms::check_launch(fn);
 }

@@ -78,6 +78,19 @@ class DDP:
             g.grad.mul_(1.0 / self.world)
         self.pending = []
 
+    def overlap_exchange(self, ready: List[torch.Tensor], groups: List, middle) -> None:
+        """Graph-replayed data-parallel steps: all-reduce the gradient regions ``ready`` (final now: the hash tables)
+        asynchronously, run ``middle`` (the replay that writes the remaining gradients) while they are in flight,
+        then all-reduce the rest, wait and average (graphs.GraphTrainer)."""
+        if self.world <= 1:
+            middle()
+            return
+        self.begin_step()
+        for g in ready:
+            self.grad_ready(g, groups)
+        middle()
+        self.finish_step(groups)
+
     def allreduce_grads(self, groups: List) -> None:
         """Average flat gradient buffers across ranks (in place): every bucket of <= bucket_bytes launched
         asynchronously, then one wait (graph-replayed steps: between the forward/backward graph and the optimizer

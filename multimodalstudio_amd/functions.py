@@ -430,8 +430,9 @@ class MLPRun:
                 dW = dWs[l]
                 db = bt if bt is not None else torch.zeros(N, device=dev)
                 tiles = ((N + 127) // 128) * ((K + 127) // 128)
-                gemm(TN, N, K, M, dZ, dZ.stride(0), Xin, Xin.stride(0), dW, K, accumulate=True,
-                     splits=_splits_for(M, tiles, self.bprec), prec=self.bprec, colsum=db)
+                _wgrad(lambda N=N, K=K, dZ=dZ, Xin=Xin, dW=dW, db=db, tiles=tiles: gemm(
+                    TN, N, K, M, dZ, dZ.stride(0), Xin, Xin.stride(0), dW, K, accumulate=True,
+                    splits=_splits_for(M, tiles, self.bprec), prec=self.bprec, colsum=db))
                 dg = gt.reshape(-1) if gt is not None else torch.zeros(N, device=dev)
                 dv = vt if vt is not None else torch.zeros(N, K, device=dev)
                 _wn_bwd(g.reshape(-1), v, self.norms[l], dW, dg, dv)
@@ -466,7 +467,13 @@ class SmallRun:
         if prec == 0 or len(params) != 3:
             return False
         N, K = params[1].shape
-        return N <= 16 and K in (128, 256, 512) and acts[0][0] in (0, 1, 2, 3) and (K == 128 or N <= 4096 // K)
+        return acts[0][0] in (0, 1, 2, 3) and SmallRun.shape_ok(N, K)
+
+    @staticmethod
+    def shape_ok(N: int, K: int) -> bool:
+        """The narrower of the two kernels' limits (mms_small_linear_bwd: K 128 up to 16 outputs, K 256 up to 8, K 512
+        up to 4), so a layer whose forward runs here always has a backward."""
+        return 1 <= N <= 16 and (K == 128 or (K in (256, 512) and N <= 2048 // K))
 
     def forward(self, x: torch.Tensor, keep: bool, last_out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """x [M, K] with unit column stride and 16-B aligned rows (a column view of a wider panel is fine)."""
@@ -679,7 +686,9 @@ class ChainRun:
                 items.append((N, K, M, A, B, dW, db))
             wn.append((g, v, l, dW, gt, vt, N, K))
         if items:
-            if ASYNC_WGRAD and _WN_BWD[0] is not None:
+            if _WGRAD_DEFER[0] is not None:
+                _wgrad(lambda items=items, prec=self.prec: gemm_tn_grouped(items, prec))
+            elif ASYNC_WGRAD and _WN_BWD[0] is not None:
                 _wgrad_async(items, self.prec, dev)
             else:
                 gemm_tn_grouped(items, self.prec)
@@ -688,6 +697,35 @@ class ChainRun:
                     torch.zeros(N, device=dev), vt if vt is not None else torch.zeros(N, K, device=dev))
         self.Y = self.x = self.bwd_packs = None
         return dx
+
+
+# Deferred weight gradients (wgrad_defer_begin / wgrad_flush): the data-parallel graph step ends its first captured
+# graph when the backward has queued the hash-table gradients (97 % of the all-reduce payload), starts
+# their all-reduce, and replays the MLPs' weight-gradient GEMMs -- queued here instead of launched -- as a second graph
+# while the exchange runs (graphs.GraphTrainer).  Everything a deferred launch reads stays referenced by its closure.
+_WGRAD_DEFER: List[Optional[list]] = [None]
+
+
+def wgrad_defer_begin() -> None:
+    if _WN_BWD[0] is None:
+        raise RuntimeError("weight gradients are deferred only inside a batched training backward (wn_bwd_begin)")
+    _WGRAD_DEFER[0] = []
+
+
+def wgrad_flush() -> None:
+    """Launch the deferred weight-gradient GEMMs in backward order (before the deferred weight-norm flush, which
+    reads their dW)."""
+    q, _WGRAD_DEFER[0] = _WGRAD_DEFER[0], None
+    for fn in q or []:
+        fn()
+
+
+def _wgrad(fn) -> None:
+    """Run a weight-gradient launch now, or queue it while the weight gradients are deferred."""
+    if _WGRAD_DEFER[0] is not None:
+        _WGRAD_DEFER[0].append(fn)
+    else:
+        fn()
 
 
 # Weight gradients on a side stream (MMS_SYNC_WGRAD=0).  Inside a training backward (deferred weight norm: nothing
@@ -984,10 +1022,12 @@ def _sdf_mlp_unfused_bwd(ctx, dout, params, dev):
     if gt is not None or vt is not None or bt is not None:
         dW3 = _dw_views([v3], dev)[0]
         db3 = bt if bt is not None else torch.zeros(N3, device=dev)
-        gemm(TN, N3, K3, M, dout, dout.stride(0), H, H.stride(0), dW3, K3, accumulate=True,
-             splits=_splits_for(M, 6, prec), prec=prec, colsum=db3)
-        gemm(TN, 1, K3, 4 * M, dout[M:], dout.stride(0), H[M:], H.stride(0), dW3, K3, accumulate=True,
-             splits=_splits_for(4 * M, 2, prec), prec=prec, colsum=db3)
+        def wg(dout=dout, H=H, dW3=dW3, db3=db3):
+            gemm(TN, N3, K3, M, dout, dout.stride(0), H, H.stride(0), dW3, K3, accumulate=True,
+                 splits=_splits_for(M, 6, prec), prec=prec, colsum=db3)
+            gemm(TN, 1, K3, 4 * M, dout[M:], dout.stride(0), H[M:], H.stride(0), dW3, K3, accumulate=True,
+                 splits=_splits_for(4 * M, 2, prec), prec=prec, colsum=db3)
+        _wgrad(wg)
         _wn_bwd(g3.reshape(-1), v3, ctx.n3, dW3, gt.reshape(-1) if gt is not None else
                         torch.zeros(N3, device=dev), vt if vt is not None else torch.zeros(N3, K3, device=dev))
     # dZ of the last hidden layer = (dout W3) * softplus'(Z) -- the activation gradient fused as aux
@@ -1302,6 +1342,8 @@ class BackgroundFunction(torch.autograd.Function):
         if grid is not None:
             grid_fwd(grid, X, X.stride(0), M, table, active, X, 39)
         ctx.grid, ctx.active, ctx.table = grid, active, table
+        if grid is not None and ctx.needs_input_grad[2]:
+            _grad_use(table)
         # base and head MLPs: 4-layer chain kernels in bf16 (mlp_runner), per-layer GEMMs otherwise
         base = mlp_runner(base_p, BG_BASE_ACTS[:nb], PRECISION["background"])
         base.forward(X, keep=True, last_out=H[:, :Fb])  # writes cols [0, Fb) of the head panel
@@ -1336,6 +1378,7 @@ class BackgroundFunction(torch.autograd.Function):
             dtable = grad_target(ctx.table) if ctx.needs_input_grad[2] else None
             dP = torch.zeros(M, 3, device=dev)
             grid_bwd(ctx.grid, ctx.X, ctx.X.stride(0), M, ctx.table, ctx.active, dX, 39, dtable, dP)
+            _grad_ready(ctx.table, dtable)
             dX[:, :3] += dP
         dpos = torch.empty(M, 3, device=dev) if ctx.needs_input_grad[0] else None
         ddirs = _zeroed_views([(R, 3)], dev)[0] if ctx.needs_input_grad[1] else None
@@ -1379,8 +1422,9 @@ def _mlp_strided_bwd(run, dy: torch.Tensor, H: torch.Tensor, Fb: int, dx_into: O
     if gt is not None or vt is not None or bt is not None:
         dW = _dw_views([v], dev)[0]
         db = bt if bt is not None else torch.zeros(N, device=dev)
-        gemm(TN, N, K, M, dZ, dZ.stride(0), H, H.stride(0), dW, K, accumulate=True,
-             splits=_splits_for(M, 1, run.bprec), prec=run.bprec, colsum=db)
+        _wgrad(lambda dZ=dZ, H=H, dW=dW, db=db: gemm(
+            TN, N, K, M, dZ, dZ.stride(0), H, H.stride(0), dW, K, accumulate=True,
+            splits=_splits_for(M, 1, run.bprec), prec=run.bprec, colsum=db))
         dg = gt.reshape(-1) if gt is not None else torch.zeros(N, device=dev)
         dv = vt if vt is not None else torch.zeros(N, K, device=dev)
         _wn_bwd(g.reshape(-1), v, run.norms[0], dW, dg, dv)

@@ -25,8 +25,13 @@ differ from the previous step's runs eagerly (early in a 100k-step run some of t
 graph is captured once they hold still.  The AdamW scalars (learning-rate schedule, bias corrections) change
 every step and are read from a device buffer instead (``mms_adamw_dev``).
 
-Multi-GPU: the RCCL gradient all-reduce stays outside the graphs (forward/backward graph, all-reduce,
-optimizer graph), so each rank may replay a different capacity and no collective is ever captured.
+Multi-GPU: the RCCL gradient all-reduce stays outside the graphs, so each rank may replay a different capacity
+and no collective is ever captured.  The data-parallel step is three graphs: (1) forward + backward with the MLPs'
+weight-gradient GEMMs deferred (functions.wgrad_defer_begin) -- when it ends, every hash-table gradient (97 % of the
+138-205 MB payload) is final, so their bucketed all-reduces are launched right after its replay; (2) the
+deferred weight-gradient GEMMs + weight-norm flush, replayed while those all-reduces run on RCCL's stream; (3) the
+rest of the all-reduce, then clip + AdamW (+ the next step's draws).  The two backward graphs are one capture split
+where pipeline.backward_batched calls ``between``.
 """
 from __future__ import annotations
 
@@ -145,7 +150,7 @@ class GraphTrainer:
         return {m: t.images[m][self.sel[m], self.coords[m][:, 1].long(), self.coords[m][:, 2].long()]
                 for m in t.modalities}
 
-    def _forward_backward(self, cap: int):
+    def _forward_backward(self, cap: int, between=None):
         t = self.t
         targets = self._targets()
         t.fields.zero_grad()
@@ -153,12 +158,13 @@ class GraphTrainer:
             t.poses.zero_grad()
         fx.zero_arena_begin(t.device)
         try:
-            return self._forward_backward_body(t, targets, cap)
+            return self._forward_backward_body(t, targets, cap, between)
         finally:
             fx.zero_arena_end()
 
-    def _forward_backward_body(self, t, targets, cap: int):
+    def _forward_backward_body(self, t, targets, cap: int, between=None):
         rays = t.raygen(self.coords)
+        fx.reset_grad_uses()
         outputs = t.model(rays, None, cap=cap)
         if t.raw:
             for m in t.modalities:
@@ -166,8 +172,47 @@ class GraphTrainer:
                 band = t.masks[m][c[:, 1].long(), c[:, 2].long()].long()[:, None]
                 outputs[m][m] = select_right_channel(outputs[m][m], band)
         losses, total = compute_loss(outputs, targets, t.modalities, t.step, max_iters=t.cfg.max_iters)
-        backward_batched(total)
+        backward_batched(total, between)
         return losses, total
+
+    def table_grads(self):
+        """Flat-buffer views of the hash-table gradients: final when the first data-parallel graph ends."""
+        return [p.grad.view(-1) for name, p in self.t.model.named_parameters() if name.endswith("hash_table")]
+
+    @staticmethod
+    def _capture_stream():
+        if torch.cuda.graph.default_capture_stream is None:
+            torch.cuda.graph.default_capture_stream = torch.cuda.Stream()
+        return torch.cuda.graph.default_capture_stream
+
+    def _capture_split(self, cap: int, mode: str):
+        """Data-parallel capture: the forward/backward split into two graphs where the backward has queued all but
+        the deferred weight gradients (pipeline.backward_batched ``between``)."""
+        g1a, g1b = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        pool = () if self.pool is None else (self.pool,)
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        live = [g1a]
+
+        def between():
+            live[0].capture_end()
+            live[0] = g1b
+            g1b.capture_begin(g1a.pool(), capture_error_mode=mode)
+
+        with torch.cuda.stream(self._capture_stream()):
+            g1a.capture_begin(*pool, capture_error_mode=mode)
+            try:
+                out = self._forward_backward(cap, between)
+            except BaseException:
+                try:
+                    live[0].capture_end()
+                except Exception:
+                    pass
+                raise
+            live[0].capture_end()
+        if live[0] is not g1b:
+            raise RuntimeError("the backward never reached its split point")
+        return g1a, g1b, out
 
     def _optimizer(self):
         t = self.t
@@ -180,15 +225,19 @@ class GraphTrainer:
         # thread-local capture mode when a process group is up: RCCL's watchdog thread queries events meanwhile
         mode = CAPTURE_MODE or ("thread_local" if self.ddp is not None else "global")
         torch.cuda.synchronize()
-        g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1, pool=self.pool, capture_error_mode=mode):
-            out = self._forward_backward(cap)
-            if self.ddp is None:
+        if self.ddp is None:
+            g1 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1, pool=self.pool, capture_error_mode=mode):
+                out = self._forward_backward(cap)
                 self._optimizer()
                 if self.tail:
                     self._tail()
+            pool = g1.pool()
+        else:
+            g1a, g1b, out = self._capture_split(cap, mode)
+            g1, pool = (g1a, g1b), g1a.pool()
         if self.pool is None:
-            self.pool = g1.pool()
+            self.pool = pool
         g2 = None
         if self.ddp is not None:
             g2 = torch.cuda.CUDAGraph()
@@ -271,9 +320,14 @@ class GraphTrainer:
             self._queue_hyper()
         self.hyper_step = None
         g1, g2, out = self.graphs[key]
-        g1.replay()
-        if self.ddp is not None:
-            self.ddp.allreduce_grads([t.fields] + ([t.poses] if t.poses is not None else []))
+        if self.ddp is None:
+            g1.replay()
+        else:
+            # the hash-table gradients' all-reduce (launched after the first graph) runs while the second graph
+            # replays the deferred weight gradients; the rest follows, then the optimizer graph
+            g1[0].replay()
+            self.ddp.overlap_exchange(self.table_grads(), [t.fields] + ([t.poses] if t.poses is not None else []),
+                                      g1[1].replay)
             g2.replay()
         if self.tail:
             self.count_event.record()

@@ -133,7 +133,7 @@ def act_bwd(dY, Z, act, beta, thr, dZ):
               float(thr), dZ.data_ptr(), dZ.stride(0), _stream())
 
 
-# split-K target: blocks per weight-gradient GEMM (measured, scratch/tn_sweep.py): one 128x128-tile block per CU for
+# split-K target: blocks per weight-gradient GEMM (measured, scripts/tn_sweep.py): one 128x128-tile block per CU for
 # bf16 operands (more splits only add float atomics), two for split-bf16x3 (3 MFMAs per product), four for fp32
 _SPLIT_BLOCKS = {0: 1024, 1: 256, 2: 512}
 

@@ -292,10 +292,40 @@ def select_right_channel(rendered: torch.Tensor, band: torch.Tensor) -> torch.Te
 # ------------------------------------------------------------------------------------------------
 # trainer
 # ------------------------------------------------------------------------------------------------
-# per-modality training views skipped by confs/grid_raw_rgb_all_views_pol_10_views.yaml (config 5: the unbalanced
-# dataset keeps 10 polarization training views out of 45)
-POL_10_VIEWS_SKIP = [0, 1, 2, 3, 5, 7, 8, 10, 11, 13, 15, 16, 17, 18, 20, 21, 23, 24, 26, 28, 30, 31, 32, 33, 35, 36,
-                     37, 38, 40, 42, 43, 45, 46, 47, 48]
+CONFS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "confs")
+# the BASELINE configurations' YAML per method (confs/: the reference files' keys read here, same schema)
+METHOD_CONF = {"grid": "grid.yaml", "grid_raw": "grid_raw.yaml", "mlp_raw": "mlp_raw.yaml",
+               "grid_raw_grid_bg_unbalanced": "grid_raw_rgb_all_views_pol_10_views.yaml"}
+
+
+def read_conf(path: str) -> dict:
+    """The training-step keys of an MMS-FW experiment YAML (the reference's confs/*.yaml schema, applied over the method
+    registry by Config.update_config, /root/reference/src/configs/configs.py:214-242): method, max_num_iterations and
+    pipeline.datamanager's modalities, eval views (eval_image_indices or eval_image_indices_per_modality), skipped
+    training views (skip_image_indices_per_modality, datamanager.py) and pixel_sampler.num_rays_per_modality."""
+    import yaml
+    with open(path) as f:
+        y = yaml.safe_load(f)
+    dm = (y.get("pipeline") or {}).get("datamanager") or {}
+    mods = list(dm.get("modalities") or [])
+    ev = dm.get("eval_image_indices_per_modality")
+    if ev is None and dm.get("eval_image_indices") is not None:
+        ev = {m: list(dm["eval_image_indices"]) for m in mods}
+    return {"method": y.get("method"), "max_num_iterations": y.get("max_num_iterations"), "modalities": mods,
+            "eval_views": {m: list(v) for m, v in (ev or {}).items()},
+            "skip_views": {m: list(v) for m, v in (dm.get("skip_image_indices_per_modality") or {}).items()},
+            "num_rays_per_modality": (dm.get("pixel_sampler") or {}).get("num_rays_per_modality")}
+
+
+def skip_views_for(method: str) -> Optional[Dict[str, List[int]]]:
+    """skip_image_indices_per_modality of the method's BASELINE YAML (config 5 keeps 10 polarization training views:
+    confs/grid_raw_rgb_all_views_pol_10_views.yaml:47-48 in the reference), None when it skips nothing."""
+    name = METHOD_CONF.get(method)
+    if name is None:
+        return None
+    return read_conf(os.path.join(CONFS, name))["skip_views"] or None
+
+
 METHODS = {
     # method name: (raw mosaicked frames, background field kind, field kind)
     "grid": (False, "nerf", "grid"),
@@ -324,12 +354,25 @@ class TrainConfig:
     own_heads_only: bool = True         # training renders each modality's rays through its own head only
 
 
-def backward_batched(total: torch.Tensor) -> None:
-    """total.backward() with the layers' weight-norm gradients applied in one batched launch at its end."""
+def backward_batched(total: torch.Tensor, between=None) -> None:
+    """total.backward() with the layers' weight-norm gradients applied in one batched launch at its end.
+
+    ``between`` (data-parallel graph steps): the MLPs' weight-gradient GEMMs are deferred, ``between()`` runs once the
+    backward has queued everything else -- the hash-table gradients are final there -- and the deferred launches and
+    the weight-norm flush follow it (graphs.GraphTrainer ends one captured graph and begins the next there)."""
     fx.wn_bwd_begin()
     try:
-        total.backward()
+        if between is not None:
+            fx.wgrad_defer_begin()
+            try:
+                total.backward()
+            finally:
+                between()
+            fx.wgrad_flush()
+        else:
+            total.backward()
     finally:
+        fx._WGRAD_DEFER[0] = None
         fx.wn_bwd_flush()
 
 

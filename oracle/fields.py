@@ -212,11 +212,21 @@ def scene_contraction_linf(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def nerf_field(x, d, P, prefix="background_model.background_field", base_layers=4, head_layers=4):
-    """NeRFField.forward (nerf_field.py:92-105) for the 'grid' method background (method_configs.py:187-212)."""
+# the config-5 background base field (method_configs.py:430-441): FeatureGridAndMLP, hash grid r = 2, MLP 71-128-128-256
+BG_GRID_MLP = dict(num_layers=3, act="ReLU", act_params=None, out_act="ReLU")
+
+
+def nerf_field(x, d, P, prefix="background_model.background_field", base_layers=4, head_layers=4,
+               grid: "GridSpec" = None, active_levels: int = 16):
+    """NeRFField.forward (nerf_field.py:92-105) for the 'grid' method background (method_configs.py:187-212); with
+    ``grid`` the base field is 'grid_raw_grid_bg_unbalanced''s FeatureGridAndMLP on the PE of the contracted position
+    (method_configs.py:428-445; feature_structures.py:153-169 splits x = PE[:3] off for the grid)."""
     xe = nerf_encoding(x, 6, 0.0, 5.0, True)
     de = nerf_encoding(d, 4, 0.0, 3.0, True)
-    feat = mlp_forward(xe, P, prefix + ".base_field", base_layers, "ReLU", None, "ReLU")
+    if grid is not None:
+        feat = feature_grid_and_mlp(xe, P, prefix + ".base_field", grid, active_levels, BG_GRID_MLP)
+    else:
+        feat = mlp_forward(xe, P, prefix + ".base_field", base_layers, "ReLU", None, "ReLU")
     density = mlp_forward(feat, P, prefix + ".density_head.field", 1, "ReLU", None, "Softplus")
     head = mlp_forward(torch.cat([feat, de], -1), P, prefix + ".head_field", head_layers, "ReLU", None, "ReLU")
     return density, head

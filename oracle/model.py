@@ -108,12 +108,22 @@ class ModelSpec:
     bg_samples: int = 16
     raw: bool = False
     fields: str = "grid"      # "grid" (hash grid + 3-layer MLPs, 4-tap gradients) | "mlp" (8-layer MLPs, autograd)
+    # background base field: None = the NeRF MLP; a GridSpec = config 5's hash grid (r = 2) + 71-128-128-256 MLP
+    bg_grid: Optional[of.GridSpec] = None
 
 
-def spec_grid(modalities: Dict[str, int], log2T: int = 19, raw: bool = False) -> ModelSpec:
+def spec_grid(modalities: Dict[str, int], log2T: int = 19, raw: bool = False, bg_kind: str = "nerf") -> ModelSpec:
+    """Methods grid / grid_raw (bg_kind "nerf"), or grid_raw_grid_bg_unbalanced (bg_kind "grid": the background base
+    field a FeatureGridAndMLP with a radius-2 hash grid, head 283-256x3-256, and the radiance model's 3-layer heads,
+    method_configs.py:428-445)."""
     s = ModelSpec(modalities=dict(modalities), grid=of.GridSpec(16, 16, 1024, log2T, 1.0), raw=raw)
     s.head_layers = {m: 3 for m in modalities}
     s.bg_head_layers = {m: 1 for m in modalities}
+    if bg_kind == "grid":
+        s.bg_grid = of.GridSpec(16, 16, 1024, log2T, 2.0)
+        s.bg_head_layers = {m: 3 for m in modalities}
+    elif bg_kind != "nerf":
+        raise ValueError(bg_kind)
     return s
 
 
@@ -203,7 +213,7 @@ def model_forward(rays: Dict[str, orr.Rays], P, spec: ModelSpec, st: StepState, 
             bn, bf = orr.background_near_far(r.origins, r.directions)
             bbins = orr.stratified_bins(bn.shape[0], spec.bg_samples, rng.background[mod])
             bsmp = orr.make_samples(bbins, bn, bf, "disparity")
-            bg = background_forward(bsmp, r, P, spec)
+            bg = background_forward(bsmp, r, P, spec, st)
         R, S = smp.starts.shape[:2]
         pos = orr.positions(o_h, d_h, smp.starts).reshape(-1, 3)
         sdf, geo, grads, hess = surface_forward(pos, P, spec, st)
@@ -245,14 +255,15 @@ def radiance_forward(pos, d_h, up_h, normals, geo, P, spec: ModelSpec, st: StepS
     return out
 
 
-def background_forward(bsmp: orr.Samples, r: orr.Rays, P, spec: ModelSpec):
+def background_forward(bsmp: orr.Samples, r: orr.Rays, P, spec: ModelSpec, st: StepState = None):
     """BackgroundModel.forward (background_model.py:73-111) with L-inf contraction."""
     N, S = bsmp.starts.shape[:2]
     pos = orr.positions(r.origins, r.directions, bsmp.starts).reshape(-1, 3)
     dirs = r.directions[:, None, :].expand(N, S, 3).reshape(-1, 3)
     ups = r.up[:, None, :].expand(N, S, 3).reshape(-1, 3)
     pos = of.scene_contraction_linf(pos)
-    density, feat = of.nerf_field(pos, dirs, P)
+    density, feat = of.nerf_field(pos, dirs, P, grid=spec.bg_grid,
+                                  active_levels=st.active_levels if st is not None else 16)
     density = density.view(N, S, -1)
     alphas = 1 - torch.exp(-(bsmp.deltas * density))
     w = orr.weights_from_alphas(alphas)

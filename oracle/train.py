@@ -18,10 +18,10 @@ from . import rays as orr
 class OracleTrainer:
     def __init__(self, state_dict: Dict[str, torch.Tensor], modalities: Dict[str, int], cams: dict, log2T: int,
                  step: int, raw: bool = False, pose: Dict[str, torch.Tensor] = None,
-                 mosaick: Dict[str, torch.Tensor] = None, fields: str = "grid"):
+                 mosaick: Dict[str, torch.Tensor] = None, fields: str = "grid", bg_kind: str = "nerf"):
         self.P = {k: v.detach().clone().float().cpu().requires_grad_(True) for k, v in state_dict.items()}
         self.spec = om.spec_mlp(modalities, raw=raw) if fields == "mlp" else om.spec_grid(modalities, log2T=log2T,
-                                                                                              raw=raw)
+                                                                                              raw=raw, bg_kind=bg_kind)
         self.cams = cams
         self.mods = list(modalities)
         self.pose = {m: (pose[m].detach().clone() if pose else torch.zeros(1, 6)).requires_grad_(True)
@@ -30,6 +30,9 @@ class OracleTrainer:
         self.mosaick = mosaick or {}      # raw methods: per-modality band masks (select_right_channel)
         self.field_state: dict = {}
         self.pose_state: dict = {}
+        # optional callable(params) run between backward and clipping: perturbation studies of the trajectory's
+        # sensitivity to last-bit gradient differences (tests/golden/make_train_parity.py --perturb)
+        self.grad_hook = None
 
     def rng(self, n_hit: Dict[str, int], n_rays: Dict[str, int]) -> om.RNG:
         """Uniform draws in the reference's order."""
@@ -59,6 +62,8 @@ class OracleTrainer:
         f = om.lr_factor(self.step)
         fields: List[torch.Tensor] = list(self.P.values())
         poses: List[torch.Tensor] = list(self.pose.values())
+        if self.grad_hook is not None:
+            self.grad_hook(fields + poses)
         om.clip_grad_norm(fields, 2.0)
         om.clip_grad_norm(poses, 2.0)
         om.adamw_step(fields, self.field_state, 1e-3 * f)

@@ -2,8 +2,9 @@
 ``python -m torch.distributed.run --nproc-per-node 2 tests/ddp_check.py <out.json>`` (both ranks on cuda:0, gloo
 collectives: RCCL needs one GPU per rank).  Not a pytest module.
 
-0. GraphTrainer(ddp) x 5 (graph replays with the all-reduce between the two captured graphs): parameters identical
-   on both ranks and the steps were replayed.
+0. GraphTrainer(ddp) x 5 (graph replays: the hash-table all-reduce launched after the first backward graph, overlapping
+   the replay of the deferred weight gradients, the rest after it): averaged gradients, parameters identical on both
+   ranks, and the steps were replayed.
 1. Trainer.compute_grads(ddp) -- hash-table gradients all-reduced while the backward still runs, the rest after --
    equals the average of the two ranks' local gradients (local pass = same batch, same device RNG seed, no ddp).
 2. Trainer.train_step(ddp) x 2: parameters identical on both ranks.
@@ -52,19 +53,34 @@ def main():
     g = GraphTrainer(tg, ddp=ddp)
     # the graph path's exchange: the local gradients the replayed forward/backward graph left, and what the
     # all-reduce between the two graphs made of them
-    seen = {"local": [], "reduced": []}
-    orig = ddp.allreduce_grads
+    # (split path: the hash-table regions are launched while the second backward graph replays, so their local values
+    # are snapshotted at launch -- ordered before the collective on the stream -- and the rest when the exchange
+    # finishes the step)
+    seen = {"local": [], "reduced": [], "early": [], "overlapped": 0}
+    orig_ready, orig_finish = ddp.grad_ready, ddp.finish_step
 
-    def spy(groups):
-        seen["local"].append([gr.grad.clone() for gr in groups])
-        orig(groups)
+    def spy_ready(grad, groups):
+        seen["early"].append((grad.data_ptr(), grad.detach().reshape(-1).clone()))
+        orig_ready(grad, groups)
+
+    def spy_finish(groups):
+        local = [gr.grad.clone() for gr in groups]
+        for ptr, early in seen["early"]:
+            for gr, lg in zip(groups, local):
+                off = (ptr - gr.grad.data_ptr()) // 4
+                if 0 <= off < gr.grad.numel():
+                    lg[off:off + early.numel()] = early
+        seen["overlapped"] += len(seen["early"])
+        seen["early"] = []
+        seen["local"].append(local)
+        orig_finish(groups)
         seen["reduced"].append([gr.grad.clone() for gr in groups])
 
-    ddp.allreduce_grads = spy
+    ddp.grad_ready, ddp.finish_step = spy_ready, spy_finish
     for _ in range(5):
         g.step()
     torch.cuda.synchronize()
-    ddp.allreduce_grads = orig
+    ddp.grad_ready, ddp.finish_step = orig_ready, orig_finish
     if seen["local"]:
         errs = []
         for local, red in zip(seen["local"], seen["reduced"]):
@@ -73,6 +89,7 @@ def main():
                 errs.append(float((rg.cpu() - mean).abs().max()) / max(float(mean.abs().max()), 1e-30))
         res["graph_grad_err"] = max(errs)
         res["graph_allreduces"] = len(seen["local"])
+        res["graph_overlapped_regions"] = seen["overlapped"]
     p = gather(tg.fields.flat)
     q = gather(tg.poses.flat)
     res["graph_params_equal"] = bool(torch.equal(p[0], p[1]) and torch.equal(q[0], q[1]))

@@ -101,3 +101,28 @@ def test_loader_matches_reference_dataset(tmp_path, tag):
         if raw:
             np.testing.assert_array_equal(ds.mosaick_masks[m].numpy(), gold[f"{tag}:{m}:mosaick_mask"], err_msg=m)
     assert float(ds.scene_box["radius"]) == float(gold[f"{tag}:radius"])
+
+
+REF_CONFS = "/root/reference/confs"
+
+
+@pytest.mark.parametrize("name", ["grid.yaml", "grid_raw.yaml", "mlp_raw.yaml", "grid_raw_rgb_all_views_pol_10_views.yaml"])
+def test_conf_extracts_match_reference(name):
+    """confs/*.yaml (the training-step keys the bench and trainer read, e.g. config 5's skipped polarization views)
+    parse to the same values as the reference's own YAML file (checked where the reference is present)."""
+    from multimodalstudio_amd.pipeline import CONFS, read_conf
+    mine = read_conf(os.path.join(CONFS, name))
+    if os.path.isdir(REF_CONFS):
+        assert mine == read_conf(os.path.join(REF_CONFS, name))
+    assert mine["num_rays_per_modality"] == 2048 and mine["max_num_iterations"] == 100000
+
+
+def test_config5_skip_views():
+    """Config 5 (grid_raw_grid_bg_unbalanced) trains polarization on 10 of the 45 non-eval views."""
+    from multimodalstudio_amd import scene as ms
+    from multimodalstudio_amd.pipeline import skip_views_for
+    skip = skip_views_for("grid_raw_grid_bg_unbalanced")
+    assert set(skip) == {"polarization"}
+    train = [v for v in range(50) if v not in ms.EVAL_VIEWS and v not in skip["polarization"]]
+    assert len(train) == 10
+    assert skip_views_for("grid_raw") is None

@@ -273,3 +273,16 @@ def test_polarization_extras():
     I = 0.5 * torch.tensor([[s0 + s1, s0 + s2, s0 - s1, s0 - s2]], dtype=torch.float64)
     assert abs(float(ev.degree_of_polarization(I)[0]) - p) < 1e-12
     assert abs(float(ev.angle_of_polarization(I)[0]) - psi) < 1e-6
+
+
+def test_small_linear_serves_only_shapes_with_a_backward(L):
+    """functions.SmallRun accepts a layer for the narrow-layer kernels only where mms_small_linear_bwd accepts it too
+    (checked through the C-ABI's argument validation: M = 0 returns after the shape checks, no device work)."""
+    from multimodalstudio_amd.functions import SmallRun
+    for K in (64, 128, 256, 512):
+        for N in range(1, 18):
+            rc_b = L.mms_small_linear_bwd(None, K, 0, K, None, N, 0, 1.0, 20.0, None, N, None, N, None, K, 0, None,
+                                          None, None)
+            rc_f = L.mms_small_linear_fwd(None, K, 0, K, None, None, N, 0, 1.0, 20.0, None, N, None)
+            ok = SmallRun.shape_ok(N, K)
+            assert ok == (rc_b == 0 and rc_f == 0), (N, K, rc_b, rc_f, _err(L))

@@ -52,6 +52,15 @@ def run_parity(dev, precision: str, gold: str = GOLD, eps=None, cfg=None, histor
         ck = float(sum(float(v.detach().double().abs().sum()) for v in tr.model.state_dict().values()))
         if f is not None:
             assert ck == pytest.approx(float(f["init_checksum"]), rel=1e-9), "model init drifted from the fixture"
+        if cfg.get("start_state"):
+            # the fixture's shared partially trained state (parameters and pose deltas), copied into the flat buffers
+            from make_train_parity import load_start_state
+            sd, poses = load_start_state(cfg, {k: v.detach().cpu() for k, v in tr.model.state_dict().items()})
+            with torch.no_grad():
+                for k, v in tr.model.state_dict().items():
+                    v.copy_(sd[k].to(dev))
+                for m, pz in (poses or {}).items():
+                    tr.pose.pose_adjustment[m].copy_(pz.to(dev))
         tr.set_step(cfg["start_step"])
         tr.fields.step_count = 0          # fresh optimizer state, as the oracle run
         # AdamW eps of the fixture's run (the reference's 1e-15 unless the fixture records another)

@@ -133,7 +133,9 @@ def run_oracle_e2e(f):
     raw = bool(f["raw"])
     key = "p:surface_model.surface_field.field.feature_grid.encoding.hash_table"
     if key in f:
-        spec = om.spec_grid({m: CHANNELS[m] for m in mods}, log2T=int(np.log2(f[key].shape[0] // 16)), raw=raw)
+        bg = "grid" if "p:background_model.background_field.base_field.feature_grid.encoding.hash_table" in f else "nerf"
+        spec = om.spec_grid({m: CHANNELS[m] for m in mods}, log2T=int(np.log2(f[key].shape[0] // 16)), raw=raw,
+                            bg_kind=bg)
     else:
         spec = om.spec_mlp({m: CHANNELS[m] for m in mods}, raw=raw)
     st = om.StepState(step=int(f["step"]))
@@ -159,7 +161,8 @@ def run_oracle_e2e(f):
 
 
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_rgb_s30000", "e2e_grid_raw_5mod_s95000",
-                                  "e2e_grid_raw_5mod_sat_s95000", "e2e_mlp_raw_rgb_s95000"])
+                                  "e2e_grid_raw_5mod_sat_s95000", "e2e_mlp_raw_rgb_s95000",
+                                  "e2e_grid_raw_gridbg_s95000"])
 def test_end_to_end(name):
     f = e2e_inputs(name)
     mods, outs, losses, total, P, poses = run_oracle_e2e(f)
