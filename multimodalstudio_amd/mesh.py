@@ -118,10 +118,14 @@ def crop_sdf_pyramid(sdf_fn, lo, hi, device, chunk: int = 1 << 21, stats: Option
         p = p.reshape(3, -1).permute(1, 0)
         if mask is None:
             sdf = evaluate(p)
+            count = p.shape[0]
         else:
             m = mask.reshape(-1)
-            if bool(m.any()):
+            count = int(m.sum())
+            if count:
                 sdf[m] = evaluate(p[m])
+        if stats is not None:
+            stats.setdefault("levels", []).append(count)      # points this pyramid level evaluated
         if pid < 3:
             mask = (torch.abs(sdf) < threshold).reshape(1, 1, cn, cn, cn)
             mask = torch.nn.functional.interpolate(mask.float(), scale_factor=2, mode="nearest").bool()

@@ -517,8 +517,86 @@ def gen_loader():
     save("loader", **out)
 
 
+def analytic_sdf(p: torch.Tensor) -> torch.Tensor:
+    """The mesh fixture's surface: a sphere (r 0.45 about (0.1, -0.05, 0.2)) united with a torus (R 0.6, r 0.12, axis z),
+    evaluated in float32 from the (float16) grid points.  tests/test_gpu_mesh.py evaluates the same expression."""
+    p = p.float()
+    c = torch.tensor([0.1, -0.05, 0.2], dtype=torch.float32)
+    sphere = torch.sqrt(((p - c) ** 2).sum(-1)) - 0.45
+    q = torch.sqrt(p[:, 0] ** 2 + p[:, 1] ** 2) - 0.6
+    torus = torch.sqrt(q ** 2 + p[:, 2] ** 2) - 0.12
+    return torch.minimum(sphere, torus)
+
+
+def gen_mesh(resolution=512, n_sample=65536):
+    """get_surface_sliding (/root/reference/src/utils/marching_cubes.py:35-171) on the analytic SDF with its
+    skimage.measure.marching_cubes call (:158) intercepted: per crop, the points each pyramid level evaluated (from the
+    reference's 100000-point evaluation chunks), and the crop's final volume z (the marching-cubes input) as its sign
+    census, float64 sum and a fixed random sample of entries.  skimage / trimesh are absent here: the triangulation
+    itself stays unpinned.  The reference moves points to .cuda(); on this CPU-only container that is the identity."""
+    import utils.marching_cubes as rmc
+    chunks, vols = [], []
+
+    def sdf_fn(pnts):
+        chunks.append(int(pnts.shape[0]))
+        return analytic_sdf(pnts)
+
+    def fake_mc(volume, level, spacing, mask=None):
+        vols.append((len(chunks), np.array(volume, dtype=np.float32, copy=True), tuple(float(x) for x in spacing)))
+        return np.zeros((0, 3)), np.zeros((0, 3), dtype=np.int64), np.zeros((0, 3)), np.zeros(0)
+
+    rmc.measure.marching_cubes = fake_mc
+    import types
+    rmc.trimesh = types.SimpleNamespace(Trimesh=lambda *a, **k: None,
+                                        util=types.SimpleNamespace(concatenate=lambda meshes: meshes))
+    # the CPU has no float16 avg_pool3d: the GPU kernel's arithmetic (fp32 sum of the 8 halves -- exact --, / 8,
+    # rounded to half) restated
+    pool = rmc.avg_pool_3d
+    rmc.avg_pool_3d = lambda x: pool(x.float()).half() if x.dtype == torch.float16 else pool(x)
+    orig_cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    try:
+        rmc.get_surface_sliding(sdf_fn, resolution=resolution, return_mesh=True)
+    finally:
+        torch.Tensor.cuda = orig_cuda
+        rmc.avg_pool_3d = pool
+    # evaluation chunks -> per-level counts: a level's chunks are 100000 points each but its last
+    levels, acc = [], 0
+    for c in chunks:
+        acc += c
+        if c < 100000:
+            levels.append(acc)
+            acc = 0
+    n_crops = (resolution // 256) ** 3
+    assert len(levels) == 4 * n_crops, (len(levels), n_crops)
+    out = {"resolution": np.int64(resolution), "level_counts": np.array(levels, dtype=np.int64).reshape(n_crops, 4)}
+    g = np.random.default_rng(7)
+    idx = g.choice(256 ** 3, n_sample, replace=False).astype(np.int64)
+    out["sample_index"] = idx
+    crops = []
+    for ci, (_, vol, spacing) in enumerate(vols):
+        # the crop this call belongs to: the one whose 4 levels the evaluation chunks just completed
+        done, acc, lv = 0, 0, 0
+        for c in chunks[:_]:
+            acc += c
+            if c < 100000:
+                lv += 1
+                acc = 0
+        crop = lv // 4 - 1
+        crops.append(crop)
+        z = vol.reshape(-1)
+        out[f"crop{crop}:neg"] = np.int64((z < 0).sum())
+        out[f"crop{crop}:sum"] = np.float64(z.astype(np.float64).sum())
+        out[f"crop{crop}:sample"] = z[idx]
+        out[f"crop{crop}:spacing"] = np.array(spacing)
+    out["surface_crops"] = np.array(crops, dtype=np.int64)
+    save("mesh_pyramid", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["hashgrid", "mlp", "raygen", "sampler", "e2e", "plugins", "eval", "loader"]
+    which = sys.argv[1:] or ["hashgrid", "mlp", "raygen", "sampler", "e2e", "plugins", "eval", "loader", "mesh"]
+    if "mesh" in which:
+        gen_mesh()
     if "loader" in which:
         gen_loader()
     if "eval" in which:

@@ -42,14 +42,35 @@ CONFIGS = {
                  rays=96, log2T=12, width=96, height=80, n_views=10, start_step=95000, steps=50, checkpoints=(25,),
                  eval_rays=2048, init_seed=654824, sampler_seed=654824, rng_seed=11, eval_seed=5, bg_samples=16),
 }
-# the raw5 shape from a shared partially trained state (make_train_parity.py pretrain raw5): 400 oracle steps of its own
-# pixel / draw streams past the initial transient (in the window above held-out rgb PSNR first falls from geometric init),
-# so every modality improves in the 50-step window the parity test replays
-CONFIGS["raw5pre"] = dict(CONFIGS["raw5"], steps=400, checkpoints=(100, 200, 300), sampler_seed=654824 + 500000,
-                          rng_seed=11 + 500000)
-CONFIGS["raw5w"] = dict(CONFIGS["raw5"], start_state="train_parity_raw5_start.npz")
+# raw5 on the 45-training-view scene (50 views, the benchmark's view count; the 10-view scene above generalises so
+# poorly that held-out rgb PSNR falls while the training loss drops): every modality's held-out PSNR rises by
+# 1.3-7 dB over the first 50 steps.  Each seed's fixture also records an oracle-prime run (every gradient perturbed by
+# 2^-22 relative per step, perturber below): the reference algorithm's own sensitivity, the gate's null scatter.
+CONFIGS["raw5v"] = dict(CONFIGS["raw5"], n_views=50, checkpoints=(10, 20, 30, 40), prime=2.0 ** -22)
+# BASELINE configs[4] shape: grid_raw_grid_bg_unbalanced (rgb + polarization on 10 of its 45 views, the hash-grid
+# background, 3-layer background heads, SO3xR3 pose refinement)
+CONFIGS["bg5"] = dict(CONFIGS["raw5v"], method="grid_raw_grid_bg_unbalanced", modalities=("rgb", "polarization"),
+                      steps=40, checkpoints=(10, 20, 30))
 CFG = CONFIGS["rgb"]
 HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def method_kind(cfg):
+    """(raw mosaicked frames, background kind) of the fixture's method (pipeline.METHODS)."""
+    from multimodalstudio_amd.pipeline import METHODS
+    raw, bg_kind, _ = METHODS[cfg["method"]]
+    return raw, bg_kind
+
+
+def train_cameras(cfg, mods):
+    """The training views: the method's YAML skip list applied (config 5 keeps 10 polarization views of the 45)."""
+    from multimodalstudio_amd import scene as ms
+    from multimodalstudio_amd.pipeline import skip_views_for
+    cams = ms.make_cameras(mods, cfg["n_views"], cfg["width"], cfg["height"], seed=0, train=True)
+    for m, skip in (skip_views_for(cfg["method"]) or {}).items():
+        if m in cams:
+            cams[m] = ms.select_views(cams[m], [v for v in cams[m].view_ids if v not in set(skip)])
+    return cams
 
 
 def load_start_state(cfg, sd: dict, poses: dict = None):
@@ -136,13 +157,13 @@ def main(name: str = "rgb", seed: int = 0, perturb: float = 0.0, out_path: str =
     cfg = seeded(CONFIGS[name], seed)
     if checkpoints is not None:
         cfg = dict(cfg, checkpoints=tuple(checkpoints))
-    raw = cfg["method"] == "grid_raw"
+    raw, bg_kind = method_kind(cfg)
     mods = list(cfg["modalities"])
     channels = {m: ms.CHANNELS[m] for m in mods}
     torch.manual_seed(cfg["init_seed"])
-    model = BaseModel(ModelSpec(channels, log2T=cfg["log2T"]))
+    model = BaseModel(ModelSpec(channels, log2T=cfg["log2T"], bg_kind=bg_kind))
     sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
-    cams = ms.make_cameras(mods, cfg["n_views"], cfg["width"], cfg["height"], seed=0, train=True)
+    cams = train_cameras(cfg, mods)
     ecams = ms.make_cameras(mods, cfg["n_views"], cfg["width"], cfg["height"], seed=0, train=False)
     cpu = torch.device("cpu")
     images = {m: ms.render_frames(cams[m], channels[m], cpu, m if raw else None) for m in mods}
@@ -153,7 +174,8 @@ def main(name: str = "rgb", seed: int = 0, perturb: float = 0.0, out_path: str =
     sampler = UniformPixelSampler(cfg["rays"], cfg["sampler_seed"])
     init_ck = param_checksum(sd)
     sd, poses = load_start_state(cfg, sd)
-    ot = OracleTrainer(sd, channels, cams, cfg["log2T"], cfg["start_step"], raw=raw, pose=poses, mosaick=masks)
+    ot = OracleTrainer(sd, channels, cams, cfg["log2T"], cfg["start_step"], raw=raw, pose=poses, mosaick=masks,
+                       bg_kind=bg_kind)
     gen = torch.Generator().manual_seed(cfg["rng_seed"])
 
     def rng_hook(n_hit, n_rays):
@@ -200,6 +222,10 @@ def main(name: str = "rgb", seed: int = 0, perturb: float = 0.0, out_path: str =
         if k % 25 == 0:
             print(f"step {k}: loss {float(out[f's{k}:loss']):.6f} ({time.time() - t0:.1f}s)", flush=True)
     evaluate("eval")
+    if cfg.get("prime") and perturb == 0:
+        # the oracle-prime companion run of the same seed
+        prime = main(name, seed, float(cfg["prime"]), checkpoints=checkpoints, save=False)
+        out.update({"prime:" + k: v for k, v in prime.items() if "psnr" in k})
     if save_state:
         st = {"p:" + k: v.detach().numpy() for k, v in ot.P.items()}
         st.update({"pose:" + m: ot.pose[m].detach().numpy() for m in mods})

@@ -162,7 +162,8 @@ def test_e2e_train_step(dev, name):
     assert worst_l2 < E2E_PARAM_L2_TOL.get(name, E2E_PARAM_L2_TOL_DEFAULT), worst_l2
 
 
-@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000", "e2e_grid_raw_5mod_sat_s95000"])
+@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000", "e2e_grid_raw_5mod_sat_s95000",
+                                  "e2e_grid_raw_gridbg_s95000"])
 def test_e2e_fast_preset_deviation(dev, name):
     """The benchmarked `fast` preset (every MLP on split-bf16x3 MFMA operands, the narrow background layers fp32 VALU)
     on the reference's fixture:

@@ -95,3 +95,46 @@ def test_model_mesh_export(dev, tmp_path):
     size = os.path.getsize(path)
     assert size == len(head) + len("end_header\n") + 12 * nv + 13 * nf
     assert ex.last_stats["evaluated"] < 0.25 * 256 ** 3
+
+
+def _fixture_sdf(p):
+    """tests/golden/make_golden.py analytic_sdf (sphere united with a torus), the same float32 expression."""
+    p = p.float()
+    c = torch.tensor([0.1, -0.05, 0.2], dtype=torch.float32, device=p.device)
+    sph = torch.sqrt(((p - c) ** 2).sum(-1)) - 0.45
+    q = torch.sqrt(p[:, 0] ** 2 + p[:, 1] ** 2) - 0.6
+    tor = torch.sqrt(q ** 2 + p[:, 2] ** 2) - 0.12
+    return torch.minimum(sph, tor)
+
+
+def test_pyramid_matches_reference_crops(dev):
+    """The coarse-to-fine SDF pyramid of every 256^3 crop against the reference's get_surface_sliding run on the same
+    analytic SDF (tests/golden/mesh_pyramid.npz, marching_cubes.py:35-171 with skimage's marching_cubes intercepted):
+    the points each pyramid level evaluates (the |sdf| < threshold masks, level by level) and the final volume handed
+    to marching cubes (sign census, sum, a fixed sample of entries).  The triangulation itself stays unpinned."""
+    from multimodalstudio_amd import mesh
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mesh_pyramid.npz")
+    f = np.load(path)
+    res = int(f["resolution"])
+    n = res // mesh.CROP
+    grid = [np.linspace(-1.0, 1.0, n + 1) for _ in range(3)]
+    idx = torch.from_numpy(f["sample_index"]).to(dev)
+    ci = 0
+    for i in range(n):
+        for j in range(n):
+            for k in range(n):
+                lo = (grid[0][i], grid[1][j], grid[2][k])
+                hi = (grid[0][i + 1], grid[1][j + 1], grid[2][k + 1])
+                stats = {}
+                z = mesh.crop_sdf_pyramid(_fixture_sdf, lo, hi, dev, stats=stats)
+                ref_levels = f["level_counts"][ci].tolist()
+                # masks from |sdf| < threshold: a point within float rounding of a threshold may flip; none did here
+                assert stats["levels"] == ref_levels, (ci, stats["levels"], ref_levels)
+                if ci in set(f["surface_crops"].tolist()):
+                    zc = z.double()
+                    assert int((z < 0).sum()) == int(f[f"crop{ci}:neg"]), ci
+                    assert abs(float(zc.sum()) - float(f[f"crop{ci}:sum"])) <= 1e-6 * float(zc.abs().sum()), ci
+                    got = z[idx].cpu().numpy()
+                    np.testing.assert_allclose(got, f[f"crop{ci}:sample"], rtol=3e-7, atol=3e-7,
+                                               err_msg=f"crop {ci}")   # sqrt to 1 ulp (4 of 65536 entries)
+                ci += 1
