@@ -137,7 +137,12 @@ class WeightPrep:
 
     def run(self, dev) -> None:
         """Recompute every registered entry (start of a model forward)."""
-        if self.norm_items and self._stale() and not torch.cuda.is_current_stream_capturing():
+        if self.norm_items and self._stale():
+            if torch.cuda.is_current_stream_capturing():
+                # a captured graph would keep reading the device tables' freed g / v storage on every replay;
+                # GraphTrainer always runs an eager step (which resets here) before it captures
+                raise RuntimeError("WeightPrep: parameters moved since registration and a stream capture is active; "
+                                   "run one eager forward before capturing")
             self.reset()
         self.fresh = False
         self.done.clear()
