@@ -60,6 +60,14 @@ int mms_hashgrid_dpos_grouped(const float* pos, int64_t Mg, int group, int64_t g
                               const float* table, int L, int log2T, int F, int interp, const float* scales,
                               float radius, int active_levels, const float* dout, int64_t ldd, float* dpos,
                               int64_t lddx, void* stream);
+/* The SDF field's MLP input panel in one launch: rows [x(3) | PE(6 pe_freqs) | hash grid(2L)] of ldx floats, for the M
+ * centre positions cpos [M, ldp] and (ntaps = 4) their tap points centre + k_t delta, rows t * M + i (t = 0 centre).
+ * Replaces SDFField.forward's input stage (surface_field.py:99-116: NeRFEncoding encodings.py:161-182 + FeatureGrid
+ * feature_structures.py:78-83 + the 4-tap points of surface_model.py:137-153); the same values as mms_geo_input_fwd
+ * followed by mms_hashgrid_fwd_grouped. */
+int mms_sdf_panel_fwd(const float* cpos, int64_t ldp, int64_t M, int ntaps, float delta, int pe_freqs,
+                      const float* table, int L, int log2T, int F, int interp, const float* scales, float radius,
+                      int active_levels, float* X, int64_t ldx, void* stream);
 
 /* ---- MLP GEMM engine (field_components/mlp.py:152-171): C = epilogue(op(A) op(B)^T).
  * trans_a = 0: A is [M, K] (lda); 1: A is stored [K, M].  trans_b = 0: B is [N, K]; 1: B is stored [K, N].

@@ -147,6 +147,79 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(const float* __restri
   }
 }
 
+// The SDF field's whole MLP input panel in one launch (SDFField.forward, surface_field.py:99-116; FeatureGridAndMLP,
+// feature_structures.py:153-169): per point the position x (centre, or centre + k_t delta for tap t,
+// surface_model.py:137-153), its positional encoding (encodings.py:161-182: sin(x_i 2^k), then sin(x_i 2^k + pi/2))
+// and its hash-grid features, in one row [x(3) | PE(6F) | grid(2L)].  Same values as mms_geo_input_fwd followed by
+// mms_hashgrid_fwd_grouped (the tap offsets are +-delta exactly, the PE the same sinf expressions), but each point's
+// row is written whole by one 16-lane group (x / PE columns lane, lane + 16, lane + 32; the level's 2 features) instead
+// of in two launches writing 156-B and 128-B parts of every 288-B row.  G = 5: points in (sample, tap) order as the
+// grouped gather; G = 1: the sampler's inference batches.
+__constant__ float kTapH[4][3] = {{1.f, -1.f, -1.f}, {-1.f, -1.f, 1.f}, {-1.f, 1.f, -1.f}, {1.f, 1.f, 1.f}};
+constexpr float kHalfPiH = 1.57079632679489661923f;  // fl32(pi / 2)
+
+template <int G>
+__global__ __launch_bounds__(256) void sdf_panel_fwd_kernel(const float* __restrict__ cpos, int64_t ldp, int64_t Mg,
+                                                            float delta, int F, const float2* __restrict__ table,
+                                                            GridParams p, float* __restrict__ X, int64_t ldx) {
+  const int64_t tid = xcd_block() * blockDim.x + threadIdx.x;
+  const int64_t q = tid >> 4;
+  const int l16 = (int)(tid & 15);
+  const int64_t g = G == 1 ? q : q / G;
+  const int t = G == 1 ? 0 : (int)(q - g * G);
+  const int64_t pt = G == 1 ? q : g + t * Mg;
+  if (g >= Mg) return;
+  float x[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    x[c] = cpos[g * ldp + c];
+    if (t > 0) x[c] = x[c] + kTapH[t - 1][c] * delta;
+  }
+  float* row = X + pt * ldx;
+  const int W = 3 + 6 * F;
+  for (int c = l16; c < W; c += 16) {
+    int coord = c, k = 0;
+    bool cosine = false;
+    if (c >= 3 && c < 3 + 3 * F) {
+      coord = (c - 3) / F;
+      k = (c - 3) - coord * F;
+    } else if (c >= 3 + 3 * F) {
+      coord = (c - 3 - 3 * F) / F;
+      k = (c - 3 - 3 * F) - coord * F;
+      cosine = true;
+    }
+    const float xc = coord == 0 ? x[0] : (coord == 1 ? x[1] : x[2]);
+    float v = xc;
+    if (c >= 3) {
+      const float sc = xc * (float)(1 << k);
+      v = cosine ? sinf(sc + kHalfPiH) : sinf(sc);
+    }
+    row[c] = v;
+  }
+  const int level = l16;
+  if (level >= p.levels) return;
+  float2 r = make_float2(0.f, 0.f);
+  if (level < p.active_levels) {
+    Corners c = make_corners(x[0], x[1], x[2], p.radius, p.inv_2r, p.scale[level], level, p.log2T, p.smooth != 0);
+    float2 f[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = table[c.idx[i]];
+    const float ox = c.ox, oy = c.oy, oz = c.oz;
+    const float nx = 1.0f - ox, ny = 1.0f - oy, nz = 1.0f - oz;
+    float2 f03, f12, f56, f47, f0312, f4756;
+    f03.x = f[0].x * ox + f[3].x * nx;  f03.y = f[0].y * ox + f[3].y * nx;
+    f12.x = f[1].x * ox + f[2].x * nx;  f12.y = f[1].y * ox + f[2].y * nx;
+    f56.x = f[5].x * ox + f[6].x * nx;  f56.y = f[5].y * ox + f[6].y * nx;
+    f47.x = f[4].x * ox + f[7].x * nx;  f47.y = f[4].y * ox + f[7].y * nx;
+    f0312.x = f03.x * oy + f12.x * ny;  f0312.y = f03.y * oy + f12.y * ny;
+    f4756.x = f47.x * oy + f56.x * ny;  f4756.y = f47.y * oy + f56.y * ny;
+    r.x = f0312.x * oz + f4756.x * nz;
+    r.y = f0312.y * oz + f4756.y * nz;
+  }
+  row[W + 2 * level] = r.x;
+  row[W + 2 * level + 1] = r.y;
+}
+
 // DPP lane moves (gfx9 encodings): quad_perm [1,0,3,2] / [2,3,0,1], row_ror:4 / :8 (rotation inside a 16-lane row),
 // row_bcast:15 / :31 (lane 15 / 31 of a row into the next row(s), masked by ROWS).  Rows not in ROWS read 0.
 template <int CTRL, int ROWS = 0xf>
@@ -488,6 +561,32 @@ MMS_EXPORT int mms_hashgrid_fwd(const float* pos, int64_t M, int64_t ldx, const 
                                 float* out, int64_t ldo, void* stream) {
   return mms_hashgrid_fwd_grouped(pos, M, 1, M, ldx, table, L, log2T, F, interp, scales, radius, active_levels, out,
                                   ldo, stream);
+}
+
+MMS_EXPORT int mms_sdf_panel_fwd(const float* cpos, int64_t ldp, int64_t M, int ntaps, float delta, int pe_freqs,
+                                 const float* table, int L, int log2T, int F, int interp, const float* scales,
+                                 float radius, int active_levels, float* X, int64_t ldx, void* stream) {
+  const char* fn = "mms_sdf_panel_fwd";
+  MMS_REQUIRE(F == 2, fn, "features_per_level must be 2");
+  MMS_REQUIRE(ntaps == 0 || ntaps == 4, fn, "ntaps must be 0 or 4");
+  MMS_REQUIRE(pe_freqs >= 1 && pe_freqs <= 16, fn, "1 to 16 encoding frequencies");
+  MMS_REQUIRE(M >= 0 && ldp >= 3 && ldx >= 3 + 6 * pe_freqs + 2 * L, fn, "bad shapes");
+  GridParams p;
+  int rc = fill_params(fn, p, L, log2T, interp, scales, radius, active_levels);
+  if (rc) return rc;
+  if (M == 0) return 0;
+  MMS_REQUIRE(cpos && table && X, fn, "null pointer");
+  const int group = ntaps + 1;
+  const unsigned blocks = mms::grid_for(M * group * 16, 256, INT32_MAX);
+  const float2* t2 = reinterpret_cast<const float2*>(table);
+  hipStream_t s = mms::as_stream(stream);
+  if (group == 5)
+    hipLaunchKernelGGL((sdf_panel_fwd_kernel<5>), dim3(blocks), dim3(256), 0, s, cpos, ldp, M, delta, pe_freqs, t2, p,
+                       X, ldx);
+  else
+    hipLaunchKernelGGL((sdf_panel_fwd_kernel<1>), dim3(blocks), dim3(256), 0, s, cpos, ldp, M, delta, pe_freqs, t2, p,
+                       X, ldx);
+  return mms::check_launch(fn);
 }
 
 MMS_EXPORT int mms_hashgrid_bwd_grouped(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx,

@@ -335,6 +335,21 @@ def grid_fwd(g: GridCfg, pos: torch.Tensor, ldx: int, M: int, table, active: int
               g.interp, g.scales_ptr, g.radius, active, out.data_ptr() + 4 * col, out.stride(0), _s())
 
 
+# the SDF input panel [x | PE | grid] in one launch (mms_sdf_panel_fwd); MMS_FUSED_PANEL=0: geo_input + grid launches
+FUSED_PANEL = os.environ.get("MMS_FUSED_PANEL", "1") != "0"
+
+
+def sdf_panel(pos: torch.Tensor, ldp: int, M: int, ntaps: int, delta: float, g: GridCfg, table, active: int,
+              X: torch.Tensor) -> None:
+    """Rows [x(3), PE(36), grid(32)] of the SDF MLP input for M positions (+ ntaps = 4 tap blocks of M rows)."""
+    if FUSED_PANEL:
+        _lib.call("mms_sdf_panel_fwd", pos.data_ptr(), ldp, M, ntaps, delta, 6, table.data_ptr(), g.L, g.log2T, g.F,
+                  g.interp, g.scales_ptr, g.radius, active, X.data_ptr(), X.stride(0), _s())
+        return
+    _lib.call("mms_geo_input_fwd", pos.data_ptr(), ldp, M, ntaps, delta, 6, X.data_ptr(), X.stride(0), _s())
+    grid_fwd(g, X, X.stride(0), (1 + ntaps) * M, table, active, X, 39, group=1 + ntaps)
+
+
 # hash-grid backward with both gradients: MMS_HASH_SPLIT=1 runs the table walk without position gradients + the
 # gather-style position-gradient kernel (scripts/hash_bench.py: the same 0.52 ms as the walk computing both, whose
 # time is the LDS merge, not its table re-gather), so the walk computes both by default
@@ -936,8 +951,7 @@ class SurfaceFunction(torch.autograd.Function):
         K0 = 3 + 36 + grid.out_dim
         X = _alloc(5 * M, K0, dev)
         d32 = float(torch.tensor(delta, dtype=torch.float32))
-        _lib.call("mms_geo_input_fwd", pos.data_ptr(), 3, M, 4, d32, 6, X.data_ptr(), X.stride(0), _s())
-        grid_fwd(grid, X, X.stride(0), 5 * M, table, active, X, 39, group=5)
+        sdf_panel(pos, 3, M, 4, d32, grid, table, active, X)
         prec = PRECISION["sdf"]
         ctx.chain = None
         if prec != 0:
@@ -1054,8 +1068,7 @@ def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> to
     dev = pos.device
     K0 = 3 + 36 + grid.out_dim
     X = _alloc(M, K0, dev)
-    _lib.call("mms_geo_input_fwd", pos.data_ptr(), pos.stride(0), M, 0, 0.0, 6, X.data_ptr(), X.stride(0), _s())
-    grid_fwd(grid, X, X.stride(0), M, table, active, X, 39)
+    sdf_panel(pos, pos.stride(0), M, 0, 0.0, grid, table, active, X)
     if PRECISION["sdf"] != 0:
         # fused chain, no hidden-layer stores, only the sdf column of the output layer (rows_full = 0), written as
         # the dense [M] vector the sampler kernel reads
@@ -1122,8 +1135,7 @@ class SDFFieldFunction(torch.autograd.Function):
         pos = pos.contiguous()
         K0 = 3 + 36 + grid.out_dim
         X = _alloc(M, K0, dev)
-        _lib.call("mms_geo_input_fwd", pos.data_ptr(), 3, M, 0, 0.0, 6, X.data_ptr(), X.stride(0), _s())
-        grid_fwd(grid, X, X.stride(0), M, table, active, X, 39)
+        sdf_panel(pos, 3, M, 0, 0.0, grid, table, active, X)
         run = mlp_runner(params, SDF_ACTS, PRECISION["sdf"])
         out = _run_forward(run, X, keep=True)
         ctx.run, ctx.X, ctx.grid, ctx.active, ctx.table = run, X, grid, active, table

@@ -705,7 +705,6 @@ class BaseModel(nn.Module):
         nm = len(mods)
         dev = rays[mods[0]]["origins"].device
         s_param = self.surface_model.volume_rendering.density_fn.variance_network.s
-        inv_s = 1.0 / self.surface_model.volume_rendering.density_fn.variance_network.get_inv_variance()  # once
         cat = (lambda ts: ts[0]) if nm == 1 else (lambda ts: torch.cat(ts, 0))
         o = cat([rays[m]["origins"] for m in mods])
         d = cat([rays[m]["directions"] for m in mods])
@@ -754,6 +753,9 @@ class BaseModel(nn.Module):
         # the ray's own modality's output reaches the loss, raw_pipeline.py:112-122), just its own
         own = self.own_heads_only and torch.is_grad_enabled()
         with torch.cuda.stream(bgs):
+            # the reported 1 / s (an output only, no loss term reads it: compute_metrics' inv_s) off the main stream
+            with torch.no_grad():
+                inv_s = 1.0 / self.surface_model.volume_rendering.density_fn.variance_network.get_inv_variance()
             nb = sp.bg_samples + 1
             blin = self._lin_dev(nb, 1.0, dev)
             bbins = torch.empty(nm * N, nb, device=dev)
@@ -775,6 +777,7 @@ class BaseModel(nn.Module):
         rows = N if cap is None else N + 1     # padded batches scatter into a dummy row N, cut off below
         if bgs is not cur:
             cur.wait_stream(bgs)
+            inv_s.record_stream(cur)
             for k in list(bg_out):
                 bg_out[k].record_stream(cur)    # made on the background stream, read (and freed) on this one
                 if torch.is_grad_enabled() and bg_out[k].requires_grad:

@@ -46,7 +46,7 @@ CONFIGS = {
 # poorly that held-out rgb PSNR falls while the training loss drops): every modality's held-out PSNR rises by
 # 1.3-7 dB over the first 50 steps.  Each seed's fixture also records an oracle-prime run (every gradient perturbed by
 # 2^-22 relative per step, perturber below): the reference algorithm's own sensitivity, the gate's null scatter.
-CONFIGS["raw5v"] = dict(CONFIGS["raw5"], n_views=50, checkpoints=(10, 20, 30, 40), prime=2.0 ** -22)
+CONFIGS["raw5v"] = dict(CONFIGS["raw5"], n_views=50, checkpoints=(10, 20, 30, 40), prime=2.0 ** -22, prime_seeds=16)
 # BASELINE configs[4] shape: grid_raw_grid_bg_unbalanced (rgb + polarization on 10 of its 45 views, the hash-grid
 # background, 3-layer background heads, SO3xR3 pose refinement)
 CONFIGS["bg5"] = dict(CONFIGS["raw5v"], method="grid_raw_grid_bg_unbalanced", modalities=("rgb", "polarization"),
@@ -222,7 +222,7 @@ def main(name: str = "rgb", seed: int = 0, perturb: float = 0.0, out_path: str =
         if k % 25 == 0:
             print(f"step {k}: loss {float(out[f's{k}:loss']):.6f} ({time.time() - t0:.1f}s)", flush=True)
     evaluate("eval")
-    if cfg.get("prime") and perturb == 0:
+    if cfg.get("prime") and perturb == 0 and seed < cfg.get("prime_seeds", 1 << 30):
         # the oracle-prime companion run of the same seed
         prime = main(name, seed, float(cfg["prime"]), checkpoints=checkpoints, save=False)
         out.update({"prime:" + k: v for k, v in prime.items() if "psnr" in k})

@@ -359,3 +359,31 @@ def test_small_linear(dev, C, K, act):
     for got, want, name in ((dX, rdx, "dX"), (dW, rdw, "dW"), (db, rdb, "db")):
         e = ((got.double().cpu() - want).abs().max() / want.abs().max()).item()
         assert e < 1e-5, f"{name}: rel err {e:.2e}"
+
+
+@pytest.mark.parametrize("ntaps,M", [(4, 5000), (0, 7001), (4, 1)])
+def test_sdf_panel_fused_equals_two_launches(dev, ntaps, M):
+    """mms_sdf_panel_fwd (x, PE and hash-grid features of the centre / tap points in one launch) writes exactly the
+    panel mms_geo_input_fwd + mms_hashgrid_fwd_grouped write (bit for bit), at partial coarse-to-fine levels too."""
+    from multimodalstudio_amd import functions as fx
+    from multimodalstudio_amd.functions import _alloc
+    g = torch.Generator().manual_seed(3 + ntaps)
+    pos = ((torch.rand(M, 3, generator=g) * 2 - 1) * 1.2).to(dev)
+    L, log2T = 16, 14
+    cfg = fx.GridCfg([float(int(16 * (1.3195079 ** l))) for l in range(L)], log2T, 1.0)
+    table = ((torch.rand(L << log2T, 2, generator=g) * 2 - 1) * 1e-2).to(dev)
+    delta = float(torch.tensor(2.0 / 1024 / 3 ** 0.5, dtype=torch.float32))
+    rows = (1 + ntaps) * M
+    for active in (16, 11):
+        outs = []
+        for fused in (True, False):
+            old, fx.FUSED_PANEL = fx.FUSED_PANEL, fused
+            try:
+                X = _alloc(rows, 71, dev)
+                X.fill_(float("nan"))
+                fx.sdf_panel(pos, 3, M, ntaps, delta, cfg, table, active, X)
+                outs.append(X[:, :71].clone())
+            finally:
+                fx.FUSED_PANEL = old
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), (ntaps, M, active)

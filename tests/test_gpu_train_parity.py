@@ -182,15 +182,18 @@ NULL_SE_MAX = PSNR_TOL / 3.3
 
 
 def null_scatter(gold: str):
-    """{tag: {mod: (mean, sd, n)}} of the fixtures' oracle' - oracle held-out PSNR differences (the 'prime:' keys)."""
+    """{tag: {mod: (mean, sd, n)}} of the fixtures' oracle' - oracle held-out PSNR differences (the 'prime:' keys; the
+    first seeds carry one), with n = the number of seeded fixtures the gate averages over: the null standard error of
+    that mean is sd / sqrt(n)."""
     per = {}
-    for path in _fixtures(gold):
+    fixtures = _fixtures(gold)
+    for path in fixtures:
         f = np.load(path)
         for k in f.files:
             if k.startswith("prime:") and k.endswith(":psnr"):
                 _, tag, m, _ = k.split(":")
                 per.setdefault(tag, {}).setdefault(m, []).append(float(f[k]) - float(f[f"{tag}:{m}:psnr"]))
-    return {tag: {m: (float(np.mean(v)), float(np.std(v, ddof=1)), len(v)) for m, v in d.items()}
+    return {tag: {m: (float(np.mean(v)), float(np.std(v, ddof=1)), len(fixtures)) for m, v in d.items()}
             for tag, d in per.items()}
 
 
