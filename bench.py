@@ -121,6 +121,22 @@ def hash_fwd_work(a):
     return role, float(M) * HASH_FWD_B
 
 
+def sdf_panel_work(a):
+    """(role, bytes) of one mms_sdf_panel_fwd launch (include/mms_hip.h argument order): the SURVEY §8(d) bytes of its
+    hash-grid lookups plus the x / PE columns it writes (3 + 6 pe_freqs floats per row)."""
+    M, ntaps, F = int(a[2]), int(a[3]), int(a[5])
+    rows = M * (ntaps + 1)
+    role = "sdf_taps" if ntaps == 4 else "sampler"
+    return role, float(rows) * (HASH_FWD_B + 4 * (3 + 6 * F))
+
+
+def rad_panel_work(a):
+    """(role, bytes) of one mms_rad_panel_fwd launch: the hash-grid lookups' SURVEY §8(d) bytes plus the x / SH / n.v
+    columns written and the geo feature read and written (4 B each way per column)."""
+    M, G = int(a[6]), int(a[8])
+    return "radiance", float(M) * (HASH_FWD_B + 4 * 29 + 8 * G)
+
+
 def work_fns():
     return {
         "mms_gemm": gemm_work,
@@ -128,6 +144,8 @@ def work_fns():
         "mms_gemm_tn_wide": gemm_grouped_work,
         "mms_mlp_chain": chain_work,
         "mms_hashgrid_fwd_grouped": hash_fwd_work,
+        "mms_sdf_panel_fwd": sdf_panel_work,
+        "mms_rad_panel_fwd": rad_panel_work,
         "mms_hashgrid_bwd_grouped": lambda a: ("sdf_taps" if a[2] == 5 else "radiance_or_bg",
                                                (float(a[1]) * a[2] * HASH_BWD_B, float(a[1]) * a[2] * HASH_BWD_ATOMIC_B)),
     }
@@ -409,6 +427,7 @@ def main():
         keys = ["kernel", "achieved", "peak", "unit", "frac", "avg_ms", "traffic", "atomic_ceiling"]
         hash_roof = {d: {k: by_name[n][k] for k in keys if k in by_name[n]}
                      for d, n in [("fwd", "mms_hashgrid_fwd_grouped:sdf_taps"), ("fwd_radiance", "mms_hashgrid_fwd_grouped:radiance"),
+                                  ("fwd", "mms_sdf_panel_fwd:sdf_taps"), ("fwd_radiance", "mms_rad_panel_fwd:radiance"),
                                   ("bwd", "mms_hashgrid_bwd_grouped:sdf_taps"),
                                   ("bwd_radiance", "mms_hashgrid_bwd_grouped:radiance_or_bg")] if n in by_name}
 

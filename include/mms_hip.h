@@ -69,6 +69,14 @@ int mms_sdf_panel_fwd(const float* cpos, int64_t ldp, int64_t M, int ntaps, floa
                       const float* table, int L, int log2T, int F, int interp, const float* scales, float radius,
                       int active_levels, float* X, int64_t ldx, void* stream);
 
+/* The radiance field's MLP input panel in one launch: rows [x(3) | SH(25) of dirs[i / S] | geo [M, G] (ldg) | n.v of
+ * normals [M, 3] and -dirs | hash grid(2L)] of ldx floats.  Replaces RadianceModel.forward's input stage
+ * (radiance_model.py:94-151: SHEncoding encodings.py:368-392, n.v, RadianceField radiance_field.py:72-77 +
+ * FeatureGrid feature_structures.py:78-83); the same values as mms_rad_input_fwd followed by mms_hashgrid_fwd. */
+int mms_rad_panel_fwd(const float* pos, int64_t ldp, const float* dirs, const float* normals, const float* geo,
+                      int64_t ldg, int64_t M, int S, int G, const float* table, int L, int log2T, int F, int interp,
+                      const float* scales, float radius, int active_levels, float* X, int64_t ldx, void* stream);
+
 /* ---- MLP GEMM engine (field_components/mlp.py:152-171): C = epilogue(op(A) op(B)^T).
  * trans_a = 0: A is [M, K] (lda); 1: A is stored [K, M].  trans_b = 0: B is [N, K]; 1: B is stored [K, N].
  * prec 0 = exact fp32 MFMA, 1 = bf16 MFMA (fp32 accumulate), 2 = split bf16x3 (near-fp32 operands).

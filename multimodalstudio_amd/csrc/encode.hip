@@ -11,6 +11,7 @@
 //   SH degree 4            utils/math.py:21-83 (SURVEY §8(c) patch 2)
 //   SceneContraction(inf)  field_components/spatial_distortions.py:90-97
 #include "common.h"
+#include "sh.h"
 
 // PE arguments must be the rounded products/sums the reference computes; keep the compiler from
 // fusing them.
@@ -233,36 +234,7 @@ __global__ void taps_combine_bwd_kernel(const float* __restrict__ grads, const f
   }
 }
 
-// ---------------------------------------------------------------- spherical harmonics (degree 4, 25)
-__device__ __forceinline__ void sh25(float x, float y, float z, float* o) {
-  const float xx = x * x, yy = y * y, zz = z * z;
-  o[0] = 0.28209479177387814f;
-  o[1] = 0.4886025119029199f * y;
-  o[2] = 0.4886025119029199f * z;
-  o[3] = 0.4886025119029199f * x;
-  o[4] = 1.0925484305920792f * x * y;
-  o[5] = 1.0925484305920792f * y * z;
-  o[6] = 0.9461746957575601f * zz - 0.31539156525251999f;
-  o[7] = 1.0925484305920792f * x * z;
-  o[8] = 0.5462742152960396f * (xx - yy);
-  o[9] = 0.5900435899266435f * y * (3 * xx - yy);
-  o[10] = 2.890611442640554f * x * y * z;
-  o[11] = 0.4570457994644658f * y * (5 * zz - 1);
-  o[12] = 0.3731763325901154f * z * (5 * zz - 3);
-  o[13] = 0.4570457994644658f * x * (5 * zz - 1);
-  o[14] = 1.445305721320277f * z * (xx - yy);
-  o[15] = 0.5900435899266435f * x * (xx - 3 * yy);
-  o[16] = 2.5033429417967046f * x * y * (xx - yy);
-  o[17] = 1.7701307697799304f * y * z * (3 * xx - yy);
-  o[18] = 0.9461746957575601f * x * y * (7 * zz - 1);
-  o[19] = 0.6690465435572892f * y * (7 * zz - 3);
-  o[20] = 0.10578554691520431f * (35 * zz * zz - 30 * zz + 3);
-  o[21] = 0.6690465435572892f * x * z * (7 * zz - 3);
-  o[22] = 0.47308734787878004f * (xx - yy) * (7 * zz - 1);
-  o[23] = 1.7701307697799304f * x * z * (xx - 3 * yy);
-  o[24] = 0.4425326924449826f * (xx * (xx - 3 * yy) - yy * (3 * xx - yy));
-}
-
+// ---------------------------------------------------------------- spherical harmonics (degree 4, 25): sh25 in sh.h
 // d/d(x,y,z) of sum_k dsh[k] * sh_k
 __device__ __forceinline__ void sh25_bwd(float x, float y, float z, const float* d, float* g) {
   const float xx = x * x, yy = y * y, zz = z * z;
@@ -321,12 +293,7 @@ __global__ void rad_input_fwd_kernel(const float* __restrict__ pos, int64_t ldp,
     sh25(d[0], d[1], d[2], sh);
 #pragma unroll
     for (int k = 0; k < 25; ++k) row[3 + k] = sh[k];
-    const float* n = normals + i * 3;
-    // torch.sum(normals * -directions, dim=-1): left-to-right sum of the three products
-    float ndv = n[0] * -d[0];
-    ndv = ndv + n[1] * -d[1];
-    ndv = ndv + n[2] * -d[2];
-    row[28 + G] = ndv;
+    row[28 + G] = ndv3(normals + i * 3, d);
   }
 }
 

@@ -31,6 +31,14 @@
 #ifndef MMS_GEMM_ABLATE
 #define MMS_GEMM_ABLATE 0
 #endif
+// Diagnostic ablation builds of the wide weight-gradient kernel (scripts/wide_ablate.py; the product library is built
+// with 0): bit 0 drops the output atomics, bit 1 the MFMAs, bit 2 the global loads, bit 3 the LDS image stores.
+#ifndef MMS_WIDE_ABLATE
+#define MMS_WIDE_ABLATE 0
+#endif
+#ifndef MMS_WIDE_PIPE
+#define MMS_WIDE_PIPE 1   // the wide kernel's two-register-set pipeline (scripts/wide_ablate.py variants pipe*)
+#endif
 #ifndef MMS_GEMM_XCDSPLIT
 #define MMS_GEMM_XCDSPLIT 1
 #endif
@@ -499,6 +507,30 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
   const int vb = (int)(t.N - cb < 0 ? 0 : (t.N - cb > 4 ? 4 : t.N - cb));
   const bool do_cs = t.colsum != nullptr && n0 == 0;
   float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+#if MMS_WIDE_PIPE
+  // two register sets: stage s + 2's loads are issued before stage s's MFMAs, and stage s + 1's image stores sit in
+  // the same basic block as those MFMAs (no branch between them), so the scheduler can interleave the conversions and
+  // LDS writes with the MFMAs and one whole stage of MFMA time covers each load's latency
+  float4 rset[2][2][NLD];
+  int nset[2] = {0, 0};
+  auto load2 = [&](int s, auto setc) {
+    constexpr int Q = decltype(setc)::value;
+    const int64_t r0 = kbeg + (int64_t)s * kWK;
+    nset[Q] = (int)(kend - r0 < kWK ? kend - r0 : kWK);   // <= 0 past the slice: the store writes zeros
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int64_t r = r0 + w + 8 * i;
+      const int64_t rc = r < kend ? r : kend - 1;
+      if constexpr ((MMS_WIDE_ABLATE & 4) != 0) {
+        rset[Q][0][i] = make_float4((float)rc, 1.f, 2.f, 3.f);
+        rset[Q][1][i] = make_float4(1.f, (float)rc, 3.f, 4.f);
+      } else {
+        rset[Q][0][i] = *reinterpret_cast<const float4*>(t.A + rc * t.lda + ca_c);
+        rset[Q][1][i] = *reinterpret_cast<const float4*>(t.B + rc * t.ldb + cb_c);
+      }
+    }
+  };
+#endif
   float4 ra[NLD], rb[NLD];
   int nrows = 0;
   auto load = [&](int s) {
@@ -508,8 +540,13 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
     for (int i = 0; i < NLD; ++i) {
       const int64_t r = r0 + w + 8 * i;
       const int64_t rc = r < kend ? r : kend - 1;
-      ra[i] = *reinterpret_cast<const float4*>(t.A + rc * t.lda + ca_c);
-      rb[i] = *reinterpret_cast<const float4*>(t.B + rc * t.ldb + cb_c);
+      if constexpr ((MMS_WIDE_ABLATE & 4) != 0) {
+        ra[i] = make_float4((float)rc, 1.f, 2.f, 3.f);
+        rb[i] = make_float4(1.f, (float)rc, 3.f, 4.f);
+      } else {
+        ra[i] = *reinterpret_cast<const float4*>(t.A + rc * t.lda + ca_c);
+        rb[i] = *reinterpret_cast<const float4*>(t.B + rc * t.ldb + cb_c);
+      }
     }
   };
   auto mask4 = [](float4 v, int valid, bool row_ok) {
@@ -520,12 +557,13 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
     v.w = valid > 3 ? v.w : 0.f;
     return v;
   };
-  auto store = [&](int buf) {
+  auto store_from = [&](int buf, const float4* xa, const float4* xb, int nr) {
+    if constexpr ((MMS_WIDE_ABLATE & 8) != 0) return;
     __bf16* base = &lds[buf][0];
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
-      const bool ok = w + 8 * i < nrows;
-      const float4 a = mask4(ra[i], va, ok), b = mask4(rb[i], vb, ok);
+      const bool ok = w + 8 * i < nr;
+      const float4 a = mask4(xa[i], va, ok), b = mask4(xb[i], vb, ok);
       if (do_cs) { cs.x += a.x; cs.y += a.y; cs.z += a.z; cs.w += a.w; }
       const int off = (w + 8 * i) * kWLD + 4 * lane;
       const bf16x4 ah = cvt4(a), bh = cvt4(b);
@@ -537,6 +575,7 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
       }
     }
   };
+  auto store = [&](int buf) { store_from(buf, ra, rb, nrows); };
   // wave-tile activity (wave-uniform): rows 64 wm + 32 i, columns 128 wn + 32 j of the block tile
   bool act_i[2], act_j[4];
 #pragma unroll
@@ -548,7 +587,8 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx16{};
-  auto compute = [&](int buf) {
+  auto compute = [&](int buf, auto allc) {
+    constexpr bool ALL = decltype(allc)::value;   // every wave-tile active: no per-tile branches around the MFMAs
     const __bf16* Ai = &lds[buf][0];
     const __bf16* Bi = &lds[buf][NIMG * IMG];
 #pragma unroll
@@ -566,10 +606,14 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        if (!act_i[i]) continue;
+        if (!ALL && !act_i[i]) continue;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if (!act_j[j]) continue;
+          if (!ALL && !act_j[j]) continue;
+          if constexpr ((MMS_WIDE_ABLATE & 2) != 0) {
+            acc[i][j][0] += (float)ah[i][0] + (float)bh[j][0];   // keeps the fragment reads live
+            continue;
+          }
           if constexpr (PREC == P_BF16X3) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
@@ -580,6 +624,36 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
     }
   };
   const int S = (int)((kend - kbeg + kWK - 1) / kWK);
+#if MMS_WIDE_PIPE
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  if (S > 0) {
+    load2(0, I0{});
+    store_from(0, rset[0][0], rset[0][1], nset[0]);
+    load2(1, I1{});
+  }
+  __syncthreads();
+  // one branch per wave for the whole loop: a wave whose tiles are all active runs the branch-free body (its MFMAs,
+  // conversions and LDS stores one basic block the scheduler interleaves)
+  auto loop = [&](auto allc) {
+    for (int s = 0; s < S; s += 2) {
+      // even stage s: set 1 holds stage s + 1; set 0 takes stage s + 2
+      load2(s + 2, I0{});
+      compute(0, allc);
+      store_from(1, rset[1][0], rset[1][1], nset[1]);
+      __syncthreads();
+      if (s + 1 >= S) break;
+      // odd stage s + 1: set 0 holds stage s + 2; set 1 takes stage s + 3
+      load2(s + 3, I1{});
+      compute(1, allc);
+      store_from(0, rset[0][0], rset[0][1], nset[0]);
+      __syncthreads();
+    }
+  };
+  const bool all_act = act_i[0] && act_i[1] && act_j[0] && act_j[1] && act_j[2] && act_j[3];
+  if (all_act) loop(std::true_type{});
+  else loop(std::false_type{});
+#else
   if (S > 0) {
     load(0);
     store(0);
@@ -587,13 +661,14 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
   }
   __syncthreads();
   for (int s = 0; s < S; ++s) {
-    compute(s & 1);
+    compute(s & 1, std::false_type{});
     if (s + 1 < S) {
       store((s + 1) & 1);
       if (s + 2 < S) load(s + 2);
     }
     __syncthreads();
   }
+#endif
   if (do_cs) {
     *reinterpret_cast<float4*>(&scs[w][4 * lane]) = cs;
     __syncthreads();
@@ -617,6 +692,7 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int tr = tr0 + (e & 3) + 8 * (e >> 2);
+        if ((MMS_WIDE_ABLATE & 1) != 0 && acc[i][j][e] != 1234.5f) continue;
         if (part != nullptr) {
           part[tr * kWT + tc] = acc[i][j][e];    // 128-B row segments per instruction: plain, coalesced stores
         } else if (m0 + tr < t.M && n0 + tc < t.N) {

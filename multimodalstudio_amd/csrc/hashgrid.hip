@@ -13,6 +13,7 @@
 // MLP input panel).  One thread per (point, level); 16 consecutive lanes cover one point's levels
 // so each wave writes 4 contiguous 128-byte output rows.
 #include "common.h"
+#include "sh.h"
 
 // Bit-exact corner selection needs the rounded product x_hat * s before floor/frac (a fused
 // multiply-subtract would change the fractional weights), so contraction is off in this file; the
@@ -218,6 +219,59 @@ __global__ __launch_bounds__(256) void sdf_panel_fwd_kernel(const float* __restr
   }
   row[W + 2 * level] = r.x;
   row[W + 2 * level + 1] = r.y;
+}
+
+// The radiance field's MLP input panel in one launch (RadianceField.forward, radiance_field.py:72-77, with
+// FeatureGridAndMLP, feature_structures.py:153-169): rows [x(3) | SH(25) of the ray direction | geo feature(G) | n.v |
+// hash grid(2L)] -- the values mms_rad_input_fwd followed by mms_hashgrid_fwd_grouped write (bit for bit), each point's
+// row written by one 16-lane group: x and SH columns by lane, geo columns lane + 16 j, n.v by lane 0, level lane's two
+// grid features.
+__global__ __launch_bounds__(256) void rad_panel_fwd_kernel(const float* __restrict__ pos, int64_t ldp,
+                                                            const float* __restrict__ dirs,
+                                                            const float* __restrict__ normals,
+                                                            const float* __restrict__ geo, int64_t ldg, int64_t M,
+                                                            int S, int G, const float2* __restrict__ table,
+                                                            GridParams p, float* __restrict__ X, int64_t ldx) {
+  const int64_t tid = xcd_block() * blockDim.x + threadIdx.x;
+  const int64_t i = tid >> 4;
+  const int l16 = (int)(tid & 15);
+  if (i >= M) return;
+  float* row = X + i * ldx;
+  const float* d = dirs + (i / S) * 3;
+  const float x0 = pos[i * ldp], x1 = pos[i * ldp + 1], x2 = pos[i * ldp + 2];
+  if (l16 < 3) row[l16] = l16 == 0 ? x0 : (l16 == 1 ? x1 : x2);
+  {
+    float sh[25];
+    sh25(d[0], d[1], d[2], sh);
+#pragma unroll
+    for (int k = 0; k < 25; ++k)
+      if ((k & 15) == l16) row[3 + k] = sh[k];
+  }
+  const float* gr = geo + i * ldg;
+  for (int k = l16; k < G; k += 16) row[28 + k] = gr[k];
+  if (l16 == 0) row[28 + G] = ndv3(normals + i * 3, d);
+  const int level = l16;
+  if (level >= p.levels) return;
+  float2 r = make_float2(0.f, 0.f);
+  if (level < p.active_levels) {
+    Corners c = make_corners(x0, x1, x2, p.radius, p.inv_2r, p.scale[level], level, p.log2T, p.smooth != 0);
+    float2 f[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = table[c.idx[k]];
+    const float ox = c.ox, oy = c.oy, oz = c.oz;
+    const float nx = 1.0f - ox, ny = 1.0f - oy, nz = 1.0f - oz;
+    float2 f03, f12, f56, f47, f0312, f4756;
+    f03.x = f[0].x * ox + f[3].x * nx;  f03.y = f[0].y * ox + f[3].y * nx;
+    f12.x = f[1].x * ox + f[2].x * nx;  f12.y = f[1].y * ox + f[2].y * nx;
+    f56.x = f[5].x * ox + f[6].x * nx;  f56.y = f[5].y * ox + f[6].y * nx;
+    f47.x = f[4].x * ox + f[7].x * nx;  f47.y = f[4].y * ox + f[7].y * nx;
+    f0312.x = f03.x * oy + f12.x * ny;  f0312.y = f03.y * oy + f12.y * ny;
+    f4756.x = f47.x * oy + f56.x * ny;  f4756.y = f47.y * oy + f56.y * ny;
+    r.x = f0312.x * oz + f4756.x * nz;
+    r.y = f0312.y * oz + f4756.y * nz;
+  }
+  row[29 + G + 2 * level] = r.x;
+  row[29 + G + 2 * level + 1] = r.y;
 }
 
 // DPP lane moves (gfx9 encodings): quad_perm [1,0,3,2] / [2,3,0,1], row_ror:4 / :8 (rotation inside a 16-lane row),
@@ -586,6 +640,24 @@ MMS_EXPORT int mms_sdf_panel_fwd(const float* cpos, int64_t ldp, int64_t M, int 
   else
     hipLaunchKernelGGL((sdf_panel_fwd_kernel<1>), dim3(blocks), dim3(256), 0, s, cpos, ldp, M, delta, pe_freqs, t2, p,
                        X, ldx);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_rad_panel_fwd(const float* pos, int64_t ldp, const float* dirs, const float* normals,
+                                 const float* geo, int64_t ldg, int64_t M, int S, int G, const float* table, int L,
+                                 int log2T, int F, int interp, const float* scales, float radius, int active_levels,
+                                 float* X, int64_t ldx, void* stream) {
+  const char* fn = "mms_rad_panel_fwd";
+  MMS_REQUIRE(F == 2, fn, "features_per_level must be 2");
+  MMS_REQUIRE(S >= 1 && G >= 0 && M >= 0 && ldp >= 3 && ldx >= 29 + G + 2 * L, fn, "bad shapes");
+  GridParams p;
+  int rc = fill_params(fn, p, L, log2T, interp, scales, radius, active_levels);
+  if (rc) return rc;
+  if (M == 0) return 0;
+  MMS_REQUIRE(pos && dirs && normals && table && X && (G == 0 || geo), fn, "null pointer");
+  hipLaunchKernelGGL(rad_panel_fwd_kernel, dim3(mms::grid_for(M * 16, 256, INT32_MAX)), dim3(256), 0,
+                     mms::as_stream(stream), pos, ldp, dirs, normals, geo, ldg, M, S, G,
+                     reinterpret_cast<const float2*>(table), p, X, ldx);
   return mms::check_launch(fn);
 }
 

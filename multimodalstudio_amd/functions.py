@@ -335,8 +335,10 @@ def grid_fwd(g: GridCfg, pos: torch.Tensor, ldx: int, M: int, table, active: int
               g.interp, g.scales_ptr, g.radius, active, out.data_ptr() + 4 * col, out.stride(0), _s())
 
 
-# the SDF input panel [x | PE | grid] in one launch (mms_sdf_panel_fwd); MMS_FUSED_PANEL=0: geo_input + grid launches
+# the SDF / radiance input panels in one launch each (mms_sdf_panel_fwd, mms_rad_panel_fwd); MMS_FUSED_PANEL=0: the
+# input-column kernel + the hash-grid gather as two launches
 FUSED_PANEL = os.environ.get("MMS_FUSED_PANEL", "1") != "0"
+FUSED_RAD_PANEL = FUSED_PANEL and os.environ.get("MMS_FUSED_RAD", "1") != "0"
 
 
 def sdf_panel(pos: torch.Tensor, ldp: int, M: int, ntaps: int, delta: float, g: GridCfg, table, active: int,
@@ -1228,9 +1230,15 @@ class RadianceFunction(torch.autograd.Function):
         dirs = dirs.contiguous()
         normals = normals.contiguous()
         geo = geo if geo.stride(1) == 1 else geo.contiguous()    # row-strided views are read in place
-        _lib.call("mms_rad_input_fwd", pos.data_ptr(), 3, dirs.data_ptr(), normals.data_ptr(), geo.data_ptr(),
-                  geo.stride(0), M, S, G, X.data_ptr(), X.stride(0), _s())
-        grid_fwd(grid, X, X.stride(0), M, table, active, X, 29 + G)
+        if FUSED_RAD_PANEL:
+            g = grid
+            _lib.call("mms_rad_panel_fwd", pos.data_ptr(), 3, dirs.data_ptr(), normals.data_ptr(), geo.data_ptr(),
+                      geo.stride(0), M, S, G, table.data_ptr(), g.L, g.log2T, g.F, g.interp, g.scales_ptr, g.radius,
+                      active, X.data_ptr(), X.stride(0), _s())
+        else:
+            _lib.call("mms_rad_input_fwd", pos.data_ptr(), 3, dirs.data_ptr(), normals.data_ptr(), geo.data_ptr(),
+                      geo.stride(0), M, S, G, X.data_ptr(), X.stride(0), _s())
+            grid_fwd(grid, X, X.stride(0), M, table, active, X, 29 + G)
         prec = PRECISION["radiance"]
         run = ChainRun(params, RAD_ACTS, prec) if prec != 0 else MLPRun(params, RAD_ACTS, prec)
         feat = run.forward(X, keep=True)

@@ -26,6 +26,7 @@ VARIANTS = {  # name: (translation unit, macro definitions)
     "stamps": ("mlp_chain", {"MMS_CHAIN_STAMPS": 1}),   # scripts/chain_stamps.py
     "ahead0": ("mlp_chain", {"MMS_CHAIN_AHEAD": 0}),
     "ss2k": ("loss_optim", {"MMS_SUMSQ_GRID": 2048, "MMS_SUMSQ_UNROLL": 4}),   # the round-3c launch shape
+    "wpipe0": ("gemm", {"MMS_WIDE_PIPE": 0}),   # the wide weight-gradient kernel's one-register-set loop (round 3)
 }
 
 

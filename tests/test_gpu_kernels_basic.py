@@ -387,3 +387,37 @@ def test_sdf_panel_fused_equals_two_launches(dev, ntaps, M):
                 fx.FUSED_PANEL = old
         torch.cuda.synchronize()
         assert torch.equal(outs[0], outs[1]), (ntaps, M, active)
+
+
+@pytest.mark.parametrize("R,S", [(70, 64), (3, 17)])
+def test_rad_panel_fused_equals_two_launches(dev, R, S):
+    """mms_rad_panel_fwd (x, SH, geo feature, n.v and hash-grid features of the radiance input in one launch) writes
+    exactly the panel mms_rad_input_fwd + mms_hashgrid_fwd_grouped write (bit for bit), geo read as a row-strided,
+    column-offset view of the SDF MLP output as in the step."""
+    from multimodalstudio_amd import _lib
+    from multimodalstudio_amd import functions as fx
+    from multimodalstudio_amd.functions import _alloc
+    g = torch.Generator().manual_seed(R * 100 + S)
+    M, G = R * S, 256
+    pos = ((torch.rand(M, 3, generator=g) * 2 - 1) * 0.9).to(dev)
+    dirs = torch.nn.functional.normalize(torch.randn(R, 3, generator=g), dim=-1).to(dev)
+    normals = torch.nn.functional.normalize(torch.randn(M, 3, generator=g), dim=-1).to(dev)
+    out = torch.randn(M, 260, generator=g).to(dev)
+    geo = out[:, 1:1 + G]
+    L, log2T = 16, 14
+    cfg = fx.GridCfg([float(int(16 * (1.3195079 ** l))) for l in range(L)], log2T, 1.0)
+    table = ((torch.rand(L << log2T, 2, generator=g) * 2 - 1) * 1e-2).to(dev)
+    K0 = 3 + 25 + G + 1 + 32
+    for active in (16, 9):
+        X1, X2 = _alloc(M, K0, dev), _alloc(M, K0, dev)
+        X1.fill_(float("nan"))
+        X2.fill_(float("nan"))
+        _lib.call("mms_rad_input_fwd", pos.data_ptr(), 3, dirs.data_ptr(), normals.data_ptr(), geo.data_ptr(),
+                  geo.stride(0), M, S, G, X1.data_ptr(), X1.stride(0), fx._s())
+        fx.grid_fwd(cfg, X1, X1.stride(0), M, table, active, X1, 29 + G)
+        _lib.call("mms_rad_panel_fwd", pos.data_ptr(), 3, dirs.data_ptr(), normals.data_ptr(), geo.data_ptr(),
+                  geo.stride(0), M, S, G, table.data_ptr(), cfg.L, cfg.log2T, cfg.F, cfg.interp, cfg.scales_ptr,
+                  cfg.radius, active, X2.data_ptr(), X2.stride(0), fx._s())
+        torch.cuda.synchronize()
+        diff = (X1[:, :K0] != X2[:, :K0]).any(0).nonzero().flatten().tolist()
+        assert not diff, (R, S, active, "columns", diff[:8], float((X1[:, :K0] - X2[:, :K0]).abs().max()))
