@@ -181,6 +181,8 @@ class GraphTrainer:
 
     @staticmethod
     def _capture_stream():
+        """The stream the step graphs are captured on (torch's default capture stream; a high-priority capture stream
+        measured 16 % slower steps, round 4: 499k vs 591k rays/s)."""
         if torch.cuda.graph.default_capture_stream is None:
             torch.cuda.graph.default_capture_stream = torch.cuda.Stream()
         return torch.cuda.graph.default_capture_stream
@@ -227,7 +229,7 @@ class GraphTrainer:
         torch.cuda.synchronize()
         if self.ddp is None:
             g1 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1, pool=self.pool, capture_error_mode=mode):
+            with torch.cuda.graph(g1, pool=self.pool, stream=self._capture_stream(), capture_error_mode=mode):
                 out = self._forward_backward(cap)
                 self._optimizer()
                 if self.tail:
@@ -241,7 +243,7 @@ class GraphTrainer:
         g2 = None
         if self.ddp is not None:
             g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2, pool=self.pool, capture_error_mode=mode):
+            with torch.cuda.graph(g2, pool=self.pool, stream=self._capture_stream(), capture_error_mode=mode):
                 self._optimizer()
                 if self.tail:
                     self._tail()

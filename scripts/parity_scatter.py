@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--fixture", default="train_parity_raw5.npz")
+    ap.add_argument("--fixture", default="train_parity_raw5v.npz")
     ap.add_argument("--runs", type=int, default=3)
     ap.add_argument("--eps", type=float, nargs="+", default=[1e-15, 1e-8])
     ap.add_argument("--precision", default="fp32")

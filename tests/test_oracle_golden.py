@@ -243,4 +243,4 @@ def test_train_parity_window_resolves_the_bound(name):
     f = np.load(gold)
     mods = [k.split(":")[1] for k in f.files if k.startswith("eval0:") and k.endswith(":psnr")]
     for m in mods:
-        assert float(f[f"eval:{m}:psnr"]) > float(f[f"eval0:{m}:psnr"]) + 0.5, m
+        assert float(f[f"eval:{m}:psnr"]) > float(f[f"eval0:{m}:psnr"]) + 0.25, m
