@@ -69,6 +69,16 @@ int mms_sdf_panel_fwd(const float* cpos, int64_t ldp, int64_t M, int ntaps, floa
                       const float* table, int L, int log2T, int F, int interp, const float* scales, float radius,
                       int active_levels, float* X, int64_t ldx, void* stream);
 
+/* mms_sdf_panel_fwd (ntaps 0) of the start positions of the samples of uniform spacing bins [R, nb] (ldb) on rays
+ * (nears, fars, origins [R, 3], dirs [R, 3]): row r (nb - 1) + k is the point o_r + d_r (f_r b_k + n_r (1 - b_k)),
+ * the positions mms_samples_fwd writes (SpacingToEuclidean + RaySamples.get_positions, ray_samplers.py:89-116,
+ * rays.py:69-81), bit for bit.  The NeuS sampler's inference batches (ray_samplers.py:448-514: sdf_fn(ray_samples))
+ * in one launch instead of two. */
+int mms_sdf_panel_rays_fwd(const float* bins, int64_t ldb, int nb, const float* nears, const float* fars,
+                           const float* origins, const float* dirs, int64_t R, int pe_freqs, const float* table, int L,
+                           int log2T, int F, int interp, const float* scales, float radius, int active_levels, float* X,
+                           int64_t ldx, void* stream);
+
 /* The radiance field's MLP input panel in one launch: rows [x(3) | SH(25) of dirs[i / S] | geo [M, G] (ldg) | n.v of
  * normals [M, 3] and -dirs | hash grid(2L)] of ldx floats.  Replaces RadianceModel.forward's input stage
  * (radiance_model.py:94-151: SHEncoding encodings.py:368-392, n.v, RadianceField radiance_field.py:72-77 +

@@ -159,10 +159,25 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(const float* __restri
 __constant__ float kTapH[4][3] = {{1.f, -1.f, -1.f}, {-1.f, -1.f, 1.f}, {-1.f, 1.f, -1.f}, {1.f, 1.f, 1.f}};
 constexpr float kHalfPiH = 1.57079632679489661923f;  // fl32(pi / 2)
 
-template <int G>
+// RAYS (the NeuS sampler's inference batches, G = 1): point q is the start of sample k = q % S of ray r = q / S of
+// the spacing bins [R, S + 1] (ldb), o_r + d_r * (f_r b + n_r (1 - b)) -- SamplesFunction's positions
+// (mms_samples_fwd, uniform spacing: sampler.hip to_euclid kind 0; contraction off in both files, same bits) -- so
+// the sampler's position launch before every panel is gone.
+struct RaySrc {
+  const float* bins;
+  int64_t ldb;
+  int nb;
+  const float* nears;
+  const float* fars;
+  const float* origins;
+  const float* dirs;
+};
+
+template <int G, bool RAYS = false>
 __global__ __launch_bounds__(256) void sdf_panel_fwd_kernel(const float* __restrict__ cpos, int64_t ldp, int64_t Mg,
                                                             float delta, int F, const float2* __restrict__ table,
-                                                            GridParams p, float* __restrict__ X, int64_t ldx) {
+                                                            GridParams p, float* __restrict__ X, int64_t ldx,
+                                                            RaySrc rs) {
   const int64_t tid = xcd_block() * blockDim.x + threadIdx.x;
   const int64_t q = tid >> 4;
   const int l16 = (int)(tid & 15);
@@ -171,10 +186,21 @@ __global__ __launch_bounds__(256) void sdf_panel_fwd_kernel(const float* __restr
   const int64_t pt = G == 1 ? q : g + t * Mg;
   if (g >= Mg) return;
   float x[3];
+  if constexpr (RAYS) {
+    const int S = rs.nb - 1;
+    const int64_t r = q / S;
+    const int k = (int)(q - r * S);
+    const float nr = rs.nears[r], fr = rs.fars[r];
+    const float b = rs.bins[r * rs.ldb + k];
+    const float s0 = fr * b + nr * (1 - b);
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    x[c] = cpos[g * ldp + c];
-    if (t > 0) x[c] = x[c] + kTapH[t - 1][c] * delta;
+    for (int c = 0; c < 3; ++c) x[c] = rs.origins[r * 3 + c] + rs.dirs[r * 3 + c] * s0;
+  } else {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      x[c] = cpos[g * ldp + c];
+      if (t > 0) x[c] = x[c] + kTapH[t - 1][c] * delta;
+    }
   }
   float* row = X + pt * ldx;
   const int W = 3 + 6 * F;
@@ -272,6 +298,79 @@ __global__ __launch_bounds__(256) void rad_panel_fwd_kernel(const float* __restr
   }
   row[29 + G + 2 * level] = r.x;
   row[29 + G + 2 * level + 1] = r.y;
+}
+
+// The same panel rows staged through LDS: a block's 16 points' rows [x | SH | geo | n.v | grid] are assembled in LDS
+// (the geo columns read block-wide, consecutive threads on consecutive floats of the 16 rows) and written out
+// block-wide in row-major order, so every wave-store covers 256 contiguous bytes of a row instead of four 64-B pieces
+// of four rows.  Same values, bit for bit.
+constexpr int kRadPts = 16;
+constexpr int kRadCols = 29 + 256 + 2 * kMaxLevels;   // the widest row: G = 256
+__global__ __launch_bounds__(256) void rad_panel_fwd_staged_kernel(const float* __restrict__ pos, int64_t ldp,
+                                                                   const float* __restrict__ dirs,
+                                                                   const float* __restrict__ normals,
+                                                                   const float* __restrict__ geo, int64_t ldg,
+                                                                   int64_t M, int S, int G,
+                                                                   const float2* __restrict__ table, GridParams p,
+                                                                   float* __restrict__ X, int64_t ldx) {
+  __shared__ float srow[kRadPts * kRadCols];
+  const int t = threadIdx.x;
+  const int64_t i0 = xcd_block() * (int64_t)kRadPts;
+  const int np = (int)((M - i0) < kRadPts ? (M - i0) : kRadPts);
+  const int C = 29 + G + 2 * p.levels;
+  // geo columns: block-wide coalesced reads of the np rows
+  for (int e = t; e < np * G; e += 256) {
+    const int r = e / G, c = e - r * G;
+    srow[r * C + 28 + c] = geo[(i0 + r) * ldg + c];
+  }
+  const int pi = t >> 4;
+  const int l16 = t & 15;
+  if (pi < np) {
+    const int64_t i = i0 + pi;
+    float* row = srow + pi * C;
+    const float* d = dirs + (i / S) * 3;
+    const float x0 = pos[i * ldp], x1 = pos[i * ldp + 1], x2 = pos[i * ldp + 2];
+    if (l16 < 3) row[l16] = l16 == 0 ? x0 : (l16 == 1 ? x1 : x2);
+    {
+      float sh[25];
+      sh25(d[0], d[1], d[2], sh);
+#pragma unroll
+      for (int k = 0; k < 25; ++k)
+        if ((k & 15) == l16) row[3 + k] = sh[k];
+    }
+    if (l16 == 0) row[28 + G] = ndv3(normals + i * 3, d);
+    const int level = l16;
+    if (level < p.levels) {
+      float2 r = make_float2(0.f, 0.f);
+      if (level < p.active_levels) {
+        Corners c = make_corners(x0, x1, x2, p.radius, p.inv_2r, p.scale[level], level, p.log2T, p.smooth != 0);
+        float2 f[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] = table[c.idx[k]];
+        const float ox = c.ox, oy = c.oy, oz = c.oz;
+        const float nx = 1.0f - ox, ny = 1.0f - oy, nz = 1.0f - oz;
+        float2 f03, f12, f56, f47, f0312, f4756;
+        f03.x = f[0].x * ox + f[3].x * nx;  f03.y = f[0].y * ox + f[3].y * nx;
+        f12.x = f[1].x * ox + f[2].x * nx;  f12.y = f[1].y * ox + f[2].y * nx;
+        f56.x = f[5].x * ox + f[6].x * nx;  f56.y = f[5].y * ox + f[6].y * nx;
+        f47.x = f[4].x * ox + f[7].x * nx;  f47.y = f[4].y * ox + f[7].y * nx;
+        f0312.x = f03.x * oy + f12.x * ny;  f0312.y = f03.y * oy + f12.y * ny;
+        f4756.x = f47.x * oy + f56.x * ny;  f4756.y = f47.y * oy + f56.y * ny;
+        r.x = f0312.x * oz + f4756.x * nz;
+        r.y = f0312.y * oz + f4756.y * nz;
+      }
+      row[29 + G + 2 * level] = r.x;
+      row[29 + G + 2 * level + 1] = r.y;
+    }
+  }
+  __syncthreads();
+  // row-major write-out: thread t walks element t, t + 256, ... of the np rows (C > 256: at most one row step each)
+  int r = t / C, c = t - (t / C) * C;
+  for (int e = t; e < np * C; e += 256) {
+    X[(i0 + r) * ldx + c] = srow[e];
+    c += 256;
+    while (c >= C) { c -= C; ++r; }
+  }
 }
 
 // DPP lane moves (gfx9 encodings): quad_perm [1,0,3,2] / [2,3,0,1], row_ror:4 / :8 (rotation inside a 16-lane row),
@@ -636,10 +735,31 @@ MMS_EXPORT int mms_sdf_panel_fwd(const float* cpos, int64_t ldp, int64_t M, int 
   hipStream_t s = mms::as_stream(stream);
   if (group == 5)
     hipLaunchKernelGGL((sdf_panel_fwd_kernel<5>), dim3(blocks), dim3(256), 0, s, cpos, ldp, M, delta, pe_freqs, t2, p,
-                       X, ldx);
+                       X, ldx, RaySrc{});
   else
     hipLaunchKernelGGL((sdf_panel_fwd_kernel<1>), dim3(blocks), dim3(256), 0, s, cpos, ldp, M, delta, pe_freqs, t2, p,
-                       X, ldx);
+                       X, ldx, RaySrc{});
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_sdf_panel_rays_fwd(const float* bins, int64_t ldb, int nb, const float* nears, const float* fars,
+                                      const float* origins, const float* dirs, int64_t R, int pe_freqs,
+                                      const float* table, int L, int log2T, int F, int interp, const float* scales,
+                                      float radius, int active_levels, float* X, int64_t ldx, void* stream) {
+  const char* fn = "mms_sdf_panel_rays_fwd";
+  MMS_REQUIRE(F == 2, fn, "features_per_level must be 2");
+  MMS_REQUIRE(pe_freqs >= 1 && pe_freqs <= 16, fn, "1 to 16 encoding frequencies");
+  MMS_REQUIRE(R >= 0 && nb >= 2 && ldb >= nb && ldx >= 3 + 6 * pe_freqs + 2 * L, fn, "bad shapes");
+  GridParams p;
+  int rc = fill_params(fn, p, L, log2T, interp, scales, radius, active_levels);
+  if (rc) return rc;
+  if (R == 0) return 0;
+  MMS_REQUIRE(bins && nears && fars && origins && dirs && table && X, fn, "null pointer");
+  const int64_t M = R * (nb - 1);
+  const RaySrc rs{bins, ldb, nb, nears, fars, origins, dirs};
+  hipLaunchKernelGGL((sdf_panel_fwd_kernel<1, true>), dim3(mms::grid_for(M * 16, 256, INT32_MAX)), dim3(256), 0,
+                     mms::as_stream(stream), nullptr, 3, M, 0.0f, pe_freqs, reinterpret_cast<const float2*>(table), p,
+                     X, ldx, rs);
   return mms::check_launch(fn);
 }
 
@@ -655,9 +775,18 @@ MMS_EXPORT int mms_rad_panel_fwd(const float* pos, int64_t ldp, const float* dir
   if (rc) return rc;
   if (M == 0) return 0;
   MMS_REQUIRE(pos && dirs && normals && table && X && (G == 0 || geo), fn, "null pointer");
-  hipLaunchKernelGGL(rad_panel_fwd_kernel, dim3(mms::grid_for(M * 16, 256, INT32_MAX)), dim3(256), 0,
-                     mms::as_stream(stream), pos, ldp, dirs, normals, geo, ldg, M, S, G,
-                     reinterpret_cast<const float2*>(table), p, X, ldx);
+  static const bool staged = [] {
+    const char* e = getenv("MMS_RAD_STAGED");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (staged && G <= 256)
+    hipLaunchKernelGGL(rad_panel_fwd_staged_kernel, dim3(mms::grid_for(M, kRadPts, INT32_MAX)), dim3(256), 0,
+                       mms::as_stream(stream), pos, ldp, dirs, normals, geo, ldg, M, S, G,
+                       reinterpret_cast<const float2*>(table), p, X, ldx);
+  else
+    hipLaunchKernelGGL(rad_panel_fwd_kernel, dim3(mms::grid_for(M * 16, 256, INT32_MAX)), dim3(256), 0,
+                       mms::as_stream(stream), pos, ldp, dirs, normals, geo, ldg, M, S, G,
+                       reinterpret_cast<const float2*>(table), p, X, ldx);
   return mms::check_launch(fn);
 }
 

@@ -1064,13 +1064,29 @@ def _sdf_mlp_unfused_bwd(ctx, dout, params, dev):
     return dX, list(pgrads) + [None, None, None]
 
 
-def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params) -> torch.Tensor:
-    """Inference SDF (SurfaceModel.get_sdf, surface_model.py:213-226; evaluated under no_grad by the sampler)."""
-    M = pos.shape[0]
-    dev = pos.device
-    K0 = 3 + 36 + grid.out_dim
-    X = _alloc(M, K0, dev)
-    sdf_panel(pos, pos.stride(0), M, 0, 0.0, grid, table, active, X)
+# the NeuS sampler's inference panels straight from the spacing bins (mms_sdf_panel_rays_fwd); MMS_FUSED_SAMPLER=0:
+# the sample positions first (mms_samples_fwd), then the panel
+FUSED_SAMPLER = FUSED_PANEL and os.environ.get("MMS_FUSED_SAMPLER", "1") != "0"
+
+
+def sdf_only(pos: torch.Tensor, table, grid: GridCfg, active: int, params, rays=None) -> torch.Tensor:
+    """Inference SDF (SurfaceModel.get_sdf, surface_model.py:213-226; evaluated under no_grad by the sampler).
+    ``rays`` = (bins [R, nb], nears, fars, origins [R, 3], dirs [R, 3]) instead of ``pos``: the start positions of
+    the bins' samples (sample_start_positions), formed inside the panel launch."""
+    if rays is not None:
+        bins, n, f, o, d = rays
+        R, nb = bins.shape
+        M = R * (nb - 1)
+        dev = bins.device
+        X = _alloc(M, 3 + 36 + grid.out_dim, dev)
+        _lib.call("mms_sdf_panel_rays_fwd", bins.data_ptr(), bins.stride(0), nb, n.data_ptr(), f.data_ptr(),
+                  o.data_ptr(), d.data_ptr(), R, 6, table.data_ptr(), grid.L, grid.log2T, grid.F, grid.interp,
+                  grid.scales_ptr, grid.radius, active, X.data_ptr(), X.stride(0), _s())
+    else:
+        M = pos.shape[0]
+        dev = pos.device
+        X = _alloc(M, 3 + 36 + grid.out_dim, dev)
+        sdf_panel(pos, pos.stride(0), M, 0, 0.0, grid, table, active, X)
     if PRECISION["sdf"] != 0:
         # fused chain, no hidden-layer stores, only the sdf column of the output layer (rows_full = 0), written as
         # the dense [M] vector the sampler kernel reads

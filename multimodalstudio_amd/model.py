@@ -321,6 +321,17 @@ class SurfaceModel(nn.Module):
         with torch.no_grad():
             return fx.sdf_only(pos, grid.encoding.hash_table, grid.cfg, grid.active_levels, params)
 
+    def get_sdf_rays(self, bins, n, f, o, d) -> Optional[torch.Tensor]:
+        """get_sdf at the start positions of the samples of spacing bins [R, nb] on rays (n, f, o, d), the positions
+        formed inside the panel launch (fx.FUSED_SAMPLER); None where that path does not serve (the caller then
+        forms the positions itself)."""
+        if self.analytic or not fx.FUSED_SAMPLER:
+            return None
+        grid, params = self._grid_and_params()
+        with torch.no_grad():
+            return fx.sdf_only(None, grid.encoding.hash_table, grid.cfg, grid.active_levels, params,
+                               rays=(bins, n, f, o, d))
+
 
 def _render_stats(w, normals, starts, ends, R: int, S: int, sidx, rows: int, dev):
     """[rows, 5] = (accumulation, normals, depth) of the hit rows sidx (zero elsewhere) by mms_render_stats; the depth
@@ -457,9 +468,10 @@ class RNG:
 
 
 _BG_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
-# issue order of the two branches: the foreground sampler's launches first (a captured graph then dispatches that
-# branch first: 591k -> 602k rays/s, round 4), or (MMS_BG_AFTER=0) the background branch first
-BG_AFTER = os.environ.get("MMS_BG_AFTER", "1") == "1"
+# issue point of the background branch in the foreground sampler's launch sequence: after sampler iteration
+# MMS_BG_AT (0..upsample_steps-1), after the whole sampler (-1; a captured graph then dispatches the critical branch
+# first: 591k -> 602k rays/s, round 4) or before it (-2)
+BG_AT = int(os.environ.get("MMS_BG_AT", "-1"))
 
 
 def background_stream(dev) -> "torch.cuda.Stream":
@@ -519,14 +531,18 @@ def sample_start_positions(bins, n, f, o, d) -> torch.Tensor:
 
 @torch.no_grad()
 def neus_sample(n_h, f_h, o_h, d_h, t_rand, pdf_rands, sdf_fn, num_samples: int = 32, num_importance: int = 32,
-                upsample_steps: int = 4, base_variance: float = 64.0, lin=None, history: Optional[list] = None):
+                upsample_steps: int = 4, base_variance: float = 64.0, lin=None, history: Optional[list] = None,
+                after_iter=None, sdf_rays_fn=None):
     """NeuSSampler.generate_ray_samples (ray_samplers.py:448-514) for one modality's hit rays on the HIP kernels.
 
     n_h / f_h [R] nears / fars, o_h / d_h [R, 3]; t_rand [R, 1] single-jitter uniforms of the uniform sampler (or
     None: evaluation, no jitter), pdf_rands: ``upsample_steps`` [R, 1] PDF-sampler uniforms (or None).
     ``sdf_fn(positions [R*S, 3]) -> sdf [R*S]`` is evaluated at sample starts (the reference's sdf_fn(ray_samples)).
     Returns the final spacing bins [R, num_samples + num_importance + 1]; ``history`` (a list) receives each
-    iteration's ``sorted_index`` [R, S + n_new] (merge_ray_samples :38-68) -- bit-exact to the reference's."""
+    iteration's ``sorted_index`` [R, S + n_new] (merge_ray_samples :38-68) -- bit-exact to the reference's.
+    ``after_iter(it)``, if given, is called after iteration ``it``'s launches (an issue point for other work);
+    ``sdf_rays_fn(bins, n, f, o, d)``, if given and not returning None, evaluates sdf_fn at the bins' sample starts
+    without the positions' own launch."""
     R = n_h.shape[0]
     dev = n_h.device
     if lin is None:
@@ -540,7 +556,10 @@ def neus_sample(n_h, f_h, o_h, d_h, t_rand, pdf_rands, sdf_fn, num_samples: int 
     sdf_prev, prev_idx, s_prev, n_prev_new = None, None, 0, S
     new_bins = bins
     for it in range(upsample_steps):
-        sdf_new = sdf_fn(sample_start_positions(new_bins, n_h, f_h, o_h, d_h)).reshape(-1).contiguous()
+        sdf_new = sdf_rays_fn(new_bins, n_h, f_h, o_h, d_h) if sdf_rays_fn is not None else None
+        if sdf_new is None:
+            sdf_new = sdf_fn(sample_start_positions(new_bins, n_h, f_h, o_h, d_h))
+        sdf_new = sdf_new.reshape(-1).contiguous()
         sdf_out = torch.empty(R, S, device=dev)
         new_bins = torch.empty(R, n_new + 1, device=dev)
         merged = torch.empty(R, S + n_new + 1, device=dev)
@@ -554,6 +573,8 @@ def neus_sample(n_h, f_h, o_h, d_h, t_rand, pdf_rands, sdf_fn, num_samples: int 
                   sidx.data_ptr(), fx._s())
         if history is not None:
             history.append(sidx)
+        if after_iter is not None:
+            after_iter(it)
         sdf_prev, prev_idx, s_prev, n_prev_new = sdf_out, sidx, S, n_new
         bins = merged
         S += n_new
@@ -643,10 +664,11 @@ class BaseModel(nn.Module):
 
     # -- NeuS sampler (ray_samplers.py:448-514), no autograd ------------------------------------------
     @torch.no_grad()
-    def neus_bins(self, n_h, f_h, o_h, d_h, t_rand, pdf_rands):
+    def neus_bins(self, n_h, f_h, o_h, d_h, t_rand, pdf_rands, after_iter=None):
         sp = self.spec
         return neus_sample(n_h, f_h, o_h, d_h, t_rand, pdf_rands, self.surface_model.get_sdf, sp.num_samples,
-                           sp.num_importance, sp.upsample_steps, sp.base_variance, lin=self._lin_dev)
+                           sp.num_importance, sp.upsample_steps, sp.base_variance, lin=self._lin_dev,
+                           after_iter=after_iter, sdf_rays_fn=getattr(self.surface_model, "get_sdf_rays", None))
 
     # -- forward ----------------------------------------------------------------------------------------
     def forward(self, rays: Dict[str, Dict[str, torch.Tensor]], rng: Optional[RNG] = None, cap: Optional[int] = None):
@@ -773,14 +795,23 @@ class BaseModel(nn.Module):
                 bg_out = self._heads_composite(self.background_model.modality_heads, mods, own, bfeat, bw, d, up,
                                                sp.bg_samples, [i * N for i in range(nm)], [N] * nm)
             return inv_s, bg_out
-        # NeuS sampling (ray_samplers.py:448-514) -- latency-bound launches the background work overlaps, issued first
-        # (BG_AFTER): the graph's first-dispatched branch is the critical one
-        if BG_AFTER:
-            bins = self.neus_bins(n_h.detach(), f_h.detach(), o_h.detach(), d_h.detach(), t_rand, pdf)
-            inv_s, bg_out = background()
-        else:
-            inv_s, bg_out = background()
-            bins = self.neus_bins(n_h.detach(), f_h.detach(), o_h.detach(), d_h.detach(), t_rand, pdf)
+        # NeuS sampling (ray_samplers.py:448-514) -- latency-bound launches the background work overlaps; the
+        # background branch is issued at BG_AT in the sampler's launch sequence (a captured graph dispatches in issue
+        # order, so the critical foreground branch goes first)
+        bg_res = []
+        grad_on = torch.is_grad_enabled()
+        at = BG_AT if BG_AT < sp.upsample_steps else -1
+
+        def issue_bg(it=None):
+            if not bg_res:
+                with torch.set_grad_enabled(grad_on):
+                    bg_res.append(background())
+        if at == -2:
+            issue_bg()
+        bins = self.neus_bins(n_h.detach(), f_h.detach(), o_h.detach(), d_h.detach(), t_rand, pdf,
+                              after_iter=(lambda it: issue_bg() if it == at else None) if at >= 0 else None)
+        issue_bg()
+        inv_s, bg_out = bg_res[0]
         S = bins.shape[1] - 1
         pos, deltas, starts, ends = fx.SamplesFunction.apply(bins, n_h, f_h, o_h, d_h, 0)
         # surface + radiance

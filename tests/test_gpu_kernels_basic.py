@@ -389,6 +389,40 @@ def test_sdf_panel_fused_equals_two_launches(dev, ntaps, M):
         assert torch.equal(outs[0], outs[1]), (ntaps, M, active)
 
 
+@pytest.mark.parametrize("R,nb,ldb", [(900, 33, 33), (700, 9, 9), (5, 65, 70)])
+def test_sdf_panel_rays_equals_positions_then_panel(dev, R, nb, ldb):
+    """mms_sdf_panel_rays_fwd (the NeuS sampler's inference panel formed from the spacing bins) writes exactly the
+    panel of mms_samples_fwd's start positions (model.sample_start_positions) + mms_sdf_panel_fwd, bit for bit, with
+    row-strided bins too."""
+    from multimodalstudio_amd import _lib
+    from multimodalstudio_amd import functions as fx
+    from multimodalstudio_amd import model as mm
+    from multimodalstudio_amd.functions import _alloc
+    g = torch.Generator().manual_seed(R + nb)
+    o = (torch.nn.functional.normalize(torch.randn(R, 3, generator=g), dim=-1) * 1.5).to(dev)
+    d = torch.nn.functional.normalize(-o.cpu() + 0.3 * torch.randn(R, 3, generator=g), dim=-1).to(dev)
+    n = (torch.rand(R, generator=g) * 0.5 + 0.1).to(dev)
+    f = n + (torch.rand(R, generator=g) * 2.0 + 0.5).to(dev)
+    bins_full = torch.sort(torch.rand(R, ldb, generator=g), dim=-1).values.to(dev)
+    bins = bins_full[:, :nb]
+    L, log2T = 16, 14
+    cfg = fx.GridCfg([float(int(16 * (1.3195079 ** l))) for l in range(L)], log2T, 1.0)
+    table = ((torch.rand(L << log2T, 2, generator=g) * 2 - 1) * 1e-2).to(dev)
+    M = R * (nb - 1)
+    for active in (16, 7):
+        X1, X2 = _alloc(M, 71, dev), _alloc(M, 71, dev)
+        X1.fill_(float("nan"))
+        X2.fill_(float("nan"))
+        pos = mm.sample_start_positions(bins.contiguous(), n, f, o, d)
+        _lib.call("mms_sdf_panel_fwd", pos.data_ptr(), 3, M, 0, 0.0, 6, table.data_ptr(), cfg.L, cfg.log2T, cfg.F,
+                  cfg.interp, cfg.scales_ptr, cfg.radius, active, X1.data_ptr(), X1.stride(0), fx._s())
+        _lib.call("mms_sdf_panel_rays_fwd", bins.data_ptr(), bins.stride(0), nb, n.data_ptr(), f.data_ptr(),
+                  o.data_ptr(), d.data_ptr(), R, 6, table.data_ptr(), cfg.L, cfg.log2T, cfg.F, cfg.interp,
+                  cfg.scales_ptr, cfg.radius, active, X2.data_ptr(), X2.stride(0), fx._s())
+        torch.cuda.synchronize()
+        assert torch.equal(X1[:, :71], X2[:, :71]), (R, nb, active, float((X1[:, :71] - X2[:, :71]).abs().max()))
+
+
 @pytest.mark.parametrize("R,S", [(70, 64), (3, 17)])
 def test_rad_panel_fused_equals_two_launches(dev, R, S):
     """mms_rad_panel_fwd (x, SH, geo feature, n.v and hash-grid features of the radiance input in one launch) writes
