@@ -390,6 +390,15 @@ int mms_adamw_scalars(double lr, double wd, double beta1, double beta2, double e
  * the host rewrites the 7 floats before each launch) */
 int mms_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* sumsq, float max_norm,
                   const float* hyper, void* stream);
+/* Several optimizer groups per launch (graph-replayed steps; each launch boundary costs ~4-5 us): the groups
+ * given by host arrays of device pointers (nseg / nbuf <= 8).  mms_zero_multi: x[k][0, n[k]) = 0 (the groups' gradients and their
+ * sum-of-squares accumulators, one launch); mms_sumsq_multi: acc[k] += sum(x[k]^2), as mms_sumsq per group;
+ * mms_adamw_dev_multi: mms_adamw_dev of every group (its sum of squares, max_norm and device scalars), bit for bit. */
+int mms_zero_multi(int nbuf, float* const* x, const int64_t* n, void* stream);
+int mms_sumsq_multi(int nseg, const float* const* x, const int64_t* n, float* const* acc, void* stream);
+int mms_adamw_dev_multi(int nseg, float* const* p, const float* const* g, float* const* m, float* const* v,
+                        const int64_t* n, const float* const* sumsq, const float* max_norm, const float* const* hyper,
+                        void* stream);
 
 /* ---- GPU-resident uniform pixel sampler (UniformPixelSampler.sample, cameras/pixel_samplers.py:71-89, over the
  * frames CacheDataloader caches, data/dataloaders.py:107-167): n draws of (frame, x, y) from Philox4x32-10

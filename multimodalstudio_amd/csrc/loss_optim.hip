@@ -149,14 +149,16 @@ __global__ void geo_loss_bwd_kernel(const float* __restrict__ grads, const float
 #ifndef MMS_SUMSQ_GRID
 #define MMS_SUMSQ_GRID 256   // blocks (grid-stride): one per CU
 #endif
-__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ acc) {
+// one block's share of sum(x^2) over x[0, n), blocks [0, nblk) of the segment; added into acc
+__device__ __forceinline__ void sumsq_seg(const float* __restrict__ x, int64_t n, float* __restrict__ acc, int64_t blk,
+                                          int64_t nblk) {
   constexpr int U = MMS_SUMSQ_UNROLL;
   const int64_t n4 = n / 4;
   const float4* x4 = reinterpret_cast<const float4*>(x);
   // U independent 16-B loads in flight per lane per iteration (one dependent load per iteration left the 138 MB
   // gradient read at 3.1 TB/s), then the remainder one at a time
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = nblk * blockDim.x;
+  int64_t i = blk * blockDim.x + threadIdx.x;
   float ps[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) ps[u] = 0.f;
@@ -174,10 +176,53 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
   float s = 0.f;
 #pragma unroll
   for (int u = 0; u < U; ++u) s += ps[u];
-  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    s += x[i] * x[i];
+  for (int64_t i = n4 * 4 + blk * blockDim.x + threadIdx.x; i < n; i += stride) s += x[i] * x[i];
   s = block_reduce_sum(s);
   if (threadIdx.x == 0) atomicAdd(acc, s);
+}
+
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ acc) {
+  sumsq_seg(x, n, acc, blockIdx.x, gridDim.x);
+}
+
+// Several optimizer groups in one launch (graph-replayed steps: each launch boundary costs ~4-5 us): segment k owns
+// blocks [b0[k], b0[k + 1]) of the grid -- the blocks its own launch would have had -- and its own operands.
+constexpr int kMaxSeg = 8;
+struct OptSegs {
+  int n;
+  int b0[kMaxSeg + 1];
+  float* p[kMaxSeg];
+  const float* g[kMaxSeg];
+  float* m[kMaxSeg];
+  float* v[kMaxSeg];
+  int64_t len[kMaxSeg];
+  float* acc[kMaxSeg];          // sumsq: accumulators; adamw: the groups' sums of squares (read)
+  float max_norm[kMaxSeg];
+  const float* hyper[kMaxSeg];
+};
+
+__device__ __forceinline__ int seg_of(const OptSegs& a, int b) {
+  int k = 0;
+  while (k + 1 < a.n && b >= a.b0[k + 1]) ++k;
+  return k;
+}
+
+__global__ __launch_bounds__(256) void sumsq_multi_kernel(OptSegs a) {
+  const int k = seg_of(a, blockIdx.x);
+  sumsq_seg(a.g[k], a.len[k], a.acc[k], blockIdx.x - a.b0[k], a.b0[k + 1] - a.b0[k]);
+}
+
+// zero fill of several buffers (the groups' gradients and sum-of-squares accumulators), 16 B per lane where aligned
+__global__ __launch_bounds__(256) void zero_multi_kernel(OptSegs a) {
+  const int k = seg_of(a, blockIdx.x);
+  float* x = a.p[k];
+  const int64_t n = a.len[k];
+  const int64_t stride = (int64_t)(a.b0[k + 1] - a.b0[k]) * blockDim.x;
+  const int64_t t0 = (int64_t)(blockIdx.x - a.b0[k]) * blockDim.x + threadIdx.x;
+  const bool al = ((uintptr_t)x & 15) == 0;
+  const int64_t n4 = al ? n / 4 : 0;
+  for (int64_t i = t0; i < n4; i += stride) reinterpret_cast<float4*>(x)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t i = n4 * 4 + t0; i < n; i += stride) x[i] = 0.f;
 }
 
 // AdamW with the clip coefficient coef = min(1, max_norm / (sqrt(sumsq) + 1e-6)) applied to g, in the operation
@@ -216,6 +261,37 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
                                                     float w1, float b2, float w2, float eps, float neg_step,
                                                     float bc2_sqrt) {
   adamw_apply(p, g, m, v, n, sumsq, max_norm, decay, w1, b2, w2, eps, neg_step, bc2_sqrt);
+}
+
+// adamw_dev_kernel of several groups in one launch (segment k: blocks [b0[k], b0[k + 1]), its own scalars)
+__global__ __launch_bounds__(256) void adamw_dev_multi_kernel(OptSegs a) {
+#pragma clang fp contract(off)
+  const int k = seg_of(a, blockIdx.x);
+  const float* h = a.hyper[k];
+  const float* __restrict__ g = a.g[k];
+  float* __restrict__ p = a.p[k];
+  float* __restrict__ m = a.m[k];
+  float* __restrict__ v = a.v[k];
+  const int64_t n = a.len[k];
+  const float decay = h[0], w1 = h[1], b2 = h[2], w2 = h[3], eps = h[4], neg_step = h[5], bc2_sqrt = h[6];
+  float coef = 1.0f;
+  if (a.acc[k] != nullptr && a.max_norm[k] > 0.f) {
+    const float total = sqrtf(a.acc[k][0]);
+    coef = fminf(a.max_norm[k] / (total + 1e-6f), 1.0f);
+  }
+  const int64_t stride = (int64_t)(a.b0[k + 1] - a.b0[k]) * blockDim.x;
+  for (int64_t i = (int64_t)(blockIdx.x - a.b0[k]) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float gi = g[i] * coef;
+    float pi = p[i] * decay;
+    float mi = m[i];
+    mi = __builtin_fmaf(w1, gi - mi, mi);
+    const float vi = v[i] * b2 + (w2 * gi) * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi + (neg_step * mi) / denom;
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
 }
 
 // the per-step scalars read on the device (graph replays): hyper = mms_adamw_scalars' 7 floats
@@ -345,6 +421,66 @@ MMS_EXPORT int mms_adamw_dev(float* p, const float* g, float* m, float* v, int64
   if (n == 0) return 0;
   hipLaunchKernelGGL(adamw_dev_kernel, dim3(mms::grid_for(n, 256, 8192)), dim3(256), 0, mms::as_stream(stream), p, g, m,
                      v, n, sumsq, max_norm, hyper);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_zero_multi(int nbuf, float* const* x, const int64_t* n, void* stream) {
+  const char* fn = "mms_zero_multi";
+  MMS_REQUIRE(nbuf >= 1 && nbuf <= kMaxSeg && x && n, fn, "1 to 8 buffers");
+  OptSegs a{};
+  a.n = nbuf;
+  a.b0[0] = 0;
+  for (int k = 0; k < nbuf; ++k) {
+    MMS_REQUIRE(n[k] >= 0 && (n[k] == 0 || x[k] != nullptr), fn, "null buffer");
+    a.p[k] = x[k];
+    a.len[k] = n[k];
+    a.b0[k + 1] = a.b0[k] + (int)mms::grid_for(n[k] / 4 + 1, 256, 2048);
+  }
+  hipLaunchKernelGGL(zero_multi_kernel, dim3(a.b0[nbuf]), dim3(256), 0, mms::as_stream(stream), a);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_sumsq_multi(int nseg, const float* const* x, const int64_t* n, float* const* acc, void* stream) {
+  const char* fn = "mms_sumsq_multi";
+  MMS_REQUIRE(nseg >= 1 && nseg <= kMaxSeg && x && n && acc, fn, "1 to 8 segments");
+  OptSegs a{};
+  a.n = nseg;
+  a.b0[0] = 0;
+  for (int k = 0; k < nseg; ++k) {
+    MMS_REQUIRE(n[k] >= 0 && acc[k] != nullptr && (n[k] == 0 || x[k] != nullptr), fn, "null buffer");
+    MMS_REQUIRE(((uintptr_t)x[k] & 15) == 0, fn, "buffers must be 16-byte aligned");
+    a.g[k] = x[k];
+    a.len[k] = n[k];
+    a.acc[k] = acc[k];
+    a.b0[k + 1] = a.b0[k] + (int)mms::grid_for(n[k] / 4 + 1, 256, MMS_SUMSQ_GRID);
+  }
+  hipLaunchKernelGGL(sumsq_multi_kernel, dim3(a.b0[nseg]), dim3(256), 0, mms::as_stream(stream), a);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_adamw_dev_multi(int nseg, float* const* p, const float* const* g, float* const* m, float* const* v,
+                                   const int64_t* n, const float* const* sumsq, const float* max_norm,
+                                   const float* const* hyper, void* stream) {
+  const char* fn = "mms_adamw_dev_multi";
+  MMS_REQUIRE(nseg >= 1 && nseg <= kMaxSeg && p && g && m && v && n && sumsq && max_norm && hyper, fn,
+              "1 to 8 segments");
+  OptSegs a{};
+  a.n = nseg;
+  a.b0[0] = 0;
+  for (int k = 0; k < nseg; ++k) {
+    MMS_REQUIRE(n[k] >= 0 && hyper[k] != nullptr, fn, "null hyper-parameter buffer");
+    MMS_REQUIRE(n[k] == 0 || (p[k] && g[k] && m[k] && v[k]), fn, "null buffer");
+    a.p[k] = p[k];
+    a.g[k] = g[k];
+    a.m[k] = m[k];
+    a.v[k] = v[k];
+    a.len[k] = n[k];
+    a.acc[k] = const_cast<float*>(sumsq[k]);
+    a.max_norm[k] = max_norm[k];
+    a.hyper[k] = hyper[k];
+    a.b0[k + 1] = a.b0[k] + (int)mms::grid_for(n[k], 256, 8192);
+  }
+  hipLaunchKernelGGL(adamw_dev_multi_kernel, dim3(a.b0[nseg]), dim3(256), 0, mms::as_stream(stream), a);
   return mms::check_launch(fn);
 }
 

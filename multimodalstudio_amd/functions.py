@@ -881,14 +881,25 @@ def _arena_grow(dev) -> None:
         a.buf = torch.empty(int(a.need * 1.25) + 4 * _ALIGN, device=dev)
 
 
-def zero_arena_begin(dev) -> None:
-    a = _ARENA
+def zero_arena_prepare(dev) -> Optional[torch.Tensor]:
+    """The buffer the next zero_arena_begin(dev, zeroed=...) will carve from (grown first if the last step needed
+    more), for a caller that zeroes it together with other buffers in one launch; None when there is none."""
     _arena_grow(dev)
+    a = _ARENA
+    return a.buf if a.buf is not None and a.buf.device == torch.device(dev) else None
+
+
+def zero_arena_begin(dev, zeroed: Optional[torch.Tensor] = None) -> None:
+    """Start a step's arena; ``zeroed``: the zero_arena_prepare buffer the caller has already zeroed."""
+    a = _ARENA
+    if zeroed is None or zeroed is not a.buf:
+        _arena_grow(dev)
+        zeroed = None
     a.dev = dev
     a.need, a.off = 0, 0
     a.in_step = not _ARENA_OFF
     a.active = a.buf is not None and a.buf.device == torch.device(dev)
-    if a.active:
+    if a.active and zeroed is None:
         a.buf.zero_()
 
 
@@ -923,6 +934,10 @@ def _zeroed_views(shapes, dev) -> List[Optional[torch.Tensor]]:
         out.append(None if sh is None else buf[off:off + n].view(tuple(sh)))
         off += pn
     return out
+
+
+def _capturing(dev) -> bool:
+    return torch.device(dev).type == "cuda" and torch.cuda.is_current_stream_capturing()
 
 
 def _copy_aligned(t: torch.Tensor) -> torch.Tensor:
@@ -2123,7 +2138,9 @@ class StepLossFunction(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         outs, targets = outs_targets[:n_mod], outs_targets[n_mod:]
         dev = grads.device
-        terms = torch.zeros(n_mod + 2, device=dev)
+        # carved from the step's zero arena in a captured step (its outputs are the graph's static buffers anyway,
+        # valid until the next replay); eager steps return buffers of their own
+        terms = _zeroed_views([(n_mod + 2,)], dev)[0] if _capturing(dev) else torch.zeros(n_mod + 2, device=dev)
         saved, scr = [], []
         for i in range(n_mod):
             o, t = outs[i], targets[i].contiguous()

@@ -35,6 +35,7 @@ where pipeline.backward_batched calls ``between``.
 """
 from __future__ import annotations
 
+import os
 import sys
 from typing import Dict, Optional, Tuple
 
@@ -46,6 +47,9 @@ from .pipeline import Trainer, backward_batched, compute_loss, curvature_factor,
 
 
 CAPTURE_MODE = None   # override of the capture_error_mode (probes)
+# the optimizer groups zeroed / clipped / stepped together (pipeline.OptimBank: 3 launches and 1 scalar upload per
+# step instead of 8 and 2); MMS_BANKED_OPTIM=0: per group
+BANKED_OPTIM = os.environ.get("MMS_BANKED_OPTIM", "1") != "0"
 
 
 def bucket_capacity(counts, granule: int, n: int) -> int:
@@ -153,10 +157,16 @@ class GraphTrainer:
     def _forward_backward(self, cap: int, between=None):
         t = self.t
         targets = self._targets()
-        t.fields.zero_grad()
-        if t.poses is not None:
-            t.poses.zero_grad()
-        fx.zero_arena_begin(t.device)
+        if BANKED_OPTIM:
+            # the gradients, the clip accumulators and the step's zero arena in one launch
+            arena = fx.zero_arena_prepare(t.device)
+            t.optim.zero_grads(() if arena is None else (arena,))
+            fx.zero_arena_begin(t.device, zeroed=arena)
+        else:
+            t.fields.zero_grad()
+            if t.poses is not None:
+                t.poses.zero_grad()
+            fx.zero_arena_begin(t.device)
         try:
             return self._forward_backward_body(t, targets, cap, between)
         finally:
@@ -218,6 +228,9 @@ class GraphTrainer:
 
     def _optimizer(self):
         t = self.t
+        if BANKED_OPTIM:
+            t.optim.step_captured()
+            return
         t.fields.step_captured()
         if t.poses is not None:
             t.poses.step_captured()
@@ -255,9 +268,12 @@ class GraphTrainer:
         """Queue this step's AdamW scalars (advances the optimizers' step counts)."""
         t = self.t
         f = lr_factor(t.step, t.cfg.max_iters)
-        t.fields.load_hyper(f)
-        if t.poses is not None:
-            t.poses.load_hyper(f)
+        if BANKED_OPTIM:
+            t.optim.load_hyper(f)
+        else:
+            t.fields.load_hyper(f)
+            if t.poses is not None:
+                t.poses.load_hyper(f)
         self.hyper_step = t.step
 
     def _drop_queued_hyper(self):

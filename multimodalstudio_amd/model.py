@@ -351,7 +351,9 @@ def _render_stats_segments(w, normals, starts, ends, off: List[int], S: int, sid
     [off[m], off[m+1]) scatter to rows m rows + sidx (zero elsewhere), the depth clipped to that segment's own sample
     midpoint range (one DepthRenderer call per modality, renderers.py:205-214)."""
     n = len(off) - 1
-    buf = torch.zeros(n * rows * 5 + 2 * n, device=dev)
+    # a captured step carves the (graph-static) outputs from the step's zero arena: no fill launch of their own
+    buf = fx._zeroed_views([(n * rows * 5 + 2 * n,)], dev)[0] if fx._capturing(dev) else \
+        torch.zeros(n * rows * 5 + 2 * n, device=dev)
     stats = buf[:n * rows * 5].view(n * rows, 5)
     rng = buf[n * rows * 5:]
     rng.fill_(float("-inf"))

@@ -8,10 +8,11 @@ gradient all-reduce (ddp.py) is a handful of large RCCL calls instead of one per
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from dataclasses import dataclass
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -196,6 +197,64 @@ class FlatGroup:
                   self.n, self.sumsq.data_ptr(), float(max_norm), self.hyper.data_ptr(), _s())
 
 
+class OptimBank:
+    """The trainer's optimizer groups (FlatGroup) stepped together in graph-replayed steps: the gradients and sum-of-
+    squares accumulators zeroed in one launch, the groups' clip norms in one, their AdamW updates in one
+    (mms_*_multi), and every group's per-step scalars in one device buffer filled by one upload.  The same
+    arithmetic as each group's step_captured; the eager path keeps the per-group calls."""
+
+    def __init__(self, groups: List[Optional[FlatGroup]]):
+        self.groups = [g for g in groups if g is not None]
+        G = len(self.groups)
+        if not 1 <= G <= 4:
+            raise ValueError("OptimBank holds 1 to 4 groups")
+        dev = self.groups[0].flat.device
+        self.hyper = torch.zeros(G * 8, device=dev)
+        for i, g in enumerate(self.groups):
+            g.hyper = self.hyper[8 * i:8 * i + 8]
+        self._hyper_host = [torch.zeros(G * 8).pin_memory() if dev.type == "cuda" else torch.zeros(G * 8)
+                            for _ in range(2)]
+        self._hyper_slot = 0
+        I64, VP, F32 = ctypes.c_int64 * G, ctypes.c_void_p * G, ctypes.c_float * G
+        gs = self.groups
+        self._sum = (G, VP(*[g.grad.data_ptr() for g in gs]), I64(*[g.n for g in gs]),
+                     VP(*[g.sumsq.data_ptr() for g in gs]))
+        self._args = [G, VP(*[g.flat.data_ptr() for g in gs]), VP(*[g.grad.data_ptr() for g in gs]),
+                      VP(*[g.m.data_ptr() for g in gs]), VP(*[g.v.data_ptr() for g in gs]), I64(*[g.n for g in gs]),
+                      VP(*[g.sumsq.data_ptr() for g in gs]), None, VP(*[g.hyper.data_ptr() for g in gs])]
+        self._F32 = F32
+
+    def zero_grads(self, extra: Sequence[torch.Tensor] = ()):
+        """Every group's gradient buffer and sum-of-squares accumulator = 0, and the ``extra`` f32 buffers (the step's
+        zero arena), in one launch."""
+        for g in self.groups:
+            g.check_grads_attached()
+        bufs = [g.grad for g in self.groups] + [g.sumsq for g in self.groups] + list(extra)
+        n = len(bufs)
+        _lib.call("mms_zero_multi", n, (ctypes.c_void_p * n)(*[b.data_ptr() for b in bufs]),
+                  (ctypes.c_int64 * n)(*[b.numel() for b in bufs]), _s())
+
+    def load_hyper(self, lr_factor: float):
+        """Graph mode, before a replay: advance every group's step and upload their scalars in one copy."""
+        host = self._hyper_host[self._hyper_slot]
+        self._hyper_slot ^= 1
+        for i, g in enumerate(self.groups):
+            lr = g._advance(lr_factor)
+            _lib.call("mms_adamw_scalars", float(lr), float(g.wd), float(g.betas[0]), float(g.betas[1]),
+                      float(g.eps), int(g.step_count), host.data_ptr() + 32 * i)
+        self.hyper.copy_(host, non_blocking=True)
+
+    def step_captured(self, max_norm: float = 2.0):
+        """clip_grad_norm_(max_norm) + AdamW of every group with device-resident scalars (two launches), the
+        accumulators zeroed by zero_grads at the step's start."""
+        for g in self.groups:
+            g.check_grads_attached()
+        _lib.call("mms_sumsq_multi", *self._sum, _s())
+        args = list(self._args)
+        args[7] = self._F32(*[float(max_norm)] * len(self.groups))
+        _lib.call("mms_adamw_dev_multi", *args, _s())
+
+
 def lr_factor(step: int, max_iters: int = 100000, warm_up_ratio=0.1, milestones=(0.5, 0.75, 0.9), gamma=0.4):
     """MultiStepWarmupScheduler.func (schedulers.py:259-266) as LambdaLR evaluates it."""
     warm = int(max_iters * warm_up_ratio)
@@ -354,6 +413,21 @@ class TrainConfig:
     own_heads_only: bool = True         # training renders each modality's rays through its own head only
 
 
+_SEEDS: Dict[tuple, torch.Tensor] = {}
+
+
+def _seed(total: torch.Tensor) -> torch.Tensor:
+    """d total / d total = 1 as a persistent tensor (made outside any capture, on the first eager step): a captured
+    backward reads it instead of filling a fresh ones_like each replay."""
+    key = (total.device, total.dtype, tuple(total.shape))
+    one = _SEEDS.get(key)
+    if one is None:
+        if total.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            return torch.ones_like(total)
+        one = _SEEDS[key] = torch.ones_like(total)
+    return one
+
+
 def backward_batched(total: torch.Tensor, between=None) -> None:
     """total.backward() with the layers' weight-norm gradients applied in one batched launch at its end.
 
@@ -365,12 +439,12 @@ def backward_batched(total: torch.Tensor, between=None) -> None:
         if between is not None:
             fx.wgrad_defer_begin()
             try:
-                total.backward()
+                total.backward(_seed(total))
             finally:
                 between()
             fx.wgrad_flush()
         else:
-            total.backward()
+            total.backward(_seed(total))
     finally:
         fx._WGRAD_DEFER[0] = None
         fx.wn_bwd_flush()
@@ -429,6 +503,7 @@ class Trainer:
         self.fields = FlatGroup(list(self.model.parameters()), lr=1e-3, weight_decay=0.01, eps=1e-15)
         pose_params = list(self.pose.parameters())
         self.poses = FlatGroup(pose_params, lr=1e-4, weight_decay=0.01, eps=1e-15) if pose_params else None
+        self.optim = OptimBank([self.fields, self.poses]) if self.fields.flat.device.type == "cuda" else None
         self.step = 0
 
     def targets_for(self, coords: Dict[str, torch.Tensor], sel: Dict[str, torch.Tensor]):

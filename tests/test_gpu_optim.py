@@ -71,3 +71,56 @@ def test_flat_adamw_matches_torch(dev, start, scale, captured):
                 err = (got - want).abs().max().item() / scale_
                 assert err < 2e-6, (t, i, name, err)
             off += k
+
+
+@pytest.mark.parametrize("scale", [1e-3, 3.0])
+def test_optim_bank_equals_per_group(dev, scale):
+    """pipeline.OptimBank (both groups zeroed, clipped and stepped in one launch each: mms_zero_multi,
+    mms_sumsq_multi, mms_adamw_dev_multi, one scalar upload) against each group's own step_captured: the same
+    parameters and moments (bit for bit while the clip is inactive; within 2e-6 relative when active, where the sums
+    of squares' float-atomic order may differ), and the sum-of-squares accumulators zeroed by zero_grads."""
+    from multimodalstudio_amd import pipeline as pl
+    g = torch.Generator().manual_seed(5)
+    shapes_a, shapes_b = [(4097, 2), (256, 71), (256,)], [(7, 6), (3,)]
+    pa0 = [torch.randn(*s, generator=g) * 0.1 for s in shapes_a]
+    pb0 = [torch.randn(*s, generator=g) * 0.1 for s in shapes_b]
+    grads = [([torch.randn(*s, generator=g) * scale for s in shapes_a],
+              [torch.randn(*s, generator=g) * scale for s in shapes_b]) for _ in range(3)]
+    runs = []
+    for banked in (False, True):
+        pa = [torch.nn.Parameter(p.clone().to(dev)) for p in pa0]
+        pb = [torch.nn.Parameter(p.clone().to(dev)) for p in pb0]
+        ga = pl.FlatGroup(pa, lr=1e-3, weight_decay=0.01, eps=1e-15)
+        gb = pl.FlatGroup(pb, lr=1e-4, weight_decay=0.01, eps=1e-15)
+        bank = pl.OptimBank([ga, gb]) if banked else None
+        for t, (gsa, gsb) in enumerate(grads):
+            if banked:
+                ga.sumsq.fill_(123.0)     # stale accumulators: zero_grads must clear them
+                gb.sumsq.fill_(7.0)
+                bank.zero_grads()
+            else:
+                ga.zero_grad()
+                gb.zero_grad()
+            for p, gg in zip(pa, gsa):
+                p.grad.copy_(gg.to(dev))
+            for p, gg in zip(pb, gsb):
+                p.grad.copy_(gg.to(dev))
+            f = pl.lr_factor(2500 + t, 20000)
+            if banked:
+                bank.load_hyper(f)
+                bank.step_captured()
+            else:
+                ga.load_hyper(f)
+                gb.load_hyper(f)
+                ga.step_captured()
+                gb.step_captured()
+        torch.cuda.synchronize()
+        runs.append([x.detach().cpu().clone() for grp in (ga, gb) for x in (grp.flat, grp.m, grp.v, grp.sumsq)])
+        assert ga.step_count == gb.step_count == 3
+    for i, (a, b) in enumerate(zip(*runs)):
+        if i % 4 == 3:     # sums of squares: float atomics in any order
+            assert torch.allclose(a, b, rtol=1e-5), (i, a, b)
+        elif scale < 1:
+            assert torch.equal(a, b), (i, float((a - b).abs().max()))
+        else:
+            assert float((a - b).abs().max()) <= 2e-6 * float(b.abs().max()), i
