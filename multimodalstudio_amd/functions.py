@@ -936,6 +936,69 @@ def _zeroed_views(shapes, dev) -> List[Optional[torch.Tensor]]:
     return out
 
 
+# Gradient accumulators shared by a tensor's consumers.  A tensor read by k autograd Functions (the rays' directions:
+# five consumers; the hit rays' directions: four; the sample positions and the SDF gradients: two) otherwise costs
+# k - 1 ATen adds per step (autograd sums the parts; each add a ~4-5 us graph node).  Its producer attaches a GradAcc
+# in the forward; every consumer on the producer's stream whose backward kernel accumulates (+=) into a zeroed buffer
+# accumulates into the accumulator's ONE buffer instead and returns None for that input; the producer -- whose
+# backward runs after all of its outputs' consumers, on the same stream -- takes the buffer (plus the parts the other
+# consumers returned) as the output's gradient.  Consumers on the background stream keep returning their parts:
+# autograd orders them with the main stream and adds them (a shared buffer across the two streams raced on the first
+# step, round 4).  MMS_GRAD_ACC=0: per-consumer buffers everywhere.
+GRAD_ACC = os.environ.get("MMS_GRAD_ACC", "1") != "0"
+
+
+class GradAcc:
+    __slots__ = ("shape", "dev", "_buf", "_home")
+
+    def __init__(self, t: torch.Tensor):
+        # made in the producer's forward, on the stream its backward will run on (autograd's stream semantics)
+        self.shape, self.dev, self._buf = tuple(t.shape), t.device, None
+        self._home = self._key()
+
+    def _key(self):
+        return torch.cuda.current_stream(self.dev).cuda_stream if self.dev.type == "cuda" else 0
+
+    def buf(self) -> torch.Tensor:
+        """The zeroed accumulation buffer (carved from the step's zero arena on first use)."""
+        if self._buf is None:
+            self._buf = _zeroed_views([self.shape], self.dev)[0]
+        return self._buf
+
+    def total(self, incoming: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        """The producer's view: the accumulated gradient (+ the parts autograd delivered)."""
+        b, self._buf = self._buf, None
+        if b is None:
+            return incoming
+        return b if incoming is None else b + incoming
+
+
+def attach_acc(t: torch.Tensor) -> torch.Tensor:
+    """Producer forward: give output ``t`` a shared gradient accumulator (GRAD_ACC)."""
+    if GRAD_ACC:
+        t._mms_acc = GradAcc(t)
+    return t
+
+
+def acc_of(t) -> Optional[GradAcc]:
+    """Consumer forward: the accumulator of input ``t`` -- None when none is attached or when this consumer runs on
+    another stream than the producer (its backward then returns its part as usual: autograd orders and adds it)."""
+    a = getattr(t, "_mms_acc", None) if t is not None else None
+    return a if a is not None and a._key() == a._home else None
+
+
+def acc_or_zeroed(acc: Optional[GradAcc], shape, dev, need: bool = True) -> Optional[torch.Tensor]:
+    """Consumer backward: the buffer its kernel accumulates into -- the shared one, or a zeroed one of its own."""
+    if not need:
+        return None
+    return acc.buf() if acc is not None else _zeroed_views([tuple(shape)], dev)[0]
+
+
+def acc_ret(acc: Optional[GradAcc], g):
+    """Consumer backward: the gradient it returns for that input (None when it went into the shared buffer)."""
+    return None if acc is not None else g
+
+
 def _capturing(dev) -> bool:
     return torch.device(dev).type == "cuda" and torch.cuda.is_current_stream_capturing()
 
@@ -962,6 +1025,7 @@ class SurfaceFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, pos, table, grid: GridCfg, active: int, delta: float, *params):
         ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
+        ctx.acc_pos = acc_of(pos)
         M = pos.shape[0]
         dev = pos.device
         pos = pos.contiguous()
@@ -996,11 +1060,16 @@ class SurfaceFunction(torch.autograd.Function):
         ctx.four_delta, ctx.delta_sq = four_delta, delta_sq
         ctx.X = X
         ctx.save_for_backward(pos, table, grads, *params)
+        ctx.acc_grads = GradAcc(grads) if GRAD_ACC else None
+        if ctx.acc_grads is not None:
+            grads._mms_acc = ctx.acc_grads
         return sdf, geo, grads, hess, normals
 
     @staticmethod
     def backward(ctx, dsdf, dgeo, dgrads, dhess, dnormals):
         pos, table, grads, *params = ctx.saved_tensors
+        if ctx.acc_grads is not None:
+            dgrads = ctx.acc_grads.total(dgrads)
         M, G = ctx.M, ctx.G
         dev = pos.device
         # dout: centre rows all 257 columns, tap rows only the sdf column (everything read is written here)
@@ -1022,14 +1091,15 @@ class SurfaceFunction(torch.autograd.Function):
         X = ctx.X
         K0 = X.stride(0)
         dtable = grad_target(ctx.table) if need_table else None
-        dP, dpos = _zeroed_views([(5 * M, 3), (M, 3)] if need_pos else [None, None], dev)
+        dP = _zeroed_views([(5 * M, 3)], dev)[0] if need_pos else None
+        dpos = acc_or_zeroed(ctx.acc_pos, (M, 3), dev, need_pos)
         grid_bwd(ctx.grid, X, K0, 5 * M, table, ctx.active, dX, 39, dtable, dP, group=5)
         _grad_ready(ctx.table_p, dtable)
         if need_pos:
             _lib.call("mms_geo_input_bwd", X.data_ptr(), K0, dX.data_ptr(), dX.stride(0), dP.data_ptr(), 3, M, 4, 6,
                       dpos.data_ptr(), 3, _s())
         ctx.run = ctx.H = ctx.W3 = ctx.X = ctx.table = ctx.chain = None
-        return (dpos, None, None, None, None, *pgrads)
+        return (acc_ret(ctx.acc_pos, dpos), None, None, None, None, *pgrads)
 
 
 def _sdf_mlp_unfused(ctx, X, M, params, dev):
@@ -1252,6 +1322,7 @@ class RadianceFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pos, dirs, normals, geo, table, grid: GridCfg, active: int, S: int, *params):
+        ctx.acc_pos, ctx.acc_dirs = acc_of(pos), acc_of(dirs)
         M = pos.shape[0]
         G = geo.shape[1]
         dev = pos.device
@@ -1295,8 +1366,9 @@ class RadianceFunction(torch.autograd.Function):
         K0 = X.stride(0)
         dtable = grad_target(ctx.table) if ctx.needs_input_grad[4] else None
         need_pos = ctx.needs_input_grad[0]
-        dP, dpos, ddirs = _zeroed_views([(M, 3) if need_pos else None, (M, 3) if need_pos else None,
-                                         (R, 3) if ctx.needs_input_grad[1] else None], dev)
+        dP = _zeroed_views([(M, 3)], dev)[0] if need_pos else None
+        dpos = acc_or_zeroed(ctx.acc_pos, (M, 3), dev, need_pos)
+        ddirs = acc_or_zeroed(ctx.acc_dirs, (R, 3), dev, ctx.needs_input_grad[1])
         grid_bwd(ctx.grid, X, K0, M, table, ctx.active, dX, 29 + G, dtable, dP)
         _grad_ready(ctx.table_p, dtable)   # the radiance table's last contribution: its all-reduce overlaps the rest
         # d geo = the panel gradient's geo columns, handed on as a view (no copy)
@@ -1306,7 +1378,7 @@ class RadianceFunction(torch.autograd.Function):
         ctx.run = None
         ctx.X = None
         ctx.table = None
-        return (dpos, ddirs, None, dgeo, None, None, None, None, *pgrads)
+        return (acc_ret(ctx.acc_pos, dpos), acc_ret(ctx.acc_dirs, ddirs), None, dgeo, None, None, None, None, *pgrads)
 
 
 class RadInputFunction(torch.autograd.Function):
@@ -1383,6 +1455,7 @@ class BackgroundFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, pos, dirs, table, S: int, nb: int, nd: int, grid: Optional[GridCfg], active: int, *params):
         ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
+        ctx.acc_dirs = acc_of(dirs)
         M = pos.shape[0]
         dev = pos.device
         base_p, dens_p, head_p = params[:3 * nb], params[3 * nb:3 * (nb + nd)], params[3 * (nb + nd):]
@@ -1437,11 +1510,11 @@ class BackgroundFunction(torch.autograd.Function):
             _grad_ready(ctx.table, dtable)
             dX[:, :3] += dP
         dpos = torch.empty(M, 3, device=dev) if ctx.needs_input_grad[0] else None
-        ddirs = _zeroed_views([(R, 3)], dev)[0] if ctx.needs_input_grad[1] else None
+        ddirs = acc_or_zeroed(ctx.acc_dirs, (R, 3), dev, ctx.needs_input_grad[1])
         _lib.call("mms_bg_input_bwd", pos.data_ptr(), ctx.X.data_ptr(), ctx.X.stride(0), dX.data_ptr(), dX.stride(0),
                   dirs.data_ptr(), dH.data_ptr(), dH.stride(0), Fb, R, S, _p(dpos), _p(ddirs), _s())
         ctx.base = ctx.dens = ctx.head = ctx.X = ctx.H = ctx.table = None
-        return (dpos, ddirs, None, None, None, None, None, None, *([None] * len(params)))
+        return (dpos, acc_ret(ctx.acc_dirs, ddirs), None, None, None, None, None, None, *([None] * len(params)))
 
 
 def _mlp_strided(run, H: torch.Tensor, Fb: int) -> torch.Tensor:
@@ -1501,6 +1574,7 @@ class NeusWeightsFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, sdf, grads, dirs, deltas, s_param, cos_anneal: float, S: int):
+        ctx.acc_grads, ctx.acc_dirs = acc_of(grads), acc_of(dirs)
         M = sdf.shape[0]
         R = M // S
         dev = sdf.device
@@ -1523,11 +1597,13 @@ class NeusWeightsFunction(torch.autograd.Function):
         R = sdf.shape[0] // S
         dev = sdf.device
         dsdf = torch.empty(sdf.shape[0], 1, device=dev)
-        dgrads, ddirs, ddeltas, ds = _zeroed_views([grads.shape, dirs.shape, deltas.shape, s_param.shape], dev)
+        ddeltas, ds = _zeroed_views([deltas.shape, s_param.shape], dev)
+        dgrads = acc_or_zeroed(ctx.acc_grads, grads.shape, dev)
+        ddirs = acc_or_zeroed(ctx.acc_dirs, dirs.shape, dev)
         _lib.call("mms_neus_weights_bwd", sdf.data_ptr(), sdf.stride(0), grads.data_ptr(), dirs.data_ptr(), deltas.data_ptr(),
                   s_param.data_ptr(), ctx.cos_anneal, R, S, alpha.data_ptr(), dw.contiguous().data_ptr(),
                   dsdf.data_ptr(), 1, dgrads.data_ptr(), ddirs.data_ptr(), ddeltas.data_ptr(), ds.data_ptr(), _s())
-        return dsdf, dgrads, ddirs, ddeltas, ds, None, None
+        return dsdf, acc_ret(ctx.acc_grads, dgrads), acc_ret(ctx.acc_dirs, ddirs), ddeltas, ds, None, None
 
 
 class DensityWeightsFunction(torch.autograd.Function):
@@ -1604,6 +1680,7 @@ class SamplesFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, bins, nears, fars, origins, dirs, kind: int):
         ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
+        ctx.acc_o, ctx.acc_d = acc_of(origins), acc_of(dirs)
         R, nb = bins.shape
         S = nb - 1
         dev = bins.device
@@ -1619,19 +1696,26 @@ class SamplesFunction(torch.autograd.Function):
         ctx.save_for_backward(bins, nears, fars, dirs)
         ctx.kind = kind
         ctx.mark_non_differentiable(ends)
+        ctx.acc_pos = GradAcc(pos) if GRAD_ACC else None
+        if ctx.acc_pos is not None:
+            pos._mms_acc = ctx.acc_pos
         return pos, deltas, starts, ends
 
     @staticmethod
     def backward(ctx, dpos, ddeltas, dstarts, dends):
         bins, nears, fars, dirs = ctx.saved_tensors
+        if ctx.acc_pos is not None:
+            dpos = ctx.acc_pos.total(dpos)
         R, nb = bins.shape
-        dn, df, do, dd = _zeroed_views([nears.shape, fars.shape, (R, 3), (R, 3)], bins.device)
+        dn, df = _zeroed_views([nears.shape, fars.shape], bins.device)
+        do = acc_or_zeroed(ctx.acc_o, (R, 3), bins.device)
+        dd = acc_or_zeroed(ctx.acc_d, (R, 3), bins.device)
         _lib.call("mms_samples_bwd", bins.data_ptr(), nb, nb, nears.data_ptr(), fars.data_ptr(), dirs.data_ptr(),
                   ctx.kind, R, _p(None if dpos is None else dpos.contiguous()),
                   _p(None if ddeltas is None else ddeltas.contiguous()),
                   _p(None if dstarts is None else dstarts.contiguous()), dn.data_ptr(), df.data_ptr(), do.data_ptr(),
                   dd.data_ptr(), _s())
-        return None, dn, df, do, dd, None
+        return None, dn, df, acc_ret(ctx.acc_o, do), acc_ret(ctx.acc_d, dd), None
 
 
 class HitGatherFunction(torch.autograd.Function):
@@ -1641,6 +1725,7 @@ class HitGatherFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, o, d, up, nears, fars):
         ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
+        ctx.acc_in = (acc_of(o), acc_of(d), acc_of(up))
         R, N = idx.shape[0], o.shape[0]
         dev = o.device
         o, d, up, nears, fars = o.contiguous(), d.contiguous(), up.contiguous(), nears.contiguous(), fars.contiguous()
@@ -1650,17 +1735,24 @@ class HitGatherFunction(torch.autograd.Function):
                   fars.data_ptr(), oh.data_ptr(), dh.data_ptr(), uh.data_ptr(), nh.data_ptr(), fh.data_ptr(), _s())
         ctx.save_for_backward(idx)
         ctx.N = N
+        ctx.acc_dh = GradAcc(dh) if GRAD_ACC else None
+        if ctx.acc_dh is not None:
+            dh._mms_acc = ctx.acc_dh
         return oh, dh, uh, nh, fh
 
     @staticmethod
     def backward(ctx, doh, ddh, duh, dnh, dfh):
         (idx,) = ctx.saved_tensors
+        if ctx.acc_dh is not None:
+            ddh = ctx.acc_dh.total(ddh)
         N = ctx.N
-        go, gd, gu, gn, gf = _zeroed_views([(N, 3), (N, 3), (N, 3), (N,), (N,)], idx.device)
+        gn, gf = _zeroed_views([(N,), (N,)], idx.device)
+        ao, ad, au = ctx.acc_in
+        go, gd, gu = [acc_or_zeroed(a, (N, 3), idx.device) for a in (ao, ad, au)]
         c = lambda t: None if t is None else t.contiguous()
         _lib.call("mms_hit_gather_bwd", idx.data_ptr(), idx.shape[0], _p(c(doh)), _p(c(ddh)), _p(c(duh)), _p(c(dnh)),
                   _p(c(dfh)), go.data_ptr(), gd.data_ptr(), gu.data_ptr(), gn.data_ptr(), gf.data_ptr(), _s())
-        return None, go, gd, gu, gn, gf
+        return None, acc_ret(ao, go), acc_ret(ad, gd), acc_ret(au, gu), gn, gf
 
 
 class PoseExpFunction(torch.autograd.Function):
@@ -1706,11 +1798,17 @@ class RaysFunction(torch.autograd.Function):
         ctx.save_for_backward(mats, coords)
         ctx.cams, ctx.off, ctx.per_cam = cams, float(pixel_offset), per_cam
         ctx.mark_non_differentiable(a, dn)
+        ctx.accs = None
+        if GRAD_ACC and ctx.needs_input_grad[0]:
+            ctx.accs = (GradAcc(o), GradAcc(d), GradAcc(u))
+            o._mms_acc, d._mms_acc, u._mms_acc = ctx.accs
         return o, d, u, a, dn
 
     @staticmethod
     def backward(ctx, do, dd, du, da, ddn):
         mats, coords = ctx.saved_tensors
+        if ctx.accs is not None:
+            do, dd, du = [a.total(g) for a, g in zip(ctx.accs, (do, dd, du))]
         cams = ctx.cams
         N = coords.shape[0]
         dm = _zeroed_views([tuple(mats.shape)], mats.device)[0]
@@ -1727,6 +1825,7 @@ class ColliderFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, origins, dirs, radius: float):
         ctx.set_materialize_grads(False)   # unused outputs' gradients arrive as None (no zero fills)
+        ctx.acc_o, ctx.acc_d = acc_of(origins), acc_of(dirs)
         N = origins.shape[0]
         dev = origins.device
         origins, dirs = origins.contiguous(), dirs.contiguous()
@@ -1746,11 +1845,12 @@ class ColliderFunction(torch.autograd.Function):
     def backward(ctx, dn, df, dbn, dbf, dmask):
         origins, dirs = ctx.saved_tensors
         N = origins.shape[0]
-        do, dd = _zeroed_views([origins.shape, dirs.shape], origins.device)
+        do = acc_or_zeroed(ctx.acc_o, origins.shape, origins.device)
+        dd = acc_or_zeroed(ctx.acc_d, dirs.shape, origins.device)
         c = lambda t: None if t is None else t.contiguous()
         _lib.call("mms_collider_bwd", origins.data_ptr(), dirs.data_ptr(), N, ctx.radius, _p(c(dn)), _p(c(df)),
                   _p(c(dbn)), _p(c(dbf)), do.data_ptr(), dd.data_ptr(), _s())
-        return do, dd, None
+        return acc_ret(ctx.acc_o, do), acc_ret(ctx.acc_d, dd), None
 
 
 def compact_padded(mask: torch.Tensor, cap: int):
@@ -1937,6 +2037,7 @@ class HeadsCompositeFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, feat, w, dirs, ups, S: int, heads, jobs, items, *rest):
         ctx.set_materialize_grads(False)
+        ctx.acc_d, ctx.acc_u = acc_of(dirs), acc_of(ups)
         n_items = len(items)
         bgs, params = rest[:n_items], rest[n_items:]
         offs, o = [], 0
@@ -2021,7 +2122,8 @@ class HeadsCompositeFunction(torch.autograd.Function):
         ddirs = dups = None
         if need_dir and any(heads[jobs[j][0]].kind == "polarization" and dvals[j] is not None
                             for j in range(len(jobs))):
-            ddirs, dups = _zeroed_views([tuple(dirs.shape), tuple(ups.shape)], dev)
+            ddirs = acc_or_zeroed(ctx.acc_d, dirs.shape, dev)
+            dups = acc_or_zeroed(ctx.acc_u, ups.shape, dev)
         for j, (h_id, r0, rays) in enumerate(jobs):
             if dvals[j] is None:
                 continue
@@ -2045,8 +2147,10 @@ class HeadsCompositeFunction(torch.autograd.Function):
             else:
                 rows += _mlp_backward(run, dy, None)
         ctx.runs = ctx.vals = None
-        return (dfeat, dw if ctx.needs_input_grad[1] else None, ddirs if ctx.needs_input_grad[2] else None,
-                dups if ctx.needs_input_grad[3] else None, None, None, None, None, *dbgs, *([None] * ctx.n_params))
+        return (dfeat, dw if ctx.needs_input_grad[1] else None,
+                acc_ret(ctx.acc_d, ddirs) if ctx.needs_input_grad[2] else None,
+                acc_ret(ctx.acc_u, dups) if ctx.needs_input_grad[3] else None, None, None, None, None, *dbgs,
+                *([None] * ctx.n_params))
 
 
 def _partitions(ranges, total: int) -> bool:
@@ -2136,6 +2240,7 @@ class StepLossFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, n_mod: int, sat_thrs, w_curv: float, S: int, counts, seg_rays: int, grads, hess, *outs_targets):
         ctx.set_materialize_grads(False)
+        ctx.acc_g = acc_of(grads)
         outs, targets = outs_targets[:n_mod], outs_targets[n_mod:]
         dev = grads.device
         # carved from the step's zero arena in a captured step (its outputs are the graph's static buffers anyway,
@@ -2194,7 +2299,8 @@ class StepLossFunction(torch.autograd.Function):
                       _p(ctx.scr[i]), dl.data_ptr(), 1.0, d.data_ptr(), d.stride(0), _s())
             douts.append(d)
         M = g.shape[0]
-        dg, dh = _zeroed_views([(M, 3), (M, 3) if h is not None else None], dev)
+        dh = _zeroed_views([(M, 3)], dev)[0] if h is not None else None
+        dg = acc_or_zeroed(ctx.acc_g, (M, 3), dev).view(M, 3)
         S = ctx.S
         if counts is None:
             _lib.call("mms_geo_loss_bwd", g.data_ptr(), _p(h), M, 1.0 / float(max(M, 1)), dl.data_ptr(), 0.1,
@@ -2208,8 +2314,8 @@ class StepLossFunction(torch.autograd.Function):
                           ctx.w_curv, dg[m * rows:].data_ptr(), _p(None if dh is None else dh[m * rows:]), _s())
         gs, hs = ctx.shape
         ctx.scr = None
-        return (None, None, None, None, None, None, dg.view(gs), (dh.view(hs) if dh is not None else None),
-                *douts, *([None] * n_mod))
+        return (None, None, None, None, None, None, acc_ret(ctx.acc_g, dg.view(gs)),
+                (dh.view(hs) if dh is not None else None), *douts, *([None] * n_mod))
 
 
 def HashGridApply(x, table, cfg: GridCfg, active: int):

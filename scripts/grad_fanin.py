@@ -37,18 +37,22 @@ def main():
         if n is None or n in seen:
             continue
         seen.add(n)
-        for nxt, _ in n.next_functions:
+        for nxt, nr in n.next_functions:
             if nxt is not None:
-                fanin[nxt].append(n.name())
+                fanin[(nxt, nr)].append(n.name())
                 stack.append(nxt)
     print(f"{len(seen)} autograd nodes")
-    for n, srcs in sorted(fanin.items(), key=lambda kv: -len(kv[1])):
+    for (n, nr), srcs in sorted(fanin.items(), key=lambda kv: -len(kv[1])):
         if len(srcs) > 1:
             extra = ""
             if n.name() == "torch::autograd::AccumulateGrad":
-                v = n.variable
-                extra = f" param {tuple(v.shape)}"
-            print(f"{len(srcs)} -> {n.name()}{extra}  from {collections.Counter(srcs).most_common()}")
+                extra = f" param {tuple(n.variable.shape)}"
+            else:
+                try:
+                    extra = f" shape {n._input_metadata[nr].shape}"
+                except Exception:
+                    pass
+            print(f"{len(srcs) - 1} add(s): {n.name()} output {nr}{extra}  from {collections.Counter(srcs).most_common()}")
     fx.zero_arena_end()
 
 
