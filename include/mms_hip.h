@@ -247,15 +247,16 @@ int mms_density_weights_fwd(const float* density, int64_t ldd, const float* delt
 int mms_density_weights_bwd(const float* density, int64_t ldd, const float* deltas, int64_t R, int S,
                             const float* alpha, const float* dweights, float* ddensity, int64_t lddd, float* ddeltas,
                             void* stream);
-/* composite sum_s w c (+ bg (1 - sum w)), scattering compacted rays to rows idx[r]
- * (Renderer.render / RadianceRenderer renderers.py:75-174; BackgroundModel sum background_model.py:101-109).
+/* composite sum_s w c (+ bg (1 - sum w)), scattering compacted rays to rows idx[r] of out [nout, C]
+ * (Renderer.render / RadianceRenderer renderers.py:75-174; BackgroundModel sum background_model.py:101-109); a ray
+ * with idx[r] >= nout (the padding rays of a fixed-capacity batch) is discarded: no output row, zero gradients.
  * bwd: dvals and dw [R, S] are written (not accumulated); dbg[idx[r]] is overwritten for hit rows (the caller
  * passes dbg = dout, the pass-through gradient of every other row). */
 int mms_composite_fwd(const float* w, const float* vals, int64_t ldv, int C, const float* bg, int64_t R, int S,
-                      const int64_t* idx, float* out, void* stream);
+                      const int64_t* idx, int64_t nout, float* out, void* stream);
 int mms_composite_bwd(const float* w, const float* vals, int64_t ldv, int C, const float* bg, int64_t R, int S,
-                      const int64_t* idx, const float* dout, float* dvals, int64_t lddv, float* dw, float* dbg,
-                      void* stream);
+                      const int64_t* idx, int64_t nout, const float* dout, float* dvals, int64_t lddv, float* dw,
+                      float* dbg, void* stream);
 /* Accumulation / normals / depth renderers (renderers.py:176-242, no grad) of compacted rays scattered to rows idx[r]:
  * out [rows, ldo >= 5] = (sum w, sum w n, sum w mid) per hit row (other rows untouched), depth clipped to the range of
  * all sample midpoints; range [2] is scratch, (-inf, -inf) on entry. */
@@ -314,7 +315,7 @@ int mms_neus_step(int64_t R, int S, const float* bins, const float* sdf_prev, in
 /* ---- rays (cameras/cameras.py:460-703, camera_utils.py:280-383, poses.py:53-67, ray_generators.py:54-81).
  * coords int [N, 3] = (camera, y, x); mats = camera_opt_to_camera [C or 1, 3, 4]; bwd dmats += (atomic). */
 /* SO(3) x R^3 exponential map of the camera-pose deltas (lie_groups.py:28-63, camera_optimizers.py:86-119):
- * tangent [B, 6] = (t, w) -> mats [B, 3, 4] = [R(w) | t]; bwd writes dtangent [B, 6] from dmats [B, 3, 4]. */
+ * tangent [B, 6] = (t, w) -> mats [B, 3, 4] = [R(w) | t]; bwd adds d tangent [B, 6] from dmats [B, 3, 4] into dtangent. */
 int mms_pose_exp_fwd(const float* tangent, int64_t B, float* mats, void* stream);
 int mms_pose_exp_bwd(const float* tangent, const float* dmats, int64_t B, float* dtangent, void* stream);
 int mms_raygen_fwd(const int* coords, int64_t N, const float* fx, const float* fy, const float* cx, const float* cy,

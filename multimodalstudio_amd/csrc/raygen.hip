@@ -432,11 +432,11 @@ __global__ void pose_exp_bwd_kernel(const float* __restrict__ tangent, const flo
 #pragma unroll
     for (int k = 0; k < 3; ++k) dw[k] += da * w[k] * inv;
   }
-  float* d = dtangent + 6 * b;
+  float* d = dtangent + 6 * b;   // accumulated: the pose parameter's own gradient buffer (functions.grad_target)
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    d[i] = g[4 * i + 3];
-    d[3 + i] = dw[i];
+    d[i] += g[4 * i + 3];
+    d[3 + i] += dw[i];
   }
 }
 

@@ -214,14 +214,15 @@ __global__ __launch_bounds__(256) void density_weights_bwd_kernel(const float* _
 __global__ __launch_bounds__(256) void composite_fwd_kernel(const float* __restrict__ w, const float* __restrict__ vals,
                                                             int64_t ldv, int C, const float* __restrict__ bg,
                                                             int64_t R, int S, const int64_t* __restrict__ idx,
-                                                            float* __restrict__ out) {
+                                                            int64_t nout, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int64_t ray = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (ray >= R) return;
+  const int64_t orow = idx ? idx[ray] : ray;
+  if (orow >= nout) return;   // a padding ray: discarded (wave-uniform)
   const int64_t i = ray * S + lane;
   const float wi = lane < S ? w[i] : 0.f;
   const float acc = wave_sum(wi);
-  const int64_t orow = idx ? idx[ray] : ray;
   for (int c = 0; c < C; ++c) {
     const float v = lane < S ? wi * vals[i * ldv + c] : 0.f;
     const float sum = wave_sum(v);
@@ -237,7 +238,7 @@ __global__ __launch_bounds__(256) void composite_fwd_kernel(const float* __restr
 __global__ __launch_bounds__(256) void composite_bwd_kernel(const float* __restrict__ w, const float* __restrict__ vals,
                                                             int64_t ldv, int C, const float* __restrict__ bg,
                                                             int64_t R, int S, const int64_t* __restrict__ idx,
-                                                            const float* __restrict__ dout,
+                                                            int64_t nout, const float* __restrict__ dout,
                                                             float* __restrict__ dvals, int64_t lddv,
                                                             float* __restrict__ dw, float* __restrict__ dbg) {
   const int lane = threadIdx.x & 63;
@@ -247,15 +248,16 @@ __global__ __launch_bounds__(256) void composite_bwd_kernel(const float* __restr
   const float wi = lane < S ? w[i] : 0.f;
   const float acc = wave_sum(wi);
   const int64_t orow = idx ? idx[ray] : ray;
+  const bool live = orow < nout;   // a padding ray (discarded in the forward): zero gradients
   float gw = 0.f;
   for (int c = 0; c < C; ++c) {
-    const float g = dout[orow * C + c];
+    const float g = live ? dout[orow * C + c] : 0.f;
     if (lane < S) {
       if (dvals) dvals[i * lddv + c] = g * wi;
       gw += g * vals[i * ldv + c];
       if (bg) gw -= g * bg[orow * C + c];
     }
-    if (lane == 0 && bg && dbg) dbg[orow * C + c] = g * (1.0f - acc);  // hit rows: overwrite the pass-through dout
+    if (lane == 0 && bg && dbg && live) dbg[orow * C + c] = g * (1.0f - acc);  // hit rows: overwrite the pass-through dout
   }
   if (lane < S && dw) dw[i] = gw;  // every weight of the ray is written (no accumulation: dw needs no zero fill)
 }
@@ -456,12 +458,12 @@ MMS_EXPORT int mms_density_weights_bwd(const float* density, int64_t ldd, const 
 }
 
 MMS_EXPORT int mms_composite_fwd(const float* w, const float* vals, int64_t ldv, int C, const float* bg, int64_t R,
-                                 int S, const int64_t* idx, float* out, void* stream) {
+                                 int S, const int64_t* idx, int64_t nout, float* out, void* stream) {
   const char* fn = "mms_composite_fwd";
   MMS_REQUIRE(S >= 1 && S <= 64, fn, "samples per ray must be in [1, 64]");
   if (R == 0) return 0;
   hipLaunchKernelGGL(composite_fwd_kernel, dim3(mms::grid_for(R * 64, 256, INT32_MAX)), dim3(256), 0,
-                     mms::as_stream(stream), w, vals, ldv, C, bg, R, S, idx, out);
+                     mms::as_stream(stream), w, vals, ldv, C, bg, R, S, idx, nout, out);
   return mms::check_launch(fn);
 }
 
@@ -481,12 +483,12 @@ MMS_EXPORT int mms_render_stats(const float* w, const float* normals, const floa
 }
 
 MMS_EXPORT int mms_composite_bwd(const float* w, const float* vals, int64_t ldv, int C, const float* bg, int64_t R,
-                                 int S, const int64_t* idx, const float* dout, float* dvals, int64_t lddv, float* dw,
-                                 float* dbg, void* stream) {
+                                 int S, const int64_t* idx, int64_t nout, const float* dout, float* dvals, int64_t lddv,
+                                 float* dw, float* dbg, void* stream) {
   const char* fn = "mms_composite_bwd";
   MMS_REQUIRE(S >= 1 && S <= 64, fn, "samples per ray must be in [1, 64]");
   if (R == 0) return 0;
   hipLaunchKernelGGL(composite_bwd_kernel, dim3(mms::grid_for(R * 64, 256, INT32_MAX)), dim3(256), 0,
-                     mms::as_stream(stream), w, vals, ldv, C, bg, R, S, idx, dout, dvals, lddv, dw, dbg);
+                     mms::as_stream(stream), w, vals, ldv, C, bg, R, S, idx, nout, dout, dvals, lddv, dw, dbg);
   return mms::check_launch(fn);
 }

@@ -1575,6 +1575,7 @@ class NeusWeightsFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, sdf, grads, dirs, deltas, s_param, cos_anneal: float, S: int):
         ctx.acc_grads, ctx.acc_dirs = acc_of(grads), acc_of(dirs)
+        ctx.s_leaf = s_param.is_leaf
         M = sdf.shape[0]
         R = M // S
         dev = sdf.device
@@ -1597,13 +1598,17 @@ class NeusWeightsFunction(torch.autograd.Function):
         R = sdf.shape[0] // S
         dev = sdf.device
         dsdf = torch.empty(sdf.shape[0], 1, device=dev)
-        ddeltas, ds = _zeroed_views([deltas.shape, s_param.shape], dev)
+        ddeltas = _zeroed_views([deltas.shape], dev)[0]
+        # the variance parameter's gradient: atomics straight into its .grad (grad_target: no AccumulateGrad add)
+        s_direct = ctx.s_leaf and s_param.requires_grad
+        ds = grad_target(s_param) if s_direct else _zeroed_views([s_param.shape], dev)[0]
         dgrads = acc_or_zeroed(ctx.acc_grads, grads.shape, dev)
         ddirs = acc_or_zeroed(ctx.acc_dirs, dirs.shape, dev)
         _lib.call("mms_neus_weights_bwd", sdf.data_ptr(), sdf.stride(0), grads.data_ptr(), dirs.data_ptr(), deltas.data_ptr(),
                   s_param.data_ptr(), ctx.cos_anneal, R, S, alpha.data_ptr(), dw.contiguous().data_ptr(),
                   dsdf.data_ptr(), 1, dgrads.data_ptr(), ddirs.data_ptr(), ddeltas.data_ptr(), ds.data_ptr(), _s())
-        return dsdf, acc_ret(ctx.acc_grads, dgrads), acc_ret(ctx.acc_dirs, ddirs), ddeltas, ds, None, None
+        return (dsdf, acc_ret(ctx.acc_grads, dgrads), acc_ret(ctx.acc_dirs, ddirs), ddeltas, None if s_direct else ds,
+                None, None)
 
 
 class DensityWeightsFunction(torch.autograd.Function):
@@ -1649,8 +1654,8 @@ class CompositeFunction(torch.autograd.Function):
         else:
             out = torch.empty(R, C, device=w.device)
             bgc = None
-        _lib.call("mms_composite_fwd", w.data_ptr(), vals.data_ptr(), C, C, _p(bgc), R, S, _p(idx), out.data_ptr(),
-                  _s())
+        _lib.call("mms_composite_fwd", w.data_ptr(), vals.data_ptr(), C, C, _p(bgc), R, S, _p(idx), out.shape[0],
+                  out.data_ptr(), _s())
         ctx.save_for_backward(w, vals, bgc, idx)
         ctx.S = S
         ctx.has_bg = bg is not None
@@ -1665,8 +1670,8 @@ class CompositeFunction(torch.autograd.Function):
         dvals = torch.empty_like(vals) if ctx.needs_input_grad[1] else None
         dw = torch.empty_like(w)                 # every weight written by the kernel
         dbg = dout.clone() if ctx.has_bg else None
-        _lib.call("mms_composite_bwd", w.data_ptr(), vals.data_ptr(), C, C, _p(bgc), R, S, _p(idx), dout.data_ptr(),
-                  _p(dvals), C, dw.data_ptr(), _p(dbg), _s())
+        _lib.call("mms_composite_bwd", w.data_ptr(), vals.data_ptr(), C, C, _p(bgc), R, S, _p(idx), dout.shape[0],
+                  dout.data_ptr(), _p(dvals), C, dw.data_ptr(), _p(dbg), _s())
         return dw, dvals, dbg, None, None
 
 
@@ -1761,6 +1766,7 @@ class PoseExpFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, tangent):
+        ctx.leaf = tangent.is_leaf and tangent.is_contiguous()
         tangent = tangent.contiguous()
         B = tangent.shape[0]
         mats = torch.empty(B, 3, 4, device=tangent.device)
@@ -1771,10 +1777,12 @@ class PoseExpFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dmats):
         (tangent,) = ctx.saved_tensors
-        dt = torch.empty_like(tangent)
+        # a leaf parameter's gradient is accumulated in place (grad_target: no AccumulateGrad add per step)
+        direct = ctx.leaf and tangent.requires_grad
+        dt = grad_target(tangent) if direct else _zeroed_views([tuple(tangent.shape)], tangent.device)[0]
         _lib.call("mms_pose_exp_bwd", tangent.data_ptr(), dmats.contiguous().data_ptr(), tangent.shape[0],
                   dt.data_ptr(), _s())
-        return dt
+        return None if direct else dt
 
 
 class RaysFunction(torch.autograd.Function):
@@ -2073,7 +2081,8 @@ class HeadsCompositeFunction(torch.autograd.Function):
             else:
                 out = torch.empty(rays if sidx is None else rows, C, device=feat.device)
             _lib.call("mms_composite_fwd", w_c[w0:].data_ptr(), v[sub * S:].data_ptr(), v.stride(0), C,
-                      _p(None if bg is None else bg.contiguous()), rays, S, _p(sidx), out.data_ptr(), _s())
+                      _p(None if bg is None else bg.contiguous()), rays, S, _p(sidx), out.shape[0], out.data_ptr(),
+                      _s())
             outs.append(out)
         ctx.heads, ctx.jobs, ctx.items, ctx.S, ctx.runs, ctx.vals = heads, jobs, items, S, runs, vals
         ctx.n_params = len(params)
@@ -2106,8 +2115,8 @@ class HeadsCompositeFunction(torch.autograd.Function):
             dbg = dout.clone() if bg is not None else None
             dwi = dw[w0:] if dw_direct else torch.empty(rays, S, device=dev)
             _lib.call("mms_composite_bwd", w[w0:].data_ptr(), v[sub * S:].data_ptr(), v.stride(0), C, _p(bg), rays, S,
-                      _p(sidx), dout.contiguous().data_ptr(), dvals[j][sub * S:].data_ptr(), dvals[j].stride(0),
-                      dwi.data_ptr(), _p(dbg), _s())
+                      _p(sidx), dout.shape[0], dout.contiguous().data_ptr(), dvals[j][sub * S:].data_ptr(),
+                      dvals[j].stride(0), dwi.data_ptr(), _p(dbg), _s())
             if not dw_direct:
                 dw[w0:w0 + rays] += dwi
             dbgs[i] = dbg

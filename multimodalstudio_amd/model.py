@@ -821,7 +821,10 @@ class BaseModel(nn.Module):
         vr = self.surface_model.volume_rendering
         w = fx.NeusWeightsFunction.apply(sdf, grads, d_h, deltas, s_param, vr._cos_anneal_ratio, S)
         feat = self.radiance_model.features(pos, d_h, normals.detach(), geo, S)
-        rows = N if cap is None else N + 1     # padded batches scatter into a dummy row N, cut off below
+        # padded batches: the statistics scatter their padding rays into a dummy row N (cut off below); the composite
+        # discards them (mms_composite nout = N), so its outputs need no cut -- no slice in the autograd graph, no
+        # padded copy of the background
+        rows = N if cap is None else N + 1
         if bgs is not cur:
             cur.wait_stream(bgs)
             inv_s.record_stream(cur)
@@ -829,11 +832,8 @@ class BaseModel(nn.Module):
                 bg_out[k].record_stream(cur)    # made on the background stream, read (and freed) on this one
                 if torch.is_grad_enabled() and bg_out[k].requires_grad:
                     bg_out[k] = _JoinBackground.apply(bg_out[k], torch.device(dev).index or 0)
-        bg_in = {}
-        for k, b in bg_out.items():
-            bg_in[k] = b if cap is None else torch.cat([b, b.new_zeros(1, b.shape[1])])
         fg = self._heads_composite(self.radiance_model.modality_heads, mods, own, feat, w, d_h, up_h, S, off[:-1], Rm,
-                                   sidx=sidx_m, bgs=bg_in, rows=rows)
+                                   sidx=sidx_m, bgs=bg_out, rows=N)
         # accumulation / normals / depth renderers (renderers.py:176-242, no grad): one launch pair for all modalities
         stats = _render_stats_segments(w, normals, starts, ends, off, S, sidx_cat, rows, dev)
         geo_batch = {"grads": grads, "hess": hess, "counts": None if cap is None else counts, "seg_rays": seg, "S": S,
@@ -841,7 +841,7 @@ class BaseModel(nn.Module):
         outputs = {}
         for i, mod in enumerate(mods):
             a, b = off[i], off[i + 1]
-            out = {h: v[:N] for (k, h), v in fg.items() if k == i}
+            out = {h: v for (k, h), v in fg.items() if k == i}
             st = stats[i * rows:i * rows + N]
             out["normals"] = st[:, 1:4]
             out["depth"] = st[:, 4:5]

@@ -30,6 +30,9 @@ class Census(TorchDispatchMode):
                 if "multimodalstudio_amd" in fr.filename:
                     site = f"{fr.filename.split('multimodalstudio_amd/')[-1]}:{fr.lineno} {fr.line.strip()[:70]}"
                     break
+            if name.startswith("aten.add"):
+                shapes = [tuple(a.shape) + (a.stride(),) for a in args if isinstance(a, torch.Tensor)]
+                site = f"{site} {shapes}"
             self.ops[(name, site)] += 1
         return func(*args, **(kwargs or {}))
 
