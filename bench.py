@@ -130,6 +130,13 @@ def sdf_panel_work(a):
     return role, float(rows) * (HASH_FWD_B + 4 * (3 + 6 * F))
 
 
+def sdf_panel_rays_work(a):
+    """(role, bytes) of one mms_sdf_panel_rays_fwd launch (the sampler's panels formed from the spacing bins): as
+    sdf_panel_work for its R (nb - 1) rows."""
+    nb, R, F = int(a[2]), int(a[7]), int(a[8])
+    return "sampler", float(R * (nb - 1)) * (HASH_FWD_B + 4 * (3 + 6 * F))
+
+
 def rad_panel_work(a):
     """(role, bytes) of one mms_rad_panel_fwd launch: the hash-grid lookups' SURVEY §8(d) bytes plus the x / SH / n.v
     columns written and the geo feature read and written (4 B each way per column)."""
@@ -145,6 +152,7 @@ def work_fns():
         "mms_mlp_chain": chain_work,
         "mms_hashgrid_fwd_grouped": hash_fwd_work,
         "mms_sdf_panel_fwd": sdf_panel_work,
+        "mms_sdf_panel_rays_fwd": sdf_panel_rays_work,
         "mms_rad_panel_fwd": rad_panel_work,
         "mms_hashgrid_bwd_grouped": lambda a: ("sdf_taps" if a[2] == 5 else "radiance_or_bg",
                                                (float(a[1]) * a[2] * HASH_BWD_B, float(a[1]) * a[2] * HASH_BWD_ATOMIC_B)),

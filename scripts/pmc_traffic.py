@@ -47,11 +47,13 @@ def label(name, grid=0):
     if "hashgrid_bwd" in name:
         # hashgrid_bwd_walk_kernel<GROUP, ...>: the SDF batch walks 5 rows (centre + 4 taps) per thread
         return "mms_hashgrid_bwd_grouped:sdf_taps" if "walk_kernel<5" in name else "mms_hashgrid_bwd_grouped:radiance_or_bg"
-    if "sdf_panel_fwd_kernel<5>" in name:
+    if "sdf_panel_fwd_kernel<5" in name:
         return "mms_sdf_panel_fwd:sdf_taps"
-    if "sdf_panel_fwd_kernel<1>" in name:
+    if "sdf_panel_fwd_kernel<1, true>" in name:
+        return "mms_sdf_panel_rays_fwd:sampler"
+    if "sdf_panel_fwd_kernel<1" in name:
         return "mms_sdf_panel_fwd:sampler"
-    if "rad_panel_fwd_kernel" in name:
+    if "rad_panel_fwd" in name:
         return "mms_rad_panel_fwd:radiance"
     if "hashgrid_fwd_kernel" in name:
         # thread per (point, level): the SDF [centre | 4 taps] batch is the launch with > 200k points
