@@ -250,13 +250,14 @@ int mms_density_weights_bwd(const float* density, int64_t ldd, const float* delt
 /* composite sum_s w c (+ bg (1 - sum w)), scattering compacted rays to rows idx[r] of out [nout, C]
  * (Renderer.render / RadianceRenderer renderers.py:75-174; BackgroundModel sum background_model.py:101-109); a ray
  * with idx[r] >= nout (the padding rays of a fixed-capacity batch) is discarded: no output row, zero gradients.
- * bwd: dvals and dw [R, S] are written (not accumulated); dbg[idx[r]] is overwritten for hit rows (the caller
- * passes dbg = dout, the pass-through gradient of every other row). */
+ * bwd: dvals and dw [R, S] are written (not accumulated); dbg[idx[r]] is written for hit rows.  The other rows:
+ * with hit = null the caller pre-fills out = bg and dbg = dout; with hit [nout] (uint8, the collider's mask: 1 exactly
+ * on the rows some ray of the batch lands on) the same launch writes out = bg / dbg = dout on the rows with hit 0. */
 int mms_composite_fwd(const float* w, const float* vals, int64_t ldv, int C, const float* bg, int64_t R, int S,
-                      const int64_t* idx, int64_t nout, float* out, void* stream);
+                      const int64_t* idx, int64_t nout, const unsigned char* hit, float* out, void* stream);
 int mms_composite_bwd(const float* w, const float* vals, int64_t ldv, int C, const float* bg, int64_t R, int S,
-                      const int64_t* idx, int64_t nout, const float* dout, float* dvals, int64_t lddv, float* dw,
-                      float* dbg, void* stream);
+                      const int64_t* idx, int64_t nout, const unsigned char* hit, const float* dout, float* dvals,
+                      int64_t lddv, float* dw, float* dbg, void* stream);
 /* Accumulation / normals / depth renderers (renderers.py:176-242, no grad) of compacted rays scattered to rows idx[r]:
  * out [rows, ldo >= 5] = (sum w, sum w n, sum w mid) per hit row (other rows untouched), depth clipped to the range of
  * all sample midpoints; range [2] is scratch, (-inf, -inf) on entry. */
@@ -371,6 +372,25 @@ int mms_geo_loss_fwd_masked(const float* grads, const float* hess, int64_t M, in
 int mms_geo_loss_bwd_masked(const float* grads, const float* hess, int64_t M, int S, const int64_t* count,
                             const int64_t* counts_all, int n_counts, const float* deik, float eik_scale,
                             const float* dcurv, float curv_scale, float* dgrads, float* dhess, void* stream);
+
+/* The step loss's terms in one launch each way (StepLossFunction, losses.py:224-265; graph-replayed steps): n_l1 L1
+ * segments (mms_l1_loss_fwd / _bwd of out[i] [N[i], C[i]] (ldo[i]) against tgt[i], SkipSaturation threshold thr[i]
+ * with the first_saturated index first[i] already formed, or null) and n_geo eikonal / curvature segments
+ * (mms_geo_loss_*_masked of grads[j] / hess[j] (rows[j] rows, count[j] or null; 1 / M_total from counts_all, or
+ * inv_total when counts_all is null)); fwd adds into loss[i], eik, curv; bwd adds d / d out into dout[i] (lddo[i]) and
+ * d / d grads, d / d hess (scales: dloss eik_scale, dloss curv_scale) into dgrads[j], dhess[j].  Host arrays of
+ * device pointers, at most 8 segments of each kind; the same arithmetic as the per-segment entry points. */
+int mms_step_loss_fwd(int n_l1, const float* const* out, const int64_t* ldo, const float* const* tgt,
+                      const int64_t* N, const int* C, const float* thr, const unsigned long long* const* first,
+                      float* const* loss, int n_geo, const float* const* grads, const float* const* hess,
+                      const int64_t* rows, int S, const int64_t* const* count, const int64_t* counts_all, int n_counts,
+                      float inv_total, float* eik, float* curv, void* stream);
+int mms_step_loss_bwd(int n_l1, const float* const* out, const int64_t* ldo, const float* const* tgt,
+                      const int64_t* N, const int* C, const float* thr, const unsigned long long* const* first,
+                      float* const* dout, const int64_t* lddo, int n_geo, const float* const* grads,
+                      const float* const* hess, const int64_t* rows, int S, const int64_t* const* count,
+                      const int64_t* counts_all, int n_counts, float inv_total, const float* dloss, float eik_scale,
+                      float curv_scale, float* const* dgrads, float* const* dhess, void* stream);
 
 /* out[0] = sum_i x[i] * w[i] in index order (device x[n], host weights w[n], n <= 16): the total training loss from
  * its terms, LossManager.compute_loss's weighted sum (losses.py:224-265; weights 1 per L1 term, 0.1 eikonal,

@@ -37,16 +37,15 @@ __global__ void first_saturated_kernel(const float* __restrict__ tgt, int64_t n,
 }
 
 // out/tgt are [N, C] with row strides; loss += sum |o - t| / (N C)
-__global__ __launch_bounds__(256) void l1_fwd_kernel(const float* __restrict__ out, int64_t ldo,
-                                                     const float* __restrict__ tgt, int64_t N, int C, float thr,
-                                                     const unsigned long long* __restrict__ first,
-                                                     float* __restrict__ loss) {
+__device__ __forceinline__ void l1_fwd_body(const float* __restrict__ out, int64_t ldo, const float* __restrict__ tgt,
+                                            int64_t N, int C, float thr, const unsigned long long* __restrict__ first,
+                                            float* __restrict__ loss, int64_t blk, int64_t nblk) {
   const int64_t n = N * C;
   float fill = 0.f;
   bool sat = false;
   if (first != nullptr && first[0] < (unsigned long long)n) { sat = true; fill = tgt[first[0]]; }
   float s = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = blk * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
     const int64_t r = i / C, c = i - r * C;
     const float t = tgt[i];
     float o = out[r * ldo + c];
@@ -57,13 +56,21 @@ __global__ __launch_bounds__(256) void l1_fwd_kernel(const float* __restrict__ o
   if (threadIdx.x == 0) atomicAdd(loss, s / (float)n);
 }
 
-__global__ void l1_bwd_kernel(const float* __restrict__ out, int64_t ldo, const float* __restrict__ tgt, int64_t N,
-                              int C, float thr, const unsigned long long* __restrict__ first,
-                              const float* __restrict__ dloss, float scale, float* __restrict__ dout, int64_t lddo) {
+__global__ __launch_bounds__(256) void l1_fwd_kernel(const float* __restrict__ out, int64_t ldo,
+                                                     const float* __restrict__ tgt, int64_t N, int C, float thr,
+                                                     const unsigned long long* __restrict__ first,
+                                                     float* __restrict__ loss) {
+  l1_fwd_body(out, ldo, tgt, N, C, thr, first, loss, blockIdx.x, gridDim.x);
+}
+
+__device__ __forceinline__ void l1_bwd_body(const float* __restrict__ out, int64_t ldo, const float* __restrict__ tgt,
+                                            int64_t N, int C, float thr, const unsigned long long* __restrict__ first,
+                                            const float* __restrict__ dloss, float scale, float* __restrict__ dout,
+                                            int64_t lddo, int64_t blk, int64_t nblk) {
   const int64_t n = N * C;
   const bool sat = first != nullptr && first[0] < (unsigned long long)n;
   const float g = dloss[0] * scale / (float)n;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = blk * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
     const int64_t r = i / C, c = i - r * C;
     const float t = tgt[i];
     const float o = out[r * ldo + c];
@@ -71,6 +78,12 @@ __global__ void l1_bwd_kernel(const float* __restrict__ out, int64_t ldo, const 
     if (sat && t > thr) d = 0.f;  // masked_fill: output replaced by a constant
     dout[r * lddo + c] += d;
   }
+}
+
+__global__ void l1_bwd_kernel(const float* __restrict__ out, int64_t ldo, const float* __restrict__ tgt, int64_t N,
+                              int C, float thr, const unsigned long long* __restrict__ first,
+                              const float* __restrict__ dloss, float scale, float* __restrict__ dout, int64_t lddo) {
+  l1_bwd_body(out, ldo, tgt, N, C, thr, first, dloss, scale, dout, lddo, blockIdx.x, gridDim.x);
 }
 
 // eikonal: sum over rows of (||g|| - 1)^2 / M_total ; curvature: sum |h0 + h1 + h2| / M_total.
@@ -84,15 +97,15 @@ __device__ __forceinline__ float inv_rows(const int64_t* counts_all, int n_count
   return 1.0f / (float)(t > 1 ? t : 1);
 }
 
-__global__ __launch_bounds__(256) void geo_loss_fwd_kernel(const float* __restrict__ grads,
-                                                           const float* __restrict__ hess, int64_t M,
-                                                           const int64_t* __restrict__ count, int S, float inv_total,
-                                                           const int64_t* __restrict__ counts_all, int n_counts,
-                                                           float* __restrict__ eik, float* __restrict__ curv) {
+__device__ __forceinline__ void geo_fwd_body(const float* __restrict__ grads, const float* __restrict__ hess, int64_t M,
+                                             const int64_t* __restrict__ count, int S, float inv_total,
+                                             const int64_t* __restrict__ counts_all, int n_counts,
+                                             float* __restrict__ eik, float* __restrict__ curv, int64_t blk,
+                                             int64_t nblk) {
   const int64_t lim = count ? (count[0] * S < M ? count[0] * S : M) : M;
   const float inv = inv_rows(counts_all, n_counts, S, inv_total);
   float se = 0.f, sc = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = blk * blockDim.x + threadIdx.x; i < lim; i += nblk * blockDim.x) {
     if (grads) {
       const float g0 = grads[i * 3], g1 = grads[i * 3 + 1], g2 = grads[i * 3 + 2];
       const float n = sqrtf(g0 * g0 + g1 * g1 + g2 * g2);
@@ -109,17 +122,26 @@ __global__ __launch_bounds__(256) void geo_loss_fwd_kernel(const float* __restri
   }
 }
 
-__global__ void geo_loss_bwd_kernel(const float* __restrict__ grads, const float* __restrict__ hess, int64_t M,
-                                    const int64_t* __restrict__ count, int S, float inv_total,
-                                    const int64_t* __restrict__ counts_all, int n_counts,
-                                    const float* __restrict__ deik, float eik_scale,
-                                    const float* __restrict__ dcurv, float curv_scale, float* __restrict__ dgrads,
-                                    float* __restrict__ dhess) {
+__global__ __launch_bounds__(256) void geo_loss_fwd_kernel(const float* __restrict__ grads,
+                                                           const float* __restrict__ hess, int64_t M,
+                                                           const int64_t* __restrict__ count, int S, float inv_total,
+                                                           const int64_t* __restrict__ counts_all, int n_counts,
+                                                           float* __restrict__ eik, float* __restrict__ curv) {
+  geo_fwd_body(grads, hess, M, count, S, inv_total, counts_all, n_counts, eik, curv, blockIdx.x, gridDim.x);
+}
+
+__device__ __forceinline__ void geo_bwd_body(const float* __restrict__ grads, const float* __restrict__ hess, int64_t M,
+                                             const int64_t* __restrict__ count, int S, float inv_total,
+                                             const int64_t* __restrict__ counts_all, int n_counts,
+                                             const float* __restrict__ deik, float eik_scale,
+                                             const float* __restrict__ dcurv, float curv_scale,
+                                             float* __restrict__ dgrads, float* __restrict__ dhess, int64_t blk,
+                                             int64_t nblk) {
   const int64_t lim = count ? (count[0] * S < M ? count[0] * S : M) : M;
   const float inv = inv_rows(counts_all, n_counts, S, inv_total);
   const float ge = deik ? deik[0] * eik_scale * inv : 0.f;
   const float gc = dcurv ? dcurv[0] * curv_scale * inv : 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = blk * blockDim.x + threadIdx.x; i < lim; i += nblk * blockDim.x) {
     if (grads && dgrads && deik) {
       const float g0 = grads[i * 3], g1 = grads[i * 3 + 1], g2 = grads[i * 3 + 2];
       const float n = sqrtf(g0 * g0 + g1 * g1 + g2 * g2);
@@ -135,6 +157,78 @@ __global__ void geo_loss_bwd_kernel(const float* __restrict__ grads, const float
       dhess[i * 3 + 1] += d;
       dhess[i * 3 + 2] += d;
     }
+  }
+}
+
+__global__ void geo_loss_bwd_kernel(const float* __restrict__ grads, const float* __restrict__ hess, int64_t M,
+                                    const int64_t* __restrict__ count, int S, float inv_total,
+                                    const int64_t* __restrict__ counts_all, int n_counts,
+                                    const float* __restrict__ deik, float eik_scale,
+                                    const float* __restrict__ dcurv, float curv_scale, float* __restrict__ dgrads,
+                                    float* __restrict__ dhess) {
+  geo_bwd_body(grads, hess, M, count, S, inv_total, counts_all, n_counts, deik, eik_scale, dcurv, curv_scale, dgrads,
+               dhess, blockIdx.x, gridDim.x);
+}
+
+// The step loss's L1 terms and geometric terms in ONE launch each way (graph-replayed steps: every launch boundary
+// costs ~4-5 us): segment k owns blocks [b0[k], b0[k + 1]) -- the blocks its own launch would have had -- and runs
+// that launch's body (mms_l1_loss_* / mms_geo_loss_*_masked, same arithmetic).
+constexpr int kMaxLossSeg = 8;
+struct LossSegs {
+  int n_l1, n_geo;
+  int b0[2 * kMaxLossSeg + 1];
+  const float* out[kMaxLossSeg];
+  int64_t ldo[kMaxLossSeg];
+  const float* tgt[kMaxLossSeg];
+  int64_t N[kMaxLossSeg];
+  int C[kMaxLossSeg];
+  float thr[kMaxLossSeg];
+  const unsigned long long* first[kMaxLossSeg];
+  float* l1[kMaxLossSeg];          // fwd: the term; bwd: dout
+  int64_t lddo[kMaxLossSeg];
+  const float* grads[kMaxLossSeg];
+  const float* hess[kMaxLossSeg];
+  float* dgrads[kMaxLossSeg];
+  float* dhess[kMaxLossSeg];
+  int64_t rows[kMaxLossSeg];
+  const int64_t* count[kMaxLossSeg];
+  const int64_t* counts_all;
+  int n_counts, S;
+  float inv_total;
+  float* eik;
+  float* curv;
+  const float* dloss;
+  float eik_scale, curv_scale;
+};
+
+__device__ __forceinline__ int loss_seg_of(const LossSegs& a, int b) {
+  int k = 0;
+  while (k + 1 < a.n_l1 + a.n_geo && b >= a.b0[k + 1]) ++k;
+  return k;
+}
+
+__global__ __launch_bounds__(256) void step_loss_fwd_kernel(LossSegs a) {
+  const int k = loss_seg_of(a, blockIdx.x);
+  const int64_t blk = blockIdx.x - a.b0[k], nblk = a.b0[k + 1] - a.b0[k];
+  if (k < a.n_l1)
+    l1_fwd_body(a.out[k], a.ldo[k], a.tgt[k], a.N[k], a.C[k], a.thr[k], a.first[k], a.l1[k], blk, nblk);
+  else {
+    const int j = k - a.n_l1;
+    geo_fwd_body(a.grads[j], a.hess[j], a.rows[j], a.count[j], a.S, a.inv_total, a.counts_all, a.n_counts, a.eik,
+                 a.curv, blk, nblk);
+  }
+}
+
+__global__ __launch_bounds__(256) void step_loss_bwd_kernel(LossSegs a) {
+  const int k = loss_seg_of(a, blockIdx.x);
+  const int64_t blk = blockIdx.x - a.b0[k], nblk = a.b0[k + 1] - a.b0[k];
+  if (k < a.n_l1)
+    l1_bwd_body(a.out[k], a.ldo[k], a.tgt[k], a.N[k], a.C[k], a.thr[k], a.first[k], a.dloss, 1.0f, a.l1[k],
+                a.lddo[k], blk, nblk);
+  else {
+    const int j = k - a.n_l1;
+    geo_bwd_body(a.grads[j], a.hess[j], a.rows[j], a.count[j], a.S, a.inv_total, a.counts_all, a.n_counts, a.dloss,
+                 a.eik_scale, a.dloss, a.curv_scale, a.dgrads[j], a.dhess[j], blk, nblk);
   }
 }
 
@@ -372,6 +466,81 @@ MMS_EXPORT int mms_geo_loss_bwd_masked(const float* grads, const float* hess, in
   hipLaunchKernelGGL(geo_loss_bwd_kernel, dim3(mms::grid_for(M, 256, 8192)), dim3(256), 0, mms::as_stream(stream),
                      grads, hess, M, count, S, 0.f, counts_all, n_counts, deik, eik_scale, dcurv, curv_scale, dgrads,
                      dhess);
+  return mms::check_launch(fn);
+}
+
+// the shared argument table of mms_step_loss_fwd / _bwd (block counts as the per-launch entry points size them)
+static int fill_loss_segs(const char* fn, LossSegs& a, int n_l1, const float* const* out, const int64_t* ldo,
+                          const float* const* tgt, const int64_t* N, const int* C, const float* thr,
+                          const unsigned long long* const* first, int n_geo, const float* const* grads,
+                          const float* const* hess, const int64_t* rows, int S, const int64_t* const* count,
+                          const int64_t* counts_all, int n_counts, float inv_total, int l1_grid, int geo_grid) {
+  MMS_REQUIRE(n_l1 >= 0 && n_l1 <= kMaxLossSeg && n_geo >= 0 && n_geo <= kMaxLossSeg && n_l1 + n_geo >= 1, fn,
+              "0 to 8 L1 and 0 to 8 geometric segments");
+  MMS_REQUIRE(n_l1 == 0 || (out && ldo && tgt && N && C && thr && first), fn, "null L1 segment table");
+  MMS_REQUIRE(n_geo == 0 || (grads && hess && rows && count), fn, "null geometric segment table");
+  a.n_l1 = n_l1;
+  a.n_geo = n_geo;
+  a.b0[0] = 0;
+  int k = 0;
+  for (int i = 0; i < n_l1; ++i, ++k) {
+    a.out[i] = out[i]; a.ldo[i] = ldo[i]; a.tgt[i] = tgt[i]; a.N[i] = N[i]; a.C[i] = C[i]; a.thr[i] = thr[i];
+    a.first[i] = first[i];
+    const int64_t n = N[i] * C[i];
+    a.b0[k + 1] = a.b0[k] + (n > 0 ? (int)mms::grid_for(n, 256, l1_grid) : 0);
+  }
+  for (int j = 0; j < n_geo; ++j, ++k) {
+    a.grads[j] = grads[j]; a.hess[j] = hess[j]; a.rows[j] = rows[j]; a.count[j] = count[j];
+    a.b0[k + 1] = a.b0[k] + (rows[j] > 0 ? (int)mms::grid_for(rows[j], 256, geo_grid) : 0);
+  }
+  a.counts_all = counts_all;
+  a.n_counts = n_counts;
+  a.S = S;
+  a.inv_total = inv_total;
+  return 0;
+}
+
+MMS_EXPORT int mms_step_loss_fwd(int n_l1, const float* const* out, const int64_t* ldo, const float* const* tgt,
+                                 const int64_t* N, const int* C, const float* thr,
+                                 const unsigned long long* const* first, float* const* loss, int n_geo,
+                                 const float* const* grads, const float* const* hess, const int64_t* rows, int S,
+                                 const int64_t* const* count, const int64_t* counts_all, int n_counts, float inv_total,
+                                 float* eik, float* curv, void* stream) {
+  const char* fn = "mms_step_loss_fwd";
+  LossSegs a{};
+  int rc = fill_loss_segs(fn, a, n_l1, out, ldo, tgt, N, C, thr, first, n_geo, grads, hess, rows, S, count,
+                          counts_all, n_counts, inv_total, 1024, 1024);
+  if (rc) return rc;
+  MMS_REQUIRE(n_l1 == 0 || loss, fn, "null loss terms");
+  for (int i = 0; i < n_l1; ++i) a.l1[i] = loss[i];
+  a.eik = eik;
+  a.curv = curv;
+  if (a.b0[n_l1 + n_geo] == 0) return 0;
+  hipLaunchKernelGGL(step_loss_fwd_kernel, dim3(a.b0[n_l1 + n_geo]), dim3(256), 0, mms::as_stream(stream), a);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_step_loss_bwd(int n_l1, const float* const* out, const int64_t* ldo, const float* const* tgt,
+                                 const int64_t* N, const int* C, const float* thr,
+                                 const unsigned long long* const* first, float* const* dout, const int64_t* lddo,
+                                 int n_geo, const float* const* grads, const float* const* hess, const int64_t* rows,
+                                 int S, const int64_t* const* count, const int64_t* counts_all, int n_counts,
+                                 float inv_total, const float* dloss, float eik_scale, float curv_scale,
+                                 float* const* dgrads, float* const* dhess, void* stream) {
+  const char* fn = "mms_step_loss_bwd";
+  LossSegs a{};
+  int rc = fill_loss_segs(fn, a, n_l1, out, ldo, tgt, N, C, thr, first, n_geo, grads, hess, rows, S, count,
+                          counts_all, n_counts, inv_total, 4096, 8192);
+  if (rc) return rc;
+  MMS_REQUIRE(dloss != nullptr && (n_l1 == 0 || (dout && lddo)) && (n_geo == 0 || (dgrads && dhess)), fn,
+              "null gradient table");
+  for (int i = 0; i < n_l1; ++i) { a.l1[i] = dout[i]; a.lddo[i] = lddo[i]; }
+  for (int j = 0; j < n_geo; ++j) { a.dgrads[j] = dgrads[j]; a.dhess[j] = dhess[j]; }
+  a.dloss = dloss;
+  a.eik_scale = eik_scale;
+  a.curv_scale = curv_scale;
+  if (a.b0[n_l1 + n_geo] == 0) return 0;
+  hipLaunchKernelGGL(step_loss_bwd_kernel, dim3(a.b0[n_l1 + n_geo]), dim3(256), 0, mms::as_stream(stream), a);
   return mms::check_launch(fn);
 }
 

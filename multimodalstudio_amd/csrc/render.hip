@@ -214,7 +214,16 @@ __global__ __launch_bounds__(256) void density_weights_bwd_kernel(const float* _
 __global__ __launch_bounds__(256) void composite_fwd_kernel(const float* __restrict__ w, const float* __restrict__ vals,
                                                             int64_t ldv, int C, const float* __restrict__ bg,
                                                             int64_t R, int S, const int64_t* __restrict__ idx,
-                                                            int64_t nout, float* __restrict__ out) {
+                                                            int64_t nout, const unsigned char* __restrict__ hit,
+                                                            unsigned cblocks, float* __restrict__ out) {
+  if (blockIdx.x >= cblocks) {
+    // the rows no ray of the batch lands on keep the background (instead of a copy of it made before the launch)
+    const int64_t n = nout * C;
+    for (int64_t e = (int64_t)(blockIdx.x - cblocks) * blockDim.x + threadIdx.x; e < n;
+         e += (int64_t)(gridDim.x - cblocks) * blockDim.x)
+      if (!hit[e / C]) out[e] = bg[e];
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const int64_t ray = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (ray >= R) return;
@@ -238,9 +247,18 @@ __global__ __launch_bounds__(256) void composite_fwd_kernel(const float* __restr
 __global__ __launch_bounds__(256) void composite_bwd_kernel(const float* __restrict__ w, const float* __restrict__ vals,
                                                             int64_t ldv, int C, const float* __restrict__ bg,
                                                             int64_t R, int S, const int64_t* __restrict__ idx,
-                                                            int64_t nout, const float* __restrict__ dout,
+                                                            int64_t nout, const unsigned char* __restrict__ hit,
+                                                            unsigned cblocks, const float* __restrict__ dout,
                                                             float* __restrict__ dvals, int64_t lddv,
                                                             float* __restrict__ dw, float* __restrict__ dbg) {
+  if (blockIdx.x >= cblocks) {
+    // the background's pass-through gradient on the rows no ray of the batch lands on
+    const int64_t n = nout * C;
+    for (int64_t e = (int64_t)(blockIdx.x - cblocks) * blockDim.x + threadIdx.x; e < n;
+         e += (int64_t)(gridDim.x - cblocks) * blockDim.x)
+      if (!hit[e / C]) dbg[e] = dout[e];
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const int64_t ray = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (ray >= R) return;
@@ -458,12 +476,16 @@ MMS_EXPORT int mms_density_weights_bwd(const float* density, int64_t ldd, const 
 }
 
 MMS_EXPORT int mms_composite_fwd(const float* w, const float* vals, int64_t ldv, int C, const float* bg, int64_t R,
-                                 int S, const int64_t* idx, int64_t nout, float* out, void* stream) {
+                                 int S, const int64_t* idx, int64_t nout, const unsigned char* hit, float* out,
+                                 void* stream) {
   const char* fn = "mms_composite_fwd";
   MMS_REQUIRE(S >= 1 && S <= 64, fn, "samples per ray must be in [1, 64]");
-  if (R == 0) return 0;
-  hipLaunchKernelGGL(composite_fwd_kernel, dim3(mms::grid_for(R * 64, 256, INT32_MAX)), dim3(256), 0,
-                     mms::as_stream(stream), w, vals, ldv, C, bg, R, S, idx, nout, out);
+  MMS_REQUIRE(hit == nullptr || (bg != nullptr && idx != nullptr), fn, "hit rows need a background and a scatter index");
+  const unsigned cb = R > 0 ? mms::grid_for(R * 64, 256, INT32_MAX) : 0;
+  const unsigned pb = hit != nullptr && nout > 0 ? mms::grid_for(nout * C, 256, 4096) : 0;
+  if (cb + pb == 0) return 0;
+  hipLaunchKernelGGL(composite_fwd_kernel, dim3(cb + pb), dim3(256), 0, mms::as_stream(stream), w, vals, ldv, C, bg, R,
+                     S, idx, nout, hit, cb, out);
   return mms::check_launch(fn);
 }
 
@@ -483,12 +505,15 @@ MMS_EXPORT int mms_render_stats(const float* w, const float* normals, const floa
 }
 
 MMS_EXPORT int mms_composite_bwd(const float* w, const float* vals, int64_t ldv, int C, const float* bg, int64_t R,
-                                 int S, const int64_t* idx, int64_t nout, const float* dout, float* dvals, int64_t lddv,
-                                 float* dw, float* dbg, void* stream) {
+                                 int S, const int64_t* idx, int64_t nout, const unsigned char* hit, const float* dout,
+                                 float* dvals, int64_t lddv, float* dw, float* dbg, void* stream) {
   const char* fn = "mms_composite_bwd";
   MMS_REQUIRE(S >= 1 && S <= 64, fn, "samples per ray must be in [1, 64]");
-  if (R == 0) return 0;
-  hipLaunchKernelGGL(composite_bwd_kernel, dim3(mms::grid_for(R * 64, 256, INT32_MAX)), dim3(256), 0,
-                     mms::as_stream(stream), w, vals, ldv, C, bg, R, S, idx, nout, dout, dvals, lddv, dw, dbg);
+  MMS_REQUIRE(hit == nullptr || (bg != nullptr && idx != nullptr), fn, "hit rows need a background and a scatter index");
+  const unsigned cb = R > 0 ? mms::grid_for(R * 64, 256, INT32_MAX) : 0;
+  const unsigned pb = hit != nullptr && dbg != nullptr && nout > 0 ? mms::grid_for(nout * C, 256, 4096) : 0;
+  if (cb + pb == 0) return 0;
+  hipLaunchKernelGGL(composite_bwd_kernel, dim3(cb + pb), dim3(256), 0, mms::as_stream(stream), w, vals, ldv, C, bg, R,
+                     S, idx, nout, hit, cb, dout, dvals, lddv, dw, dbg);
   return mms::check_launch(fn);
 }

@@ -1655,7 +1655,7 @@ class CompositeFunction(torch.autograd.Function):
             out = torch.empty(R, C, device=w.device)
             bgc = None
         _lib.call("mms_composite_fwd", w.data_ptr(), vals.data_ptr(), C, C, _p(bgc), R, S, _p(idx), out.shape[0],
-                  out.data_ptr(), _s())
+                  None, out.data_ptr(), _s())
         ctx.save_for_backward(w, vals, bgc, idx)
         ctx.S = S
         ctx.has_bg = bg is not None
@@ -1671,7 +1671,7 @@ class CompositeFunction(torch.autograd.Function):
         dw = torch.empty_like(w)                 # every weight written by the kernel
         dbg = dout.clone() if ctx.has_bg else None
         _lib.call("mms_composite_bwd", w.data_ptr(), vals.data_ptr(), C, C, _p(bgc), R, S, _p(idx), dout.shape[0],
-                  dout.data_ptr(), _p(dvals), C, dw.data_ptr(), _p(dbg), _s())
+                  None, dout.data_ptr(), _p(dvals), C, dw.data_ptr(), _p(dbg), _s())
         return dw, dvals, dbg, None, None
 
 
@@ -2073,16 +2073,18 @@ class HeadsCompositeFunction(torch.autograd.Function):
             vals.append(v)
         w_c = w.contiguous()
         outs = []
-        for (j, sub, rays, w0, sidx, rows), bg in zip(items, bgs):
+        for (j, sub, rays, w0, sidx, rows, hit), bg in zip(items, bgs):
             v = vals[j]
             C = v.shape[1]
+            hit = hit if bg is not None and sidx is not None else None
             if bg is not None:
-                out = bg.detach().clone().contiguous()
+                # with the hit mask the launch itself keeps the background on the rows no ray lands on
+                out = torch.empty(bg.shape, device=bg.device) if hit is not None else bg.detach().clone().contiguous()
             else:
                 out = torch.empty(rays if sidx is None else rows, C, device=feat.device)
             _lib.call("mms_composite_fwd", w_c[w0:].data_ptr(), v[sub * S:].data_ptr(), v.stride(0), C,
-                      _p(None if bg is None else bg.contiguous()), rays, S, _p(sidx), out.shape[0], out.data_ptr(),
-                      _s())
+                      _p(None if bg is None else bg.contiguous()), rays, S, _p(sidx), out.shape[0], _p(hit),
+                      out.data_ptr(), _s())
             outs.append(out)
         ctx.heads, ctx.jobs, ctx.items, ctx.S, ctx.runs, ctx.vals = heads, jobs, items, S, runs, vals
         ctx.n_params = len(params)
@@ -2103,7 +2105,7 @@ class HeadsCompositeFunction(torch.autograd.Function):
         dw_direct = _partitions(w_ranges, R)
         dvals = [None] * len(jobs)
         dbgs = [None] * len(items)
-        for i, ((j, sub, rays, w0, sidx, rows), dout) in enumerate(zip(items, douts)):
+        for i, ((j, sub, rays, w0, sidx, rows, hit), dout) in enumerate(zip(items, douts)):
             if dout is None:
                 continue
             v = ctx.vals[j]
@@ -2112,10 +2114,12 @@ class HeadsCompositeFunction(torch.autograd.Function):
                 dvals[j] = _alloc(v.shape[0], C, dev) if _job_covered(j, items, live) else \
                     _zeroed_views([(v.shape[0], (C + 3) // 4 * 4)], dev)[0][:, :C]
             bg = bgs[i]
-            dbg = dout.clone() if bg is not None else None
+            hit = hit if bg is not None and sidx is not None else None
+            dout = dout.contiguous()
+            dbg = None if bg is None else (torch.empty(dout.shape, device=dev) if hit is not None else dout.clone())
             dwi = dw[w0:] if dw_direct else torch.empty(rays, S, device=dev)
             _lib.call("mms_composite_bwd", w[w0:].data_ptr(), v[sub * S:].data_ptr(), v.stride(0), C, _p(bg), rays, S,
-                      _p(sidx), dout.shape[0], dout.contiguous().data_ptr(), dvals[j][sub * S:].data_ptr(),
+                      _p(sidx), dout.shape[0], _p(hit), dout.data_ptr(), dvals[j][sub * S:].data_ptr(),
                       dvals[j].stride(0), dwi.data_ptr(), _p(dbg), _s())
             if not dw_direct:
                 dw[w0:w0 + rays] += dwi
@@ -2255,6 +2259,10 @@ class StepLossFunction(torch.autograd.Function):
         # carved from the step's zero arena in a captured step (its outputs are the graph's static buffers anyway,
         # valid until the next replay); eager steps return buffers of their own
         terms = _zeroed_views([(n_mod + 2,)], dev)[0] if _capturing(dev) else torch.zeros(n_mod + 2, device=dev)
+        ctx.fused = FUSED_STEP_LOSS and all(t is None for t in sat_thrs) and n_mod <= 8
+        if ctx.fused:
+            return StepLossFunction._forward_fused(ctx, n_mod, w_curv, S, counts, seg_rays, grads, hess, outs,
+                                                   targets, terms, dev)
         saved, scr = [], []
         for i in range(n_mod):
             o, t = outs[i], targets[i].contiguous()
@@ -2291,6 +2299,70 @@ class StepLossFunction(torch.autograd.Function):
         return total, terms
 
     @staticmethod
+    def _geo_segs(g, h, counts, seg_rays: int, S: int):
+        """(grads, hess, rows, count) per geometric segment, counts_all, n_counts, inv_total."""
+        M = g.shape[0]
+        if counts is None:
+            return [(g, h, M, None)], None, 0, 1.0 / float(max(M, 1))
+        n = counts.shape[0]
+        rows = seg_rays * S
+        return [(g[m * rows:], None if h is None else h[m * rows:], rows, counts[m:]) for m in range(n)], counts, n, 0.0
+
+    @staticmethod
+    def _forward_fused(ctx, n_mod, w_curv, S, counts, seg_rays, grads, hess, outs, targets, terms, dev):
+        """forward's terms by mms_step_loss_fwd (one launch for every L1 and geometric segment; no SkipSaturation)."""
+        ol = [o if o.stride(1) == 1 else o.contiguous() for o in outs]
+        tl = [t.contiguous() for t in targets]
+        g = grads.reshape(-1, 3).contiguous()
+        h = hess.reshape(-1, 3).contiguous() if hess is not None else None
+        segs, call, nc, inv = StepLossFunction._geo_segs(g, h, counts, seg_rays, S)
+        n, ng = n_mod, len(segs)
+        VP, I64 = ctypes.c_void_p, ctypes.c_int64
+        _lib.call("mms_step_loss_fwd", n, (VP * n)(*[o.data_ptr() for o in ol]), (I64 * n)(*[o.stride(0) for o in ol]),
+                  (VP * n)(*[t.data_ptr() for t in tl]), (I64 * n)(*[t.shape[0] for t in tl]),
+                  (ctypes.c_int * n)(*[t.shape[1] for t in tl]), (ctypes.c_float * n)(*([0.0] * n)),
+                  (VP * n)(*([None] * n)), (VP * n)(*[terms[i:].data_ptr() for i in range(n)]), ng,
+                  (VP * ng)(*[sg[0].data_ptr() for sg in segs]), (VP * ng)(*[_p(sg[1]) for sg in segs]),
+                  (I64 * ng)(*[sg[2] for sg in segs]), S, (VP * ng)(*[_p(sg[3]) for sg in segs]), _p(call), nc, inv,
+                  terms[n_mod:].data_ptr(), terms[n_mod + 1:].data_ptr(), _s())
+        w = [1.0] * n_mod + [0.1] + ([float(w_curv)] if h is not None else [])
+        total = torch.empty((), device=dev)
+        _lib.call("mms_weighted_sum", terms.data_ptr(), len(w), _f32arr(w), total.data_ptr(), _s())
+        ctx.mark_non_differentiable(terms)
+        ctx.save_for_backward(g, h, counts, *[x for pair in zip(ol, tl) for x in pair])
+        ctx.n_mod, ctx.scr, ctx.w_curv, ctx.S, ctx.seg_rays = n_mod, None, float(w_curv), S, seg_rays
+        ctx.shape = (tuple(grads.shape), None if hess is None else tuple(hess.shape))
+        ctx.out_shapes = [tuple(o.shape) for o in outs]
+        return total, terms
+
+    @staticmethod
+    def _backward_fused(ctx, dl, g, h, counts, saved):
+        n_mod, dev, S = ctx.n_mod, g.device, ctx.S
+        douts = [_zeroed_views([ctx.out_shapes[i]], dev)[0] for i in range(n_mod)]
+        M = g.shape[0]
+        dh = _zeroed_views([(M, 3)], dev)[0] if h is not None else None
+        dg = acc_or_zeroed(ctx.acc_g, (M, 3), dev).view(M, 3)
+        segs, call, nc, inv = StepLossFunction._geo_segs(g, h, counts, ctx.seg_rays, S)
+        rows = [sg[2] for sg in segs]
+        offs = [0]
+        for r in rows[:-1]:
+            offs.append(offs[-1] + r)
+        ol, tl = saved[0::2], saved[1::2]
+        n, ng = n_mod, len(segs)
+        VP, I64 = ctypes.c_void_p, ctypes.c_int64
+        _lib.call("mms_step_loss_bwd", n, (VP * n)(*[o.data_ptr() for o in ol]), (I64 * n)(*[o.stride(0) for o in ol]),
+                  (VP * n)(*[t.data_ptr() for t in tl]), (I64 * n)(*[t.shape[0] for t in tl]),
+                  (ctypes.c_int * n)(*[t.shape[1] for t in tl]), (ctypes.c_float * n)(*([0.0] * n)),
+                  (VP * n)(*([None] * n)), (VP * n)(*[d.data_ptr() for d in douts]),
+                  (I64 * n)(*[d.stride(0) for d in douts]), ng, (VP * ng)(*[sg[0].data_ptr() for sg in segs]),
+                  (VP * ng)(*[_p(sg[1]) for sg in segs]), (I64 * ng)(*rows), S, (VP * ng)(*[_p(sg[3]) for sg in segs]),
+                  _p(call), nc, inv, dl.data_ptr(), 0.1, ctx.w_curv, (VP * ng)(*[dg[o:].data_ptr() for o in offs]),
+                  (VP * ng)(*[(None if dh is None else dh[o:].data_ptr()) for o in offs]), _s())
+        gs, hs = ctx.shape
+        return (None, None, None, None, None, None, acc_ret(ctx.acc_g, dg.view(gs)),
+                (dh.view(hs) if dh is not None else None), *douts, *([None] * n_mod))
+
+    @staticmethod
     def backward(ctx, dtotal, dterms):
         g, h, counts, *saved = ctx.saved_tensors
         n_mod = ctx.n_mod
@@ -2298,6 +2370,8 @@ class StepLossFunction(torch.autograd.Function):
         if dtotal is None:
             return (None,) * (8 + 2 * n_mod)
         dl = dtotal.contiguous()
+        if ctx.fused:
+            return StepLossFunction._backward_fused(ctx, dl, g, h, counts, saved)
         douts = []
         for i in range(n_mod):
             o, t = saved[2 * i], saved[2 * i + 1]
@@ -2325,6 +2399,11 @@ class StepLossFunction(torch.autograd.Function):
         ctx.scr = None
         return (None, None, None, None, None, None, acc_ret(ctx.acc_g, dg.view(gs)),
                 (dh.view(hs) if dh is not None else None), *douts, *([None] * n_mod))
+
+
+# the step loss's L1 and geometric terms in one launch each way (mms_step_loss_fwd / _bwd) when no modality uses the
+# SkipSaturation fill; MMS_FUSED_STEP_LOSS=0: one launch per term and segment
+FUSED_STEP_LOSS = os.environ.get("MMS_FUSED_STEP_LOSS", "1") != "0"
 
 
 def HashGridApply(x, table, cfg: GridCfg, active: int):

@@ -833,7 +833,7 @@ class BaseModel(nn.Module):
                 if torch.is_grad_enabled() and bg_out[k].requires_grad:
                     bg_out[k] = _JoinBackground.apply(bg_out[k], torch.device(dev).index or 0)
         fg = self._heads_composite(self.radiance_model.modality_heads, mods, own, feat, w, d_h, up_h, S, off[:-1], Rm,
-                                   sidx=sidx_m, bgs=bg_out, rows=N)
+                                   sidx=sidx_m, bgs=bg_out, rows=N, hits=[mask[i * N:(i + 1) * N] for i in range(nm)])
         # accumulation / normals / depth renderers (renderers.py:176-242, no grad): one launch pair for all modalities
         stats = _render_stats_segments(w, normals, starts, ends, off, S, sidx_cat, rows, dev)
         geo_batch = {"grads": grads, "hess": hess, "counts": None if cap is None else counts, "seg_rays": seg, "S": S,
@@ -858,7 +858,7 @@ class BaseModel(nn.Module):
         return outputs, drew
 
     def _heads_composite(self, heads: nn.ModuleDict, mods, own: bool, feat, w, dirs, ups, S: int, seg_off, seg_rays,
-                         sidx=None, bgs=None, rows=None):
+                         sidx=None, bgs=None, rows=None, hits=None):
         """Every (modality segment, head) output of one branch through HeadsCompositeFunction: {(segment, head name):
         [rows, C]}.  With gradients each pair is a job of its own (its head's backward covers exactly its rows);
         without (evaluation) each head runs once over the whole batch and the pairs composite slices of it."""
@@ -888,7 +888,8 @@ class BaseModel(nn.Module):
                     jobs.append((hid, 0, sum(seg_rays)))
                     job_of_head[hid] = len(jobs) - 1
                 j, sub = job_of_head[hid], seg_off[i]
-            items.append((j, sub, seg_rays[i], seg_off[i], None if sidx is None else sidx[i], rows))
+            items.append((j, sub, seg_rays[i], seg_off[i], None if sidx is None else sidx[i], rows,
+                          None if hits is None else hits[i]))
             bg_list.append(bg)
             keys.append((i, h))
         if items:
