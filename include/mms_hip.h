@@ -260,12 +260,12 @@ int mms_composite_bwd(const float* w, const float* vals, int64_t ldv, int C, con
                       int64_t lddv, float* dw, float* dbg, void* stream);
 /* Accumulation / normals / depth renderers (renderers.py:176-242, no grad) of compacted rays scattered to rows idx[r]:
  * out [rows, ldo >= 5] = (sum w, sum w n, sum w mid) per hit row (other rows untouched), depth clipped to the range of
- * all sample midpoints; range [2] is scratch, (-inf, -inf) on entry. */
+ * all sample midpoints; range [2] is scratch (order-preserving unsigned images of the extremes), zeros on entry. */
 int mms_render_stats(const float* w, const float* normals, const float* starts, const float* ends, int64_t R, int S,
                      const int64_t* idx, float* out, int64_t ldo, float* range, void* stream);
 /* the same for every modality of a batched hit set in one launch pair: segment m = rays [seg_off[m], seg_off[m+1])
  * (seg_off: HOST array of n_seg + 1 <= 9 offsets), its rays scatter to out rows m * seg_rows + sidx[r] (sidx: the
- * ray's row within its modality) and its depth clips to its own midpoint range (range [2 n_seg], (-inf, -inf) on
+ * ray's row within its modality) and its depth clips to its own midpoint range (range [2 n_seg] scratch, zeros on
  * entry) -- one DepthRenderer call per modality's RayBundle (renderers.py:205-214, base_model.py:146-159). */
 int mms_render_stats_segments(const float* w, const float* normals, const float* starts, const float* ends, int n_seg,
                               const int64_t* seg_off, int S, const int64_t* sidx, float* out, int64_t ldo,

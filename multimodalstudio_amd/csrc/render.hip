@@ -284,8 +284,17 @@ __global__ __launch_bounds__(256) void composite_bwd_kernel(const float* __restr
 // Accumulation / normals / depth renderers (renderers.py:176-242) for compacted rays scattered to rows idx[r]:
 // acc = sum_s w, nrm = sum_s w n, dep = sum_s w (start + end) / 2, and the depth's clip range: the min / max of all
 // sample midpoints (torch.clip(depth, steps.min(), steps.max()), renderers.py:205-214) reduced into range[2] by
-// float atomics (order-independent: min / max are exact) as range = (max(-mid), max(mid)); range must hold
-// (-inf, -inf) before the launch.
+// atomics (order-independent: min / max are exact) as range = (max(-mid), max(mid)), each kept as the order-preserving
+// unsigned image of the float (ord_f32), so a zeroed range (the step's zero arena, no fill launch) is below every
+// value; range must hold zeros before the launch.
+__device__ __forceinline__ unsigned ord_f32(float x) {
+  const unsigned u = __float_as_uint(x);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f32(unsigned u) {
+  if (u == 0u) return -INFINITY;   // nothing reduced: as the -inf the float form started from
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
 __global__ __launch_bounds__(256) void render_stats_kernel(const float* __restrict__ w, const float* __restrict__ nrm,
                                                            const float* __restrict__ starts,
                                                            const float* __restrict__ ends, int64_t R, int S,
@@ -324,8 +333,8 @@ __global__ __launch_bounds__(256) void render_stats_kernel(const float* __restri
     lo = fminf(fminf(sl[0], sl[1]), fminf(sl[2], sl[3]));
     hi = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
     if (lo <= hi) {
-      atomicMax(range, -lo);
-      atomicMax(range + 1, hi);
+      atomicMax(reinterpret_cast<unsigned*>(range), ord_f32(-lo));
+      atomicMax(reinterpret_cast<unsigned*>(range) + 1, ord_f32(hi));
     }
   }
 }
@@ -336,7 +345,8 @@ __global__ void render_clip_kernel(int64_t R, const int64_t* __restrict__ idx, f
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   float* d = out + (idx ? idx[r] : r) * ldo + 4;
-  d[0] = fminf(fmaxf(d[0], -range[0]), range[1]);
+  const unsigned* ur = reinterpret_cast<const unsigned*>(range);
+  d[0] = fminf(fmaxf(d[0], -unord_f32(ur[0])), unord_f32(ur[1]));
 }
 
 // Every modality's statistics in one launch pair: segment m (blockIdx.y) holds the rays [off[m], off[m + 1]) of the
@@ -388,8 +398,8 @@ __global__ __launch_bounds__(256) void render_stats_seg_kernel(const float* __re
     lo = fminf(fminf(sl[0], sl[1]), fminf(sl[2], sl[3]));
     hi = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
     if (lo <= hi) {
-      atomicMax(range + 2 * seg, -lo);
-      atomicMax(range + 2 * seg + 1, hi);
+      atomicMax(reinterpret_cast<unsigned*>(range) + 2 * seg, ord_f32(-lo));
+      atomicMax(reinterpret_cast<unsigned*>(range) + 2 * seg + 1, ord_f32(hi));
     }
   }
 }
@@ -400,7 +410,8 @@ __global__ void render_clip_seg_kernel(SegOff so, const int64_t* __restrict__ si
   const int64_t r = so.off[seg] + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= so.off[seg + 1]) return;
   float* d = out + (seg * seg_rows + sidx[r]) * ldo + 4;
-  d[0] = fminf(fmaxf(d[0], -range[2 * seg]), range[2 * seg + 1]);
+  const unsigned* ur = reinterpret_cast<const unsigned*>(range);
+  d[0] = fminf(fmaxf(d[0], -unord_f32(ur[2 * seg])), unord_f32(ur[2 * seg + 1]));
 }
 
 }  // namespace

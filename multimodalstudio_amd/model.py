@@ -338,8 +338,7 @@ def _render_stats(w, normals, starts, ends, R: int, S: int, sidx, rows: int, dev
     is clipped to the min / max of all sample midpoints as DepthRenderer does (renderers.py:205-214)."""
     buf = torch.zeros(rows * 5 + 2, device=dev)
     stats = buf[:rows * 5].view(rows, 5)
-    rng = buf[rows * 5:]
-    rng.fill_(float("-inf"))
+    rng = buf[rows * 5:]       # zeros: the kernels' order-preserving range images start below every value
     with torch.no_grad():
         _lib.call("mms_render_stats", w.data_ptr(), normals.detach().contiguous().data_ptr(), starts.data_ptr(),
                   ends.data_ptr(), R, S, sidx.data_ptr(), stats.data_ptr(), 5, rng.data_ptr(), fx._s())
@@ -355,8 +354,7 @@ def _render_stats_segments(w, normals, starts, ends, off: List[int], S: int, sid
     buf = fx._zeroed_views([(n * rows * 5 + 2 * n,)], dev)[0] if fx._capturing(dev) else \
         torch.zeros(n * rows * 5 + 2 * n, device=dev)
     stats = buf[:n * rows * 5].view(n * rows, 5)
-    rng = buf[n * rows * 5:]
-    rng.fill_(float("-inf"))
+    rng = buf[n * rows * 5:]   # zeros: the kernels' order-preserving range images start below every value
     seg = (ctypes.c_int64 * (n + 1))(*off)
     with torch.no_grad():
         _lib.call("mms_render_stats_segments", w.data_ptr(), normals.detach().contiguous().data_ptr(),
