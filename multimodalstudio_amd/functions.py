@@ -728,23 +728,30 @@ class ChainRun:
 _WGRAD_DEFER: List[Optional[list]] = [None]
 
 
-def wgrad_defer_begin() -> None:
+_WGRAD_DEFER_STREAM: List[Optional[int]] = [None]
+
+
+def wgrad_defer_begin(this_stream_only: bool = False) -> None:
+    """Queue the MLPs' weight-gradient launches until wgrad_flush; ``this_stream_only``: only those issued on the
+    calling stream (the background stream's stay inline, beside the main stream's work)."""
     if _WN_BWD[0] is None:
         raise RuntimeError("weight gradients are deferred only inside a batched training backward (wn_bwd_begin)")
     _WGRAD_DEFER[0] = []
+    _WGRAD_DEFER_STREAM[0] = _s() if this_stream_only else None
 
 
 def wgrad_flush() -> None:
     """Launch the deferred weight-gradient GEMMs in backward order (before the deferred weight-norm flush, which
     reads their dW)."""
     q, _WGRAD_DEFER[0] = _WGRAD_DEFER[0], None
+    _WGRAD_DEFER_STREAM[0] = None
     for fn in q or []:
         fn()
 
 
 def _wgrad(fn) -> None:
     """Run a weight-gradient launch now, or queue it while the weight gradients are deferred."""
-    if _WGRAD_DEFER[0] is not None:
+    if _WGRAD_DEFER[0] is not None and (_WGRAD_DEFER_STREAM[0] is None or _WGRAD_DEFER_STREAM[0] == _s()):
         _WGRAD_DEFER[0].append(fn)
     else:
         fn()
