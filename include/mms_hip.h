@@ -318,6 +318,13 @@ int mms_neus_step(int64_t R, int S, const float* bins, const float* sdf_prev, in
 /* SO(3) x R^3 exponential map of the camera-pose deltas (lie_groups.py:28-63, camera_optimizers.py:86-119):
  * tangent [B, 6] = (t, w) -> mats [B, 3, 4] = [R(w) | t]; bwd adds d tangent [B, 6] from dmats [B, 3, 4] into dtangent. */
 int mms_pose_exp_fwd(const float* tangent, int64_t B, float* mats, void* stream);
+/* count[0] += the number of rays of coords [N, 3] whose ray (mms_raygen_fwd with the pose matrices exp(tangent [B, 6])
+ * -- or the given mats [B, 3, 4] when tangent is null --, B <= 256) hits the sphere of mms_collider_fwd (count zeroed
+ * by the caller), in one launch: the pose exp map, ray generation, collider and compaction count of the next step's
+ * rays (the same device functions, so the count is the one the step's own compaction finds). */
+int mms_count_hits(const int* coords, int64_t N, const float* fx, const float* fy, const float* cx, const float* cy,
+                   const float* c2w, const float* dist, const float* tangent, const float* mats, int B,
+                   int mat_per_cam, float pixel_offset, float radius, int64_t* count, void* stream);
 int mms_pose_exp_bwd(const float* tangent, const float* dmats, int64_t B, float* dtangent, void* stream);
 int mms_raygen_fwd(const int* coords, int64_t N, const float* fx, const float* fy, const float* cx, const float* cy,
                    const float* c2w, const float* dist, const float* mats, int mat_per_cam, float pixel_offset,

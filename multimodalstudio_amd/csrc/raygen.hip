@@ -82,6 +82,16 @@ __device__ __forceinline__ void rotate(const Pose& P, float u, float v, float o[
   }
 }
 
+// the normalised ray direction of camera-plane point (u, v) under pose P (returns the norm before normalising)
+__device__ __forceinline__ float unit_dir(const Pose& P, float u, float v, float* w) {
+  float o[3];
+  rotate(P, u, v, o);
+  const float n = sqrtf(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+  const float dn = fmaxf(n, 1e-12f);
+  for (int i = 0; i < 3; ++i) w[i] = o[i] / dn;
+  return n;
+}
+
 __global__ void raygen_fwd_kernel(const int* __restrict__ coords, int64_t N, const float* __restrict__ fxs,
                                   const float* __restrict__ fys, const float* __restrict__ cxs,
                                   const float* __restrict__ cys, const float* __restrict__ c2w,
@@ -95,12 +105,8 @@ __global__ void raygen_fwd_kernel(const int* __restrict__ coords, int64_t N, con
     const Pose P = compose(c2w + c * 12, mats + (mat_per_cam ? c * 12 : 0));
     float w[3][3];
     for (int s = 0; s < 3; ++s) {
-      float o[3];
-      rotate(P, u[s], v[s], o);
-      const float n = sqrtf(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+      const float n = unit_dir(P, u[s], v[s], w[s]);
       if (s == 0 && dnorm) dnorm[r] = n;
-      const float dn = fmaxf(n, 1e-12f);
-      for (int i = 0; i < 3; ++i) w[s][i] = o[i] / dn;
     }
     for (int i = 0; i < 3; ++i) {
       dirs[r * 3 + i] = w[0][i];
@@ -194,6 +200,17 @@ __global__ __launch_bounds__(256) void raygen_bwd_kernel(const int* __restrict__
 }
 
 // ------------------------------------------------------------------ collider
+// the sphere collider's (d . o, ||o||^2-term discriminant) of one ray -- shared by the collider and the fused hit
+// count (mms_count_hits), so both decide hits bit-identically
+__device__ __forceinline__ float sphere_under(const float* o, const float* d, float radius, float& dot) {
+  dot = d[0] * o[0];
+  dot = dot + d[1] * o[1];
+  dot = dot + d[2] * o[2];
+  // origins.norm(p=2): ATen's CPU norm accumulates the squares with FMAs (bit-exact to torch.norm)
+  const float on = sqrtf(__builtin_fmaf(o[2], o[2], __builtin_fmaf(o[1], o[1], o[0] * o[0])));
+  return dot * dot - (on * on - radius * radius);
+}
+
 __global__ void collider_fwd_kernel(const float* __restrict__ origins, const float* __restrict__ dirs, int64_t N,
                                     float radius, float* __restrict__ nears, float* __restrict__ fars,
                                     unsigned char* __restrict__ mask, float* __restrict__ bg_nears,
@@ -201,12 +218,8 @@ __global__ void collider_fwd_kernel(const float* __restrict__ origins, const flo
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < N; r += (int64_t)gridDim.x * blockDim.x) {
     const float* o = origins + r * 3;
     const float* d = dirs + r * 3;
-    float dot = d[0] * o[0];
-    dot = dot + d[1] * o[1];
-    dot = dot + d[2] * o[2];
-    // origins.norm(p=2): ATen's CPU norm accumulates the squares with FMAs (bit-exact to torch.norm)
-    const float on = sqrtf(__builtin_fmaf(o[2], o[2], __builtin_fmaf(o[1], o[1], o[0] * o[0])));
-    const float under = dot * dot - (on * on - radius * radius);
+    float dot;
+    const float under = sphere_under(o, d, radius, dot);
     const bool hit = under > 0.01f;
     const float sq = sqrtf(fmaxf(under, 0.01f));
     const float nr = fmaxf(sq * -1.0f - dot, 0.01f);
@@ -365,10 +378,7 @@ __device__ __forceinline__ Skew skew_of(const float* w) {
   return s;
 }
 
-__global__ void pose_exp_fwd_kernel(const float* __restrict__ tangent, int64_t B, float* __restrict__ mats) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const float* tv = tangent + 6 * b;
+__device__ __forceinline__ void pose_exp_one(const float* __restrict__ tv, float* __restrict__ o) {
   const float w[3] = {tv[3], tv[4], tv[5]};
   const float nrm = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
   const float ang = sqrtf(fmaxf(nrm, 1e-4f));
@@ -376,7 +386,6 @@ __global__ void pose_exp_fwd_kernel(const float* __restrict__ tangent, int64_t B
   const float f1 = inv * sinf(ang);
   const float f2 = inv * inv * (1.0f - cosf(ang));
   const Skew K = skew_of(w);
-  float* o = mats + 12 * b;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
 #pragma unroll
@@ -385,6 +394,57 @@ __global__ void pose_exp_fwd_kernel(const float* __restrict__ tangent, int64_t B
       o[4 * i + j] = (f1 * K.k[i][j] + f2 * k2) + (i == j ? 1.f : 0.f);
     }
     o[4 * i + 3] = tv[i];
+  }
+}
+
+__global__ void pose_exp_fwd_kernel(const float* __restrict__ tangent, int64_t B, float* __restrict__ mats) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  pose_exp_one(tangent + 6 * b, mats + 12 * b);
+}
+
+// The next step's hit count in ONE launch (graphs.GraphTrainer's tail): pose exp map (or the given matrices; every block
+// forms them in LDS), ray origin / direction and the sphere hit test of every ray, and the count added into count[0]
+// (zeroed beforehand) -- the same device functions as pose_exp_fwd / raygen_fwd / collider_fwd + compact, so the
+// count is the one the step's own compaction will find.  One ray per thread over the grid (a single block walking
+// 2048 rays measured slower than the four launches it replaces).
+constexpr int kCountMaxMats = 256;
+__global__ __launch_bounds__(256) void count_hits_kernel(const int* __restrict__ coords, int64_t N,
+                                                          const float* __restrict__ fxs, const float* __restrict__ fys,
+                                                          const float* __restrict__ cxs, const float* __restrict__ cys,
+                                                          const float* __restrict__ c2w, const float* __restrict__ dist,
+                                                          const float* __restrict__ tangent,
+                                                          const float* __restrict__ mats_in, int B, int mat_per_cam,
+                                                          float off, float radius, int64_t* __restrict__ count) {
+  __shared__ float smats[kCountMaxMats * 12];
+  __shared__ int wsum[16];
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    if (tangent != nullptr) {
+      pose_exp_one(tangent + 6 * b, smats + 12 * b);
+    } else {
+      for (int k = 0; k < 12; ++k) smats[12 * b + k] = mats_in[12 * b + k];
+    }
+  }
+  __syncthreads();
+  int cnt = 0;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < N; r += (int64_t)gridDim.x * blockDim.x) {
+    const int c = coords[r * 3], yi = coords[r * 3 + 1], xi = coords[r * 3 + 2];
+    float u[3], v[3];
+    cam_coords(xi, yi, off, fxs[c], fys[c], cxs[c], cys[c], dist ? dist + c * 6 : nullptr, u, v);
+    const Pose P = compose(c2w + c * 12, smats + (mat_per_cam ? c * 12 : 0));
+    float d[3];
+    unit_dir(P, u[0], v[0], d);
+    float dot;
+    cnt += sphere_under(P.t, d, radius, dot) > 0.01f ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tot = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) tot += (unsigned long long)wsum[k];
+    if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(count), tot);
   }
 }
 
@@ -562,6 +622,20 @@ MMS_EXPORT int mms_collider_bwd(const float* origins, const float* dirs, int64_t
   if (N == 0) return 0;
   hipLaunchKernelGGL(collider_bwd_kernel, dim3(mms::grid_for(N, 256, 16384)), dim3(256), 0, mms::as_stream(stream),
                      origins, dirs, N, radius, dnears, dfars, dbg_nears, dbg_fars, dorig, ddirs);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_count_hits(const int* coords, int64_t N, const float* fx, const float* fy, const float* cx,
+                              const float* cy, const float* c2w, const float* dist, const float* tangent,
+                              const float* mats, int B, int mat_per_cam, float pixel_offset, float radius,
+                              int64_t* count, void* stream) {
+  const char* fn = "mms_count_hits";
+  MMS_REQUIRE(B >= 1 && B <= kCountMaxMats, fn, "1 to 256 pose matrices");
+  MMS_REQUIRE(coords && fx && fy && cx && cy && c2w && count && (tangent || mats), fn, "null pointer");
+  MMS_REQUIRE(N >= 0, fn, "negative ray count");
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(count_hits_kernel, dim3(mms::grid_for(N, 256, 1024)), dim3(256), 0, mms::as_stream(stream), coords,
+                     N, fx, fy, cx, cy, c2w, dist, tangent, mats, B, mat_per_cam, pixel_offset, radius, count);
   return mms::check_launch(fn);
 }
 

@@ -50,6 +50,9 @@ CAPTURE_MODE = None   # override of the capture_error_mode (probes)
 # the optimizer groups zeroed / clipped / stepped together (pipeline.OptimBank: 3 launches and 1 scalar upload per
 # step instead of 8 and 2); MMS_BANKED_OPTIM=0: per group
 BANKED_OPTIM = os.environ.get("MMS_BANKED_OPTIM", "1") != "0"
+# the tail's next-step hit count in one launch (mms_count_hits, MMS_FUSED_COUNT=1); default: pose exp + raygen +
+# collider + compact
+FUSED_COUNT = os.environ.get("MMS_FUSED_COUNT", "0") == "1"
 
 
 def bucket_capacity(counts, granule: int, n: int) -> int:
@@ -81,6 +84,8 @@ class GraphTrainer:
         self.count_dev = torch.zeros(len(mods), dtype=torch.int64, device=dev)
         self.count_host = torch.zeros(len(mods), dtype=torch.int64).pin_memory()
         self.idx_scratch = torch.empty(n, dtype=torch.int64, device=dev)
+        # identity pose matrices (pose refinement off) for the fused hit count, made here: outside any capture
+        self._eye = {dev: torch.eye(4, device=dev)[None, :3, :4].contiguous()}
         self.side = torch.cuda.Stream(device=dev)
         self.graphs: Dict[tuple, Tuple[torch.cuda.CUDAGraph, Optional[torch.cuda.CUDAGraph], tuple]] = {}
         self.pool = None
@@ -120,12 +125,29 @@ class GraphTrainer:
         return coords
 
     @torch.no_grad()
-    def _count_hits(self):
+    def _count_hits(self, zeroed: bool = False):
         """Enqueue ray generation (current pose deltas) + collider + compaction count for the staged rays and the
         count's copy into pinned host memory (no synchronisation)."""
         t = self.t
         dev = t.device
+        if FUSED_COUNT and not zeroed:
+            self.count_dev.zero_()    # (a captured step zeroes it at its start, with the gradients: zeroed=True)
         for i, m in enumerate(t.modalities):
+            if FUSED_COUNT:
+                # pose exp map, ray generation, collider and count in one launch (mms_count_hits)
+                pa = t.pose.pose_adjustment
+                tangent = pa[m].detach() if (t.pose.mode != "off" and m in pa) else None
+                if tangent is None:
+                    mats, B = self._eye[dev], 1
+                else:
+                    tangent = tangent.contiguous()
+                    mats, B = None, tangent.shape[0]
+                cams = t.cams[m]
+                _lib.call("mms_count_hits", self.coords[m].data_ptr(), self.n, cams.fx.data_ptr(), cams.fy.data_ptr(),
+                          cams.cx.data_ptr(), cams.cy.data_ptr(), cams.c2w.data_ptr(), fx._p(cams.distortion),
+                          fx._p(tangent), fx._p(mats), B, 1 if B > 1 else 0, float(t.raygen.pixel_offset), 1.0,
+                          self.count_dev[i:i + 1].data_ptr(), fx._s())
+                continue
             mats = t.pose.matrices(m, dev)
             o, d, _, _, _ = fx.RaysFunction.apply(mats, self.coords[m], t.cams[m], t.raygen.pixel_offset)
             mask = fx.ColliderFunction.apply(o, d, 1.0)[4]
@@ -144,7 +166,7 @@ class GraphTrainer:
         optimizer just updated), so the host only waits for that count -- no eager ray generation, collider or
         synchronisation between two replays.  Captured at the end of each graph."""
         self.t.gpu_sampler.sample()
-        self._count_hits()
+        self._count_hits(zeroed=BANKED_OPTIM)
 
     # -- the captured work ---------------------------------------------------------------------------
     def _targets(self):
@@ -160,7 +182,9 @@ class GraphTrainer:
         if BANKED_OPTIM:
             # the gradients, the clip accumulators and the step's zero arena in one launch
             arena = fx.zero_arena_prepare(t.device)
-            t.optim.zero_grads(() if arena is None else (arena,))
+            # (+ the hit counter the tail's mms_count_hits adds into; the host has read it before this replay)
+            extra = ((self.count_dev.view(torch.float32),) if FUSED_COUNT else ()) + (() if arena is None else (arena,))
+            t.optim.zero_grads(extra)
             fx.zero_arena_begin(t.device, zeroed=arena)
         else:
             t.fields.zero_grad()

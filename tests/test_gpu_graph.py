@@ -72,3 +72,38 @@ def test_graph_trainer_matches_eager(dev, precision, max_iters, start):
     assert runner.stats["replays"] >= 4 and runner.stats["captures"] >= 1, runner.stats
     assert eager.step == graphed.step and eager.fields.step_count == graphed.fields.step_count
     assert rel.max() < 1e-3
+
+
+@pytest.mark.parametrize("pose", ["shared", "per_camera", "off"])
+def test_fused_hit_count_equals_unfused(dev, pose):
+    """graphs.GraphTrainer's tail hit count in one launch (mms_count_hits: pose exp map, ray generation, collider and
+    count in one block) equals the four-launch count (RaysFunction + ColliderFunction + mms_compact) for shared and
+    per-camera pose deltas of growing size, pixels drawn by the trainer's own sampler."""
+    from multimodalstudio_amd import graphs
+    from multimodalstudio_amd import pipeline as pl
+    cfg = pl.TrainConfig(method="grid", modalities=("rgb",), num_rays_per_modality=2048, log2T=14, n_views=10,
+                         width=160, height=128)
+    tr = pl.Trainer(cfg, dev)
+    if pose != "shared":
+        n = tr.cams["rgb"].num
+        tr.pose = pl.CameraOptimizer(["rgb"], {"rgb": n}, shared=False, mode="off" if pose == "off" else "SO3xR3").to(dev)
+        tr.raygen.pose_optimizer = tr.pose
+    runner = graphs.GraphTrainer(tr, granule=64)
+    g = torch.Generator().manual_seed(7)
+    old = graphs.FUSED_COUNT
+    try:
+        for scale in (0.0, 1e-3, 3e-2, 0.3):
+            if pose != "off":
+                with torch.no_grad():
+                    pa = tr.pose.pose_adjustment["rgb"]
+                    pa.copy_((torch.rand(pa.shape, generator=g) * 2 - 1) * scale)
+            runner._stage_inputs()
+            counts = []
+            for fused in (False, True):
+                graphs.FUSED_COUNT = fused
+                runner.count_dev.fill_(-1)
+                counts.append(runner.hit_counts())
+            assert counts[0] == counts[1], (scale, counts)
+            assert 0 < counts[0][0] <= 2048
+    finally:
+        graphs.FUSED_COUNT = old
