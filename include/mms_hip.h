@@ -399,6 +399,10 @@ int mms_step_loss_bwd(int n_l1, const float* const* out, const int64_t* ldo, con
                       const int64_t* counts_all, int n_counts, float inv_total, const float* dloss, float eik_scale,
                       float curv_scale, float* const* dgrads, float* const* dhess, void* stream);
 
+/* out[0] = 1 / clip(exp(10 s[0]), 1e-6, 1e6): SingleVarianceNetwork's reported 1 / inv_variance
+ * (single_variance.py:34-36, the model output inv_s) in one launch instead of four elementwise ones. */
+int mms_inv_variance(const float* s, float* out, void* stream);
+
 /* out[0] = sum_i x[i] * w[i] in index order (device x[n], host weights w[n], n <= 16): the total training loss from
  * its terms, LossManager.compute_loss's weighted sum (losses.py:224-265; weights 1 per L1 term, 0.1 eikonal,
  * 5e-4 x schedule curvature, method_configs.py:252-253). */

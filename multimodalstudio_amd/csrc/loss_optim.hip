@@ -666,6 +666,24 @@ __global__ void weighted_sum_kernel(const float* __restrict__ x, int n, WSumArgs
 }
 }  // namespace
 
+namespace {
+// SingleVarianceNetwork's reported 1 / inv_variance = 1 / clip(exp(10 s), 1e-6, 1e6) (single_variance.py:34-36), the
+// float operations of its torch form (mul, exp, clamp, reciprocal) in one thread
+__global__ void inv_variance_kernel(const float* __restrict__ s, float* __restrict__ out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const float e = expf(s[0] * 10.0f);
+    out[0] = 1.0f / fminf(fmaxf(e, 1e-6f), 1e6f);
+  }
+}
+}  // namespace
+
+MMS_EXPORT int mms_inv_variance(const float* s, float* out, void* stream) {
+  const char* fn = "mms_inv_variance";
+  MMS_REQUIRE(s && out, fn, "null pointer");
+  hipLaunchKernelGGL(inv_variance_kernel, dim3(1), dim3(64), 0, mms::as_stream(stream), s, out);
+  return mms::check_launch(fn);
+}
+
 MMS_EXPORT int mms_weighted_sum(const float* x, int n, const float* w, float* out, void* stream) {
   const char* fn = "mms_weighted_sum";
   MMS_REQUIRE(n >= 1 && n <= 16, fn, "1 to 16 terms");

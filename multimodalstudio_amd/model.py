@@ -784,7 +784,12 @@ class BaseModel(nn.Module):
             with torch.cuda.stream(bgs):
                 # the reported 1 / s (an output only, no loss term reads it: compute_metrics' inv_s) off the main stream
                 with torch.no_grad():
-                    inv_s = 1.0 / self.surface_model.volume_rendering.density_fn.variance_network.get_inv_variance()
+                    vn = self.surface_model.volume_rendering.density_fn.variance_network
+                    if vn.s.device.type == "cuda":
+                        inv_s = torch.empty_like(vn.s)     # one launch (mms_inv_variance) for the four torch ops
+                        _lib.call("mms_inv_variance", vn.s.data_ptr(), inv_s.data_ptr(), fx._s())
+                    else:
+                        inv_s = 1.0 / vn.get_inv_variance()
                 nb = sp.bg_samples + 1
                 blin = self._lin_dev(nb, 1.0, dev)
                 bbins = torch.empty(nm * N, nb, device=dev)

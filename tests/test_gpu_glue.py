@@ -217,3 +217,17 @@ def test_weight_norm_bwd_batched_matches_immediate(dev):
         assert float((grads[0] - grads[1]).abs().max()) <= 1e-4 * scale
     finally:
         fx.set_precision("fp32")
+
+
+def test_inv_variance_equals_torch(dev):
+    """mms_inv_variance (the model's reported 1 / inv_variance in one launch) equals SingleVarianceNetwork's torch
+    expression 1.0 / exp(10 s).clip(1e-6, 1e6) bit for bit, clip bounds included."""
+    from multimodalstudio_amd import _lib
+    from multimodalstudio_amd import functions as fx
+    for v in (0.3, -0.2, 0.0123, 1.7, -3.0, 2.5, 0.29999):
+        s = torch.tensor([v], device=dev)
+        out = torch.empty_like(s)
+        _lib.call("mms_inv_variance", s.data_ptr(), out.data_ptr(), fx._s())
+        ref = 1.0 / torch.exp(s * 10.0).clip(1e-6, 1e6)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), (v, out.item(), ref.item())
