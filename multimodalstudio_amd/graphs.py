@@ -56,7 +56,14 @@ FUSED_COUNT = os.environ.get("MMS_FUSED_COUNT", "1") != "0"
 
 
 def bucket_capacity(counts, granule: int, n: int) -> int:
-    """Fixed foreground capacity for hit counts ``counts``: the largest, rounded up to ``granule``, at most n."""
+    """Fixed foreground capacity for hit counts ``counts``: the largest, rounded up to ``granule``, at most n.
+
+    Invariant: a replayed step's own compaction count is <= the capacity chosen here.  The counts come from the
+    previous step's tail (mms_count_hits with the poses that step's optimizer wrote), which is the same ray
+    generation and collider arithmetic as the step's own RaysFunction + ColliderFunction + compaction
+    (test_gpu_graph.py::test_fused_hit_count_equals_unfused pins the equality).  The composite relies on it: hit rows
+    are written only by a composited ray (mms_composite_fwd's padding blocks fill the non-hit rows), so a hit ray past
+    the capacity would leave its output row unwritten."""
     c = max(counts)
     return min(n, -(-c // granule) * granule)
 
@@ -161,12 +168,13 @@ class GraphTrainer:
         torch.cuda.current_stream().synchronize()
         return [int(c) for c in self.count_host.tolist()]
 
-    def _tail(self):
+    def _tail(self, captured: bool = False):
         """Device-sampler steps end by drawing the NEXT step's pixels and counting its hits (with the poses this step's
         optimizer just updated), so the host only waits for that count -- no eager ray generation, collider or
-        synchronisation between two replays.  Captured at the end of each graph."""
+        synchronisation between two replays.  Captured at the end of each graph (``captured``: the step zeroed the
+        hit counter with its gradients, OptimBank.zero_grads); after an eager step the counter is zeroed here."""
         self.t.gpu_sampler.sample()
-        self._count_hits(zeroed=BANKED_OPTIM)
+        self._count_hits(zeroed=captured and BANKED_OPTIM)
 
     # -- the captured work ---------------------------------------------------------------------------
     def _targets(self):
@@ -270,7 +278,7 @@ class GraphTrainer:
                 out = self._forward_backward(cap)
                 self._optimizer()
                 if self.tail:
-                    self._tail()
+                    self._tail(captured=True)
             pool = g1.pool()
         else:
             g1a, g1b, out = self._capture_split(cap, mode)
@@ -283,7 +291,7 @@ class GraphTrainer:
             with torch.cuda.graph(g2, pool=self.pool, stream=self._capture_stream(), capture_error_mode=mode):
                 self._optimizer()
                 if self.tail:
-                    self._tail()
+                    self._tail(captured=True)
         self.graphs[key] = (g1, g2, out)
         self.stats["captures"] += 1
 

@@ -465,6 +465,10 @@ class RNG:
     uniform: Dict[str, torch.Tensor] = field(default_factory=dict)
     pdf: Dict[str, List[torch.Tensor]] = field(default_factory=dict)
     background: Dict[str, torch.Tensor] = field(default_factory=dict)
+    # final NeuS spacing bins per modality ([N_hit, S + 1]): given for EVERY modality of a batch, they replace the
+    # up-sampler's output (the parity tests pin the rest of the step on the reference's own samples; the sampler is
+    # pinned on its own, bit-exact given the reference's SDFs)
+    bins: Dict[str, torch.Tensor] = field(default_factory=dict)
 
 
 _BG_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
@@ -813,8 +817,19 @@ class BaseModel(nn.Module):
                     bg_res.append(background())
         if at == -2:
             issue_bg()
-        bins = self.neus_bins(n_h.detach(), f_h.detach(), o_h.detach(), d_h.detach(), t_rand, pdf,
-                              after_iter=(lambda it: issue_bg() if it == at else None) if at >= 0 else None)
+        if all(m in rng.bins for m in mods):
+            # injected samples: each modality's bins, fixed-capacity segments padded with their first ray's bins (the
+            # padding rows repeat the first hit ray)
+            parts = []
+            for i, m in enumerate(mods):
+                b = rng.bins[m][:Rm[i]]
+                if b.shape[0] < Rm[i]:
+                    b = torch.cat([b, b[:1].expand(Rm[i] - b.shape[0], -1)])
+                parts.append(b)
+            bins = cat(parts).contiguous()
+        else:
+            bins = self.neus_bins(n_h.detach(), f_h.detach(), o_h.detach(), d_h.detach(), t_rand, pdf,
+                                  after_iter=(lambda it: issue_bg() if it == at else None) if at >= 0 else None)
         issue_bg()
         inv_s, bg_out = bg_res[0]
         S = bins.shape[1] - 1

@@ -197,6 +197,9 @@ class FlatGroup:
                   self.n, self.sumsq.data_ptr(), float(max_norm), self.hyper.data_ptr(), _s())
 
 
+ZERO_MULTI_MAX = 8      # buffers per mms_zero_multi launch (kMaxSeg, csrc/loss_optim.hip)
+
+
 class OptimBank:
     """The trainer's optimizer groups (FlatGroup) stepped together in graph-replayed steps: the gradients and sum-of-
     squares accumulators zeroed in one launch, the groups' clip norms in one, their AdamW updates in one
@@ -230,9 +233,13 @@ class OptimBank:
         for g in self.groups:
             g.check_grads_attached()
         bufs = [g.grad for g in self.groups] + [g.sumsq for g in self.groups] + list(extra)
-        n = len(bufs)
-        _lib.call("mms_zero_multi", n, (ctypes.c_void_p * n)(*[b.data_ptr() for b in bufs]),
-                  (ctypes.c_int64 * n)(*[b.numel() for b in bufs]), _s())
+        # one launch per ZERO_MULTI_MAX buffers (mms_zero_multi's segment table): one launch for the trainer's two
+        # groups + hit counter + arena, more only for larger banks
+        for i in range(0, len(bufs), ZERO_MULTI_MAX):
+            part = bufs[i:i + ZERO_MULTI_MAX]
+            n = len(part)
+            _lib.call("mms_zero_multi", n, (ctypes.c_void_p * n)(*[b.data_ptr() for b in part]),
+                      (ctypes.c_int64 * n)(*[b.numel() for b in part]), _s())
 
     def load_hyper(self, lr_factor: float):
         """Graph mode, before a replay: advance every group's step and upload their scalars in one copy."""

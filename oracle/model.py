@@ -262,8 +262,10 @@ def background_forward(bsmp: orr.Samples, r: orr.Rays, P, spec: ModelSpec, st: S
     dirs = r.directions[:, None, :].expand(N, S, 3).reshape(-1, 3)
     ups = r.up[:, None, :].expand(N, S, 3).reshape(-1, 3)
     pos = of.scene_contraction_linf(pos)
+    # the background grid keeps every level at every step: BackgroundModel registers no training callbacks
+    # (background_model.py:120-125), so FeatureGrid.set_mask never runs and hash_encoding_mask stays all ones
     density, feat = of.nerf_field(pos, dirs, P, grid=spec.bg_grid,
-                                  active_levels=st.active_levels if st is not None else 16)
+                                  active_levels=spec.bg_grid.num_levels if spec.bg_grid is not None else 16)
     density = density.view(N, S, -1)
     alphas = 1 - torch.exp(-(bsmp.deltas * density))
     w = orr.weights_from_alphas(alphas)

@@ -1,0 +1,175 @@
+"""The benchmarked configuration at its own size against the reference (VERDICT r4 "what's missing" #1).
+
+Fixture tests/golden/e2e_full_grid_rgb_l19.npz: one reference fwd + loss + bwd of BASELINE configs[1] -- grid.yaml,
+rgb, 2048 rays, log2T 19 (/root/reference/confs/grid.yaml:58-59), model step 95000, the benchmark's 50-view 640 x 512
+rig -- written by tests/golden/make_golden.py (e2e_full) by running the reference in the build container.  Its
+parameters are regenerated here (tests/fullsize_state.py: seeded init, formula tables, the SDF MLP's grid columns
+given weights so the SDF table gradient is not identically zero, checksum-checked); of the two 64 MiB table gradients
+it keeps per-level norms and 32768 sampled nonzero entries each.  876 of the 2048 rays hit the sphere (the bench's
+~56k samples per step).  The fixture also holds the up-sampler's inputs, each iteration's SDF values and
+sorted_index.
+
+Why the sampler is pinned on its own here.  The formula tables are per-entry noise, so at 2^19 entries and 1/1024
+cells the SDF is rough on the scale of a sample step, and the NeuS up-sampler's inverse CDF turns last-ulp SDF
+differences (GPU vs CPU GEMM summation order) into bin shifts of up to 3e-3 on ~14 % of the rays; through the rough
+SDF those shifts move the rays' gradients and hessians by O(1) of their scale.  That is the sampler's sensitivity,
+not a kernel error: measured (scripts/fullsize_diag.py) on the rays whose bins agree, radiance is within 5e-5.  So:
+  * test_fullsize_sampler_bit_exact -- the HIP up-sampler fed the reference's hit rays, uniforms and per-iteration
+    SDFs reproduces the final bins and all four sorted_index tensors bit for bit (north_star: "sample indices
+    bit-exact");
+  * the rest of the step on the reference's own samples (model.RNG.bins), at the dynamic path's fp32 bounds
+    (test_gpu_e2e.assert_e2e_bounds), through every path the bench uses at that size -- the wide weight-gradient
+    engine over ~280k rows with many split-K slices, the XCD-ordered hash walk over a 2^19 table, the multi-block
+    compaction: the eager dynamic step, fixed-capacity batches at the capacity graphs.bucket_capacity picks
+    (granule 64: 896 rows, 20 padding) and at cap = N (2048 rows, 1172 padding), and the step captured as a HIP graph
+    at that capacity and replayed (twice: the second replay starts from the gradients the graph itself zeroes) with
+    the trainer's batched backward;
+  * the free-running step (the HIP sampler on the HIP SDF): the loss, the hit mask, the share of rays whose bins agree
+    to 2e-5 and the radiance on those rays;
+  * the benchmarked `fast` preset on the reference's samples, at the small fixtures' fast bounds.
+"""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_e2e import GEO_TOL_FAST, E2ECase, assert_e2e_bounds, e2e_report, load, print_report, rel_err
+
+pytestmark = pytest.mark.gpu
+NAME = "e2e_full_grid_rgb_l19"
+
+
+def granule_cap(f):
+    from multimodalstudio_amd.graphs import bucket_capacity
+    mods = [str(m) for m in f["mods"]]
+    n = f[f"{mods[0]}:coords"].shape[0]
+    return bucket_capacity([int(np.asarray(f[f"{m}:mask"]).sum()) for m in mods], 64, n)
+
+
+def test_fullsize_sampler_bit_exact(dev):
+    from multimodalstudio_amd import model as mm
+    f = load(NAME)
+    m = "rgb"
+    T = lambda a: torch.from_numpy(np.asarray(a)).to(dev)  # noqa: E731
+    n_h, f_h = T(f[f"{m}:hit:nears"]).reshape(-1).contiguous(), T(f[f"{m}:hit:fars"]).reshape(-1).contiguous()
+    o_h, d_h = T(f[f"{m}:hit:origins"]).contiguous(), T(f[f"{m}:hit:directions"]).contiguous()
+    R = n_h.shape[0]
+    assert R == int(f[f"{m}:mask"].sum())
+    t_rand = T(f["rand:0"])
+    pdf = [T(f[f"rand:{1 + i}"]) for i in range(4)]
+    sdfs = [T(f[f"{m}:sampler:sdf{i}"]).reshape(-1).contiguous() for i in range(4)]
+    calls = []
+
+    def sdf_fn(pos):
+        assert pos.shape[0] == sdfs[len(calls)].shape[0]
+        calls.append(pos.shape[0])
+        return sdfs[len(calls) - 1]
+    hist = []
+    bins = mm.neus_sample(n_h, f_h, o_h, d_h, t_rand, pdf, sdf_fn, history=hist)
+    torch.cuda.synchronize()
+    assert len(calls) == 4
+    ref = f[f"{m}:bins"]
+    got = bins.cpu().numpy()
+    print(f"full-size sampler: {R} rays, bins exact {np.mean(got == ref):.4f}, max |d| {np.abs(got - ref).max():.3e}")
+    assert np.array_equal(got, ref)
+    for i in range(4):
+        assert np.array_equal(hist[i].cpu().numpy().astype(np.int64),
+                              f[f"{m}:sampler:sorted_index{i}"].astype(np.int64)), i
+
+
+@pytest.mark.parametrize("which", ["dynamic", "granule", "all_rays"])
+def test_fullsize_step_on_reference_samples(dev, which):
+    f = load(NAME)
+    cap = {"dynamic": None, "granule": granule_cap(f), "all_rays": f["rgb:coords"].shape[0]}[which]
+    case = E2ECase(f, dev, inject_bins=True)
+    outs, losses, total = case.run_step(cap, batched=which != "dynamic")
+    torch.cuda.synchronize()
+    report = e2e_report(f, case.mods, case.model, case.pose, outs, total, cap=cap)
+    print_report(f"{NAME} {which} cap={cap}", report, case.mods)
+    assert report["rgb:bins_abs"] == 0.0
+    assert_e2e_bounds(NAME, report, case.mods)
+
+
+def test_fullsize_graph_replay(dev):
+    from multimodalstudio_amd import functions as fx
+    f = load(NAME)
+    cap = granule_cap(f)
+    assert cap % 64 == 0 and cap - int(f["rgb:mask"].sum()) > 0, cap
+    case = E2ECase(f, dev, inject_bins=True)
+    params = case.params()
+
+    def step():
+        fx.zero_arena_begin(dev)
+        try:
+            fx.reset_grad_uses()
+            return case.run_step(cap, batched=True)
+        finally:
+            fx.zero_arena_end()
+
+    # one eager step first (as GraphTrainer: gradients allocated, the zero arena sized, lazy per-stream state made),
+    # on a side stream
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert all(p.grad is not None for p in params)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for p in params:
+            p.grad.zero_()
+        outs, losses, total = step()
+    for p in params:
+        p.grad.fill_(7.0)       # the replay must start from its own zeroed gradients
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    report = e2e_report(f, case.mods, case.model, case.pose, outs, total, cap=cap)
+    print_report(f"{NAME} graph cap={cap}", report, case.mods)
+    assert_e2e_bounds(NAME, report, case.mods)
+
+
+def test_fullsize_free_running(dev):
+    """The HIP sampler on the HIP SDF (no injection): what the chaos above leaves checkable."""
+    f = load(NAME)
+    case = E2ECase(f, dev)
+    outs, losses, total = case.run_step(None)
+    torch.cuda.synchronize()
+    o = outs["rgb"]
+    loss_rel = abs(total.item() - float(f["loss"])) / abs(float(f["loss"]))
+    assert np.array_equal(o["mask"].cpu().numpy().astype(bool), f["rgb:mask"])
+    db = np.abs(o["bins"].cpu().numpy() - f["rgb:bins"]).max(1)
+    agree = db <= 2e-5
+    hit = np.nonzero(f["rgb:mask"])[0]
+    e = np.abs(o["rgb"].detach().cpu().numpy() - f["rgb:out:rgb"]).max(1)[hit]
+    scale = np.abs(f["rgb:out:rgb"]).max()
+    print(f"free-running: loss rel {loss_rel:.3e}, rays with bins within 2e-5: {agree.mean():.3f}, radiance on them "
+          f"{e[agree].max() / scale:.3e}, on the others {e[~agree].max() / scale if (~agree).any() else 0:.3e}")
+    assert loss_rel < 5e-4             # measured 6.9e-5
+    assert agree.mean() > 0.75         # measured 0.86
+    assert e[agree].max() / scale < 2e-4   # measured 5e-5
+
+
+def test_fullsize_fast_preset(dev):
+    """The benchmarked `fast` preset (every MLP on split-bf16x3) on the reference's samples: the small fixtures'
+    fast bounds (test_gpu_e2e.test_e2e_fast_preset_deviation)."""
+    from multimodalstudio_amd import functions as fx
+    f = load(NAME)
+    fx.set_precision("fast")
+    try:
+        case = E2ECase(f, dev, inject_bins=True)
+        outs, losses, total = case.run_step(granule_cap(f), batched=True)
+        torch.cuda.synchronize()
+    finally:
+        fx.set_precision("fp32")
+    loss_rel = abs(total.item() - float(f["loss"])) / abs(float(f["loss"]))
+    got = outs["rgb"]["rgb"].detach().cpu().numpy().astype(np.float64)
+    ref = f["rgb:out:rgb"].astype(np.float64)
+    rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-2)
+    n = int(outs["rgb"]["count"].item())
+    geo = {k: rel_err(outs["rgb"][k][:n].detach().cpu(), f[f"rgb:out:{k}"]) for k in ("gradients", "hessians")}
+    print(f"fast full-size: loss rel {loss_rel:.3e}, radiance rel mean {rel.mean():.3e} max {rel.max():.3e}, {geo}")
+    assert loss_rel < 2e-4
+    assert rel.mean() < 3e-4 and rel.max() < 2.5e-2
+    for k, e in geo.items():
+        assert e < GEO_TOL_FAST[k], (k, e)

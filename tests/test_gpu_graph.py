@@ -1,8 +1,11 @@
 """Graph-captured steps (multimodalstudio_amd/graphs.py) against the reference and against the eager path.
 
-* Fixed-capacity foreground batches (BaseModel.forward(cap=N): every ray slot kept, padding rows repeat the first
-  hit ray) on the reference's golden end-to-end vectors, with the tolerances of the dynamic path
-  (tests/test_gpu_e2e.py): the padding changes nothing.
+* Fixed-capacity foreground batches (BaseModel.forward(cap=...): padding rows repeat the first hit ray) on the
+  reference's golden end-to-end vectors, checked at exactly the dynamic path's fp32 bounds
+  (test_gpu_e2e.assert_e2e_bounds: loss / radiance / accumulation / depth 1e-4, normals and SDF gradients 2e-3,
+  hessians 0.15, bins 2e-5, parameter gradients 2e-3 max and 1e-3 relative L2, pose gradients 5e-3) -- the padding
+  rows must change nothing.  The 8-ray fixtures run at cap = N (their largest capacity); the benchmark configuration
+  at its own size, with the 64-ray granule bucket_capacity picks, is tests/test_gpu_fullsize.py.
 * GraphTrainer replays vs eager Trainer.train_step from the same initial state on the same pixel draws, with the
   sampler jitter off (eval-mode sampler, so both paths see identical samples): per-step losses within 1e-3
   relative over 6 steps (the first is eager, then captures and replays).  Not bit-exact: float-atomic gradient
@@ -13,28 +16,20 @@ import numpy as np
 import pytest
 import torch
 
-from test_gpu_e2e import load, rel_err, run_hip_e2e
+from test_gpu_e2e import assert_e2e_bounds, e2e_report, load, print_report, run_hip_e2e
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000", "e2e_grid_raw_gridbg_s95000"])
+@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000", "e2e_grid_raw_5mod_sat_s95000",
+                                  "e2e_grid_raw_gridbg_s95000"])
 def test_e2e_fixed_capacity(dev, name):
     f = load(name)
     N = f[f"{str(f['mods'][0])}:coords"].shape[0]
     mods, model, pose, outs, losses, total = run_hip_e2e(f, dev, cap=N)
-    assert abs(total.item() - float(f["loss"])) / abs(float(f["loss"])) < 1e-4
-    for m in mods:
-        o = outs[m]
-        cnt = int(o["count"].item())
-        assert cnt == int(np.asarray(f[f"{m}:out:gradients"]).shape[0])
-        assert rel_err(o[m].detach().cpu(), f[f"{m}:out:{m}"]) < 1e-4, m
-        assert rel_err(o["accumulation"].cpu(), f[f"{m}:out:accumulation"]) < 1e-4, m
-        assert rel_err(o["normals"].cpu(), f[f"{m}:out:normals"]) < 2e-3, m
-        assert rel_err(o["gradients"][:cnt].detach().cpu(), f[f"{m}:out:gradients"]) < 2e-3, m
-        assert rel_err(pose.pose_adjustment[m].grad.cpu(), f[f"{m}:dpose"]) < 5e-2, m
-    worst = max(rel_err(p.grad.cpu(), f["g:" + k]) for k, p in model.named_parameters() if "g:" + k in f)
-    assert worst < 5e-2
+    report = e2e_report(f, mods, model, pose, outs, total, cap=N)
+    print_report(name + f" cap={N}", report, mods)
+    assert_e2e_bounds(name, report, mods)
 
 
 @pytest.mark.parametrize("precision,max_iters,start", [("fp32", 100000, 95000), ("fast", 100000, 95000),
@@ -105,5 +100,33 @@ def test_fused_hit_count_equals_unfused(dev, pose):
                 counts.append(runner.hit_counts())
             assert counts[0] == counts[1], (scale, counts)
             assert 0 < counts[0][0] <= 2048
+    finally:
+        graphs.FUSED_COUNT = old
+
+
+def test_tail_count_after_eager_steps(dev):
+    """after an EAGER step the tail's fused hit count must start from zero (a captured step zeroes the
+    counter with its gradients; an eager one does not).  Three eager steps with a tail each: every staged count equals
+    the unfused count of the same staged pixels (it used to grow by the previous count every step)."""
+    from multimodalstudio_amd import graphs
+    from multimodalstudio_amd import pipeline as pl
+    cfg = pl.TrainConfig(method="grid", modalities=("rgb",), num_rays_per_modality=512, log2T=14, n_views=10,
+                         width=160, height=128, gpu_sampler=True)
+    tr = pl.Trainer(cfg, dev)
+    tr.set_step(95000)
+    runner = graphs.GraphTrainer(tr, granule=64)
+    assert runner.tail
+    old = graphs.FUSED_COUNT
+    runner._stage_inputs()
+    try:
+        for _ in range(3):
+            runner._eager_with_tail(runner.coords)
+            runner.count_event.synchronize()
+            staged = [int(c) for c in runner.count_host.tolist()]
+            graphs.FUSED_COUNT = False
+            ref = runner.hit_counts()
+            graphs.FUSED_COUNT = old
+            assert staged == ref, (staged, ref)
+            assert 0 < ref[0] <= 512
     finally:
         graphs.FUSED_COUNT = old

@@ -121,11 +121,12 @@ def test_neus_sampler_bit_exact():
 
 # ------------------------------------------------------------------------------------------------
 def e2e_inputs(name):
+    from fullsize_state import with_fullsize_params
     f = load(name)
     if "params_from" in f:
         p = load(str(f["params_from"]))
         f.update({k: v for k, v in p.items() if k.startswith("p:")})
-    return f
+    return with_fullsize_params(f)
 
 
 def run_oracle_e2e(f):
@@ -163,7 +164,8 @@ def run_oracle_e2e(f):
 
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_rgb_s30000", "e2e_grid_raw_5mod_s95000",
                                   "e2e_grid_raw_5mod_sat_s95000", "e2e_mlp_raw_rgb_s95000",
-                                  "e2e_grid_raw_gridbg_s95000"])
+                                  "e2e_grid_raw_gridbg_s95000", "e2e_grid_raw_gridbg_s30000",
+                                  "e2e_full_grid_rgb_l19"])
 def test_end_to_end(name):
     f = e2e_inputs(name)
     mods, outs, losses, total, P, poses = run_oracle_e2e(f)
@@ -184,6 +186,22 @@ def test_end_to_end(name):
             scale = np.abs(ref).max() + 1e-12
             err = np.abs(p.grad.numpy() - ref).max()
             assert err <= 2e-3 * scale + 1e-9, (k, err, scale)
+    check_compact_table_grads(f, {k: p.grad for k, p in P.items()}, 1e-4)
+
+
+def check_compact_table_grads(f, grads, rel):
+    """The full-size fixture's hash-table gradients: per-level L2 norms within ``rel`` and the sampled nonzero entries
+    within ``rel`` of the table gradient's scale."""
+    for key in [k for k in f if k.startswith("gtab_level_norm:")]:
+        k = key.split(":", 1)[1]
+        g = torch.as_tensor(grads[k]).detach().cpu().double()
+        norms = g.reshape(16, -1).norm(dim=1).numpy()
+        np.testing.assert_allclose(norms, f[key], rtol=rel, atol=rel * f[key].max(), err_msg=k)
+        idx = torch.as_tensor(f["gtab_idx:" + k].astype(np.int64))
+        val = g.reshape(-1)[idx].numpy()
+        ref = f["gtab_val:" + k]
+        scale = np.abs(ref).max()
+        assert np.abs(val - ref).max() <= rel * scale, (k, np.abs(val - ref).max() / scale)
 
 
 def test_pixel_sampler_reproduces_reference_coords():
@@ -244,3 +262,23 @@ def test_train_parity_window_resolves_the_bound(name):
     mods = [k.split(":")[1] for k in f.files if k.startswith("eval0:") and k.endswith(":psnr")]
     for m in mods:
         assert float(f[f"eval:{m}:psnr"]) > float(f[f"eval0:{m}:psnr"]) + 0.25, m
+
+
+def test_fullsize_sampler_bit_exact():
+    """The oracle's NeuS up-sampler on the full-size fixture's hit rays, uniforms and per-iteration reference SDFs
+    reproduces the reference's final bins and every iteration's sorted_index bit for bit."""
+    f = load("e2e_full_grid_rgb_l19")
+    m = "rgb"
+    sdfs = [T(f[f"{m}:sampler:sdf{i}"]) for i in range(4)]
+    calls = []
+
+    def sdf_fn(pts):
+        calls.append(1)
+        return sdfs[len(calls) - 1]
+    smp, hist = orr.neus_sample(T(f[f"{m}:hit:nears"]), T(f[f"{m}:hit:fars"]), T(f[f"{m}:hit:origins"]),
+                                T(f[f"{m}:hit:directions"]), sdf_fn, T(f["rand:0"]),
+                                [T(f[f"rand:{1 + i}"]) for i in range(4)])
+    assert len(calls) == 4
+    assert np.array_equal(smp.spacing_bins.numpy(), f[f"{m}:bins"])
+    for i in range(4):
+        assert np.array_equal(hist[i].numpy(), f[f"{m}:sampler:sorted_index{i}"].astype(np.int64)), i
