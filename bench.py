@@ -112,6 +112,11 @@ def chain_work(a):
     return f"{PREC_NAMES[prec]}:{role}{'_bwd' if bwd else '_fwd'}", (flops, nbytes)
 
 
+def chain16_work(a):
+    """chain_work of one mms_mlp_chain16 launch (mms_mlp_chain's arguments without the input scaling: a[8:] shifted)."""
+    return chain_work(list(a[:8]) + [None] * 5 + list(a[8:]))
+
+
 def hash_fwd_work(a):
     """(role, SURVEY §8(d) bytes) of one mms_hashgrid_fwd(_grouped) launch: the SDF batch [centre | 4 taps] (the dominant
     launch), the sampler's / background's smaller 72-column panels, or the radiance panel."""
@@ -150,6 +155,7 @@ def work_fns():
         "mms_gemm_tn_grouped": gemm_grouped_work,
         "mms_gemm_tn_wide": gemm_grouped_work,
         "mms_mlp_chain": chain_work,
+        "mms_mlp_chain16": chain16_work,
         "mms_hashgrid_fwd_grouped": hash_fwd_work,
         "mms_sdf_panel_fwd": sdf_panel_work,
         "mms_sdf_panel_rays_fwd": sdf_panel_rays_work,
@@ -425,7 +431,8 @@ def main():
         # headline (north_star / SURVEY §8(d)): MFMA utilisation of the fused geometry-MLP chain, forward, rated by
         # its algorithmic 2MNK flops against the dense bf16 MFMA peak; the hash-grid lookups against HBM beside it
         by_name = {k["kernel"]: k for k in kernels}
-        sdf = [k for k in kernels if k["kernel"].startswith("mms_mlp_chain:") and k["kernel"].endswith(":sdf_fwd")]
+        sdf = [k for k in kernels if k["kernel"].startswith(("mms_mlp_chain:", "mms_mlp_chain16:"))
+               and k["kernel"].endswith(":sdf_fwd")]
         top = sdf[0] if sdf else (kernels[0] if kernels else None)
         if top is not None:
             roof = {k: top[k] for k in ["bound", "achieved", "peak", "unit", "frac", "traffic"] if k in top}

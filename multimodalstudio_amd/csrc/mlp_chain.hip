@@ -25,87 +25,9 @@
 // weights' rounding is the mixed-precision "bf16 weights, fp32 master" one -- at 2 MFMAs and half the weight
 // traffic of PREC 2); fp32 accumulation.
 #include "common.h"
-
-#include <utility>
-
+#include "chain_common.h"
 
 namespace {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// streamed activations bypass the caches' retention (non-temporal), so the packed weights the waves re-read
-// from L2 at every k-step stay resident
-__device__ __forceinline__ f32x4 ld_nt4(const float* p) { return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p)); }
-__device__ __forceinline__ void st_nt4(float* p, f32x4 v) { __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p)); }
-
-struct ChainLayer {
-  const __bf16* a_hi;  // packed A operand [32 nt][16 ks] (mms_mlp_pack)
-  const __bf16* a_lo;  // split-bf16x3 residual image, or null
-  const float* bias;   // forward: [N], or null
-  const float* aux;    // backward: forward output Y [rows][ldaux] whose act' scales the product, or null
-  int64_t ldaux;
-  float* out;          // fp32 store [rows][ldo] of the layer result, or null
-  int64_t ldo;
-  int N;               // valid output columns
-  int act;             // forward: activation; backward: derivative taken at aux
-};
-
-struct ChainArgs {
-  const float* X;      // layer-0 input [rows][ldx], K0 valid columns (16-B aligned rows)
-  int64_t ldx;
-  int K0;
-  int64_t M;
-  int64_t rows_full;   // SDF tap rows (>= rows_full): forward keeps only column 0 of the last layer,
-                       // backward reads only column 0 of the input
-  const float* xaux;   // backward: input first scaled by act'(xaux) (the last forward activation), or null
-  int64_t ldxaux;
-  int xact;
-  float* xout;         // backward: store of the scaled input (dZ of the last forward layer), or null
-  int64_t ldxout;
-  float beta, thr;     // Softplus(beta, threshold)
-  const float* w2row0; // forward: fp32 row 0 of the last layer's weight for the single-output row blocks
-  float* tap_part;     // backward, SDF taps: per-block partials [blocks from rows_full / 128][ld_tap] of
-  int64_t ld_tap;      //   sum over rows >= rows_full of X[m, 0] * aux0[m, :] (cols < N0) and of X[m, 0] (col N0)
-  ChainLayer L[4];     // 3 or 4 layers (kernel template NL)
-};
-
-// activation derivative from the forward OUTPUT y (compile-time activation: branch-free epilogues)
-template <int ACT>
-__device__ __forceinline__ float act_grad_out(float y, float beta, float thr) {
-  if constexpr (ACT == 1) return y > 0.f ? 1.f : 0.f;
-  if constexpr (ACT == 2) {
-    const float by = y * beta;
-    return by > thr ? 1.f : 1.0f - __builtin_amdgcn_exp2f(-by * 1.4426950408889634f);
-  }
-  if constexpr (ACT == 3) return y * (1.0f - y);
-  return 1.f;
-}
-
-// forward activation (the bf16 modes' hardware-transcendental forms of mms::act_fwd_fast, without branches)
-template <int ACT>
-__device__ __forceinline__ float act_fwd(float v, float beta, float thr) {
-  if constexpr (ACT == 1) return v > 0.f ? v : 0.f;
-  if constexpr (ACT == 2) {
-    const float bx = v * beta;
-    const float e = __builtin_amdgcn_exp2f(bx * 1.4426950408889634f);
-    const float sp = __builtin_amdgcn_logf(1.0f + e) * (0.6931471805599453f * __builtin_amdgcn_rcpf(beta));
-    return bx > thr ? v : sp;
-  }
-  if constexpr (ACT == 3) return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f));
-  return v;
-}
-
-template <int PREC>
-__device__ __forceinline__ void split8(const float* v, bf16x8& hi, bf16x8& lo) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 b = (__bf16)v[j];
-    hi[j] = b;
-    if constexpr (PREC >= 2) lo[j] = (__bf16)(v[j] - (float)b);
-  }
-}
 
 template <int PREC>
 __device__ __forceinline__ void mma(floatx16& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
@@ -129,7 +51,6 @@ constexpr int kDepth = 2;           // k-steps a load is issued ahead of its use
 constexpr int kRing = kDepth + 1;   // ring slots: the one being read + kDepth in flight
 constexpr int kMaxTiles = 10;  // widest chain layer: 10 column tiles (320 units)
 constexpr int kSlot = 21;  // 1 KiB chunks per ring slot: hi + lo images of up to 10 tiles, + 1 spare (dummy loads)
-typedef __attribute__((address_space(3))) void lds_void;
 
 // Diagnostic build only (MMS_CHAIN_STAMPS=1, scripts/lib_variants.py "stamps"; the product library has none): each
 // wave accumulates s_memtime deltas per layer l -- [4 l] the k-steps' wait + barrier, [4 l + 1] ring / input issue and
@@ -162,29 +83,9 @@ __device__ __forceinline__ void stamp_seg(unsigned long long* st, unsigned long 
 #endif
 }
 
-template <int PREC>
-constexpr int nimg() { return PREC == 2 ? 2 : 1; }
-
 // loads per wave per k-step when NTL tiles are staged (uniform over the 4 waves: padded with dummy loads)
 template <int PREC, int NTL>
 constexpr int stage_per() { return (nimg<PREC>() * NTL + 3) / 4; }
-
-// wait until at most N vector-memory operations of this wave are outstanding and its LDS reads have returned,
-// then the block barrier (one asm statement with a memory clobber: no LDS read of the ring moves above either).
-// lgkmcnt(0): gfx950's back-off barrier gets no compiler-inserted wait before an asm s_barrier, so without it a
-// lagging wave's ds_read of slot (s - 1) % 3 could still be in flight when another wave's LDS-DMA overwrites that
-// slot as (s + 2) % 3.  The MFMAs already wait on those reads, so the extra wait costs nothing.
-template <int N>
-__device__ __forceinline__ void wait_vm_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-
-// 16 B per lane, global -> LDS (lane-linear at lds_addr), issued as inline asm: the compiler does not see an LDS
-// DMA, so it does not guard every later LDS read of the ring with a full vmcnt(0) drain (which waited out the
-// prefetch of the next two k-steps); the ring's ordering is the explicit wait_vm_barrier above.
-__device__ __forceinline__ void lds_dma16(const void* src, uint32_t lds_addr) {
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr) : "memory", "m0");
-}
 
 // issue k-step s's fragments of tiles [0, NTL) (hi, then lo) into ring slot s % kRing
 template <int PREC, int NT, int NTL>
@@ -202,16 +103,6 @@ __device__ __forceinline__ void stage(const ChainLayer& Ly, int s, int wave, int
     const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&ring[s % kRing][real ? c : kSlot - 1][0]);
     lds_dma16(src, __builtin_amdgcn_readfirstlane(dst));
   }
-}
-
-// compile-time loop: f(std::integral_constant<int, i>) for i in [0, N)
-template <typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 // vector-memory instructions get_b(s) issues: GE at even s, GO at odd s (none before the layer starts)
@@ -969,18 +860,34 @@ __device__ __forceinline__ int64_t perm_col(int64_t c) {
   return (c & ~(int64_t)15) | (q & 3) | ((q & 4) << 1) | ((q & 8) >> 1);
 }
 
-// one element i of a packed image (fragment-major destination: (k-step s, tile t) block, lane r + 32 h, element j)
+// 16x16x32 layout (chain16.hip): a register-fed 32-unit k-step holds units 4 g + j (j < 4) and 16 + 4 g + j - 4 of the
+// step at K position 8 g + j
+__device__ __forceinline__ int64_t perm_col16(int64_t c) {
+  const int64_t q = c & 31, gq = q >> 3, j = q & 7;
+  return (c & ~(int64_t)31) | (j < 4 ? 4 * gq + j : 16 + 4 * gq + (j - 4));
+}
+
+// one element i of a packed image, fragment-major.  permute bit 0: the register-fed column order; bit 1: the 16x16x32
+// layout ((k-step s of 32 columns, tile t of 16 rows) block, lane r + 16 (q >> 3), element q & 7) instead of 32x32x16
+// ((k-step of 16, tile of 32) block, lane r + 32 (q >> 3))
 __device__ __forceinline__ void pack_elem(const float* __restrict__ W, int64_t N, int64_t K, int64_t ldw, int transpose,
                                           int permute, int64_t rows, int64_t cols, __bf16* __restrict__ hi,
                                           __bf16* __restrict__ lo, int64_t i) {
   const int64_t R = transpose ? K : N, C = transpose ? N : K;
-  const int64_t nt = rows / 32;
+  const bool l16 = (permute & 2) != 0;
+  const int64_t nt = rows / (l16 ? 16 : 32);
   const int64_t row = i / cols, c = i - row * cols;
-  const int64_t src = permute ? perm_col(c) : c;
+  const int64_t src = (permute & 1) ? (l16 ? perm_col16(c) : perm_col(c)) : c;
   float v = 0.f;
   if (row < R && src < C) v = transpose ? W[src * ldw + row] : W[row * ldw + src];
-  const int64_t s = c >> 4, q = c & 15, t = row >> 5, r = row & 31;
-  const int64_t o = ((s * nt + t) * 64 + r + 32 * (q >> 3)) * 8 + (q & 7);
+  int64_t o;
+  if (l16) {
+    const int64_t s = c >> 5, q = c & 31, t = row >> 4, r = row & 15;
+    o = ((s * nt + t) * 64 + r + 16 * (q >> 3)) * 8 + (q & 7);
+  } else {
+    const int64_t s = c >> 4, q = c & 15, t = row >> 5, r = row & 31;
+    o = ((s * nt + t) * 64 + r + 32 * (q >> 3)) * 8 + (q & 7);
+  }
   const __bf16 b = (__bf16)v;
   hi[o] = b;
   if (lo != nullptr) lo[o] = (__bf16)(v - (float)b);
@@ -1035,7 +942,8 @@ MMS_EXPORT int mms_mlp_pack(const float* W, int64_t N, int64_t K, int64_t ldw, i
   const char* fn = "mms_mlp_pack";
   MMS_REQUIRE(N > 0 && K > 0 && ldw >= K, fn, "bad weight shape");
   MMS_REQUIRE(rows >= (transpose ? K : N) && cols >= (transpose ? N : K), fn, "packed image smaller than the weight");
-  MMS_REQUIRE(rows % 32 == 0 && cols % 16 == 0, fn, "packed image must be [32 x tiles][16 x k-steps]");
+  MMS_REQUIRE((permute & 2) ? (rows % 16 == 0 && cols % 32 == 0) : (rows % 32 == 0 && cols % 16 == 0), fn,
+              "packed image must be [32 x tiles][16 x k-steps] (16x16x32 layout: [16 x tiles][32 x k-steps])");
   MMS_REQUIRE(W && hi, fn, "null pointer");
   hipLaunchKernelGGL(pack_kernel, dim3(mms::grid_for(rows * cols, 256, 4096)), dim3(256), 0, mms::as_stream(stream), W,
                      N, K, ldw, transpose, permute, rows, cols, reinterpret_cast<__bf16*>(hi),

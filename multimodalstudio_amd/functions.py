@@ -198,7 +198,7 @@ class WeightPrep:
         return W, nrm
 
     def packed(self, W: torch.Tensor, rows: int, cols: int, transpose: bool, permute: bool, prec: int):
-        key = (W.data_ptr(), tuple(W.shape), rows, cols, bool(transpose), bool(permute), int(prec))
+        key = (W.data_ptr(), tuple(W.shape), rows, cols, bool(transpose), int(permute), int(prec))
         e = self.pack.get(key)
         N, K = W.shape
         if e is None:
@@ -541,6 +541,14 @@ class SmallRun:
 
 # the SDF taps' weight-gradient row inside the backward chain (MMS_TAP_WGRAD=0: a grouped weight-gradient item)
 TAP_WGRAD_IN_CHAIN = os.environ.get("MMS_TAP_WGRAD", "1") != "0"
+# the SDF chain at two waves per SIMD (mms_mlp_chain16: 16x16x32 MFMA tiles); MMS_CHAIN16=0: the 32x32x16 chain
+CHAIN16 = os.environ.get("MMS_CHAIN16", "1") != "0"
+
+
+def _chain16_shape(L: int, K0: int, Ns, acts, cprec: int, bcprec: int) -> bool:
+    """The chains mms_mlp_chain16 serves: the SDF MLP 71-256-256-257 (Softplus hidden layers, identity output)."""
+    return (CHAIN16 and L == 3 and 64 < K0 <= 96 and list(Ns) == [256, 256, 257] and list(acts) == [2, 2, 0]
+            and cprec in (1, 2) and bcprec in (1, 2))
 
 
 class ChainRun:
@@ -565,8 +573,9 @@ class ChainRun:
         if self.L not in (3, 4):
             raise ValueError("chains of 3 or 4 layers")
         self.beta, self.thr = float(acts[0][1]), float(acts[0][2])
+        self.l16 = False      # set per forward: the shape runs on mms_mlp_chain16
 
-    def _pack(self, W, rows: int, cols: int, transpose: bool, permute: bool, prec: Optional[int] = None):
+    def _pack(self, W, rows: int, cols: int, transpose: bool, permute: int, prec: Optional[int] = None):
         prec = self.cprec if prec is None else prec
         prep = _ACTIVE_PREP[0]
         if prep is not None:
@@ -585,6 +594,7 @@ class ChainRun:
                xaux=None, xact: int = 0, xout=None, w2row0=None, tap_part=None):
         prec = self.bcprec if backward else self.cprec
         n = self.L
+        l16 = self.l16
         VP = ctypes.c_void_p * n
         his = VP(*[p[0].data_ptr() for p in packs])
         los = VP(*[(p[1].data_ptr() if p[1] is not None else None) for p in packs])
@@ -596,6 +606,14 @@ class ChainRun:
         ns = (ctypes.c_int * n)(*Ns)
         ac = (ctypes.c_int * n)(*acts)
         cast = lambda a: ctypes.cast(a, ctypes.c_void_p)
+        if l16:
+            if xaux is not None or xout is not None:
+                raise ValueError("mms_mlp_chain16 takes no input scaling")
+            _lib.call("mms_mlp_chain16", prec, int(backward), n, X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
+                      cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux), cast(os_), cast(ldo), cast(ns),
+                      cast(ac), self.beta, self.thr, _p(w2row0), _p(tap_part),
+                      0 if tap_part is None else tap_part.stride(0), _s())
+            return
         _lib.call("mms_mlp_chain", prec, int(backward), n, X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
                   _p(xaux), 0 if xaux is None else xaux.stride(0), int(xact), _p(xout),
                   0 if xout is None else xout.stride(0), cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux),
@@ -618,9 +636,16 @@ class ChainRun:
             self.Ws.append(W)
             self.norms.append(nrm)
         Ns = [W.shape[0] for W in self.Ws]
-        nt = [(n + 31) // 32 for n in Ns]
-        packs = [self._pack(self.Ws[0], 32 * nt[0], 16 * ((K0 + 15) // 16), False, False)] + \
-                [self._pack(self.Ws[l], 32 * nt[l], 32 * nt[l - 1], False, True) for l in range(1, L)]
+        self.l16 = _chain16_shape(L, K0, Ns, [a[0] for a in self.acts], self.cprec, self.bcprec)
+        up = lambda n, k: k * ((n + k - 1) // k)  # noqa: E731
+        if self.l16:
+            # the 16x16x32 layout (permute bit 1): 16-row tiles, 32-column k-steps
+            packs = [self._pack(self.Ws[0], up(Ns[0], 16), up(K0, 32), False, 2)] + \
+                    [self._pack(self.Ws[l], up(Ns[l], 16), up(Ns[l - 1], 32), False, 3) for l in range(1, L)]
+        else:
+            nt = [(n + 31) // 32 for n in Ns]
+            packs = [self._pack(self.Ws[0], 32 * nt[0], 16 * ((K0 + 15) // 16), False, False)] + \
+                    [self._pack(self.Ws[l], 32 * nt[l], 32 * nt[l - 1], False, True) for l in range(1, L)]
         self.rows_full = M if rows_full is None else int(rows_full)
         if dense_col0 and self.rows_full != 0:
             raise ValueError("dense_col0 needs rows_full = 0")
@@ -642,8 +667,12 @@ class ChainRun:
         permuted)."""
         L = self.L
         Ns = [W.shape[0] for W in self.Ws]
-        up = lambda n, k: k * ((n + k - 1) // k)
+        up = lambda n, k: k * ((n + k - 1) // k)  # noqa: E731
         p = self.bcprec
+        if self.l16:
+            return [self._pack(self.Ws[L - 1], up(Ns[L - 2], 16), up(Ns[L - 1], 32), True, 2, p)] + \
+                   [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 16), up(Ns[l], 32), True, 3, p)
+                    for l in range(L - 2, -1, -1)]
         return [self._pack(self.Ws[L - 1], up(Ns[L - 2], 32), up(Ns[L - 1], 16), True, False, p)] + \
                [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 32), up(Ns[l], 32), True, True, p)
                 for l in range(L - 2, -1, -1)]
