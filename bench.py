@@ -53,7 +53,9 @@ DTYPES = {"fp32": "fp32",
                      "preset, fp32 elsewhere",
           "fast_x2": "bf16 MFMA (fp32 accumulate; SDF MLP chain bf16 weights x split-bf16 activations -- not a parity "
                      "preset: hessians off), fp32 elsewhere",
-          "bf16x3": "split-bf16x3 MFMA (fp32-accurate), fp32 elsewhere"}
+          "bf16x3": "split-bf16x3 MFMA (fp32-accurate), fp32 elsewhere",
+          "fast_w16": "split-bf16x3 MFMA (bf16 hi + lo operands, fp32 accumulate) for every MLP forward and data "
+                      "gradient, bf16 MFMA (fp32 accumulate) for the MLP weight gradients, fp32 elsewhere"}
 HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per lookup, forward
 HASH_BWD_B = 128 + 12 + 16 * 8 * 2 * (4 + 4)    # bytes per lookup, backward (table grads)
 HASH_BWD_ATOMIC_B = 16 * 8 * 2 * 4              # the float-atomic bytes one backward lookup adds into the table
@@ -112,11 +114,6 @@ def chain_work(a):
     return f"{PREC_NAMES[prec]}:{role}{'_bwd' if bwd else '_fwd'}", (flops, nbytes)
 
 
-def chain16_work(a):
-    """chain_work of one mms_mlp_chain16 launch (mms_mlp_chain's arguments without the input scaling: a[8:] shifted)."""
-    return chain_work(list(a[:8]) + [None] * 5 + list(a[8:]))
-
-
 def hash_fwd_work(a):
     """(role, SURVEY §8(d) bytes) of one mms_hashgrid_fwd(_grouped) launch: the SDF batch [centre | 4 taps] (the dominant
     launch), the sampler's / background's smaller 72-column panels, or the radiance panel."""
@@ -155,7 +152,7 @@ def work_fns():
         "mms_gemm_tn_grouped": gemm_grouped_work,
         "mms_gemm_tn_wide": gemm_grouped_work,
         "mms_mlp_chain": chain_work,
-        "mms_mlp_chain16": chain16_work,
+        "mms_mlp_chain16": chain_work,      # (the same arguments)
         "mms_hashgrid_fwd_grouped": hash_fwd_work,
         "mms_sdf_panel_fwd": sdf_panel_work,
         "mms_sdf_panel_rays_fwd": sdf_panel_rays_work,

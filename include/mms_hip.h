@@ -142,14 +142,16 @@ int mms_mlp_chain(int prec, int backward, int n_layers, const float* X, int64_t 
                   const void* const* a_hi, const void* const* a_lo, const float* const* bias, const float* const* aux,
                   const int64_t* ldaux, float* const* out, const int64_t* ldo, const int* N, const int* act,
                   float beta, float thr, const float* w2row0, float* tap_part, int64_t ld_tap, void* stream);
-/* The SDF chain at two waves per SIMD (16x16x32 MFMA tiles, 16 rows per wave, 8 waves per 128-row block): same
- * arguments, semantics and reference interfaces as mms_mlp_chain for the 3-layer SDF chain 71-256-256-257 (Softplus
- * hidden layers; forward with or without hidden stores, single-output rows >= rows_full; backward with the taps'
- * tap_part), prec 1 or 2, no input scaling (xaux / xout).  Weights packed with permute bit 1 set (the 16x16x32
- * layout: 16 ceil(N/16) x 32 ceil(K/32)); layers >= 1 with bit 0 too.  Replaces the same ReLU/Softplus MLP as
- * mms_mlp_chain (mlp.py:152-209 under weight norm, surface_field.py:99-116). */
+/* The SDF and radiance chains at two waves per SIMD (16x16x32 MFMA tiles, 16 rows per wave, 8 waves per 128-row
+ * block): same arguments, semantics and reference interfaces as mms_mlp_chain for the 3-layer SDF chain 71-256-256-257
+ * (Softplus hidden layers; forward with or without hidden stores and single-output rows >= rows_full; backward with
+ * the taps' tap_part) and the radiance chain 317-256-256-256 (ReLU; forward storing the hidden layers; backward with
+ * the input scaled by xaux and stored to xout, >= 32 ceil(K0/32) columns), prec 1 or 2.  Weights packed with permute
+ * bit 1 set (the 16x16x32 layout: 16 ceil(N/16) x 32 ceil(K/32)); layers >= 1 with bit 0 too.  Replaces the same
+ * weight-normed MLP as mms_mlp_chain (mlp.py:152-209; surface_field.py:99-116, radiance_field.py:72-77). */
 int mms_mlp_chain16(int prec, int backward, int n_layers, const float* X, int64_t ldx, int K0, int64_t M,
-                    int64_t rows_full, const void* const* a_hi, const void* const* a_lo, const float* const* bias,
+                    int64_t rows_full, const float* xaux, int64_t ldxaux, int xact, float* xout, int64_t ldxout,
+                    const void* const* a_hi, const void* const* a_lo, const float* const* bias,
                     const float* const* aux, const int64_t* ldaux, float* const* out, const int64_t* ldo,
                     const int* N, const int* act, float beta, float thr, const float* w2row0, float* tap_part,
                     int64_t ld_tap, void* stream);

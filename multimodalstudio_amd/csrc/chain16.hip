@@ -27,10 +27,21 @@
 
 namespace {
 
+// Diagnostic builds only (scripts/lib_variants.py "c16a<N>"; the product library has 0): ablation bits -- 1: no MFMA
+// (the fragment reads kept), 2: no weight DMA, 4: no block barrier (waits kept), 8: no epilogue VALU / stores,
+// 16: no input DMA (pre), 32: no vmcnt wait (the DMAs still issued), 64: weight DMA into the spare chunk only
+#ifndef MMS_C16_ABL
+#define MMS_C16_ABL 0
+#endif
+
+// k-steps a load is issued ahead of its use in the SDF chains (the radiance chains' LDS holds one: depth 1)
+#ifndef MMS_C16_SDF_DEPTH
+#define MMS_C16_SDF_DEPTH 1
+#endif
+
 constexpr int kW16 = 8;                 // waves per block (two per SIMD), 16 rows each
 constexpr int kRows16 = 16 * kW16;      // 128 rows per block
-constexpr int kMaxT16 = 17;             // widest staged layer: 17 tiles (the SDF's 257 outputs)
-constexpr int kSlot16 = 2 * kMaxT16 + 1;  // 1 KiB chunks per ring slot: hi + lo images, + 1 spare (dummy loads)
+constexpr int kMaxT16 = 20;             // widest layer: 20 tiles (the radiance backward's 317 input columns)
 
 template <int PREC>
 __device__ __forceinline__ void mma16(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
@@ -42,14 +53,35 @@ __device__ __forceinline__ void mma16(f32x4& acc, const bf16x8& ah, const bf16x8
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
 }
 
+// streamed inputs (layer-0 rows, xaux, the backward's Y sources) by non-temporal LDS-DMA (MMS_C16_NT, default on)
+#ifndef MMS_C16_NT
+#define MMS_C16_NT 1
+#endif
+__device__ __forceinline__ void dma_stream(const void* src, uint32_t lds_addr) {
+  if constexpr ((MMS_C16_ABL & 16) != 0) return;
+  if constexpr (MMS_C16_NT != 0) lds_dma16_nt(src, lds_addr);
+  else lds_dma16(src, lds_addr);
+}
+
+template <int N>
+__device__ __forceinline__ void wait16() {
+  if constexpr ((MMS_C16_ABL & 32) != 0)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr ((MMS_C16_ABL & 4) != 0)
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+  else
+    wait_vm_barrier<N>();
+}
+
 // LDS-DMA instructions per wave per k-step staging NT tiles (uniform over the 8 waves: padded with dummy loads)
 template <int PREC, int NT>
 constexpr int stage_per16() { return (nimg<PREC>() * NT + kW16 - 1) / kW16; }
 
-// k-step s's weight fragments of tiles [0, NT) (hi, then lo) into ring slot s & 1.  Packed images are fragment-major:
+// k-step s's weight fragments of tiles [0, NT) (hi, then lo) into ring slot s % RING.  Packed images are fragment-major:
 // fragment (k-step s, tile t) is one contiguous 1 KiB block at element ((s * NT + t) * 64 + lane) * 8.
-template <int PREC, int NT>
-__device__ __forceinline__ void stage16(const ChainLayer& Ly, int s, int wave, int lane, bf16x8 (*ring)[kSlot16][64]) {
+template <int PREC, int NT, int SLOT, int RING>
+__device__ __forceinline__ void stage16(const ChainLayer& Ly, int s, int wave, int lane, bf16x8 (*ring)[SLOT][64]) {
+  if constexpr ((MMS_C16_ABL & 2) != 0) return;
   constexpr int TOTAL = nimg<PREC>() * NT;
 #pragma unroll
   for (int i = 0; i < stage_per16<PREC, NT>(); ++i) {
@@ -60,7 +92,8 @@ __device__ __forceinline__ void stage16(const ChainLayer& Ly, int s, int wave, i
     const __bf16* base = Ly.a_hi;
     if constexpr (PREC == 2) base = img ? Ly.a_lo : Ly.a_hi;
     const __bf16* src = base + ((int64_t)(s * NT + t) * 64 + lane) * 8;
-    const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&ring[s & 1][real ? c : kSlot16 - 1][0]);
+    const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>(
+        (lds_void*)&ring[s % RING][(real && (MMS_C16_ABL & 64) == 0) ? c : SLOT - 1][0]);
     lds_dma16(src, __builtin_amdgcn_readfirstlane(dst));
   }
 }
@@ -70,31 +103,109 @@ __device__ __forceinline__ void stage16(const ChainLayer& Ly, int s, int wave, i
 // issues pre(s + 1) (PRE LDS-DMA instructions: inputs / derivative sources) and the weight DMA of step s + 1, then
 // get_b(s) (GOPS vector-memory instructions: the stores of the lazy epilogue).  The wait before step s is exact: only
 // get_b(s - 1)'s stores may stay in flight, so no store or prefetch holds a k-step up (vmcnt retires in issue order).
-template <int PREC, int NT, int KS, int GOPS, typename Pre, typename GetB>
+// The same staging through VGPRs (MMS_C16_VSTAGE): global_load_dwordx4 at step s - 1, ds_write_b128 into the slot after
+// that step's MFMAs (the loads have the whole step to land)
+#ifndef MMS_C16_VSTAGE
+#define MMS_C16_VSTAGE 0
+#endif
+template <int PREC, int NT>
+__device__ __forceinline__ void stage16_load(const ChainLayer& Ly, int s, int wave, int lane,
+                                             bf16x8 (&w)[stage_per16<PREC, NT>()]) {
+  constexpr int TOTAL = nimg<PREC>() * NT;
+#pragma unroll
+  for (int i = 0; i < stage_per16<PREC, NT>(); ++i) {
+    const int c = wave + kW16 * i;
+    const int cc = c < TOTAL ? c : 0;
+    const int img = cc / NT, t = cc - img * NT;
+    const __bf16* base = Ly.a_hi;
+    if constexpr (PREC == 2) base = img ? Ly.a_lo : Ly.a_hi;
+    w[i] = *reinterpret_cast<const bf16x8*>(base + ((int64_t)(s * NT + t) * 64 + lane) * 8);
+  }
+}
+template <int PREC, int NT, int SLOT>
+__device__ __forceinline__ void stage16_store(bf16x8 (*slot)[64], int wave, int lane,
+                                              const bf16x8 (&w)[stage_per16<PREC, NT>()]) {
+  constexpr int TOTAL = nimg<PREC>() * NT;
+#pragma unroll
+  for (int i = 0; i < stage_per16<PREC, NT>(); ++i) {
+    const int c = wave + kW16 * i;
+    if (c < TOTAL) slot[c][lane] = w[i];
+  }
+}
+
+template <int GOPS>
+constexpr int gops16(int s) { return s < 0 ? 0 : GOPS; }
+
+template <int PREC, int NT, int KS, int PRE, int GOPS, int SLOT, int DEP, typename Pre, typename GetB>
 __device__ __forceinline__ void run_layer16(const ChainLayer& Ly, int ks, int nt, f32x4 (&acc)[NT], int wave, int lane,
-                                            bf16x8 (*ring)[kSlot16][64], Pre&& pre, GetB&& get_b) {
-  wait_vm_barrier<63>();  // every wave is done with both ring slots (previous layer / launch prologue)
-  if (ks > 0) {
-    pre(0);
-    stage16<PREC, NT>(Ly, 0, wave, lane, ring);
+                                            bf16x8 (*ring)[SLOT][64], Pre&& pre, GetB&& get_b) {
+  constexpr int kDep16 = DEP, kRing16 = DEP + 1;
+  constexpr int PER = stage_per16<PREC, NT>();
+  wait16<63>();  // every wave is done with the ring slots (previous layer / launch prologue)
+  if constexpr (MMS_C16_VSTAGE != 0) {
+    static_assert(DEP == 1, "register staging: one k-step ahead");
+    bf16x8 w[PER];
+    if (ks > 0) {
+      pre(0);
+      stage16_load<PREC, NT>(Ly, 0, wave, lane, w);
+      stage16_store<PREC, NT, SLOT>(ring[0], wave, lane, w);
+    }
+    static_for<KS>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      if (s < ks) {
+        wait16<gops16<GOPS>(s - 1)>();
+        if (s + 1 < ks) {
+          pre(s + 1);
+          stage16_load<PREC, NT>(Ly, s + 1, wave, lane, w);
+        }
+        bf16x8 bh, bl;
+        get_b(s, bh, bl);
+        const bf16x8* slot = &ring[s & 1][0][0];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          if (t < nt) {
+            const bf16x8 ah = slot[t * 64 + lane];
+            const bf16x8 al = PREC == 2 ? slot[(NT + t) * 64 + lane] : ah;
+            mma16<PREC>(acc[t], ah, al, bh, bl);
+          }
+        }
+        if (s + 1 < ks) stage16_store<PREC, NT, SLOT>(ring[(s + 1) & 1], wave, lane, w);
+      }
+    });
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < kDep16; ++j) {
+    if (j < ks) {
+      pre(j);
+      stage16<PREC, NT, SLOT, kRing16>(Ly, j, wave, lane, ring);
+    }
   }
   static_for<KS>([&](auto sc) {
     constexpr int s = decltype(sc)::value;
     if (s < ks) {
-      wait_vm_barrier<(s >= 1 ? GOPS : 0)>();   // this wave's step-s loads landed, and (barrier) every wave's
-      if (s + 1 < ks) {
-        pre(s + 1);
-        stage16<PREC, NT>(Ly, s + 1, wave, lane, ring);
+      // younger than this wave's step-s loads: get_b(s - kDep16 .. s - 1) and the loads of the steps already issued
+      // after s (min(kDep16 - 1, ks - 1 - s) of them)
+      static_assert(kDep16 == 1 || kDep16 == 2, "one or two k-steps ahead");
+      constexpr int kG = gops16<GOPS>(s - 1) + (kDep16 == 2 ? gops16<GOPS>(s - 2) : 0);
+      if (kDep16 == 2 && s + 1 < ks) wait16<kG + PRE + PER>();
+      else wait16<kG>();
+      if (s + kDep16 < ks) {
+        pre(s + kDep16);
+        stage16<PREC, NT, SLOT, kRing16>(Ly, s + kDep16, wave, lane, ring);
       }
       bf16x8 bh, bl;
       get_b(s, bh, bl);
-      const bf16x8* slot = &ring[s & 1][0][0];
+      const bf16x8* slot = &ring[s % kRing16][0][0];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         if (t < nt) {
           const bf16x8 ah = slot[t * 64 + lane];
           const bf16x8 al = PREC == 2 ? slot[(NT + t) * 64 + lane] : ah;
-          mma16<PREC>(acc[t], ah, al, bh, bl);
+          if constexpr ((MMS_C16_ABL & 1) != 0)
+            asm volatile("" ::"v"(ah), "v"(al), "v"(bh), "v"(bl));
+          else
+            mma16<PREC>(acc[t], ah, al, bh, bl);
         }
       }
     }
@@ -116,11 +227,19 @@ __device__ __forceinline__ float row16_sum(float v) {
 // NT0 / NT1 / NT2 16-unit tiles; the epilogue of layer l (bias, activation, KEEP: fp32 store of 16 B per lane per tile,
 // bf16 split) runs lazily in layer l + 1's k-step s for tiles 2 s, 2 s + 1.  Backward: the same on the transposed
 // weights, last layer first; dZ = acc * act'(Y) with Y arriving by LDS-DMA, stored (for the weight gradients) and split.
-template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, bool KEEP>
+template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, int XA, bool KEEP, int DEP>
 __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
-  __shared__ __attribute__((aligned(1024))) bf16x8 ring[2][kSlot16][64];
+  constexpr int kRing16 = DEP + 1;   // ring slots: the one being read + DEP in flight
+  constexpr int NTMAX = NT0 > NT1 ? (NT0 > NT2 ? NT0 : NT2) : (NT1 > NT2 ? NT1 : NT2);
+  static_assert(NTMAX <= kMaxT16, "layer wider than the ring");
+  constexpr int SLOT = nimg<PREC>() * NTMAX + 1;   // 1 KiB chunks per ring slot: hi + lo images, + 1 spare (dummy loads)
+  __shared__ __attribute__((aligned(1024))) bf16x8 ring[kRing16][SLOT][64];
   // per-wave input slices (layer 0) and derivative sources (backward layers 1, 2): [slot][wave][2 x 64 lane chunks]
-  __shared__ __attribute__((aligned(1024))) f32x4 xring[2][kW16][2][64];
+  __shared__ __attribute__((aligned(1024))) f32x4 xring[kRing16][kW16][2][64];
+  // backward of the radiance chain (XIO): the input is scaled by the last forward ReLU's derivative (xaux, its
+  // slices beside the input's) and the scaled rows stored (xout: dZ of the last forward layer, for the weight gradients)
+  constexpr bool XIO = BWD && XA != 0;
+  __shared__ __attribute__((aligned(1024))) f32x4 aring[XIO ? kRing16 : 1][XIO ? kW16 : 1][2][64];
   __shared__ __attribute__((aligned(16))) float sbias[BWD ? 1 : 3][BWD ? 1 : 16 * kMaxT16];
   __shared__ __attribute__((aligned(16))) float sw0[BWD ? 1 : 16 * NT1];   // forward: last layer's weight row 0
   // the SDF backward: the taps' share of the last forward layer's weight-gradient row 0 (per-wave partial rows)
@@ -162,20 +281,33 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
   for (int t = 0; t < NT0; ++t) acc0[t] = zero;
   {
     const float* xr = a.X + mc * a.ldx;
+    const float* xa = XIO ? a.xaux + mc * a.ldxaux : nullptr;
+    float* xo = XIO ? a.xout + mc * a.ldxout : nullptr;
     // backward on tap rows: only input column 0 is live (a block of tap rows needs k-step 0 alone)
     const int ks0 = (BWD && !blockfull) ? 1 : KS0;
     auto pre = [&](int s) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int col = 32 * s + 8 * g + 4 * j;
-        lds_dma16(xr + (col < a.K0 ? col : 0), __builtin_amdgcn_readfirstlane(
-                      (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&xring[s & 1][wave][j][0])));
+        const int c = col < a.K0 ? col : 0;
+        dma_stream(xr + c, __builtin_amdgcn_readfirstlane(
+                              (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&xring[s % kRing16][wave][j][0])));
+        if constexpr (XIO)
+          dma_stream(xa + c, __builtin_amdgcn_readfirstlane(
+                                (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&aring[s % kRing16][wave][j][0])));
       }
     };
     auto get_b = [&](int s, bf16x8& bh, bf16x8& bl) {
       const int k0 = 32 * s + 8 * g;
-      const f32x4 x0v = xring[s & 1][wave][0][lane], x1v = xring[s & 1][wave][1][lane];
+      const f32x4 x0v = xring[s % kRing16][wave][0][lane], x1v = xring[s % kRing16][wave][1][lane];
       float v[8] = {x0v[0], x0v[1], x0v[2], x0v[3], x1v[0], x1v[1], x1v[2], x1v[3]};
+      if constexpr (XIO) {
+        // scaled first, masked after: columns past K0 hold whatever the padded rows hold (possibly non-finite)
+        const f32x4 w0 = aring[s % kRing16][wave][0][lane], w1 = aring[s % kRing16][wave][1][lane];
+        const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= act_grad_out<XA>(wv[j], a.beta, a.thr);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (k0 + j >= a.K0) v[j] = 0.f;
@@ -185,10 +317,15 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
           for (int j = 0; j < 8; ++j)
             if (k0 + j > 0) v[j] = 0.f;
         }
+        if constexpr (XIO) {
+          // xout rows hold at least 32 ks0 columns (dispatch): two unguarded 16-B stores, zeros past K0
+          st_nt4(xo + k0, f32x4{v[0], v[1], v[2], v[3]});
+          st_nt4(xo + k0 + 4, f32x4{v[4], v[5], v[6], v[7]});
+        }
       }
       split8<PREC>(v, bh, bl);
     };
-    run_layer16<PREC, NT0, KS0, 0>(a.L[0], ks0, NT0, acc0, wave, lane, ring, pre, get_b);
+    run_layer16<PREC, NT0, KS0, XIO ? 4 : 2, XIO ? 2 : 0, SLOT, DEP>(a.L[0], ks0, NT0, acc0, wave, lane, ring, pre, get_b);
   }
   if constexpr (kTapW) asm volatile("" ::"v"(x0));   // x0's load waited for here, not inside a k-loop
 
@@ -200,12 +337,12 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
       const float* yr = lp->aux + mc * lp->ldaux;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        lds_dma16(yr + 32 * s + 16 * j + 4 * g, __builtin_amdgcn_readfirstlane(
-                      (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&xring[s & 1][wave][j][0])));
+        dma_stream(yr + 32 * s + 16 * j + 4 * g, __builtin_amdgcn_readfirstlane(
+                      (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&xring[s % kRing16][wave][j][0])));
     };
   };
   auto nopre = [](int) {};
-  constexpr int kGOPS = (BWD || KEEP) ? 2 : 0;
+  constexpr int kGOPS = (MMS_C16_ABL & 8) ? 0 : ((BWD || KEEP) ? 2 : 0);
 
   // ---- layer 1
   f32x4 acc1[NT1];
@@ -215,7 +352,13 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
                   bf16x8& bl) {
     constexpr int ACT = decltype(actc)::value;
     float v[8];
-    if constexpr (!BWD) {
+    if constexpr ((MMS_C16_ABL & 8) != 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = accp[2 * s][i];
+        v[4 + i] = accp[2 * s + 1][i];
+      }
+    } else if constexpr (!BWD) {
       const f32x4 b0 = *reinterpret_cast<const f32x4*>(sb + 32 * s + 4 * g);
       const f32x4 b1 = *reinterpret_cast<const f32x4*>(sb + 32 * s + 16 + 4 * g);
 #pragma unroll
@@ -229,7 +372,7 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
         st_nt4(o + 16, f32x4{v[4], v[5], v[6], v[7]});
       }
     } else {
-      const f32x4 y0 = xring[s & 1][wave][0][lane], y1 = xring[s & 1][wave][1][lane];
+      const f32x4 y0 = xring[s % kRing16][wave][0][lane], y1 = xring[s % kRing16][wave][1][lane];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         v[i] = accp[2 * s][i] * act_grad_out<ACT>(y0[i], a.beta, a.thr);
@@ -262,9 +405,10 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
       feed(acc0, a.L[0], sbias[0], std::integral_constant<int, A0>{}, tapw, s, bh, bl);
     };
     if constexpr (BWD)
-      run_layer16<PREC, NT1, NT0 / 2, kGOPS>(a.L[1], NT0 / 2, NT1, acc1, wave, lane, ring, pre_y(a.L[0]), get_b);
+      run_layer16<PREC, NT1, NT0 / 2, 2, kGOPS, SLOT, DEP>(a.L[1], NT0 / 2, NT1, acc1, wave, lane, ring, pre_y(a.L[0]),
+                                                     get_b);
     else
-      run_layer16<PREC, NT1, NT0 / 2, kGOPS>(a.L[1], NT0 / 2, NT1, acc1, wave, lane, ring, nopre, get_b);
+      run_layer16<PREC, NT1, NT0 / 2, 0, kGOPS, SLOT, DEP>(a.L[1], NT0 / 2, NT1, acc1, wave, lane, ring, nopre, get_b);
   }
 
   // ---- layer 2 (the last)
@@ -278,9 +422,10 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
       feed(acc1, a.L[1], sbias[BWD ? 0 : 1], std::integral_constant<int, A1>{}, false, s, bh, bl);
     };
     if constexpr (BWD)
-      run_layer16<PREC, NT2, NT1 / 2, kGOPS>(a.L[2], NT1 / 2, nt2, acc2, wave, lane, ring, pre_y(a.L[1]), get_b);
+      run_layer16<PREC, NT2, NT1 / 2, 2, kGOPS, SLOT, DEP>(a.L[2], NT1 / 2, nt2, acc2, wave, lane, ring, pre_y(a.L[1]),
+                                                     get_b);
     else
-      run_layer16<PREC, NT2, NT1 / 2, kGOPS>(a.L[2], NT1 / 2, nt2, acc2, wave, lane, ring, nopre, get_b);
+      run_layer16<PREC, NT2, NT1 / 2, 0, kGOPS, SLOT, DEP>(a.L[2], NT1 / 2, nt2, acc2, wave, lane, ring, nopre, get_b);
     // epilogue: forward + bias (+ activation A2), backward dx; columns < N (forward tap rows: column 0 alone)
     if (a.L[2].out != nullptr) {
       float* orow = a.L[2].out + mc * a.L[2].ldo;
@@ -347,30 +492,46 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
   }
 }
 
-template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, bool KEEP>
+template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, int XA, bool KEEP,
+          int DEP = 1>
 void launch_chain16(const ChainArgs& a, hipStream_t s) {
   const unsigned blocks = (unsigned)((a.M + kRows16 - 1) / kRows16);
-  hipLaunchKernelGGL((chain16_kernel<PREC, KS0, NT0, NT1, NT2, BWD, A0, A1, A2, KEEP>), dim3(blocks), dim3(512), 0, s,
-                     a);
+  hipLaunchKernelGGL((chain16_kernel<PREC, KS0, NT0, NT1, NT2, BWD, A0, A1, A2, XA, KEEP, DEP>), dim3(blocks), dim3(512),
+                     0, s, a);
 }
 
-// The served chains (ks0 = ceil(K0 / 32), nt_l = ceil(N_l / 16)): the SDF MLP 71-256-256-257, Softplus(100) hidden
-// layers, identity output.  Forward: hidden layers stored (training) or not (the sampler's queries).  Backward: the
-// derivative ids of layers 1, 0, the input dY of the last layer (identity: no scaling).
+// The served chains (ks0 = ceil(K0 / 32), nt_l = ceil(N_l / 16)):
+//   SDF 71-256-256-257, Softplus(100) hidden layers, identity output (surface_field.py:99-116).  Forward with the
+//     hidden layers stored (training) or not (the sampler's queries); backward with the derivative ids of layers 1, 0.
+//   radiance 317-256-256-256, ReLU x 3 (radiance_field.py:72-77).  Forward with the hidden layers stored; backward
+//     with the input scaled by the last ReLU's derivative (xaux, stored to xout).
 template <int PREC>
 bool dispatch_chain16(int ks0, const int* nt, bool bwd, const ChainArgs& a, hipStream_t s) {
   const int a0 = a.L[0].act, a1 = a.L[1].act, a2 = a.L[2].act;
   const bool hidden_full = a.L[0].N == 256 && a.L[1].N == 256;
-  if (!bwd && ks0 == 3 && nt[0] == 16 && nt[1] == 16 && nt[2] == 17 && a0 == 2 && a1 == 2 && a2 == 0 && hidden_full) {
-    const bool keep = a.L[0].out != nullptr && a.L[1].out != nullptr;
-    const bool nokeep = a.L[0].out == nullptr && a.L[1].out == nullptr;
-    if (keep) { launch_chain16<PREC, 3, 16, 16, 17, false, 2, 2, 0, true>(a, s); return true; }
-    if (nokeep) { launch_chain16<PREC, 3, 16, 16, 17, false, 2, 2, 0, false>(a, s); return true; }
+  const bool keep = a.L[0].out != nullptr && a.L[1].out != nullptr;
+  const bool nokeep = a.L[0].out == nullptr && a.L[1].out == nullptr;
+  const bool bwd_hidden = a.L[0].aux && a.L[0].out && a.L[1].aux && a.L[1].out;
+  const bool noxa = a.xaux == nullptr && a.xout == nullptr;
+  if (!hidden_full) return false;
+  if (!bwd && ks0 == 3 && nt[0] == 16 && nt[1] == 16 && nt[2] == 17 && a0 == 2 && a1 == 2 && a2 == 0) {
+    if (keep) { launch_chain16<PREC, 3, 16, 16, 17, false, 2, 2, 0, 0, true, MMS_C16_SDF_DEPTH>(a, s); return true; }
+    if (nokeep) { launch_chain16<PREC, 3, 16, 16, 17, false, 2, 2, 0, 0, false, MMS_C16_SDF_DEPTH>(a, s); return true; }
     return false;
   }
-  if (bwd && ks0 == 9 && nt[0] == 16 && nt[1] == 16 && nt[2] == 5 && a0 == 2 && a1 == 2 && a2 == 0 && hidden_full &&
-      a.xaux == nullptr && a.xout == nullptr && a.L[0].aux && a.L[0].out && a.L[1].aux && a.L[1].out) {
-    launch_chain16<PREC, 9, 16, 16, 5, true, 2, 2, 0, false>(a, s);
+  if (bwd && ks0 == 9 && nt[0] == 16 && nt[1] == 16 && nt[2] == 5 && a0 == 2 && a1 == 2 && a2 == 0 && noxa &&
+      bwd_hidden) {
+    launch_chain16<PREC, 9, 16, 16, 5, true, 2, 2, 0, 0, false, MMS_C16_SDF_DEPTH>(a, s);
+    return true;
+  }
+  if (!bwd && ks0 == 10 && nt[0] == 16 && nt[1] == 16 && nt[2] == 16 && a0 == 1 && a1 == 1 && a2 == 1 && keep &&
+      a.rows_full >= a.M) {
+    launch_chain16<PREC, 10, 16, 16, 16, false, 1, 1, 1, 0, true>(a, s);
+    return true;
+  }
+  if (bwd && ks0 == 8 && nt[0] == 16 && nt[1] == 16 && nt[2] == 20 && a0 == 1 && a1 == 1 && a2 == 0 && bwd_hidden &&
+      a.xaux != nullptr && a.xact == 1 && a.xout != nullptr && a.ldxout >= 32 * ks0 && a.rows_full >= a.M) {
+    launch_chain16<PREC, 8, 16, 16, 20, true, 1, 1, 0, 1, false>(a, s);
     return true;
   }
   return false;
@@ -381,7 +542,8 @@ inline bool aligned16_(const void* p) { return ((uintptr_t)p & 15) == 0; }
 }  // namespace
 
 MMS_EXPORT int mms_mlp_chain16(int prec, int backward, int n_layers, const float* X, int64_t ldx, int K0, int64_t M,
-                               int64_t rows_full, const void* const* a_hi, const void* const* a_lo,
+                               int64_t rows_full, const float* xaux, int64_t ldxaux, int xact, float* xout,
+                               int64_t ldxout, const void* const* a_hi, const void* const* a_lo,
                                const float* const* bias, const float* const* aux, const int64_t* ldaux,
                                float* const* out, const int64_t* ldo, const int* N, const int* act, float beta,
                                float thr, const float* w2row0, float* tap_part, int64_t ld_tap, void* stream) {
@@ -392,9 +554,13 @@ MMS_EXPORT int mms_mlp_chain16(int prec, int backward, int n_layers, const float
   if (M == 0) return 0;
   MMS_REQUIRE(X && a_hi && N && act && out && ldo, fn, "null pointer");
   MMS_REQUIRE(aligned16_(X) && ldx % 4 == 0 && ldx >= K0, fn, "input rows must be 16-B aligned");
+  MMS_REQUIRE(!backward || xaux == nullptr || (aligned16_(xaux) && ldxaux % 4 == 0 && ldxaux >= K0), fn,
+              "xaux rows must be 16-B aligned");
+  MMS_REQUIRE(!backward || xout == nullptr || (aligned16_(xout) && ldxout % 4 == 0), fn, "xout rows must be 16-B aligned");
   ChainArgs a;
   a.X = X; a.ldx = ldx; a.K0 = K0; a.M = M; a.rows_full = rows_full < 0 ? M : rows_full;
-  a.xaux = nullptr; a.ldxaux = 0; a.xact = 0; a.xout = nullptr; a.ldxout = 0;
+  a.xaux = backward ? xaux : nullptr; a.ldxaux = ldxaux; a.xact = xact;
+  a.xout = backward ? xout : nullptr; a.ldxout = ldxout;
   a.beta = beta; a.thr = thr;
   a.w2row0 = backward ? nullptr : w2row0;
   a.tap_part = backward ? tap_part : nullptr;
@@ -430,6 +596,7 @@ MMS_EXPORT int mms_mlp_chain16(int prec, int backward, int n_layers, const float
   hipStream_t s = mms::as_stream(stream);
   const bool ok = prec == 1 ? dispatch_chain16<1>(ks0, nt, backward != 0, a, s)
                             : dispatch_chain16<2>(ks0, nt, backward != 0, a, s);
-  MMS_REQUIRE(ok, fn, "unsupported chain shape or activations (the SDF 71-256-256-257 Softplus chain only)");
+  MMS_REQUIRE(ok, fn, "unsupported chain shape or activations (SDF 71-256-256-257 Softplus and radiance "
+                      "317-256-256-256 ReLU chains only)");
   return mms::check_launch(fn);
 }

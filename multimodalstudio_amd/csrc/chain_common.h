@@ -107,6 +107,11 @@ __device__ __forceinline__ void wait_vm_barrier() {
 __device__ __forceinline__ void lds_dma16(const void* src, uint32_t lds_addr) {
   asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr) : "memory", "m0");
 }
+// the same for streamed data read once (activations): non-temporal, so it does not evict the weights every block
+// re-reads from L2
+__device__ __forceinline__ void lds_dma16_nt(const void* src, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(src), "s"(lds_addr) : "memory", "m0");
+}
 
 // compile-time loop: f(std::integral_constant<int, i>) for i in [0, N)
 template <typename F, int... I>

@@ -48,8 +48,13 @@ PRESETS = {
     "fast_m4": {"sdf": 2, "radiance": 4, "heads": 4, "pol_head": 2, "background": 4, "mlp": 0},
     "bf16x3": {"sdf": 2, "radiance": 2, "heads": 2, "pol_head": 2, "background": 2, "mlp": 2},
 }
+# weight gradients dW += dZ^T X of every chain-run MLP on bf16 operands (fp32 accumulation over the ~280k rows), the
+# forward and backward-data chains unchanged: the reference GPU's fp16 autocast runs these GEMMs on 16-bit operands too
+# (trainer.py:51); the data gradients that propagate to the SDF geometry, the hash tables and the poses keep split-bf16x3
+PRESETS["fast_w16"] = dict(PRESETS["fast"], wgrad=1)
 for _p in PRESETS.values():
     _p.setdefault("sdf_chain", 0)      # 0: the chain runs on the "sdf" GEMM precision
+    _p.setdefault("wgrad", 0)          # 0: the weight gradients on the family's backward operand mode
 # NOT a parity preset: the SDF chain on bf16 weights x split activations (mms_mlp_chain prec 3, two MFMAs per product;
 # with bf16-ROUNDED weights the SDF is a different, rippled function: 56x the reference's hessian scale off on the
 # e2e fixtures and a 24x larger curvature loss over the rgb training trajectory), kept to measure what the curvature
@@ -541,14 +546,20 @@ class SmallRun:
 
 # the SDF taps' weight-gradient row inside the backward chain (MMS_TAP_WGRAD=0: a grouped weight-gradient item)
 TAP_WGRAD_IN_CHAIN = os.environ.get("MMS_TAP_WGRAD", "1") != "0"
-# the SDF chain at two waves per SIMD (mms_mlp_chain16: 16x16x32 MFMA tiles); MMS_CHAIN16=0: the 32x32x16 chain
-CHAIN16 = os.environ.get("MMS_CHAIN16", "1") != "0"
+# the SDF / radiance chains at two waves per SIMD (mms_mlp_chain16: 16x16x32 MFMA tiles, 16 rows per wave) instead of
+# the 32x32x16 chain at one (MMS_CHAIN16=1).  Not the default: both kernels issue the same weight-staging VMEM
+# instructions per 128 rows and k-step, which bound them alike (step A/B 610k vs 622k rays/s)
+CHAIN16 = os.environ.get("MMS_CHAIN16", "0") == "1"
 
 
 def _chain16_shape(L: int, K0: int, Ns, acts, cprec: int, bcprec: int) -> bool:
-    """The chains mms_mlp_chain16 serves: the SDF MLP 71-256-256-257 (Softplus hidden layers, identity output)."""
-    return (CHAIN16 and L == 3 and 64 < K0 <= 96 and list(Ns) == [256, 256, 257] and list(acts) == [2, 2, 0]
-            and cprec in (1, 2) and bcprec in (1, 2))
+    """The chains mms_mlp_chain16 serves: the SDF MLP 71-256-256-257 (Softplus hidden layers, identity output) and the
+    radiance MLP 317-256-256-256 (ReLU)."""
+    if not (CHAIN16 and L == 3 and cprec in (1, 2) and bcprec in (1, 2)):
+        return False
+    sdf = 64 < K0 <= 96 and list(Ns) == [256, 256, 257] and list(acts) == [2, 2, 0]
+    rad = 288 < K0 <= 320 and list(Ns) == [256, 256, 256] and list(acts) == [1, 1, 1]
+    return sdf or rad
 
 
 class ChainRun:
@@ -606,15 +617,8 @@ class ChainRun:
         ns = (ctypes.c_int * n)(*Ns)
         ac = (ctypes.c_int * n)(*acts)
         cast = lambda a: ctypes.cast(a, ctypes.c_void_p)
-        if l16:
-            if xaux is not None or xout is not None:
-                raise ValueError("mms_mlp_chain16 takes no input scaling")
-            _lib.call("mms_mlp_chain16", prec, int(backward), n, X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
-                      cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux), cast(os_), cast(ldo), cast(ns),
-                      cast(ac), self.beta, self.thr, _p(w2row0), _p(tap_part),
-                      0 if tap_part is None else tap_part.stride(0), _s())
-            return
-        _lib.call("mms_mlp_chain", prec, int(backward), n, X.data_ptr(), X.stride(0), K0, X.shape[0], rows_full,
+        _lib.call("mms_mlp_chain16" if l16 else "mms_mlp_chain", prec, int(backward), n, X.data_ptr(), X.stride(0), K0,
+                  X.shape[0], rows_full,
                   _p(xaux), 0 if xaux is None else xaux.stride(0), int(xact), _p(xout),
                   0 if xout is None else xout.stride(0), cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux),
                   cast(os_), cast(ldo), cast(ns), cast(ac), self.beta, self.thr, _p(w2row0), _p(tap_part),
@@ -688,7 +692,7 @@ class ChainRun:
         acts = [a[0] for a in self.acts]
         packs = self.bwd_packs if self.bwd_packs is not None else self._bwd_packs(K0)
         # the scaled input's store writes 16 ceil(N/16) columns per row (zeros past N)
-        dZl = _alloc(M, 16 * ((Ns[L - 1] + 15) // 16), dev)[:, :Ns[L - 1]] if acts[L - 1] != 0 else None
+        dZl = _alloc(M, 32 * ((Ns[L - 1] + 31) // 32), dev)[:, :Ns[L - 1]] if acts[L - 1] != 0 else None
         dZ = [_alloc(M, Ns[l], dev) for l in range(L - 1)]
         dx = dx_out if dx_out is not None else _alloc(M, K0, dev)
         dy = dy if dy.stride(1) == 1 and dy.stride(0) % 4 == 0 else _copy_aligned(dy)
@@ -737,12 +741,13 @@ class ChainRun:
                 items.append((N, K, M, A, B, dW, db))
             wn.append((g, v, l, dW, gt, vt, N, K))
         if items:
+            wp = PRECISION.get("wgrad", 0) or self.prec     # the weight gradients' operand mode (preset "wgrad")
             if _WGRAD_DEFER[0] is not None:
-                _wgrad(lambda items=items, prec=self.prec: gemm_tn_grouped(items, prec))
+                _wgrad(lambda items=items, prec=wp: gemm_tn_grouped(items, prec))
             elif ASYNC_WGRAD and _WN_BWD[0] is not None:
-                _wgrad_async(items, self.prec, dev)
+                _wgrad_async(items, wp, dev)
             else:
-                gemm_tn_grouped(items, self.prec)
+                gemm_tn_grouped(items, wp)
         for g, v, l, dW, gt, vt, N, K in wn:
             _wn_bwd(g.reshape(-1), v, self.norms[l], dW, gt.reshape(-1) if gt is not None else
                     torch.zeros(N, device=dev), vt if vt is not None else torch.zeros(N, K, device=dev))

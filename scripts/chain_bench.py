@@ -48,8 +48,8 @@ def kernel_us(fn, reps=10):
         fn()
     torch.cuda.synchronize()
     sys.path.insert(0, ROOT)
-    from bench import chain16_work, chain_work
-    _lib.TIMER.start({"mms_mlp_chain": chain_work, "mms_mlp_chain16": chain16_work})
+    from bench import chain_work
+    _lib.TIMER.start({"mms_mlp_chain": chain_work, "mms_mlp_chain16": chain_work})
     for _ in range(reps):
         fn()
     torch.cuda.synchronize()

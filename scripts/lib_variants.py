@@ -28,6 +28,12 @@ VARIANTS = {  # name: (translation unit, macro definitions)
     "ss2k": ("loss_optim", {"MMS_SUMSQ_GRID": 2048, "MMS_SUMSQ_UNROLL": 4}),   # the round-3c launch shape
     "wpipe0": ("gemm", {"MMS_WIDE_PIPE": 0}),   # the wide weight-gradient kernel's one-register-set loop (round 3)
 }
+# the two-waves-per-SIMD chain's ablations (csrc/chain16.hip MMS_C16_ABL bits: 1 no MFMA, 2 no weight DMA, 4 no
+# barrier, 8 no epilogue)
+VARIANTS.update({f"c16a{n}": ("chain16", {"MMS_C16_ABL": n}) for n in (1, 2, 4, 8, 3, 9, 12, 6, 16, 32, 64, 48)})
+VARIANTS["c16d2"] = ("chain16", {"MMS_C16_SDF_DEPTH": 2})   # the SDF chains' weight ring two k-steps deep
+VARIANTS["c16v"] = ("chain16", {"MMS_C16_VSTAGE": 1})       # weights staged through VGPRs instead of LDS-DMA
+VARIANTS["c16nt0"] = ("chain16", {"MMS_C16_NT": 0})         # streamed inputs with the default cache policy
 
 
 def main():

@@ -81,7 +81,7 @@ def test_chain_vs_golden(dev, name, prec, chain16):
     X = _panel(f["x"], dev)
     run = fx.ChainRun(params, CASES[name], prec)
     y = run.forward(X, keep=True)
-    assert run.l16 == (chain16 and name == "geo")
+    assert run.l16 == chain16
     Y = [t.detach().clone() for t in run.Y]
     dy = _panel(f["dy"], dev)
     dx = run.backward(dy)
