@@ -121,7 +121,9 @@ int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const 
  * SDF field (71-256-256-257, Softplus(100), surface_field.py:99-116), the radiance field (317-256-256-256, ReLU,
  * radiance_field.py:72-77) and the background NeRF (n_layers = 4: base 39-256-256-256-256 and head
  * 283-256-256-256-128, ReLU, nerf_field.py:92-105).  Layers are computed transposed so each layer's MFMA
- * accumulator feeds the next layer from registers.  prec 1 = bf16, 2 = split bf16x3 operands (fp32 accumulate).
+ * accumulator feeds the next layer from registers.  prec 1 = bf16, 2 = split bf16x3 operands (fp32 accumulate),
+ * 3 = split activations x bf16 weights (SDF), 5 = fp16 operands (forward radiance / head / background chains: the
+ * reference GPU's fp16 autocast precision, trainer.py:51; fp16-packed weights, permute bit 2).
  * Per-layer arrays (a_hi, a_lo, bias, aux, ldaux, out, ldo, N, act) have n_layers entries.
  * Forward (backward = 0): out[l] = act_l(X_l W_l^T + b_l) (the hidden outs are stored together or, 3 layers, not at
  *   all); rows >= rows_full compute / store only output column 0 of the last layer (the SDF taps), in fp32 from
@@ -158,7 +160,8 @@ int mms_mlp_chain16(int prec, int backward, int n_layers, const float* X, int64_
 /* bf16 (hi, and lo = residual if non-NULL) image of W [N, K] (ldw) as an MFMA A operand of rows x cols:
  * transpose = 0 -> A = W, 1 -> A = W^T; permute bit 0 stores each k-step in register-fed order (32x32x16: columns
  * 0-3, 8-11, 4-7, 12-15 of a 16-column step; 16x16x32: K position 8 g + j <- column 4 g + j (j < 4) or 16 + 4 g +
- * j - 4 of a 32-column step).  permute bit 1 selects the 16x16x32 layout (mms_mlp_chain16).  Zero padded; rows % 32
+ * j - 4 of a 32-column step).  permute bit 1 selects the 16x16x32 layout (mms_mlp_chain16); bit 2 writes an fp16 image
+ * (hi only, fp16 bits in the 16-bit buffer: mms_mlp_chain prec 5).  Zero padded; rows % 32
  * == 0, cols % 16 == 0 (16x16x32: rows % 16, cols % 32).  Fragment-major: the fragment of (k-step s, row tile t) is
  * one 1 KiB block at element ((s * tiles + t) * 64 + lane) * 8. */
 int mms_mlp_pack(const float* W, int64_t N, int64_t K, int64_t ldw, int transpose, int permute, int64_t rows,

@@ -63,6 +63,13 @@ __device__ __forceinline__ void dma_stream(const void* src, uint32_t lds_addr) {
   else lds_dma16(src, lds_addr);
 }
 
+// per-wave streamed inputs (layer-0 rows, xaux, the backward's Y sources) loaded straight into VGPRs one k-step ahead
+// (MMS_C16_VIN) instead of by LDS-DMA; the k-step then consumes them (get_b) BEFORE issuing the next step's loads, so the
+// compiler's own vmcnt waits never count the invisible weight DMAs issued after a load
+#ifndef MMS_C16_VIN
+#define MMS_C16_VIN 0
+#endif
+
 template <int N>
 __device__ __forceinline__ void wait16() {
   if constexpr ((MMS_C16_ABL & 32) != 0)
@@ -174,6 +181,35 @@ __device__ __forceinline__ void run_layer16(const ChainLayer& Ly, int ks, int nt
     });
     return;
   }
+  if constexpr (MMS_C16_VIN != 0) {
+    static_assert(DEP == 1, "VGPR-staged inputs: one k-step ahead");
+    if (ks > 0) {
+      pre(0);
+      stage16<PREC, NT, SLOT, kRing16>(Ly, 0, wave, lane, ring);
+    }
+    static_for<KS>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      if (s < ks) {
+        wait16<0>();   // step s's loads and DMAs landed, and get_b(s - 1)'s stores (issued before them) retired
+        bf16x8 bh, bl;
+        get_b(s, bh, bl);
+        if (s + 1 < ks) {
+          pre(s + 1);
+          stage16<PREC, NT, SLOT, kRing16>(Ly, s + 1, wave, lane, ring);
+        }
+        const bf16x8* slot = &ring[s & 1][0][0];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          if (t < nt) {
+            const bf16x8 ah = slot[t * 64 + lane];
+            const bf16x8 al = PREC == 2 ? slot[(NT + t) * 64 + lane] : ah;
+            mma16<PREC>(acc[t], ah, al, bh, bl);
+          }
+        }
+      }
+    });
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < kDep16; ++j) {
     if (j < ks) {
@@ -275,6 +311,7 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
     }
   }
 
+  f32x4 vin[2][2], vina[2][2];   // MMS_C16_VIN: the streamed inputs' register ring [slot][piece]
   // ---- layer 0: B operand from memory (lane (r, g) takes columns 32 s + 8 g .. + 7 of its row), natural K order
   f32x4 acc0[NT0];
 #pragma unroll
@@ -290,6 +327,11 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
       for (int j = 0; j < 2; ++j) {
         const int col = 32 * s + 8 * g + 4 * j;
         const int c = col < a.K0 ? col : 0;
+        if constexpr (MMS_C16_VIN != 0) {
+          vin[s & 1][j] = ld_nt4(xr + c);
+          if constexpr (XIO) vina[s & 1][j] = ld_nt4(xa + c);
+          continue;
+        }
         dma_stream(xr + c, __builtin_amdgcn_readfirstlane(
                               (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&xring[s % kRing16][wave][j][0])));
         if constexpr (XIO)
@@ -299,11 +341,13 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
     };
     auto get_b = [&](int s, bf16x8& bh, bf16x8& bl) {
       const int k0 = 32 * s + 8 * g;
-      const f32x4 x0v = xring[s % kRing16][wave][0][lane], x1v = xring[s % kRing16][wave][1][lane];
+      const f32x4 x0v = MMS_C16_VIN ? vin[s & 1][0] : xring[s % kRing16][wave][0][lane];
+      const f32x4 x1v = MMS_C16_VIN ? vin[s & 1][1] : xring[s % kRing16][wave][1][lane];
       float v[8] = {x0v[0], x0v[1], x0v[2], x0v[3], x1v[0], x1v[1], x1v[2], x1v[3]};
       if constexpr (XIO) {
         // scaled first, masked after: columns past K0 hold whatever the padded rows hold (possibly non-finite)
-        const f32x4 w0 = aring[s % kRing16][wave][0][lane], w1 = aring[s % kRing16][wave][1][lane];
+        const f32x4 w0 = MMS_C16_VIN ? vina[s & 1][0] : aring[s % kRing16][wave][0][lane];
+        const f32x4 w1 = MMS_C16_VIN ? vina[s & 1][1] : aring[s % kRing16][wave][1][lane];
         const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= act_grad_out<XA>(wv[j], a.beta, a.thr);
@@ -337,7 +381,10 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
       const float* yr = lp->aux + mc * lp->ldaux;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        dma_stream(yr + 32 * s + 16 * j + 4 * g, __builtin_amdgcn_readfirstlane(
+        if constexpr (MMS_C16_VIN != 0)
+          vin[s & 1][j] = ld_nt4(yr + 32 * s + 16 * j + 4 * g);
+        else
+          dma_stream(yr + 32 * s + 16 * j + 4 * g, __builtin_amdgcn_readfirstlane(
                       (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&xring[s % kRing16][wave][j][0])));
     };
   };
@@ -372,7 +419,8 @@ __global__ __launch_bounds__(512) void chain16_kernel(ChainArgs a) {
         st_nt4(o + 16, f32x4{v[4], v[5], v[6], v[7]});
       }
     } else {
-      const f32x4 y0 = xring[s % kRing16][wave][0][lane], y1 = xring[s % kRing16][wave][1][lane];
+      const f32x4 y0 = MMS_C16_VIN ? vin[s & 1][0] : xring[s % kRing16][wave][0][lane];
+      const f32x4 y1 = MMS_C16_VIN ? vin[s & 1][1] : xring[s % kRing16][wave][1][lane];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         v[i] = accp[2 * s][i] * act_grad_out<ACT>(y0[i], a.beta, a.thr);

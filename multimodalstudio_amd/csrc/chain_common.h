@@ -76,8 +76,19 @@ __device__ __forceinline__ float act_fwd(float v, float beta, float thr) {
   return v;
 }
 
+// PREC 5: fp16 operands (the reference GPU's autocast precision, trainer.py:51), one image, the fp16 bits carried in the
+// bf16x8 vector type (mma reinterprets them)
 template <int PREC>
 __device__ __forceinline__ void split8(const float* v, bf16x8& hi, bf16x8& lo) {
+  if constexpr (PREC == 5) {
+    typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+    f16x8 h;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h[j] = (_Float16)v[j];
+    hi = __builtin_bit_cast(bf16x8, h);
+    lo = hi;
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const __bf16 b = (__bf16)v[j];

@@ -37,6 +37,12 @@ __device__ __forceinline__ void mma(floatx16& acc, const bf16x8& ah, const bf16x
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
   }
   if constexpr (PREC == 3) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  if constexpr (PREC == 5) {
+    typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, ah), __builtin_bit_cast(f16x8, bh), acc, 0,
+                                                 0, 0);
+    return;
+  }
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
 }
 
@@ -793,7 +799,7 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
       else launch_chain<PREC, 5, 8, 8, 9, false, 2, 2, 0, 0, false>(a, s);
       return true;
     }
-    if constexpr (PREC != 3) {   // (split activations: the SDF chains only)
+    if constexpr (PREC != 3 && PREC != 5) {   // (split activations: the SDF chains only; fp16: forward only)
       if (!bwd && ks0 == 20 && nt[0] == 8 && nt[1] == 8 && nt[2] == 8 && a0 == 1 && a1 == 1 && a2 == 1 &&
           hidden_full && keep) {
         launch_chain<PREC, 20, 8, 8, 8, false, 1, 1, 1, 0, true>(a, s);
@@ -809,6 +815,20 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
         a.xout == nullptr && bwd_hidden) {
       launch_chain<PREC, 17, 8, 8, 3, true, 2, 2, 0, 0>(a, s);
       return true;
+    }
+    if constexpr (PREC == 5) {
+      // fp16 forward chains: radiance 317-256-256-256 ReLU, the plain / polarization heads 256-64-64-C
+      if (!bwd && ks0 == 20 && nt[0] == 8 && nt[1] == 8 && nt[2] == 8 && a0 == 1 && a1 == 1 && a2 == 1 &&
+          hidden_full && keep) {
+        launch_chain<PREC, 20, 8, 8, 8, false, 1, 1, 1, 0, true>(a, s);
+        return true;
+      }
+      if (!bwd && ks0 == 16 && nt[0] == 2 && nt[1] == 2 && nt[2] == 1 && a0 == 1 && a1 == 1 && hidden64 && keep &&
+          (a2 == 3 || a2 == 0)) {
+        if (a2 == 3) launch_chain<PREC, 16, 2, 2, 1, false, 1, 1, 3, 0, true>(a, s);
+        else launch_chain<PREC, 16, 2, 2, 1, false, 1, 1, 0, 0, true>(a, s);
+        return true;
+      }
     }
     if constexpr (PREC == 1 || PREC == 2) {
       // the plain modality heads 256-64-64-C (ReLU, ReLU, Sigmoid; field_heads.py:71-88), C <= 32, bf16 or split-bf16x3
@@ -836,8 +856,8 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
     }
     return false;
   }
-  // 4-layer chains: the background MLPs, bf16 or split-bf16x3
-  if constexpr (PREC == 1 || PREC == 2) {
+  // 4-layer chains: the background MLPs, bf16 or split-bf16x3 (fp16: forward only)
+  if constexpr (PREC == 1 || PREC == 2 || PREC == 5) {
     if (nl != 4 || nt[0] != 8 || nt[1] != 8 || nt[2] != 8 || a0 != 1 || a1 != 1 || a2 != 1) return false;
     if (!bwd && hidden_full && keep && a3 == 1) {
       // base 39-256x4 (NeRF background), head 283-256-256-256-128 (NeRF) / -256 (config-5 grid background)
@@ -845,7 +865,7 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
       if (ks0 == 18 && nt[3] == 4) { launch_chain<PREC, 18, 8, 8, 4, false, 1, 1, 1, 0, true, 4>(a, s); return true; }
       if (ks0 == 18 && nt[3] == 8) { launch_chain<PREC, 18, 8, 8, 8, false, 1, 1, 1, 0, true, 4>(a, s); return true; }
     }
-    if (bwd && a3 == 0 && xio && bwd_hidden) {
+    if (PREC != 5 && bwd && a3 == 0 && xio && bwd_hidden) {
       if (ks0 == 16 && nt[3] == 2) { launch_chain<PREC, 16, 8, 8, 2, true, 1, 1, 0, 1, false, 4>(a, s); return true; }
       if (ks0 == 8 && nt[3] == 9) { launch_chain<PREC, 8, 8, 8, 9, true, 1, 1, 0, 1, false, 4>(a, s); return true; }
       if (ks0 == 16 && nt[3] == 9) { launch_chain<PREC, 16, 8, 8, 9, true, 1, 1, 0, 1, false, 4>(a, s); return true; }
@@ -887,6 +907,10 @@ __device__ __forceinline__ void pack_elem(const float* __restrict__ W, int64_t N
   } else {
     const int64_t s = c >> 4, q = c & 15, t = row >> 5, r = row & 31;
     o = ((s * nt + t) * 64 + r + 32 * (q >> 3)) * 8 + (q & 7);
+  }
+  if (permute & 4) {   // fp16 image (bits stored in the bf16 buffer; mms_mlp_chain prec 5)
+    hi[o] = __builtin_bit_cast(__bf16, (_Float16)v);
+    return;
   }
   const __bf16 b = (__bf16)v;
   hi[o] = b;
@@ -958,7 +982,8 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
                              float* const* out, const int64_t* ldo, const int* N, const int* act, float beta,
                              float thr, const float* w2row0, float* tap_part, int64_t ld_tap, void* stream) {
   const char* fn = "mms_mlp_chain";
-  MMS_REQUIRE(prec >= 1 && prec <= 3, fn, "prec must be 1 (bf16), 2 (split bf16x3) or 3 (split activations)");
+  MMS_REQUIRE((prec >= 1 && prec <= 3) || prec == 5, fn,
+              "prec must be 1 (bf16), 2 (split bf16x3), 3 (split activations) or 5 (fp16, forward chains)");
   MMS_REQUIRE(n_layers == 3 || n_layers == 4, fn, "chains of 3 or 4 layers");
   MMS_REQUIRE(M >= 0 && K0 > 0, fn, "bad shape");
   if (M == 0) return 0;
@@ -1007,6 +1032,7 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
   hipStream_t s = mms::as_stream(stream);
   const bool ok = prec == 1   ? dispatch_chain<1>(n_layers, ks0, nt, backward != 0, a, s)
                   : prec == 2 ? dispatch_chain<2>(n_layers, ks0, nt, backward != 0, a, s)
+                  : prec == 5 ? dispatch_chain<5>(n_layers, ks0, nt, backward != 0, a, s)
                               : dispatch_chain<3>(n_layers, ks0, nt, backward != 0, a, s);
   MMS_REQUIRE(ok, fn, "unsupported chain shape or activations (SDF 71-256-256-257 Softplus, radiance 317-256-256-256 "
                       "ReLU, background 39-256x4 and 283-256-256-256-128 ReLU chains only)");

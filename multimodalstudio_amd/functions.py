@@ -52,6 +52,11 @@ PRESETS = {
 # forward and backward-data chains unchanged: the reference GPU's fp16 autocast runs these GEMMs on 16-bit operands too
 # (trainer.py:51); the data gradients that propagate to the SDF geometry, the hash tables and the poses keep split-bf16x3
 PRESETS["fast_w16"] = dict(PRESETS["fast"], wgrad=1)
+# the reference GPU's own forward precision for the radiance, head and background MLPs: their forward chains on fp16
+# operands (one fp16 MFMA per product, fp32 accumulation -- autocast "16-mixed", trainer.py:51), their backward-data
+# chains and weight gradients split-bf16x3 (wider than the reference's fp16 backward: no loss scaling needed); the SDF
+# chain stays split-bf16x3 throughout (its 4-tap hessians)
+PRESETS["fast_h16"] = dict(PRESETS["fast"], radiance=5, heads=5, pol_head=5, background=5)
 for _p in PRESETS.values():
     _p.setdefault("sdf_chain", 0)      # 0: the chain runs on the "sdf" GEMM precision
     _p.setdefault("wgrad", 0)          # 0: the weight gradients on the family's backward operand mode
@@ -64,13 +69,14 @@ PRECISION = dict(PRESETS["fp32"])
 
 
 def fwd_prec(p: int) -> int:
-    """GEMM / chain operand mode of a family's forward: PRECISION value 4 = split-bf16x3 forward, bf16 backward."""
+    """GEMM / chain operand mode of a family's forward: PRECISION value 4 = split-bf16x3 forward, bf16 backward; 5 =
+    fp16 forward (the fused chain), split-bf16x3 backward."""
     return 2 if p == 4 else p
 
 
 def bwd_prec(p: int) -> int:
     """... and of its backward (data and weight gradients)."""
-    return 1 if p == 4 else p
+    return 1 if p == 4 else (2 if p == 5 else p)
 
 
 def set_precision(mode: str) -> None:
@@ -572,14 +578,15 @@ class ChainRun:
 
     def __init__(self, params: Sequence[torch.Tensor], acts: Sequence[Tuple[int, float, float]], prec: int,
                  chain_prec: int = 0):
-        if prec not in (1, 2, 4):
-            raise ValueError("the fused chain runs the bf16 (1), split-bf16x3 (2) and x3-forward (4) modes")
+        if prec not in (1, 2, 4, 5):
+            raise ValueError("the fused chain runs the bf16 (1), split-bf16x3 (2), x3-forward (4) and fp16-forward (5) "
+                             "modes")
         self.params, self.acts = list(params), list(acts)
         # the forward chain's operand mode (or chain_prec 3: split activations x bf16 weights); the backward chain and
         # the weight gradients run bwd_prec (mode 4: split-bf16x3 forward, bf16 backward)
         self.prec = bwd_prec(int(prec))
         self.cprec = int(chain_prec) or fwd_prec(int(prec))
-        self.bcprec = self.prec if int(prec) == 4 else self.cprec
+        self.bcprec = self.prec if int(prec) in (4, 5) else self.cprec
         self.L = len(self.params) // 3
         if self.L not in (3, 4):
             raise ValueError("chains of 3 or 4 layers")
@@ -588,6 +595,8 @@ class ChainRun:
 
     def _pack(self, W, rows: int, cols: int, transpose: bool, permute: int, prec: Optional[int] = None):
         prec = self.cprec if prec is None else prec
+        if prec == 5:
+            permute = int(permute) | 4      # fp16 image (mms_mlp_pack permute bit 2), hi only
         prep = _ACTIVE_PREP[0]
         if prep is not None:
             return prep.packed(W, rows, cols, transpose, permute, prec)
@@ -1237,8 +1246,8 @@ def _chain_shape(params, acts, prec: int = 2) -> bool:
         if (dims == [71, 256, 256, 257] and a == (2, 2, 0)) or (dims == [317, 256, 256, 256] and a == (1, 1, 1)):
             return True
         # the modality heads 256-64-64-C, C <= 32: plain (Sigmoid out) and polarization (Stokes, no out activation)
-        return prec in (1, 2, 4) and dims[:3] == [256, 64, 64] and dims[3] <= 32 and a in ((1, 1, 3), (1, 1, 0))
-    if len(params) == 12 and prec in (1, 2, 4) and a == (1, 1, 1, 1):
+        return prec in (1, 2, 4, 5) and dims[:3] == [256, 64, 64] and dims[3] <= 32 and a in ((1, 1, 3), (1, 1, 0))
+    if len(params) == 12 and prec in (1, 2, 4, 5) and a == (1, 1, 1, 1):
         return dims in ([39, 256, 256, 256, 256], [283, 256, 256, 256, 128], [283, 256, 256, 256, 256])
     return False
 
@@ -1249,6 +1258,8 @@ def mlp_runner(params, acts, prec: int):
     every precision)."""
     if prec != 0 and _chain_shape(params, acts, prec):
         return ChainRun(params, acts, prec)
+    if prec == 5:
+        prec = 2        # fp16 forwards are a fused-chain mode: other shapes keep split-bf16x3
     if SmallRun.serves(params, acts, prec):
         return SmallRun(params, acts, prec)
     return MLPRun(params, acts, prec)

@@ -4,6 +4,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+export MMS_CHAIN16=${MMS_CHAIN16:-1}
 for v in ${VARIANTS:-base}; do
   echo "== $v" >> gpurun_out/abl.log
   if [ $v = base ]; then

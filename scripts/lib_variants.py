@@ -34,6 +34,7 @@ VARIANTS.update({f"c16a{n}": ("chain16", {"MMS_C16_ABL": n}) for n in (1, 2, 4, 
 VARIANTS["c16d2"] = ("chain16", {"MMS_C16_SDF_DEPTH": 2})   # the SDF chains' weight ring two k-steps deep
 VARIANTS["c16v"] = ("chain16", {"MMS_C16_VSTAGE": 1})       # weights staged through VGPRs instead of LDS-DMA
 VARIANTS["c16nt0"] = ("chain16", {"MMS_C16_NT": 0})         # streamed inputs with the default cache policy
+VARIANTS["c16vin"] = ("chain16", {"MMS_C16_VIN": 1})        # streamed inputs into VGPRs instead of LDS-DMA
 
 
 def main():

@@ -336,3 +336,64 @@ def test_chain_head(dev, C, prec, out):
     assert rel(dx.cpu(), d) < TOL[1]
     for i, p in enumerate(params):
         assert rel(p.grad.cpu(), ref[i]) < TOL[1], (i, rel(p.grad.cpu(), ref[i]))
+
+
+@pytest.mark.parametrize("dims,acts", [
+    ([317, 256, 256, 256], [(1, 1.0, 20.0)] * 3),                                   # radiance
+    ([256, 64, 64, 3], [(1, 1.0, 20.0), (1, 1.0, 20.0), (3, 1.0, 20.0)]),         # plain head (Sigmoid)
+    ([256, 64, 64, 3], [(1, 1.0, 20.0), (1, 1.0, 20.0), (0, 1.0, 20.0)]),         # polarization head (Stokes)
+    ([39, 256, 256, 256, 256], [(1, 1.0, 20.0)] * 4),                              # background base
+    ([283, 256, 256, 256, 128], [(1, 1.0, 20.0)] * 4)])                            # background head
+def test_chain_fp16_forward(dev, dims, acts):
+    """Preset fast_h16: the radiance / head / background forward chains on fp16 operands (mms_mlp_chain prec 5, one
+    fp16 MFMA per product, fp32 accumulation -- the reference GPU's autocast precision).  Forward vs fp64 within 3e-3
+    of each output's scale (fp16's 11-bit operands over K <= 317); the backward chain of the same run is split-bf16x3
+    and is checked against the fp64 backward taken at the kernel's own activations to the split-bf16x3 bound."""
+    from multimodalstudio_amd import functions as fx
+    g = torch.Generator().manual_seed(sum(dims))
+    L = len(dims) - 1
+    params = []
+    for k, n in zip(dims[:-1], dims[1:]):
+        v = torch.randn(n, k, generator=g) / k ** 0.5
+        params += [torch.linalg.vector_norm(v, dim=1, keepdim=True).to(dev).requires_grad_(True),
+                   v.to(dev).requires_grad_(True), (torch.randn(n, generator=g) * 0.1).to(dev).requires_grad_(True)]
+    assert fx._chain_shape(params, acts, 5)
+    M = 3000
+    x = torch.randn(M, dims[0], generator=g) * 0.5
+    run = fx.ChainRun(params, acts, 5)
+    assert run.cprec == 5 and run.bcprec == 2
+    y = run.forward(_panel(x, dev), keep=True)
+    Y = [t.detach().clone() for t in run.Y]
+    h = x.double()
+    for l in range(L):
+        gg, v, b = [p.detach().double().cpu() for p in params[3 * l: 3 * l + 3]]
+        h = h @ torch._weight_norm(v, gg, 0).T + b
+        act = acts[l][0]
+        h = torch.relu(h) if act == 1 else (torch.sigmoid(h) if act == 3 else h)
+    e_fwd = rel(y.detach().cpu(), h)
+    dy = torch.randn(M, dims[-1], generator=g)
+    dx = run.backward(_panel(dy, dev))
+    torch.cuda.synchronize()
+    # fp64 backward at the kernel's own activations (ReLU / Sigmoid derivatives from its outputs)
+    ins = [x.double()] + [t.double().cpu() for t in Y[:L - 1]]
+    d = dy.double()
+    errs = {}
+    for l in range(L - 1, -1, -1):
+        act = acts[l][0]
+        yl = Y[l].double().cpu()
+        if act == 1:
+            d = d * (yl > 0)
+        elif act == 3:
+            d = d * yl * (1 - yl)
+        gg = params[3 * l].detach().double().cpu().requires_grad_(True)
+        v = params[3 * l + 1].detach().double().cpu().requires_grad_(True)
+        W = torch._weight_norm(v, gg, 0)
+        W.backward(d.T @ ins[l])
+        errs[f"v{l}"] = rel(params[3 * l + 1].grad.cpu(), v.grad)
+        errs[f"b{l}"] = rel(params[3 * l + 2].grad.cpu(), d.sum(0))
+        d = d @ W.detach()
+    errs["dx"] = rel(dx.cpu(), d)
+    print(dims, f"fp16 forward rel {e_fwd:.2e}", {k: f"{v:.1e}" for k, v in errs.items()})
+    assert e_fwd < 3e-3
+    for k, v in errs.items():
+        assert v < TOL[2], (k, v)

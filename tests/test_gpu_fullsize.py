@@ -32,7 +32,8 @@ not a kernel error: measured (scripts/fullsize_diag.py) on the rays whose bins a
     Loss within 1e-4 of the reference, hit mask and counts exact;
   * the free-running step (the HIP sampler on the HIP SDF): the loss, the hit mask, the share of rays whose bins agree
     to 2e-5 and the radiance on those rays;
-  * the benchmarked `fast` preset on the reference's samples, at the small fixtures' fast bounds.
+  * the throughput presets (fast_h16, benchmarked, and fast) on the reference's samples, at the small fixtures' fast
+    bounds.
 """
 import os
 
@@ -40,7 +41,7 @@ import numpy as np
 import pytest
 import torch
 
-from test_gpu_e2e import GEO_TOL_FAST, GOLD, E2ECase, load, rel_err, rel_l2
+from test_gpu_e2e import FAST_PRESETS, GEO_TOL_FAST, GOLD, E2ECase, load, rel_err, rel_l2
 
 pytestmark = pytest.mark.gpu
 NAME = "e2e_full_grid_rgb_l19"
@@ -200,12 +201,13 @@ def test_fullsize_free_running(dev):
     assert e[agree].max() / scale < 2e-4   # measured 5e-5
 
 
-def test_fullsize_fast_preset(dev):
-    """The benchmarked `fast` preset (every MLP on split-bf16x3) on the reference's samples: the small fixtures'
-    fast bounds (test_gpu_e2e.test_e2e_fast_preset_deviation)."""
+@pytest.mark.parametrize("preset", FAST_PRESETS)
+def test_fullsize_fast_preset(dev, preset):
+    """The throughput presets (the benchmarked fast_h16 and the all-split-bf16x3 fast) on the reference's samples: the
+    small fixtures' fast bounds (test_gpu_e2e.test_e2e_fast_preset_deviation)."""
     from multimodalstudio_amd import functions as fx
     f = load(NAME)
-    fx.set_precision("fast")
+    fx.set_precision(preset)
     try:
         case = E2ECase(f, dev, inject_bins=True)
         outs, losses, total = case.run_step(granule_cap(f), batched=True)
@@ -218,7 +220,7 @@ def test_fullsize_fast_preset(dev):
     rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-2)
     n = int(outs["rgb"]["count"].item())
     geo = {k: rel_err(outs["rgb"][k][:n].detach().cpu(), f[f"rgb:out:{k}"]) for k in ("gradients", "hessians")}
-    print(f"fast full-size: loss rel {loss_rel:.3e}, radiance rel mean {rel.mean():.3e} max {rel.max():.3e}, {geo}")
+    print(f"{preset} full-size: loss rel {loss_rel:.3e}, radiance rel mean {rel.mean():.3e} max {rel.max():.3e}, {geo}")
     assert loss_rel < 2e-4
     assert rel.mean() < 3e-4 and rel.max() < 2.5e-2
     for k, e in geo.items():

@@ -20,7 +20,10 @@ import pytest
 import torch
 
 # the benchmarked preset under test (MMS_FAST_PRESET overrides it)
-FAST = os.environ.get("MMS_FAST_PRESET", "fast")
+# the throughput presets under the gate: the benchmarked one (fast_h16: fp16 radiance / head / background forwards, the
+# reference GPU's autocast precision) and the all-split-bf16x3 one (MMS_FAST_PRESET picks one alone)
+FAST_PRESETS = [os.environ["MMS_FAST_PRESET"]] if "MMS_FAST_PRESET" in os.environ else ["fast_h16", "fast"]
+FAST = FAST_PRESETS[0]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden", "train_parity_rgb.npz")
@@ -220,8 +223,9 @@ def test_train_parity_fp32(dev):
 
 
 @pytest.mark.gpu
-def test_train_parity_fast_preset(dev):
-    cfg, runs, means = _repeated(dev, FAST)
+@pytest.mark.parametrize("precision", FAST_PRESETS)
+def test_train_parity_fast_preset(dev, precision):
+    cfg, runs, means = _repeated(dev, precision)
     for _, _, losses, _, ref, rel in runs:
         assert abs(losses.mean() - ref.mean()) / ref.mean() < 2e-2
     _check_psnr(cfg, means)
@@ -232,7 +236,7 @@ GOLD_BG5 = os.path.join(HERE, "golden", "train_parity_bg5.npz")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("precision", ["fp32", FAST])
+@pytest.mark.parametrize("precision", ["fp32"] + FAST_PRESETS)
 def test_train_parity_grid_raw_5mod(dev, precision):
     """BASELINE configs[2] shape (grid_raw, five mosaicked modalities incl. polarization with saturated highlights, the
     45-training-view scene): mean dPSNR over the 16 seeded fixtures within 0.1 dB per modality at every checkpoint of a
@@ -247,7 +251,7 @@ def test_train_parity_grid_raw_5mod(dev, precision):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("precision", ["fp32", FAST])
+@pytest.mark.parametrize("precision", ["fp32"] + FAST_PRESETS)
 def test_train_parity_config5(dev, precision):
     """BASELINE configs[4] shape (grid_raw_grid_bg_unbalanced: rgb + polarization on 10 of its 45 views, hash-grid
     background with 3-layer heads, SO3xR3 pose refinement): the first steps' losses and the seeds' mean dPSNR as the
