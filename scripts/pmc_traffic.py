@@ -16,7 +16,7 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PREC = {"0": "fp32", "1": "bf16", "2": "bf16x3", "3": "bf16x2"}
+PREC = {"0": "fp32", "1": "bf16", "2": "bf16x3", "3": "bf16x2", "5": "fp16"}
 MODE = {("false", "false"): "NT", ("false", "true"): "NN", ("true", "true"): "TN"}
 
 
