@@ -43,8 +43,8 @@ BF16_MFMA_PEAK_TF = 2500.0  # dense bf16 MFMA peak (no sparsity), MI355X_MICROAR
 # split-bf16x3 runs 3 bf16 MFMAs per f32 product: its ceiling for the algorithmic 2MNK flops is a third
 # (bf16x2: the SDF chain's split activations x bf16 weights, 2 bf16 MFMAs per product)
 MFMA_PEAK_TF = {"fp32": F32_MFMA_PEAK_TF, "bf16": BF16_MFMA_PEAK_TF, "bf16x3": BF16_MFMA_PEAK_TF / 3,
-                "bf16x2": BF16_MFMA_PEAK_TF / 2, "fp16": BF16_MFMA_PEAK_TF}
-PREC_NAMES = {0: "fp32", 1: "bf16", 2: "bf16x3", 3: "bf16x2", 5: "fp16"}
+                "bf16x2": BF16_MFMA_PEAK_TF / 2, "fp16": BF16_MFMA_PEAK_TF, "fp16-rowscaled": BF16_MFMA_PEAK_TF}
+PREC_NAMES = {0: "fp32", 1: "bf16", 2: "bf16x3", 3: "bf16x2", 5: "fp16", 6: "fp16-rowscaled"}
 DTYPES = {"fp32": "fp32",
           "fast": "split-bf16x3 MFMA (bf16 hi + lo operands, fp32 accumulate) for every MLP, fp32 elsewhere",
           "fast_bf16": "bf16 MFMA (fp32 accumulate; SDF MLP and polarization heads split-bf16x3) -- not a parity "
@@ -57,7 +57,11 @@ DTYPES = {"fp32": "fp32",
           "fast_w16": "split-bf16x3 MFMA (bf16 hi + lo operands, fp32 accumulate) for every MLP forward and data "
                       "gradient, bf16 MFMA (fp32 accumulate) for the MLP weight gradients, fp32 elsewhere",
           "fast_h16": "fp16 MFMA (fp32 accumulate: the reference's autocast) for the radiance / head / background MLP "
-                      "forwards, split-bf16x3 for their backward and for the SDF MLP, fp32 elsewhere"}
+                      "forwards, split-bf16x3 for their backward and for the SDF MLP, fp32 elsewhere",
+          "fast_h16b": "fp16 MFMA (fp32 accumulate: the reference's autocast) for the radiance / head / background MLP "
+                       "forwards and for every MLP's backward-data chain after its first layer (per-row power-of-two "
+                       "scaled), split-bf16x3 for the SDF MLP forward, the chains' first backward layer and the weight "
+                       "gradients, fp32 elsewhere"}
 HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per lookup, forward
 HASH_BWD_B = 128 + 12 + 16 * 8 * 2 * (4 + 4)    # bytes per lookup, backward (table grads)
 HASH_BWD_ATOMIC_B = 16 * 8 * 2 * 4              # the float-atomic bytes one backward lookup adds into the table
@@ -369,7 +373,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--precision", default="fast_h16", choices=list(DTYPES),
+    ap.add_argument("--precision", default="fast_h16b", choices=list(DTYPES),
                     help="MLP GEMM precision preset (functions.PRESETS); fp32 = reference-parity mode")
     ap.add_argument("--sampler", default="device", choices=["device", "host"],
                     help="pixel sampler: HBM-resident frames + device Philox draws (default), or the reference-order "

@@ -123,7 +123,10 @@ int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const 
  * 283-256-256-256-128, ReLU, nerf_field.py:92-105).  Layers are computed transposed so each layer's MFMA
  * accumulator feeds the next layer from registers.  prec 1 = bf16, 2 = split bf16x3 operands (fp32 accumulate),
  * 3 = split activations x bf16 weights (SDF), 5 = fp16 operands (forward radiance / head / background chains: the
- * reference GPU's fp16 autocast precision, trainer.py:51; fp16-packed weights, permute bit 2).
+ * reference GPU's fp16 autocast precision, trainer.py:51; fp16-packed weights, permute bit 2), 6 = backward only:
+ * the first layer (B = dY from memory) split bf16x3 (a_lo[0] required), the register-fed layers on fp16 operands with
+ * a per-row power-of-two scale (each row's largest |dZ| to [2^13, 2^14), undone on the fp32 accumulators) -- the
+ * reference's fp16 autocast backward without a global loss scale; layers >= 1 packed as for prec 5.
  * Per-layer arrays (a_hi, a_lo, bias, aux, ldaux, out, ldo, N, act) have n_layers entries.
  * Forward (backward = 0): out[l] = act_l(X_l W_l^T + b_l) (the hidden outs are stored together or, 3 layers, not at
  *   all); rows >= rows_full compute / store only output column 0 of the last layer (the SDF taps), in fp32 from

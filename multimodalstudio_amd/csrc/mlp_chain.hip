@@ -23,7 +23,8 @@
 // activations only (bf16 weights W~ = bf16(W), acc += W~ (h_hi + h_lo): the chain computes the MLP of the rounded
 // weights with ~16-bit activations, so the SDF's tap differences stay exact differences of ONE function -- its
 // weights' rounding is the mixed-precision "bf16 weights, fp32 master" one -- at 2 MFMAs and half the weight
-// traffic of PREC 2); fp32 accumulation.
+// traffic of PREC 2); PREC 5: fp16 operands (forward chains); PREC 6 (backward chains): layer 0 as PREC 2, the
+// register-fed layers fp16 with a per-row power-of-two scale (row_scale); fp32 accumulation.
 #include "common.h"
 #include "chain_common.h"
 
@@ -521,6 +522,36 @@ __device__ __forceinline__ void lazy_fwd_b(int s, floatx16 (&accp)[NT], bf16x8* 
 #endif
 }
 
+// PREC 6 (backward chains only): layer 0 (B from memory) in split-bf16x3, the register-fed layers on fp16 operands
+// with a per-row power-of-two scale.  row_scale: the row's largest |dZ| (both unit halves: lanes r, r + 32) brought
+// to [2^13, 2^14) -- fp16's 11 significant bits for every value within 2^-27 of the row maximum, no overflow -- in
+// place, before the B split; returns the inverse scale the next layer's accumulators (same data row on the lane) are
+// multiplied by (exact: powers of two).
+template <int NT>
+__device__ __forceinline__ float row_scale(floatx16 (&acc)[NT]) {
+  float mx = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fabsf(acc[t][i]));
+  mx = fmaxf(mx, __shfl_xor(mx, 32));
+  int e = __builtin_amdgcn_frexp_expf(mx);  // mx < 2^e (0 for mx = 0)
+  e = e < -100 ? -100 : (e > 100 ? 100 : e);
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = __builtin_amdgcn_ldexpf(acc[t][i], 14 - e);
+  return __builtin_amdgcn_ldexpf(1.f, e - 14);
+}
+
+template <int NT>
+__device__ __forceinline__ void unscale(floatx16 (&acc)[NT], float inv) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] *= inv;
+}
+
 // Activations are template arguments (A0..A2: layer activations, forward ids or backward derivative ids; XA: the
 // backward's input scaling).  The forward's epilogue of layer l is LAZY: tile t is finished (bias, activation,
 // store, bf16 split) inside layer l + 1's k-step 2 t, right before the MFMAs that consume it, so its VALU and
@@ -549,6 +580,9 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   const bool anyfull = m0 < a.rows_full;   // wave-uniform
   const bool blockfull = mb < a.rows_full;  // block-uniform
   const floatx16 zero = {};
+  // operand modes: layer 0 and the register-fed layers (differ only for the backward's PREC 6)
+  constexpr int P0 = PREC == 6 ? 2 : PREC, PR = PREC == 6 ? 5 : PREC;
+  static_assert(PREC != 6 || BWD, "PREC 6 is a backward mode");
 #if MMS_CHAIN_STAMPS
   unsigned long long st[kStamps] = {};
   unsigned long long st_last = chain_stamp();
@@ -632,9 +666,9 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
           st_nt4(xo + k0 + 4, f32x4{v[4], v[5], v[6], v[7]});
         }
       }
-      split8<PREC>(v, bh, bl);
+      split8<P0>(v, bh, bl);
     };
-    run_layer<PREC, NT0, NT0, KS0, XIO ? 4 : 2, XIO ? 2 : 0, XIO ? 2 : 0>(a.L[0], ks0, NT0, acc0, wave, lane, ring,
+    run_layer<P0, NT0, NT0, KS0, XIO ? 4 : 2, XIO ? 2 : 0, XIO ? 2 : 0>(a.L[0], ks0, NT0, acc0, wave, lane, ring,
                                                                          pre, get_b MMS_ST(0));
   }
   auto nopre = [](int) {};
@@ -642,6 +676,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   // previous layer; backward layers 1 and 2 take B from registers (no memory instructions)
   constexpr int kGE = (!BWD && KEEP) ? 4 : 0;
   bf16x8 b1h[2 * NT0], b1l[2 * NT0];
+  float inv1 = 1.f;   // PREC 6: inverse scale of layer 1's accumulators
   if constexpr (BWD) {
     // the SDF backward (3 layers, Softplus, input = the last forward layer's dY): the taps' dW_last row 0 on the way
     if (kTapW && a.tap_part != nullptr && mb + 128 > a.rows_full)
@@ -649,7 +684,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     else
       epilogue_bwd_staged<NT0, A0, false, NL == 4 ? MMS_CHAIN_YAHEAD4 : MMS_CHAIN_YAHEAD>(acc0, a.L[0], m0, a.M, scr,
                                                                                         lane, a.beta, a.thr);
-    to_b<PREC, NT0>(acc0, b1h, b1l);
+    if constexpr (PREC == 6) inv1 = row_scale<NT0>(acc0);
+    to_b<PR, NT0>(acc0, b1h, b1l);
   }
 
   // ---- layer 1: B operand from layer 0's registers
@@ -657,7 +693,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
 #pragma unroll
   for (int t = 0; t < NT1; ++t) acc1[t] = zero;
   {
-    run_layer<PREC, NT1, NT1, 2 * NT0, 0, kGE, 0>(a.L[1], 2 * NT0, NT1, acc1, wave, lane, ring, nopre,
+    run_layer<PR, NT1, NT1, 2 * NT0, 0, kGE, 0>(a.L[1], 2 * NT0, NT1, acc1, wave, lane, ring, nopre,
                                        [&](int s, bf16x8& bh, bf16x8& bl) {
       if constexpr (!BWD)
         lazy_fwd_b<PREC, A0, KEEP, NT0>(s, acc0, b1h, b1l, sbias[0], a.L[0].out, a.L[0].ldo, m0, a.M, scr, lane, a.beta,
@@ -667,13 +703,16 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   }
   // ---- the last layer (index LL = NL - 1), fed by the registers of layer LP = LL - 1 (NT1 tiles, activation A1).
   // Forward: SDF tap rows need only the sdf column tile; a block of tap rows stages only that tile.
-  auto last_layer = [&](floatx16 (&accp)[NT1], auto lpc) {
+  auto last_layer = [&](floatx16 (&accp)[NT1], auto lpc, float invp) {
     constexpr int LP = decltype(lpc)::value, LL = LP + 1;
     bf16x8 b2h[2 * NT1], b2l[2 * NT1];
+    float inv2 = 1.f;
     if constexpr (BWD) {
+      if constexpr (PREC == 6) unscale<NT1>(accp, invp);
       epilogue_bwd_staged<NT1, A1, false, NL == 4 ? MMS_CHAIN_YAHEAD4 : MMS_CHAIN_YAHEAD>(accp, a.L[LP], m0, a.M, scr,
                                                                                         lane, a.beta, a.thr);
-      to_b<PREC, NT1>(accp, b2h, b2l);
+      if constexpr (PREC == 6) inv2 = row_scale<NT1>(accp);
+      to_b<PR, NT1>(accp, b2h, b2l);
     }
     floatx16 acc2[NT2];
 #pragma unroll
@@ -686,7 +725,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
       bh = b2h[s]; bl = b2l[s];
     };
     if (BWD || blockfull) {
-      run_layer<PREC, NT2, NT2, 2 * NT1, 0, kGE, 0>(a.L[LL], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2
+      run_layer<PR, NT2, NT2, 2 * NT1, 0, kGE, 0>(a.L[LL], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2
                                                     MMS_ST(LL));
     } else {
       // a block of SDF tap rows (or the sampler's inference rows) needs only output 0 of the last layer: a 256-long
@@ -708,6 +747,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
         __builtin_nontemporal_store(p + sbias[LL][0], a.L[LL].out + m * a.L[LL].ldo);
       return;
     }
+    if constexpr (PREC == 6) unscale<NT2>(acc2, inv2);
     if constexpr (BWD && A2 == 0) {
       if (a.L[LL].out != nullptr) epilogue_out_staged<NT2>(acc2, a.L[LL], nt2, m0, a.M, scr, lane);
     } else if constexpr (!BWD && KEEP) {   // (the per-wave scratch exists for KEEP forwards)
@@ -723,23 +763,26 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   if constexpr (NL == 4) {
     // ---- middle layer 2: B operand from layer 1's registers (same width and activation as layer 1)
     bf16x8 bmh[2 * NT1], bml[2 * NT1];
+    float invm = 1.f;
     if constexpr (BWD) {
+      if constexpr (PREC == 6) unscale<NT1>(acc1, inv1);
       epilogue_bwd_staged<NT1, A1, false, MMS_CHAIN_YAHEAD4>(acc1, a.L[1], m0, a.M, scr, lane, a.beta, a.thr);
-      to_b<PREC, NT1>(acc1, bmh, bml);
+      if constexpr (PREC == 6) invm = row_scale<NT1>(acc1);
+      to_b<PR, NT1>(acc1, bmh, bml);
     }
     floatx16 accm[NT1];
 #pragma unroll
     for (int t = 0; t < NT1; ++t) accm[t] = zero;
-    run_layer<PREC, NT1, NT1, 2 * NT1, 0, kGE, 0>(a.L[2], 2 * NT1, NT1, accm, wave, lane, ring, nopre,
+    run_layer<PR, NT1, NT1, 2 * NT1, 0, kGE, 0>(a.L[2], 2 * NT1, NT1, accm, wave, lane, ring, nopre,
                                                   [&](int s, bf16x8& bh, bf16x8& bl) {
       if constexpr (!BWD)
         lazy_fwd_b<PREC, A1, KEEP, NT1>(s, acc1, bmh, bml, sbias[1], a.L[1].out, a.L[1].ldo, m0, a.M, scr, lane, a.beta,
                                         a.thr);
       bh = bmh[s]; bl = bml[s];
     } MMS_ST(2));
-    last_layer(accm, std::integral_constant<int, 2>{});
+    last_layer(accm, std::integral_constant<int, 2>{}, invm);
   } else {
-    last_layer(acc1, std::integral_constant<int, 1>{});
+    last_layer(acc1, std::integral_constant<int, 1>{}, inv1);
   }
 #if MMS_CHAIN_STAMPS
   stamp_seg(st, &st_last, 16);
@@ -793,18 +836,22 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
   const bool xio = !noxa && a.xact == 1 && a.xout != nullptr && a.ldxout >= 16 * ks0;
   const bool xio3 = !noxa && a.xact == 3 && a.xout != nullptr && a.ldxout >= 16 * ks0;
   if (nl == 3) {
-    if (!bwd && ks0 == 5 && nt[0] == 8 && nt[1] == 8 && nt[2] == 9 && a0 == 2 && a1 == 2 && a2 == 0 && hidden_full &&
+    if (PREC != 6 && !bwd && ks0 == 5 && nt[0] == 8 && nt[1] == 8 && nt[2] == 9 && a0 == 2 && a1 == 2 && a2 == 0 && hidden_full &&
         (keep || nokeep)) {
-      if (keep) launch_chain<PREC, 5, 8, 8, 9, false, 2, 2, 0, 0, true>(a, s);
-      else launch_chain<PREC, 5, 8, 8, 9, false, 2, 2, 0, 0, false>(a, s);
+      if constexpr (PREC != 6) {
+        if (keep) launch_chain<PREC, 5, 8, 8, 9, false, 2, 2, 0, 0, true>(a, s);
+        else launch_chain<PREC, 5, 8, 8, 9, false, 2, 2, 0, 0, false>(a, s);
+      }
       return true;
     }
-    if constexpr (PREC != 3 && PREC != 5) {   // (split activations: the SDF chains only; fp16: forward only)
+    if constexpr (PREC != 3 && PREC != 5 && PREC != 6) {   // (split activations: the SDF chains only)
       if (!bwd && ks0 == 20 && nt[0] == 8 && nt[1] == 8 && nt[2] == 8 && a0 == 1 && a1 == 1 && a2 == 1 &&
           hidden_full && keep) {
         launch_chain<PREC, 20, 8, 8, 8, false, 1, 1, 1, 0, true>(a, s);
         return true;
       }
+    }
+    if constexpr (PREC != 3 && PREC != 5) {   // (fp16 chains: forward only; PREC 6 is their backward)
       if (bwd && ks0 == 16 && nt[0] == 8 && nt[1] == 8 && nt[2] == 10 && a0 == 1 && a1 == 1 && a2 == 0 && xio &&
           bwd_hidden) {
         launch_chain<PREC, 16, 8, 8, 10, true, 1, 1, 0, 1>(a, s);
@@ -828,6 +875,14 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
         if (a2 == 3) launch_chain<PREC, 16, 2, 2, 1, false, 1, 1, 3, 0, true>(a, s);
         else launch_chain<PREC, 16, 2, 2, 1, false, 1, 1, 0, 0, true>(a, s);
         return true;
+      }
+    }
+    if constexpr (PREC == 6) {
+      // the modality heads' backward (plain: input scaled by the Sigmoid's derivative; polarization: plain)
+      if (bwd && ks0 == 1 && nt[0] == 2 && nt[1] == 2 && nt[2] == 8 && a0 == 1 && a1 == 1 && a2 == 0 && bwd_stored &&
+          hidden64) {
+        if (xio3) { launch_chain<PREC, 1, 2, 2, 8, true, 1, 1, 0, 3>(a, s); return true; }
+        if (noxa && a.xout == nullptr) { launch_chain<PREC, 1, 2, 2, 8, true, 1, 1, 0, 0>(a, s); return true; }
       }
     }
     if constexpr (PREC == 1 || PREC == 2) {
@@ -856,14 +911,16 @@ bool dispatch_chain(int nl, int ks0, const int* nt, bool bwd, const ChainArgs& a
     }
     return false;
   }
-  // 4-layer chains: the background MLPs, bf16 or split-bf16x3 (fp16: forward only)
-  if constexpr (PREC == 1 || PREC == 2 || PREC == 5) {
+  // 4-layer chains: the background MLPs, bf16 or split-bf16x3 (fp16: forward only; PREC 6: backward only)
+  if constexpr (PREC == 1 || PREC == 2 || PREC == 5 || PREC == 6) {
     if (nl != 4 || nt[0] != 8 || nt[1] != 8 || nt[2] != 8 || a0 != 1 || a1 != 1 || a2 != 1) return false;
-    if (!bwd && hidden_full && keep && a3 == 1) {
+    if (PREC != 6 && !bwd && hidden_full && keep && a3 == 1) {
       // base 39-256x4 (NeRF background), head 283-256-256-256-128 (NeRF) / -256 (config-5 grid background)
-      if (ks0 == 3 && nt[3] == 8) { launch_chain<PREC, 3, 8, 8, 8, false, 1, 1, 1, 0, true, 4>(a, s); return true; }
-      if (ks0 == 18 && nt[3] == 4) { launch_chain<PREC, 18, 8, 8, 4, false, 1, 1, 1, 0, true, 4>(a, s); return true; }
-      if (ks0 == 18 && nt[3] == 8) { launch_chain<PREC, 18, 8, 8, 8, false, 1, 1, 1, 0, true, 4>(a, s); return true; }
+      if constexpr (PREC != 6) {
+        if (ks0 == 3 && nt[3] == 8) { launch_chain<PREC, 3, 8, 8, 8, false, 1, 1, 1, 0, true, 4>(a, s); return true; }
+        if (ks0 == 18 && nt[3] == 4) { launch_chain<PREC, 18, 8, 8, 4, false, 1, 1, 1, 0, true, 4>(a, s); return true; }
+        if (ks0 == 18 && nt[3] == 8) { launch_chain<PREC, 18, 8, 8, 8, false, 1, 1, 1, 0, true, 4>(a, s); return true; }
+      }
     }
     if (PREC != 5 && bwd && a3 == 0 && xio && bwd_hidden) {
       if (ks0 == 16 && nt[3] == 2) { launch_chain<PREC, 16, 8, 8, 2, true, 1, 1, 0, 1, false, 4>(a, s); return true; }
@@ -982,8 +1039,9 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
                              float* const* out, const int64_t* ldo, const int* N, const int* act, float beta,
                              float thr, const float* w2row0, float* tap_part, int64_t ld_tap, void* stream) {
   const char* fn = "mms_mlp_chain";
-  MMS_REQUIRE((prec >= 1 && prec <= 3) || prec == 5, fn,
-              "prec must be 1 (bf16), 2 (split bf16x3), 3 (split activations) or 5 (fp16, forward chains)");
+  MMS_REQUIRE((prec >= 1 && prec <= 3) || prec == 5 || (prec == 6 && backward), fn,
+              "prec must be 1 (bf16), 2 (split bf16x3), 3 (split activations), 5 (fp16, forward chains) or 6 (backward: "
+              "split bf16x3 first layer, row-scaled fp16 after)");
   MMS_REQUIRE(n_layers == 3 || n_layers == 4, fn, "chains of 3 or 4 layers");
   MMS_REQUIRE(M >= 0 && K0 > 0, fn, "bad shape");
   if (M == 0) return 0;
@@ -1008,11 +1066,12 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
   for (int l = 0; l < 4; ++l) a.L[l] = ChainLayer{};
   for (int l = 0; l < n_layers; ++l) {
     MMS_REQUIRE(a_hi[l] != nullptr && N[l] > 0, fn, "missing layer weights");
-    MMS_REQUIRE(prec != 2 || (a_lo && a_lo[l] != nullptr), fn, "split bf16x3 needs the residual images");
+    const bool split = prec == 2 || (prec == 6 && l == 0);
+    MMS_REQUIRE(!split || (a_lo && a_lo[l] != nullptr), fn, "split bf16x3 needs the residual images");
     MMS_REQUIRE(act[l] >= 0 && act[l] <= 3, fn, "bad activation id");
     ChainLayer& L = a.L[l];
     L.a_hi = reinterpret_cast<const __bf16*>(a_hi[l]);
-    L.a_lo = prec == 2 ? reinterpret_cast<const __bf16*>(a_lo[l]) : nullptr;
+    L.a_lo = split ? reinterpret_cast<const __bf16*>(a_lo[l]) : nullptr;
     L.bias = (!backward && bias) ? bias[l] : nullptr;
     L.aux = (backward && aux) ? aux[l] : nullptr;
     L.ldaux = (backward && ldaux) ? ldaux[l] : 0;
@@ -1033,6 +1092,7 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
   const bool ok = prec == 1   ? dispatch_chain<1>(n_layers, ks0, nt, backward != 0, a, s)
                   : prec == 2 ? dispatch_chain<2>(n_layers, ks0, nt, backward != 0, a, s)
                   : prec == 5 ? dispatch_chain<5>(n_layers, ks0, nt, backward != 0, a, s)
+                  : prec == 6 ? dispatch_chain<6>(n_layers, ks0, nt, backward != 0, a, s)
                               : dispatch_chain<3>(n_layers, ks0, nt, backward != 0, a, s);
   MMS_REQUIRE(ok, fn, "unsupported chain shape or activations (SDF 71-256-256-257 Softplus, radiance 317-256-256-256 "
                       "ReLU, background 39-256x4 and 283-256-256-256-128 ReLU chains only)");

@@ -57,9 +57,15 @@ PRESETS["fast_w16"] = dict(PRESETS["fast"], wgrad=1)
 # chains and weight gradients split-bf16x3 (wider than the reference's fp16 backward: no loss scaling needed); the SDF
 # chain stays split-bf16x3 throughout (its 4-tap hessians)
 PRESETS["fast_h16"] = dict(PRESETS["fast"], radiance=5, heads=5, pol_head=5, background=5)
+# ... and the reference's fp16 backward-data chains too (mms_mlp_chain prec 6): every chain's backward on fp16 operands
+# after its first layer (that one's input, dY from memory, stays split-bf16x3), each row scaled by a power of two to
+# its largest |dZ| (no global loss scale, no underflow), fp32 accumulation and fp32 dZ stores; the weight gradients
+# and every forward unchanged
+PRESETS["fast_h16b"] = dict(PRESETS["fast_h16"], bwd16=1)
 for _p in PRESETS.values():
     _p.setdefault("sdf_chain", 0)      # 0: the chain runs on the "sdf" GEMM precision
     _p.setdefault("wgrad", 0)          # 0: the weight gradients on the family's backward operand mode
+    _p.setdefault("bwd16", 0)          # 1: split-bf16x3 backward-data chains run prec 6
 # NOT a parity preset: the SDF chain on bf16 weights x split activations (mms_mlp_chain prec 3, two MFMAs per product;
 # with bf16-ROUNDED weights the SDF is a different, rippled function: 56x the reference's hessian scale off on the
 # e2e fixtures and a 24x larger curvature loss over the rgb training trajectory), kept to measure what the curvature
@@ -587,6 +593,8 @@ class ChainRun:
         self.prec = bwd_prec(int(prec))
         self.cprec = int(chain_prec) or fwd_prec(int(prec))
         self.bcprec = self.prec if int(prec) in (4, 5) else self.cprec
+        if PRECISION.get("bwd16", 0) and self.bcprec == 2:
+            self.bcprec = 6
         self.L = len(self.params) // 3
         if self.L not in (3, 4):
             raise ValueError("chains of 3 or 4 layers")
@@ -682,12 +690,13 @@ class ChainRun:
         Ns = [W.shape[0] for W in self.Ws]
         up = lambda n, k: k * ((n + k - 1) // k)  # noqa: E731
         p = self.bcprec
+        p0, pr = (2, 5) if p == 6 else (p, p)     # prec 6: the first layer split-bf16x3, the rest fp16
         if self.l16:
             return [self._pack(self.Ws[L - 1], up(Ns[L - 2], 16), up(Ns[L - 1], 32), True, 2, p)] + \
                    [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 16), up(Ns[l], 32), True, 3, p)
                     for l in range(L - 2, -1, -1)]
-        return [self._pack(self.Ws[L - 1], up(Ns[L - 2], 32), up(Ns[L - 1], 16), True, False, p)] + \
-               [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 32), up(Ns[l], 32), True, True, p)
+        return [self._pack(self.Ws[L - 1], up(Ns[L - 2], 32), up(Ns[L - 1], 16), True, False, p0)] + \
+               [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 32), up(Ns[l], 32), True, True, pr)
                 for l in range(L - 2, -1, -1)]
 
     def backward(self, dy: torch.Tensor, dx_out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -50,7 +50,7 @@ CAPTURE_MODE = None   # override of the capture_error_mode (probes)
 # the optimizer groups zeroed / clipped / stepped together (pipeline.OptimBank: 3 launches and 1 scalar upload per
 # step instead of 8 and 2); MMS_BANKED_OPTIM=0: per group
 BANKED_OPTIM = os.environ.get("MMS_BANKED_OPTIM", "1") != "0"
-# the tail's next-step hit count in one launch (mms_count_hits; 618.7k -> 620.5k rays/s, scripts/gpu_r5f.sh);
+# the tail's next-step hit count in one launch (mms_count_hits; 618.7k -> 620.5k rays/s, 2 x 2 A/B);
 # MMS_FUSED_COUNT=0: pose exp + raygen + collider + compact
 FUSED_COUNT = os.environ.get("MMS_FUSED_COUNT", "1") != "0"
 

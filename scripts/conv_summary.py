@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--runs", default="gpurun_out/conv3k_*_s*.json")
     ap.add_argument("--prev", default=None)
     ap.add_argument("--keep-prev", nargs="*", default=["fp32"], help="variants of --prev merged in")
+    ap.add_argument("--base", default="fp32", help="the variant the others are paired against")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     runs = {}
@@ -35,9 +36,9 @@ def main():
         last = d["history"][-1]
         runs.setdefault(m.group(1), {})[m.group(2)] = {"psnr": last["psnr"], "wall_s": last["wall_s"]}
     summary = {}
-    base = runs.get("fp32", {})
+    base = runs.get(a.base, {})
     for v, rs in sorted(runs.items()):
-        if v == "fp32":
+        if v == a.base:
             continue
         seeds = sorted(set(rs) & set(base), key=int)
         if not seeds:
@@ -52,7 +53,7 @@ def main():
         allm = [sum(rs[s]["psnr"][m] - base[s]["psnr"][m] for m in mods) / len(mods) for s in seeds]
         mean = sum(allm) / len(allm)
         sd = math.sqrt(sum((x - mean) ** 2 for x in allm) / max(1, len(allm) - 1))
-        summary[v] = {"seeds": seeds, "paired_dpsnr_vs_fp32": per, "all_modality_mean": round(mean, 4),
+        summary[v] = {"seeds": seeds, f"paired_dpsnr_vs_{a.base}": per, "all_modality_mean": round(mean, 4),
                       "all_modality_se": round(sd / math.sqrt(len(allm)), 4)}
         print(f"{v:22s} seeds {','.join(seeds):18s} " + " ".join(f"{m} {p['mean']:+.3f}±{p['se']:.3f}"
                                                                for m, p in per.items()) +

@@ -397,3 +397,80 @@ def test_chain_fp16_forward(dev, dims, acts):
     assert e_fwd < 3e-3
     for k, v in errs.items():
         assert v < TOL[2], (k, v)
+
+
+@pytest.mark.parametrize("dims,acts,M,rows_full", [
+    ([71, 256, 256, 257], CASES["geo"], 777, 777),                                 # SDF
+    ([71, 256, 256, 257], CASES["geo"], 20013, 3990),                              # SDF with tap rows
+    ([317, 256, 256, 256], [(1, 1.0, 20.0)] * 3, 3000, None),                      # radiance
+    ([256, 64, 64, 3], [(1, 1.0, 20.0), (1, 1.0, 20.0), (3, 1.0, 20.0)], 3000, None),   # plain head (Sigmoid)
+    ([256, 64, 64, 3], [(1, 1.0, 20.0), (1, 1.0, 20.0), (0, 1.0, 20.0)], 3000, None),   # polarization head
+    ([39, 256, 256, 256, 256], [(1, 1.0, 20.0)] * 4, 3000, None),                  # background base
+    ([283, 256, 256, 256, 128], [(1, 1.0, 20.0)] * 4, 3000, None)],                # background head
+    ids=["sdf", "sdf_taps", "radiance", "head", "pol_head", "bg_base", "bg_head"])
+def test_chain_fp16_backward(dev, dims, acts, M, rows_full):
+    """Preset fast_h16b: every backward-data chain on mms_mlp_chain prec 6 -- its first layer (B = dY from memory)
+    split-bf16x3, the register-fed layers on fp16 operands with a per-row power-of-two scale (the reference GPU's fp16
+    autocast backward, without its global loss scale).  dX and every parameter gradient vs the fp64 backward taken at
+    the kernel's own forward activations within 3e-3 of each tensor's scale (fp16's 11-bit operands over K <= 256;
+    split-bf16x3 measures ~1e-5 here), finite everywhere; rows of very different magnitude (1e-6 .. 1e3 in dY) keep
+    that relative accuracy per row (the row scale), and the tap rows read only column 0."""
+    from multimodalstudio_amd import functions as fx
+    g = torch.Generator().manual_seed(sum(dims) + M)
+    L = len(dims) - 1
+    params = []
+    for k, n in zip(dims[:-1], dims[1:]):
+        v = torch.randn(n, k, generator=g) / k ** 0.5
+        params += [torch.linalg.vector_norm(v, dim=1, keepdim=True).to(dev).requires_grad_(True),
+                   v.to(dev).requires_grad_(True), (torch.randn(n, generator=g) * 0.1).to(dev).requires_grad_(True)]
+    sdf = dims[0] == 71
+    prec = 2 if sdf else 5
+    old = dict(fx.PRECISION)
+    fx.PRECISION["bwd16"] = 1
+    try:
+        run = fx.ChainRun(params, acts, prec)
+        assert run.bcprec == 6 and not run.l16
+        x = torch.randn(M, dims[0], generator=g) * 0.5
+        run.forward(_panel(x, dev), keep=True, rows_full=rows_full)
+        Y = [t.detach().clone() for t in run.Y]
+        dy = torch.randn(M, dims[-1], generator=g)
+        dy *= 10.0 ** torch.randint(-6, 4, (M, 1), generator=g).double().float()    # per-row magnitudes
+        rf = M if rows_full is None else rows_full
+        dyr = dy.double().clone()
+        dyr[rf:, 1:] = 0.0
+        dy[rf:, 1:] = float("nan")          # never read
+        dx = run.backward(_panel(dy, dev))
+        torch.cuda.synchronize()
+    finally:
+        fx.PRECISION.clear()
+        fx.PRECISION.update(old)
+    ins = [x.double()] + [t.double().cpu() for t in Y[:L - 1]]
+    d = dyr
+    errs = {}
+    for l in range(L - 1, -1, -1):
+        act, beta, _ = acts[l]
+        if l < L - 1 or act != 0:
+            yl = Y[l].double().cpu()
+            if act == 1:
+                d = d * (yl > 0)
+            elif act == 2:
+                d = d * (1 - torch.exp(-beta * yl))
+            elif act == 3:
+                d = d * yl * (1 - yl)
+        gg = params[3 * l].detach().double().cpu().requires_grad_(True)
+        v = params[3 * l + 1].detach().double().cpu().requires_grad_(True)
+        W = torch._weight_norm(v, gg, 0)
+        W.backward(d.T @ ins[l])
+        errs[f"v{l}"] = rel(params[3 * l + 1].grad.cpu(), v.grad)
+        errs[f"g{l}"] = rel(params[3 * l].grad.cpu(), gg.grad)
+        errs[f"b{l}"] = rel(params[3 * l + 2].grad.cpu(), d.sum(0))
+        d = d @ W.detach()
+    assert torch.isfinite(dx).all()
+    errs["dx"] = rel(dx.cpu(), d)
+    # per-row relative error of dX (the row scale keeps small rows as accurate as large ones)
+    dxc = dx.cpu().double()
+    row_err = ((dxc - d).abs().amax(1) / d.abs().amax(1).clamp_min(1e-300)).max().item()
+    print(dims, rows_full, {k: f"{v:.1e}" for k, v in errs.items()}, f"row max {row_err:.1e}")
+    for k, v in errs.items():
+        assert v < 3e-3, (k, v)
+    assert row_err < 1e-2

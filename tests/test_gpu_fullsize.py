@@ -32,7 +32,7 @@ not a kernel error: measured (scripts/fullsize_diag.py) on the rays whose bins a
     Loss within 1e-4 of the reference, hit mask and counts exact;
   * the free-running step (the HIP sampler on the HIP SDF): the loss, the hit mask, the share of rays whose bins agree
     to 2e-5 and the radiance on those rays;
-  * the throughput presets (fast_h16, benchmarked, and fast) on the reference's samples, at the small fixtures' fast
+  * the throughput presets (fast_h16b, benchmarked, and fast) on the reference's samples, at the small fixtures' fast
     bounds.
 """
 import os
@@ -41,7 +41,7 @@ import numpy as np
 import pytest
 import torch
 
-from test_gpu_e2e import FAST_PRESETS, GEO_TOL_FAST, GOLD, E2ECase, load, rel_err, rel_l2
+from test_gpu_e2e import FAST_DPOSE, FAST_GRAD_L2, FAST_PRESETS, GEO_TOL_FAST, GOLD, E2ECase, load, rel_err, rel_l2
 
 pytestmark = pytest.mark.gpu
 NAME = "e2e_full_grid_rgb_l19"
@@ -203,7 +203,7 @@ def test_fullsize_free_running(dev):
 
 @pytest.mark.parametrize("preset", FAST_PRESETS)
 def test_fullsize_fast_preset(dev, preset):
-    """The throughput presets (the benchmarked fast_h16 and the all-split-bf16x3 fast) on the reference's samples: the
+    """The throughput presets (the benchmarked fast_h16b and the all-split-bf16x3 fast) on the reference's samples: the
     small fixtures' fast bounds (test_gpu_e2e.test_e2e_fast_preset_deviation)."""
     from multimodalstudio_amd import functions as fx
     f = load(NAME)
@@ -225,3 +225,19 @@ def test_fullsize_fast_preset(dev, preset):
     assert rel.mean() < 3e-4 and rel.max() < 2.5e-2
     for k, e in geo.items():
         assert e < GEO_TOL_FAST[k], (k, e)
+    # every parameter gradient (relative L2; the tables on their fixed sample) and the pose gradient vs the reference
+    worst, wk = 0.0, None
+    for k, p in case.model.named_parameters():
+        g = p.grad.detach()
+        if "g:" + k in f:
+            e = rel_l2(g.cpu(), f["g:" + k])
+        elif "gtab_val:" + k in f:
+            idx = torch.from_numpy(f["gtab_idx:" + k].astype(np.int64)).to(g.device)
+            e = rel_l2(g.reshape(-1)[idx].cpu(), f["gtab_val:" + k])
+        else:
+            continue
+        if e > worst:
+            worst, wk = e, k
+    dpose = rel_err(case.pose.pose_adjustment["rgb"].grad.cpu(), f["rgb:dpose"])
+    print(f"  worst parameter gradient relative L2 {worst:.3e} ({wk}), dpose {dpose:.3e}")
+    assert worst < FAST_GRAD_L2 and dpose < FAST_DPOSE
