@@ -54,10 +54,13 @@ __device__ __forceinline__ void mma(floatx16& acc, const bf16x8& ah, const bf16x
 // MFMAs (one wave per SIMD) left every k-step waiting on L2 latency: 6 % of the MFMA rate.
 // Packed images are fragment-major (mms_mlp_pack): fragment (k-step s, tile t) is one contiguous 1 KiB block at
 // element ((s * NT + t) * 64 + lane) * 8.
-constexpr int kDepth = 2;           // k-steps a load is issued ahead of its use (3 measured no faster)
-constexpr int kRing = kDepth + 1;   // ring slots: the one being read + kDepth in flight
+// The ring is D + 1 slots deep (D = k-steps a load is issued ahead of its use): D = MMS_CHAIN_DEPTH where the block's
+// LDS allows it (chain_kernel's kD), else 2.  A slot holds the largest k-step of the kernel's layers (hi + lo images of
+// its tiles) + 1 spare chunk (the dummy loads that even out the waves' DMA counts).
+#ifndef MMS_CHAIN_DEPTH
+#define MMS_CHAIN_DEPTH 2
+#endif
 constexpr int kMaxTiles = 10;  // widest chain layer: 10 column tiles (320 units)
-constexpr int kSlot = 21;  // 1 KiB chunks per ring slot: hi + lo images of up to 10 tiles, + 1 spare (dummy loads)
 
 // Diagnostic build only (MMS_CHAIN_STAMPS=1, scripts/lib_variants.py "stamps"; the product library has none): each
 // wave accumulates s_memtime deltas per layer l -- [4 l] the k-steps' wait + barrier, [4 l + 1] ring / input issue and
@@ -94,9 +97,12 @@ __device__ __forceinline__ void stamp_seg(unsigned long long* st, unsigned long 
 template <int PREC, int NTL>
 constexpr int stage_per() { return (nimg<PREC>() * NTL + 3) / 4; }
 
-// issue k-step s's fragments of tiles [0, NTL) (hi, then lo) into ring slot s % kRing
-template <int PREC, int NT, int NTL>
-__device__ __forceinline__ void stage(const ChainLayer& Ly, int s, int wave, int lane, bf16x8 (*ring)[kSlot][64]) {
+// issue k-step s's fragments of tiles [0, NTL) (hi, then lo) into ring slot s % (D + 1)
+constexpr int cmax(int x, int y) { return x > y ? x : y; }
+
+template <int PREC, int NT, int NTL, int D, int SLOT>
+__device__ __forceinline__ void stage(const ChainLayer& Ly, int s, int wave, int lane, bf16x8 (*ring)[SLOT][64]) {
+  static_assert(nimg<PREC>() * NTL < SLOT, "ring slot too small");
   constexpr int TOTAL = nimg<PREC>() * NTL;
 #pragma unroll
   for (int i = 0; i < stage_per<PREC, NTL>(); ++i) {
@@ -107,7 +113,7 @@ __device__ __forceinline__ void stage(const ChainLayer& Ly, int s, int wave, int
     const __bf16* base = Ly.a_hi;
     if constexpr (PREC == 2) base = img ? Ly.a_lo : Ly.a_hi;  // a select of two values (no divergent address)
     const __bf16* src = base + ((int64_t)(s * NT + t) * 64 + lane) * 8;
-    const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&ring[s % kRing][real ? c : kSlot - 1][0]);
+    const uint32_t dst = (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)&ring[s % (D + 1)][real ? c : SLOT - 1][0]);
     lds_dma16(src, __builtin_amdgcn_readfirstlane(dst));
   }
 }
@@ -116,51 +122,63 @@ __device__ __forceinline__ void stage(const ChainLayer& Ly, int s, int wave, int
 template <int GE, int GO>
 constexpr int gops(int s) { return s < 0 ? 0 : ((s & 1) ? GO : GE); }
 
+// the exact wait before a k-step: KG younger get_b instructions plus n = min(N, f) younger steps' PP loads each
+template <int KG, int PP, int N>
+__device__ __forceinline__ void wait_younger(int f) {
+  if constexpr (N == 0) {
+    wait_vm_barrier<KG>();
+  } else {
+    if (f >= N) wait_vm_barrier<KG + N * PP>();
+    else wait_younger<KG, PP, N - 1>(f);
+  }
+}
+
+// sum of gops over the D get_b steps before s
+template <int GE, int GO, int D>
+constexpr int gops_before(int s) { return D == 0 ? 0 : gops<GE, GO>(s - D) + gops_before<GE, GO, (D > 0 ? D - 1 : 0)>(s); }
+
 // one layer: acc[t] (t < nt) += sum_{s < ks} A(s, t) . B(s); B(s) = get_b(s) (compile-time s: register arrays).
 // ks and NTL are block-uniform (every wave takes part in every barrier); nt may be smaller per wave (nt <= NTL).
-// Pipeline, kDepth k-steps deep for everything a k-step reads from memory: step t issues pre(t + kDepth) (the
-// layer-0 input slices, PRE instructions) and the ring DMA of step t + kDepth (PER instructions), then get_b(t) (GE /
-// GO instructions: the lazy epilogue's stores, the backward's dZ stores).  The wait before step s is EXACT: it lets
-// every instruction issued after step s's own loads stay in flight -- get_b(s - kDepth .. s - 1) and the pre / DMA
-// of the steps already issued after s -- so neither a store nor a later prefetch holds up a k-step (vmcnt retires in
-// issue order, stores included).  Every counted instruction is issued unconditionally (clamped rows, no exec-skipped
-// branches), so the counts are exact for every wave.
-template <int PREC, int NT, int NTL, int KS, int PRE, int GE, int GO, typename Pre, typename GetB>
+// Pipeline, D k-steps deep for everything a k-step reads from memory: step t issues pre(t + D) (the layer-0 input
+// slices, PRE instructions) and the ring DMA of step t + D (PER instructions), then get_b(t) (GE / GO instructions:
+// the lazy epilogue's stores, the backward's dZ stores).  The wait before step s is EXACT: it lets every instruction
+// issued after step s's own loads stay in flight -- get_b(s - D .. s - 1) and the pre / DMA of the steps already
+// issued after s -- so neither a store nor a later prefetch holds up a k-step (vmcnt retires in issue order, stores
+// included).  Every counted instruction is issued unconditionally (clamped rows, no exec-skipped branches), so the
+// counts are exact for every wave.
+template <int PREC, int NT, int NTL, int KS, int PRE, int GE, int GO, int D, int SLOT, typename Pre, typename GetB>
 __device__ __forceinline__ void run_layer(const ChainLayer& Ly, int ks, int nt, floatx16 (&acc)[NT], int wave,
-                                          int lane, bf16x8 (*ring)[kSlot][64], Pre&& pre, GetB&& get_b,
+                                          int lane, bf16x8 (*ring)[SLOT][64], Pre&& pre, GetB&& get_b,
                                           unsigned long long* st = nullptr, unsigned long long* st_last = nullptr) {
   constexpr int PER = stage_per<PREC, NTL>();
+  static_assert(D >= 1 && D <= 4, "ring depth");
   stamp_seg(st, st_last, 3);
   wait_vm_barrier<63>();  // every wave is done with the ring (previous layer / launch prologue)
 #pragma unroll
-  for (int j = 0; j < kDepth; ++j) {
+  for (int j = 0; j < D; ++j) {
     if (j < ks) {
       pre(j);
-      stage<PREC, NT, NTL>(Ly, j, wave, lane, ring);
+      stage<PREC, NT, NTL, D>(Ly, j, wave, lane, ring);
     }
   }
   static_for<KS>([&](auto sc) {
     constexpr int s = decltype(sc)::value;
     if (s < ks) {
-      // this wave's loads of step s have landed, and (barrier) every wave's; slot (s + kDepth) % kRing is free.
-      // Younger instructions: get_b(s - kDepth .. s - 1) and the f = min(kDepth - 1, ks - 1 - s) steps issued after s.
-      static_assert(kDepth >= 1 && kDepth <= 3, "kG sums the last kDepth get_b steps");
-      constexpr int kG = (kDepth >= 3 ? gops<GE, GO>(s - 3) : 0) + (kDepth >= 2 ? gops<GE, GO>(s - 2) : 0) +
-                         gops<GE, GO>(s - 1);
-      const int f = ks - 1 - s;
+      // this wave's loads of step s have landed, and (barrier) every wave's; slot (s + D) % (D + 1) is free.
+      // Younger instructions: get_b(s - D .. s - 1) and the min(D - 1, ks - 1 - s) steps issued after s.
+      constexpr int kG = gops_before<GE, GO, D>(s);
+      static_assert(kG + (D - 1) * (PRE + PER) <= 63, "vmcnt range");
       stamp_seg(st, st_last, 2);
-      if (kDepth >= 3 && f >= 2) wait_vm_barrier<kG + (kDepth - 1) * (PRE + PER)>();
-      else if (kDepth >= 2 && f >= 1) wait_vm_barrier<kG + (kDepth >= 3 ? 1 : kDepth - 1) * (PRE + PER)>();
-      else wait_vm_barrier<kG>();
+      wait_younger<kG, PRE + PER, D - 1>(ks - 1 - s);
       stamp_seg(st, st_last, 0);
-      if (s + kDepth < ks) {
-        pre(s + kDepth);
-        stage<PREC, NT, NTL>(Ly, s + kDepth, wave, lane, ring);
+      if (s + D < ks) {
+        pre(s + D);
+        stage<PREC, NT, NTL, D>(Ly, s + D, wave, lane, ring);
       }
       bf16x8 bh, bl;
       get_b(s, bh, bl);
       stamp_seg(st, st_last, 1);
-      const bf16x8* slot = &ring[s % kRing][0][0];
+      const bf16x8* slot = &ring[s % (D + 1)][0][0];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         if (t < nt) {
@@ -560,10 +578,24 @@ __device__ __forceinline__ void unscale(floatx16 (&acc)[NT], float inv) {
 // background NeRF MLPs, 4 layers).  Backward: the same structure on the transposed weights, last layer first.
 template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, int XA, bool KEEP, int NL>
 __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
-  __shared__ __attribute__((aligned(1024))) bf16x8 ring[kRing][kSlot][64];
+  // operand modes: layer 0 and the register-fed layers (differ only for the backward's PREC 6)
+  constexpr int P0 = PREC == 6 ? 2 : PREC, PR = PREC == 6 ? 5 : PREC;
+  static_assert(PREC != 6 || BWD, "PREC 6 is a backward mode");
+  // ring slot: the largest k-step (images x tiles) of the kernel's layers + the spare chunk; depth: MMS_CHAIN_DEPTH
+  // where the block's LDS holds it
+  constexpr int kSlotK = cmax(nimg<P0>() * NT0, nimg<PR>() * cmax(NT1, NT2)) + 1;
+  constexpr bool kXio = BWD && XA != 0;
+  constexpr int kStageB = (BWD || KEEP) ? 4 * 32 * kScr * 4 : 16;
+  auto lds_for = [](int d) constexpr {
+    return (d + 1) * (kSlotK * 1024 + (kXio ? 2 : 1) * 8192) + kStageB + NL * 32 * kMaxTiles * 4 + 32 * NT1 * 4 +
+           4 * (32 * NT0 + 4) * 4;
+  };
+  constexpr int kD = (MMS_CHAIN_DEPTH >= 4 && lds_for(4) <= 160 * 1024) ? 4
+                     : (MMS_CHAIN_DEPTH >= 3 && lds_for(3) <= 160 * 1024) ? 3 : 2;
+  __shared__ __attribute__((aligned(1024))) bf16x8 ring[kD + 1][kSlotK][64];
   // layer-0 input slices (and, backward radiance chain, the xaux slices): [slot][wave][2 x 64 lane chunks]
-  __shared__ __attribute__((aligned(1024))) f32x4 xring[kRing][4][128];
-  __shared__ __attribute__((aligned(1024))) f32x4 aring[(BWD && XA != 0) ? kRing : 1][4][128];
+  __shared__ __attribute__((aligned(1024))) f32x4 xring[kD + 1][4][128];
+  __shared__ __attribute__((aligned(1024))) f32x4 aring[kXio ? kD + 1 : 1][4][128];
   __shared__ __attribute__((aligned(16))) float sbias[NL][32 * kMaxTiles];  // forward biases, zero padded
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar staging addresses
@@ -580,9 +612,6 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   const bool anyfull = m0 < a.rows_full;   // wave-uniform
   const bool blockfull = mb < a.rows_full;  // block-uniform
   const floatx16 zero = {};
-  // operand modes: layer 0 and the register-fed layers (differ only for the backward's PREC 6)
-  constexpr int P0 = PREC == 6 ? 2 : PREC, PR = PREC == 6 ? 5 : PREC;
-  static_assert(PREC != 6 || BWD, "PREC 6 is a backward mode");
 #if MMS_CHAIN_STAMPS
   unsigned long long st[kStamps] = {};
   unsigned long long st_last = chain_stamp();
@@ -626,7 +655,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     // loads, so it inserts no vmcnt waits of its own into the k-loop (compiler-visible loads drew vmcnt(0..3) waits
     // there that also drained the weight prefetch).  Quads past K0 read column 0 and are zeroed in get_b.
     auto pre = [&](int s) {
-      const int slot = s % kRing;
+      const int slot = s % (kD + 1);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int col = 16 * s + 4 * (2 * j + (lane >> 5));
@@ -640,12 +669,12 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     };
     auto get_b = [&](int s, bf16x8& bh, bf16x8& bl) {
       const int k0 = 16 * s + 8 * h;
-      const f32x4* xs = &xring[s % kRing][wave][0];
+      const f32x4* xs = &xring[s % (kD + 1)][wave][0];
       const f32x4 x0 = xs[64 * h + r], x1 = xs[64 * h + 32 + r];
       float v[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
       if constexpr (XIO) {
         // scaled first, masked after: columns past K0 hold whatever the padded rows hold (possibly non-finite)
-        const f32x4* as = &aring[s % kRing][wave][0];
+        const f32x4* as = &aring[s % (kD + 1)][wave][0];
         const f32x4 w0 = as[64 * h + r], w1 = as[64 * h + 32 + r];
         const float wv[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
 #pragma unroll
@@ -668,7 +697,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
       }
       split8<P0>(v, bh, bl);
     };
-    run_layer<P0, NT0, NT0, KS0, XIO ? 4 : 2, XIO ? 2 : 0, XIO ? 2 : 0>(a.L[0], ks0, NT0, acc0, wave, lane, ring,
+    run_layer<P0, NT0, NT0, KS0, XIO ? 4 : 2, XIO ? 2 : 0, XIO ? 2 : 0, kD>(a.L[0], ks0, NT0, acc0, wave, lane, ring,
                                                                          pre, get_b MMS_ST(0));
   }
   auto nopre = [](int) {};
@@ -693,7 +722,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
 #pragma unroll
   for (int t = 0; t < NT1; ++t) acc1[t] = zero;
   {
-    run_layer<PR, NT1, NT1, 2 * NT0, 0, kGE, 0>(a.L[1], 2 * NT0, NT1, acc1, wave, lane, ring, nopre,
+    run_layer<PR, NT1, NT1, 2 * NT0, 0, kGE, 0, kD>(a.L[1], 2 * NT0, NT1, acc1, wave, lane, ring, nopre,
                                        [&](int s, bf16x8& bh, bf16x8& bl) {
       if constexpr (!BWD)
         lazy_fwd_b<PREC, A0, KEEP, NT0>(s, acc0, b1h, b1l, sbias[0], a.L[0].out, a.L[0].ldo, m0, a.M, scr, lane, a.beta,
@@ -725,7 +754,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
       bh = b2h[s]; bl = b2l[s];
     };
     if (BWD || blockfull) {
-      run_layer<PR, NT2, NT2, 2 * NT1, 0, kGE, 0>(a.L[LL], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2
+      run_layer<PR, NT2, NT2, 2 * NT1, 0, kGE, 0, kD>(a.L[LL], 2 * NT1, nt2, acc2, wave, lane, ring, nopre, get_b2
                                                     MMS_ST(LL));
     } else {
       // a block of SDF tap rows (or the sampler's inference rows) needs only output 0 of the last layer: a 256-long
@@ -773,7 +802,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     floatx16 accm[NT1];
 #pragma unroll
     for (int t = 0; t < NT1; ++t) accm[t] = zero;
-    run_layer<PR, NT1, NT1, 2 * NT1, 0, kGE, 0>(a.L[2], 2 * NT1, NT1, accm, wave, lane, ring, nopre,
+    run_layer<PR, NT1, NT1, 2 * NT1, 0, kGE, 0, kD>(a.L[2], 2 * NT1, NT1, accm, wave, lane, ring, nopre,
                                                   [&](int s, bf16x8& bh, bf16x8& bl) {
       if constexpr (!BWD)
         lazy_fwd_b<PREC, A1, KEEP, NT1>(s, acc1, bmh, bml, sbias[1], a.L[1].out, a.L[1].ldo, m0, a.M, scr, lane, a.beta,

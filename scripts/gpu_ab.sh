@@ -19,7 +19,7 @@ for rep in $(seq 1 ${REPS:-2}); do
         if [[ $it == P=* ]]; then prec=(--precision "${it#P=}"); else envs+=("$it"); fi
       done
     fi
-    out=gpurun_out/ab_${TAG}_${v//[=,]/_}_$rep
+    out=gpurun_out/ab_${TAG}_$(echo "$v" | tr "=,/." "____")_$rep
     env "${envs[@]}" timeout -k 10 300 python -u bench.py ${ARGS:---no-cpu-baseline --secondary ''} "${prec[@]}" > $out.json 2> $out.err
     echo "$v rep $rep: $(python -c "import json,sys; d=json.loads(open('$out.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'])")"
   done

@@ -27,6 +27,8 @@ VARIANTS = {  # name: (translation unit, macro definitions)
     "ahead0": ("mlp_chain", {"MMS_CHAIN_AHEAD": 0}),
     "ss2k": ("loss_optim", {"MMS_SUMSQ_GRID": 2048, "MMS_SUMSQ_UNROLL": 4}),   # the round-3c launch shape
     "wpipe0": ("gemm", {"MMS_WIDE_PIPE": 0}),   # the wide weight-gradient kernel's one-register-set loop (round 3)
+    "d3": ("mlp_chain", {"MMS_CHAIN_DEPTH": 3}),  # the chains' weight / input ring three k-steps deep (where LDS allows)
+    "d4": ("mlp_chain", {"MMS_CHAIN_DEPTH": 4}),
 }
 # the two-waves-per-SIMD chain's ablations (csrc/chain16.hip MMS_C16_ABL bits: 1 no MFMA, 2 no weight DMA, 4 no
 # barrier, 8 no epilogue)

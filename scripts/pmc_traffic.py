@@ -16,7 +16,7 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PREC = {"0": "fp32", "1": "bf16", "2": "bf16x3", "3": "bf16x2", "5": "fp16"}
+PREC = {"0": "fp32", "1": "bf16", "2": "bf16x3", "3": "bf16x2", "5": "fp16", "6": "fp16-rowscaled"}
 MODE = {("false", "false"): "NT", ("false", "true"): "NN", ("true", "true"): "TN"}
 
 
@@ -39,7 +39,7 @@ def label(name, grid=0):
     m = re.search(r"gemm_kernel<(\d), (true|false), (true|false), (true|false)>", name)
     if m:
         return f"mms_gemm:{PREC[m.group(1)]}:{MODE.get((m.group(2), m.group(3)), '??')}"
-    m = re.search(r"chain_kernel<(\d), (\d+), \d+, \d+, (\d+), (true|false), \d, \d, \d, \d, (true|false), (\d)(?:, \d)?>",
+    m = re.search(r"chain_kernel<(\d), (\d+), \d+, \d+, (\d+), (true|false), \d, \d, \d, \d, (true|false), (\d)(?:, \w+)?>",
                   name)
     if m:
         key = (m.group(4) == "true", int(m.group(2)), int(m.group(3)), int(m.group(6)), m.group(5) == "true")
