@@ -271,15 +271,29 @@ def test_e2e_fast_preset_deviation(dev, name, preset):
     dpose = max(report[f"{m}:dpose"] for m in mods)
     print(f"  worst parameter gradient {report['worst_param']:.3e} (relative L2 {report['worst_l2']:.3e}), "
           f"worst dpose {dpose:.3e}")
-    assert report["worst_l2"] < FAST_GRAD_L2 and dpose < FAST_DPOSE, (report["worst_l2"], dpose)
+    l2 = {k: rel_l2(p.grad.cpu(), f["g:" + k]) for k, p in model.named_parameters() if "g:" + k in f}
+    for k in sorted(l2, key=lambda k: -l2[k])[:6]:
+        print(f"    {k:80s} relative L2 {l2[k]:.3e}")
+    bl2, bpose = fast_grad_bounds(preset)
+    assert report["worst_l2"] < bl2 and dpose < bpose, (report["worst_l2"], dpose)
 
 
 # fast preset geometry bounds (fp32 mode: gradients 2e-3, hessians 0.15)
 # (split-bf16x3 operands carry ~17 significant bits: measured gradients 2.4e-3, hessians 0.9 of the reference's hessian
 # scale on both fixtures; the bf16-weight SDF chain -- preset fast_x2 -- measured 56 and fails)
 GEO_TOL_FAST = {"gradients": 5e-3, "hessians": 1.5}
-# parameter gradients (relative L2, worst tensor) and pose gradients of the throughput presets
-FAST_GRAD_L2, FAST_DPOSE = 5e-2, 5e-2
+# parameter gradients (relative L2 of the worst tensor) and pose gradients (scale-relative max) of the throughput
+# presets against the reference's, about 2x the worst measured over the four fixtures and the full-size one (round 5):
+# fast 1.5e-2 / 3.9e-2; fast_h16 and fast_h16b alike 3.2e-2 / 6.8e-2 -- the fp16 forward operands (2^-11) move
+# near-zero ReLU pre-activations of the background, radiance and head MLPs across zero (the row-scaled fp16 backward adds
+# nothing measurable), and the free-running sampler's bins follow the SDF's rounding.  The fp32 parity mode's bounds
+# are 1e-3 / 5e-3 (test_e2e_train_step).
+FAST_GRAD_BOUNDS = {"fast": (3e-2, 8e-2)}
+FAST_GRAD_BOUNDS_FP16 = (6e-2, 0.14)
+
+
+def fast_grad_bounds(preset):
+    return FAST_GRAD_BOUNDS.get(preset, FAST_GRAD_BOUNDS_FP16)
 
 
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_gridbg_s95000"])

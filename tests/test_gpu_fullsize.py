@@ -41,7 +41,7 @@ import numpy as np
 import pytest
 import torch
 
-from test_gpu_e2e import FAST_DPOSE, FAST_GRAD_L2, FAST_PRESETS, GEO_TOL_FAST, GOLD, E2ECase, load, rel_err, rel_l2
+from test_gpu_e2e import FAST_PRESETS, GEO_TOL_FAST, GOLD, E2ECase, fast_grad_bounds, load, rel_err, rel_l2
 
 pytestmark = pytest.mark.gpu
 NAME = "e2e_full_grid_rgb_l19"
@@ -240,4 +240,5 @@ def test_fullsize_fast_preset(dev, preset):
             worst, wk = e, k
     dpose = rel_err(case.pose.pose_adjustment["rgb"].grad.cpu(), f["rgb:dpose"])
     print(f"  worst parameter gradient relative L2 {worst:.3e} ({wk}), dpose {dpose:.3e}")
-    assert worst < FAST_GRAD_L2 and dpose < FAST_DPOSE
+    bl2, bpose = fast_grad_bounds(preset)
+    assert worst < bl2 and dpose < bpose
