@@ -135,13 +135,16 @@ int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const 
  * Backward-data (backward = 1): X = dY of the last forward layer (rows >= rows_full: column 0 only), optionally
  *   scaled by act'(xaux) (stored to xout); out[l] = (prev . W^T) * act_l'(aux[l]) with act' evaluated from the
  *   forward output aux[l] (NULL: no scaling); the last out = dX.
- * SDF backward only (3 layers, Softplus, rows_full < M): tap_part [ceil(M / 128) - rows_full / 128][ld_tap > N[0]]
- *   receives one row per 128-row block holding rows >= rows_full: that block's share of the last forward layer's
+ * SDF backward only (3 layers, Softplus, rows_full < M): tap_part [ceil(M / B) - rows_full / B][ld_tap > N[0]]
+ *   (B = mms_mlp_chain_block_rows()) receives one row per B-row block holding rows >= rows_full: that block's share of
+ *   the last forward layer's
  *   weight-gradient row 0, sum over its rows >= rows_full of X[m, 0] * aux[0][m, :] (columns < N[0]), and of the bias
  *   gradient, sum of X[m, 0] (column N[0]) -- the taps' sdf column, surface_model.py:137-153 (reduce with
  *   mms_rowsum_add); NULL: not computed. 
  * a_hi / a_lo: per-layer packed weights from mms_mlp_pack (bf16, 32 ceil(N/32) x 16 ceil(K/16)); layers >= 1 are
  * register-fed and must be packed with permute = 1.  All row pitches multiples of 4 floats, 16-B aligned. */
+/* Rows per mms_mlp_chain block (128; 64 in a build with two blocks per CU): the tap_part row granularity. */
+int mms_mlp_chain_block_rows(void);
 int mms_mlp_chain(int prec, int backward, int n_layers, const float* X, int64_t ldx, int K0, int64_t M,
                   int64_t rows_full, const float* xaux, int64_t ldxaux, int xact, float* xout, int64_t ldxout,
                   const void* const* a_hi, const void* const* a_lo, const float* const* bias, const float* const* aux,

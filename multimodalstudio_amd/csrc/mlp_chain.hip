@@ -60,6 +60,13 @@ __device__ __forceinline__ void mma(floatx16& acc, const bf16x8& ah, const bf16x
 #ifndef MMS_CHAIN_DEPTH
 #define MMS_CHAIN_DEPTH 2
 #endif
+// waves per block (32 rows each): 4 (one block of 128 rows per CU), or 2 (64-row blocks, two of them per CU when the
+// LDS allows: their k-step barriers and epilogues then run independently of each other)
+#ifndef MMS_CHAIN_NW
+#define MMS_CHAIN_NW 4
+#endif
+constexpr int kNW = MMS_CHAIN_NW;
+constexpr int kRowsB = 32 * kNW;
 constexpr int kMaxTiles = 10;  // widest chain layer: 10 column tiles (320 units)
 
 // Diagnostic build only (MMS_CHAIN_STAMPS=1, scripts/lib_variants.py "stamps"; the product library has none): each
@@ -93,9 +100,9 @@ __device__ __forceinline__ void stamp_seg(unsigned long long* st, unsigned long 
 #endif
 }
 
-// loads per wave per k-step when NTL tiles are staged (uniform over the 4 waves: padded with dummy loads)
+// loads per wave per k-step when NTL tiles are staged (uniform over the block's waves: padded with dummy loads)
 template <int PREC, int NTL>
-constexpr int stage_per() { return (nimg<PREC>() * NTL + 3) / 4; }
+constexpr int stage_per() { return (nimg<PREC>() * NTL + kNW - 1) / kNW; }
 
 // issue k-step s's fragments of tiles [0, NTL) (hi, then lo) into ring slot s % (D + 1)
 constexpr int cmax(int x, int y) { return x > y ? x : y; }
@@ -106,7 +113,7 @@ __device__ __forceinline__ void stage(const ChainLayer& Ly, int s, int wave, int
   constexpr int TOTAL = nimg<PREC>() * NTL;
 #pragma unroll
   for (int i = 0; i < stage_per<PREC, NTL>(); ++i) {
-    const int c = wave + 4 * i;
+    const int c = wave + kNW * i;
     const bool real = c < TOTAL;
     const int cc = real ? c : 0;
     const int img = cc / NTL, t = cc - img * NTL;
@@ -585,24 +592,25 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   // where the block's LDS holds it
   constexpr int kSlotK = cmax(nimg<P0>() * NT0, nimg<PR>() * cmax(NT1, NT2)) + 1;
   constexpr bool kXio = BWD && XA != 0;
-  constexpr int kStageB = (BWD || KEEP) ? 4 * 32 * kScr * 4 : 16;
+  constexpr int kStageB = (BWD || KEEP) ? kNW * 32 * kScr * 4 : 16;
   auto lds_for = [](int d) constexpr {
-    return (d + 1) * (kSlotK * 1024 + (kXio ? 2 : 1) * 8192) + kStageB + NL * 32 * kMaxTiles * 4 + 32 * NT1 * 4 +
-           4 * (32 * NT0 + 4) * 4;
+    return (d + 1) * (kSlotK * 1024 + (kXio ? 2 : 1) * 2048 * kNW) + kStageB + NL * 32 * kMaxTiles * 4 +
+           32 * NT1 * 4 + kNW * (32 * NT0 + 4) * 4;
   };
-  constexpr int kD = (MMS_CHAIN_DEPTH >= 4 && lds_for(4) <= 160 * 1024) ? 4
-                     : (MMS_CHAIN_DEPTH >= 3 && lds_for(3) <= 160 * 1024) ? 3 : 2;
+  constexpr int kLdsCap = (160 / (4 / kNW)) * 1024;   // the block's share of the CU's 160 KiB
+  constexpr int kD = (MMS_CHAIN_DEPTH >= 4 && lds_for(4) <= kLdsCap) ? 4
+                     : (MMS_CHAIN_DEPTH >= 3 && lds_for(3) <= kLdsCap) ? 3 : 2;
   __shared__ __attribute__((aligned(1024))) bf16x8 ring[kD + 1][kSlotK][64];
   // layer-0 input slices (and, backward radiance chain, the xaux slices): [slot][wave][2 x 64 lane chunks]
-  __shared__ __attribute__((aligned(1024))) f32x4 xring[kD + 1][4][128];
-  __shared__ __attribute__((aligned(1024))) f32x4 aring[kXio ? kD + 1 : 1][4][128];
+  __shared__ __attribute__((aligned(1024))) f32x4 xring[kD + 1][kNW][128];
+  __shared__ __attribute__((aligned(1024))) f32x4 aring[kXio ? kD + 1 : 1][kNW][128];
   __shared__ __attribute__((aligned(16))) float sbias[NL][32 * kMaxTiles];  // forward biases, zero padded
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar staging addresses
   const int r = lane & 31, h = lane >> 5;
-  // 128 rows per block, 32 per wave.  Waves past M keep running on clamped rows (no stores): every wave takes part
+  // kRowsB rows per block, 32 per wave.  Waves past M keep running on clamped rows (no stores): every wave takes part
   // in the block's barriers.
-  const int64_t mb = (int64_t)blockIdx.x * 128;
+  const int64_t mb = (int64_t)blockIdx.x * kRowsB;
   const int64_t m0 = mb + 32 * wave;
   const int64_t m = m0 + r;
   const bool mval = m < a.M;
@@ -622,17 +630,17 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   __shared__ __attribute__((aligned(16))) float sw0[BWD ? 1 : 32 * NT1];  // forward: last layer's weight row 0 (fp32)
   // per-wave staging of the row-contiguous stores (forward KEEP) and of the backward's Y loads / dZ stores
   constexpr bool kStage = BWD || KEEP;
-  __shared__ __attribute__((aligned(16))) float sscr[kStage ? 4 : 1][32 * kScr];
+  __shared__ __attribute__((aligned(16))) float sscr[kStage ? kNW : 1][32 * kScr];
   float* scr = &sscr[kStage ? wave : 0][0];
   // the SDF backward (3 layers, Softplus, input = the last forward layer's dY): the taps' dW_last row-0 partials
   constexpr bool kTapW = BWD && NL == 3 && A0 == 2 && XA == 0;
-  __shared__ __attribute__((aligned(16))) float stap[kTapW ? 4 : 1][32 * NT0 + 4];
+  __shared__ __attribute__((aligned(16))) float stap[kTapW ? kNW : 1][32 * NT0 + 4];
   if constexpr (!BWD) {
 #pragma unroll
     for (int l = 0; l < NL; ++l)
-      for (int i = threadIdx.x; i < 32 * kMaxTiles; i += 256)
+      for (int i = threadIdx.x; i < 32 * kMaxTiles; i += 64 * kNW)
         sbias[l][i] = (a.L[l].bias != nullptr && i < a.L[l].N) ? a.L[l].bias[i] : 0.f;
-    for (int i = threadIdx.x; i < 32 * NT1; i += 256) sw0[i] = (a.w2row0 != nullptr && i < a.L[1].N) ? a.w2row0[i] : 0.f;
+    for (int i = threadIdx.x; i < 32 * NT1; i += 64 * kNW) sw0[i] = (a.w2row0 != nullptr && i < a.L[1].N) ? a.w2row0[i] : 0.f;
   }  // (visible after the first layer's opening barrier)
 
   // ---- layer 0: B operand from memory, natural k order
@@ -708,7 +716,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
   float inv1 = 1.f;   // PREC 6: inverse scale of layer 1's accumulators
   if constexpr (BWD) {
     // the SDF backward (3 layers, Softplus, input = the last forward layer's dY): the taps' dW_last row 0 on the way
-    if (kTapW && a.tap_part != nullptr && mb + 128 > a.rows_full)
+    if (kTapW && a.tap_part != nullptr && mb + kRowsB > a.rows_full)
       epilogue_bwd_staged<NT0, A0, kTapW>(acc0, a.L[0], m0, a.M, scr, lane, a.beta, a.thr, &a, &stap[wave][0]);
     else
       epilogue_bwd_staged<NT0, A0, false, NL == 4 ? MMS_CHAIN_YAHEAD4 : MMS_CHAIN_YAHEAD>(acc0, a.L[0], m0, a.M, scr,
@@ -823,10 +831,15 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
 #endif
 #undef MMS_ST
   if constexpr (kTapW) {
-    if (a.tap_part != nullptr && mb + 128 > a.rows_full) {
+    if (a.tap_part != nullptr && mb + kRowsB > a.rows_full) {
       __syncthreads();
-      float* row = a.tap_part + (int64_t)(blockIdx.x - a.rows_full / 128) * a.ld_tap;
-      for (int i = threadIdx.x; i <= 32 * NT0; i += 256) row[i] = ((stap[0][i] + stap[1][i]) + stap[2][i]) + stap[3][i];
+      float* row = a.tap_part + (int64_t)(blockIdx.x - a.rows_full / kRowsB) * a.ld_tap;
+      for (int i = threadIdx.x; i <= 32 * NT0; i += 64 * kNW) {
+        float v = stap[0][i];
+#pragma unroll
+        for (int w = 1; w < kNW; ++w) v += stap[w][i];
+        row[i] = v;
+      }
     }
   }
 }
@@ -834,8 +847,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
 template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, int XA, bool KEEP = false,
           int NL = 3>
 void launch_chain(const ChainArgs& a, hipStream_t s) {
-  const unsigned blocks = (unsigned)((a.M + 127) / 128);
-  hipLaunchKernelGGL((chain_kernel<PREC, KS0, NT0, NT1, NT2, BWD, A0, A1, A2, XA, KEEP, NL>), dim3(blocks), dim3(256), 0,
+  const unsigned blocks = (unsigned)((a.M + kRowsB - 1) / kRowsB);
+  hipLaunchKernelGGL((chain_kernel<PREC, KS0, NT0, NT1, NT2, BWD, A0, A1, A2, XA, KEEP, NL>), dim3(blocks), dim3(64 * kNW), 0,
                      s, a);
 }
 
@@ -1060,6 +1073,8 @@ MMS_EXPORT int mms_mlp_pack(const float* W, int64_t N, int64_t K, int64_t ldw, i
                      reinterpret_cast<__bf16*>(lo));
   return mms::check_launch(fn);
 }
+
+MMS_EXPORT int mms_mlp_chain_block_rows(void) { return kRowsB; }
 
 MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* X, int64_t ldx, int K0, int64_t M,
                              int64_t rows_full, const float* xaux, int64_t ldxaux, int xact, float* xout,

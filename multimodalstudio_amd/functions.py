@@ -730,7 +730,8 @@ class ChainRun:
         tap_part = None
         if tapw:
             n0 = Ns[L - 2]
-            tap_part = torch.empty(-(-M // 128) - rf // 128, n0 + 4, device=dev)
+            B = 128 if self.l16 else _lib.lib().mms_mlp_chain_block_rows()
+            tap_part = torch.empty(-(-M // B) - rf // B, n0 + 4, device=dev)
         self._chain(True, dy, Ns[L - 1], rf, packs, [None] * L, [Y[l] for l in order] + [None],
                     [dZ[l] for l in order] + [dx], [Ns[l] for l in order] + [K0], [acts[l] for l in order] + [0],
                     xaux=Y[L - 1] if acts[L - 1] != 0 else None, xact=acts[L - 1], xout=dZl, tap_part=tap_part)

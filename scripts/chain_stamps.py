@@ -43,6 +43,7 @@ def report(name, st, groups):
 
 def main():
     from multimodalstudio_amd import _lib, functions as fx
+    fx.PRECISION["bwd16"] = int(os.environ.get("MMS_STAMP_BWD16", "1"))   # the backward chains on prec 6 (fast_h16b)
     lib = _lib.lib()
     lib.mms_chain_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
     lib.mms_chain_stamps.restype = ctypes.c_int

@@ -29,6 +29,7 @@ VARIANTS = {  # name: (translation unit, macro definitions)
     "wpipe0": ("gemm", {"MMS_WIDE_PIPE": 0}),   # the wide weight-gradient kernel's one-register-set loop (round 3)
     "d3": ("mlp_chain", {"MMS_CHAIN_DEPTH": 3}),  # the chains' weight / input ring three k-steps deep (where LDS allows)
     "d4": ("mlp_chain", {"MMS_CHAIN_DEPTH": 4}),
+    "nw2": ("mlp_chain", {"MMS_CHAIN_NW": 2}),    # 64-row chain blocks (two per CU where the LDS holds them)
 }
 # the two-waves-per-SIMD chain's ablations (csrc/chain16.hip MMS_C16_ABL bits: 1 no MFMA, 2 no weight DMA, 4 no
 # barrier, 8 no epilogue)
