@@ -330,7 +330,13 @@ __device__ __forceinline__ void epi_tile_store(const floatx16& acc, int t, float
 // epilogue loads anyway (the grouped weight-gradient launch would re-read 4 M rows x 1 KB of Y for that one row):
 // per lane 4 rows x 4 columns per tile, reduced over the wave's rows by xor shuffles into the wave's LDS row `sp`
 // (plain LDS stores: nothing here adds a vector-memory instruction the k-loops' exact vmcnt waits would count); the
-// block writes its partial row once, at the end of the kernel.
+// block writes its partial row once, at the end of the kernel.  (Storing the per-lane partials unreduced, 8 rows per
+// wave, and summing them at the end measured equal: tap blocks -2 %, the step within noise, round 5.)
+// Diagnostic builds only (MMS_CHAIN_EPI_ABL bits, scripts/lib_variants.py with the stamp build): 1 = no Y loads
+// (constant activations), 2 = no dZ stores, 4 = no scratch round trips (accumulator-layout values used as they are).
+#ifndef MMS_CHAIN_EPI_ABL
+#define MMS_CHAIN_EPI_ABL 0
+#endif
 template <int NT, int ACT, bool TAPW = false, int YMAX = MMS_CHAIN_YAHEAD>
 __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const ChainLayer& Ly, int64_t m0, int64_t M,
                                                     float* scr, int lane, float beta, float thr,
@@ -358,7 +364,10 @@ __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const C
   f32x4 y[YA][4];
   auto load = [&](int t, f32x4* dst) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dst[j] = ld_nt4(Ly.aux + rows[j] * Ly.ldaux + 32 * t + 4 * q);
+    for (int j = 0; j < 4; ++j) {
+      if constexpr ((MMS_CHAIN_EPI_ABL & 1) != 0) dst[j] = f32x4{0.3f, 0.2f, 0.1f, 0.4f};
+      else dst[j] = ld_nt4(Ly.aux + rows[j] * Ly.ldaux + 32 * t + 4 * q);
+    }
   };
 #pragma unroll
   for (int t = 0; t < YA; ++t) load(t, y[t]);
@@ -381,24 +390,30 @@ __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const C
       }
       if (lane < 8) *reinterpret_cast<f32x4*>(sp + 32 * t + 4 * q) = sw;
     }
+    constexpr bool kScrRT = (MMS_CHAIN_EPI_ABL & 4) == 0;
+    f32x4 ycopy[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(scr + (8 * j + (lane >> 3)) * kScr + 4 * q) = yt[j];
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (kScrRT) *reinterpret_cast<f32x4*>(scr + (8 * j + (lane >> 3)) * kScr + 4 * q) = yt[j];
+      else ycopy[j] = yt[j];
+    }
     if (t + YA < NT) load(t + YA, yt);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const f32x4 yv = *reinterpret_cast<const f32x4*>(scr + r * kScr + 8 * g + 4 * h);
+      const f32x4 yv = kScrRT ? *reinterpret_cast<const f32x4*>(scr + r * kScr + 8 * g + 4 * h) : ycopy[g];
       f32x4 v;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         v[i] = acc[t][4 * g + i] * act_grad_out<ACT>(yv[i], beta, thr);
         acc[t][4 * g + i] = v[i];
       }
-      *reinterpret_cast<f32x4*>(scr + r * kScr + 8 * g + 4 * h) = v;
+      if constexpr (kScrRT) *reinterpret_cast<f32x4*>(scr + r * kScr + 8 * g + 4 * h) = v;
+      else ycopy[g] = v;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(scr + (8 * j + (lane >> 3)) * kScr + 4 * q);
-      st_nt4(Ly.out + rows[j] * Ly.ldo + 32 * t + 4 * q, v);
+      const f32x4 v = kScrRT ? *reinterpret_cast<const f32x4*>(scr + (8 * j + (lane >> 3)) * kScr + 4 * q) : ycopy[j];
+      if constexpr ((MMS_CHAIN_EPI_ABL & 2) == 0) st_nt4(Ly.out + rows[j] * Ly.ldo + 32 * t + 4 * q, v);
     }
   }
   if constexpr (TAPW) {

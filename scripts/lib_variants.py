@@ -31,6 +31,9 @@ VARIANTS = {  # name: (translation unit, macro definitions)
     "d4": ("mlp_chain", {"MMS_CHAIN_DEPTH": 4}),
     "nw2": ("mlp_chain", {"MMS_CHAIN_NW": 2}),    # 64-row chain blocks (two per CU where the LDS holds them)
 }
+# the backward epilogue's ablations on the stamp build (MMS_CHAIN_EPI_ABL bits: 1 no Y loads, 2 no dZ stores, 4 no
+# scratch round trips)
+VARIANTS.update({f"stampsE{n}": ("mlp_chain", {"MMS_CHAIN_STAMPS": 1, "MMS_CHAIN_EPI_ABL": n}) for n in (1, 2, 4, 3, 7)})
 # the two-waves-per-SIMD chain's ablations (csrc/chain16.hip MMS_C16_ABL bits: 1 no MFMA, 2 no weight DMA, 4 no
 # barrier, 8 no epilogue)
 VARIANTS.update({f"c16a{n}": ("chain16", {"MMS_C16_ABL": n}) for n in (1, 2, 4, 8, 3, 9, 12, 6, 16, 32, 64, 48)})
