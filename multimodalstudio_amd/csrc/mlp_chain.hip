@@ -599,7 +599,7 @@ __device__ __forceinline__ void unscale(floatx16 (&acc)[NT], float inv) {
 // NL = 4: a middle register-fed layer of NT1 tiles with activation A1 sits between layer 1 and the last layer (the
 // background NeRF MLPs, 4 layers).  Backward: the same structure on the transposed weights, last layer first.
 template <int PREC, int KS0, int NT0, int NT1, int NT2, bool BWD, int A0, int A1, int A2, int XA, bool KEEP, int NL>
-__global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
+__global__ __launch_bounds__(64 * kNW) void chain_kernel(ChainArgs a) {
   // operand modes: layer 0 and the register-fed layers (differ only for the backward's PREC 6)
   constexpr int P0 = PREC == 6 ? 2 : PREC, PR = PREC == 6 ? 5 : PREC;
   static_assert(PREC != 6 || BWD, "PREC 6 is a backward mode");
@@ -612,7 +612,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs a) {
     return (d + 1) * (kSlotK * 1024 + (kXio ? 2 : 1) * 2048 * kNW) + kStageB + NL * 32 * kMaxTiles * 4 +
            32 * NT1 * 4 + kNW * (32 * NT0 + 4) * 4;
   };
-  constexpr int kLdsCap = (160 / (4 / kNW)) * 1024;   // the block's share of the CU's 160 KiB
+  constexpr int kLdsCap = (kNW >= 4 ? 160 : 160 * kNW / 4) * 1024;   // the block's share of the CU's 160 KiB
   constexpr int kD = (MMS_CHAIN_DEPTH >= 4 && lds_for(4) <= kLdsCap) ? 4
                      : (MMS_CHAIN_DEPTH >= 3 && lds_for(3) <= kLdsCap) ? 3 : 2;
   __shared__ __attribute__((aligned(1024))) bf16x8 ring[kD + 1][kSlotK][64];
