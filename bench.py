@@ -61,7 +61,9 @@ DTYPES = {"fp32": "fp32",
           "fast_h16b": "fp16 MFMA (fp32 accumulate: the reference's autocast) for the radiance / head / background MLP "
                        "forwards and for every MLP's backward-data chain after its first layer (per-row power-of-two "
                        "scaled), split-bf16x3 for the SDF MLP forward, the chains' first backward layer and the weight "
-                       "gradients, fp32 elsewhere"}
+                       "gradients, fp32 elsewhere",
+          "fast_h16bw": "as fast_h16b with bf16 MFMA (fp32 accumulate) for the MLP weight gradients -- not the "
+                        "benchmarked preset, fp32 elsewhere"}
 HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per lookup, forward
 HASH_BWD_B = 128 + 12 + 16 * 8 * 2 * (4 + 4)    # bytes per lookup, backward (table grads)
 HASH_BWD_ATOMIC_B = 16 * 8 * 2 * 4              # the float-atomic bytes one backward lookup adds into the table
