@@ -190,6 +190,38 @@ __device__ __forceinline__ void copy_cols_any(const float* __restrict__ src, int
     copy_cols<int64_t>(src, lds, dst, ldd, M, G, b0);
 }
 
+// dst[r, 1 + c] = src[r, c] for c < G with 16-B aligned rows on both sides (dst's row pitch and base, src's): thread
+// per (row, 16-B destination chunk) -- chunk 0 writes columns 1..3 alone (column 0 is the other blocks' sdf gradient),
+// the others one float4 each, built from the source chunk and its predecessor's last element; the destination's
+// columns past G + 1 inside the last chunk get zeros (the chains mask columns past K0).  A quarter of copy_cols'
+// instructions for the SDF's 256 geo columns.
+__device__ __forceinline__ void copy_cols_shift1_vec(const float* __restrict__ src, int64_t lds, float* __restrict__ dst,
+                                                     int64_t ldd, int64_t M, int G, unsigned b0) {
+  const int nch = (G + 1 + 3) / 4;   // destination chunks covering columns 0 .. G
+  const int64_t n = M * nch;
+  for (int64_t e = (int64_t)(blockIdx.x - b0) * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)(gridDim.x - b0) * blockDim.x) {
+    const int64_t r = e / nch;
+    const int k = (int)(e - r * nch);
+    const float* sr = src + r * lds;
+    float* dr = dst + r * ldd;
+    if (k == 0) {
+      for (int c = 1; c < 4 && c <= G; ++c) dr[c] = sr[c - 1];
+      continue;
+    }
+    const int c0 = 4 * k - 1;          // source column of the chunk's first element
+    // the source chunks k - 1 and k (16-B aligned; chunk k's columns past G lie inside the source row and are dropped)
+    const float4 prev = *reinterpret_cast<const float4*>(sr + 4 * k - 4);
+    const float4 cur = 4 * k < G ? *reinterpret_cast<const float4*>(sr + 4 * k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 v;
+    v.x = prev.w;
+    v.y = c0 + 1 < G ? cur.x : 0.f;
+    v.z = c0 + 2 < G ? cur.y : 0.f;
+    v.w = c0 + 3 < G ? cur.z : 0.f;
+    *reinterpret_cast<float4*>(dr + 4 * k) = v;
+  }
+}
+
 // backward: writes d sdf into column 0 of dOut rows (centre + taps) (overwrite), plus the centre rows' own sdf
 // gradient (dsdf) and, in the blocks past tap_blocks, the geo-feature gradient into columns 1..G of the centre rows
 // (copy_cols)
@@ -199,7 +231,10 @@ __global__ void taps_combine_bwd_kernel(const float* __restrict__ grads, const f
                                         int64_t lddo, const float* __restrict__ dsdf, int64_t ldds,
                                         const float* __restrict__ dgeo, int64_t ldg, int G, unsigned tap_blocks) {
   if (blockIdx.x >= tap_blocks) {
-    copy_cols_any(dgeo, ldg, dout + 1, lddo, M, G, tap_blocks);
+    const bool vec = dgeo != nullptr && ((uintptr_t)dout & 15) == 0 && lddo % 4 == 0 && lddo >= 4 * ((G + 4) / 4) &&
+                     ((uintptr_t)dgeo & 15) == 0 && ldg % 4 == 0 && ldg >= 4 * ((G + 3) / 4);
+    if (vec) copy_cols_shift1_vec(dgeo, ldg, dout, lddo, M, G, tap_blocks);
+    else copy_cols_any(dgeo, ldg, dout + 1, lddo, M, G, tap_blocks);
     return;
   }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += (int64_t)tap_blocks * blockDim.x) {

@@ -231,3 +231,38 @@ def test_inv_variance_equals_torch(dev):
         ref = 1.0 / torch.exp(s * 10.0).clip(1e-6, 1e6)
         torch.cuda.synchronize()
         assert torch.equal(out, ref), (v, out.item(), ref.item())
+
+
+@pytest.mark.parametrize("aligned", [True, False])
+def test_taps_combine_bwd_geo_columns(dev, aligned):
+    """mms_taps_combine_bwd's geo-gradient columns: the centre rows' columns 1..G are the radiance panel gradient's geo
+    columns bit for bit, through the float4 path (16-B aligned rows on both sides, columns past G + 1 in the last chunk
+    zeroed) and through the element-wise fallback (an unaligned source); column 0 of every row is the sdf gradient of
+    the tap formula, the same on both paths."""
+    from multimodalstudio_amd import _lib
+    from multimodalstudio_amd import functions as fx
+    g = torch.Generator().manual_seed(5)
+    M, G = 1000, 256
+    grads = torch.randn(M, 3, generator=g).to(dev)
+    dgrads = torch.randn(M, 3, generator=g).to(dev)
+    dhess = torch.randn(M, 3, generator=g).to(dev)
+    dsdf = torch.randn(M, 1, generator=g).to(dev)
+    panel = torch.randn(M, 320, generator=g).to(dev)   # the radiance panel pitch (16-B rows)
+    dgeo = panel[:, 28:28 + G] if aligned else panel[:, 29:29 + G]
+    dout = torch.full((5 * M, 260), float("nan"), device=dev)
+    _lib.call("mms_taps_combine_bwd", grads.data_ptr(), dgrads.data_ptr(), dhess.data_ptr(), None, M, 4.5e-3, 1.3e-6,
+              dout.data_ptr(), dout.stride(0), dsdf.data_ptr(), dsdf.stride(0), dgeo.data_ptr(), dgeo.stride(0), G,
+              fx._s())
+    torch.cuda.synchronize()
+    assert torch.equal(dout[:M, 1:G + 1], dgeo)
+    if aligned:
+        assert torch.equal(dout[:M, G + 1:], torch.zeros(M, 260 - G - 1, device=dev))
+    assert torch.isfinite(dout[:, 0]).all()
+    ref = dout[:, 0].clone()
+    dout2 = torch.full_like(dout, float("nan"))
+    dgeo2 = panel[:, 29:29 + G]     # unaligned: element-wise path
+    _lib.call("mms_taps_combine_bwd", grads.data_ptr(), dgrads.data_ptr(), dhess.data_ptr(), None, M, 4.5e-3, 1.3e-6,
+              dout2.data_ptr(), dout2.stride(0), dsdf.data_ptr(), dsdf.stride(0), dgeo2.data_ptr(), dgeo2.stride(0), G,
+              fx._s())
+    torch.cuda.synchronize()
+    assert torch.equal(dout2[:, 0], ref)
