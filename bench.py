@@ -43,7 +43,7 @@ BF16_MFMA_PEAK_TF = 2500.0  # dense bf16 MFMA peak (no sparsity), MI355X_MICROAR
 # split-bf16x3 runs 3 bf16 MFMAs per f32 product: its ceiling for the algorithmic 2MNK flops is a third
 # (bf16x2: the SDF chain's split activations x bf16 weights, 2 bf16 MFMAs per product)
 MFMA_PEAK_TF = {"fp32": F32_MFMA_PEAK_TF, "bf16": BF16_MFMA_PEAK_TF, "bf16x3": BF16_MFMA_PEAK_TF / 3,
-                "bf16x2": BF16_MFMA_PEAK_TF / 2, "fp16": BF16_MFMA_PEAK_TF, "fp16-rowscaled": BF16_MFMA_PEAK_TF}
+                "bf16x2": BF16_MFMA_PEAK_TF / 2, "fp16": BF16_MFMA_PEAK_TF}
 PREC_NAMES = {0: "fp32", 1: "bf16", 2: "bf16x3", 3: "bf16x2", 5: "fp16", 6: "fp16-rowscaled"}
 DTYPES = {"fp32": "fp32",
           "fast": "split-bf16x3 MFMA (bf16 hi + lo operands, fp32 accumulate) for every MLP, fp32 elsewhere",
@@ -64,6 +64,8 @@ DTYPES = {"fp32": "fp32",
                        "gradients, fp32 elsewhere",
           "fast_h16bw": "as fast_h16b with bf16 MFMA (fp32 accumulate) for the MLP weight gradients -- not the "
                         "benchmarked preset, fp32 elsewhere"}
+# the benchmarked preset (tests/test_cpu_host.py::test_benchmarked_preset_* guard its numerics)
+DEFAULT_PRECISION = "fast_h16b"
 HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per lookup, forward
 HASH_BWD_B = 128 + 12 + 16 * 8 * 2 * (4 + 4)    # bytes per lookup, backward (table grads)
 HASH_BWD_ATOMIC_B = 16 * 8 * 2 * 4              # the float-atomic bytes one backward lookup adds into the table
@@ -105,7 +107,8 @@ def chain_work(a):
     st = [outs[i] is not None for i in range(nl)]
     mid = sum(n[l - 1] * n[l] for l in range(1, nl - 1))
     if bwd:
-        flops = 2.0 * (rf * K0 + (M - rf)) * n[0] + 2.0 * M * (mid + n[nl - 2] * n[nl - 1])
+        f0 = 2.0 * (rf * K0 + (M - rf)) * n[0]       # the first backward layer (B = dY from memory)
+        flops = f0 + 2.0 * M * (mid + n[nl - 2] * n[nl - 1])
         nbytes = 4.0 * ((rf * K0 + (M - rf)) + M * sum(n[l] * st[l] for l in range(nl)) + M * sum(n[:nl - 1]))
     else:
         flops = 2.0 * M * (K0 * n[0] + mid) + 2.0 * (rf * n[nl - 1] + (M - rf)) * n[nl - 2]
@@ -119,7 +122,12 @@ def chain_work(a):
         role = "head"                      # the modality heads 256-64-64-C (bwd: 64-64-256 from C)
     else:
         role = ("sdf" if width < 128 else "radiance") + ("_infer" if (not bwd and rf == 0) else "")
-    return f"{PREC_NAMES[prec]}:{role}{'_bwd' if bwd else '_fwd'}", (flops, nbytes)
+    label = f"{PREC_NAMES[prec]}:{role}{'_bwd' if bwd else '_fwd'}"
+    if prec == 6 and bwd:
+        # fp16-rowscaled: the first backward layer runs split-bf16x3 (3 MFMAs per product), the register-fed layers
+        # one fp16 MFMA: the third element is the launch's work in single-MFMA-equivalent flops (its mode ceiling)
+        return label, (flops, nbytes, flops + 2.0 * f0)
+    return label, (flops, nbytes)
 
 
 def hash_fwd_work(a):
@@ -160,7 +168,6 @@ def work_fns():
         "mms_gemm_tn_grouped": gemm_grouped_work,
         "mms_gemm_tn_wide": gemm_grouped_work,
         "mms_mlp_chain": chain_work,
-        "mms_mlp_chain16": chain_work,      # (the same arguments)
         "mms_hashgrid_fwd_grouped": hash_fwd_work,
         "mms_sdf_panel_fwd": sdf_panel_work,
         "mms_sdf_panel_rays_fwd": sdf_panel_rays_work,
@@ -181,7 +188,7 @@ def kernel_records(summ, timing_steps: int, precision: str):
         rec = {"kernel": name, "avg_ms": round(ms, 5), "launches_per_step": launches_per_step,
                "ms_per_step": round(ms * launches_per_step, 4), "traffic": None}
         if name.startswith("mms_gemm") or name.startswith("mms_mlp_chain"):   # (incl. the grouped weight gradients)
-            flops, nbytes = work
+            flops, nbytes = work[:2]
             mode = name.split(":")[1]      # "mms_gemm:<precision>:<NT|NN|TN>", "mms_mlp_chain:<precision>:<role>"
             peak = F32_MFMA_PEAK_TF if mode == "fp32" else BF16_MFMA_PEAK_TF
             ach = flops / (ms * 1e-3) / 1e12
@@ -190,6 +197,10 @@ def kernel_records(summ, timing_steps: int, precision: str):
             if mode in ("bf16x3", "bf16x2"):
                 rec.update({"mode_peak": round(MFMA_PEAK_TF[mode], 1),
                             "frac_of_mode_peak": round(ach / MFMA_PEAK_TF[mode], 4)})
+            elif mode == "fp16-rowscaled" and len(work) > 2:
+                # priced per layer: the split-bf16x3 first layer at a third of the peak, the fp16 layers at the peak
+                mp = BF16_MFMA_PEAK_TF * flops / work[2]
+                rec.update({"mode_peak": round(mp, 1), "frac_of_mode_peak": round(ach / mp, 4)})
         else:
             atomic = None
             if isinstance(work, tuple):
@@ -375,7 +386,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--precision", default="fast_h16b", choices=list(DTYPES),
+    ap.add_argument("--precision", default=DEFAULT_PRECISION, choices=list(DTYPES),
                     help="MLP GEMM precision preset (functions.PRESETS); fp32 = reference-parity mode")
     ap.add_argument("--sampler", default="device", choices=["device", "host"],
                     help="pixel sampler: HBM-resident frames + device Philox draws (default), or the reference-order "
@@ -436,7 +447,7 @@ def main():
         # headline (north_star / SURVEY §8(d)): MFMA utilisation of the fused geometry-MLP chain, forward, rated by
         # its algorithmic 2MNK flops against the dense bf16 MFMA peak; the hash-grid lookups against HBM beside it
         by_name = {k["kernel"]: k for k in kernels}
-        sdf = [k for k in kernels if k["kernel"].startswith(("mms_mlp_chain:", "mms_mlp_chain16:"))
+        sdf = [k for k in kernels if k["kernel"].startswith("mms_mlp_chain:")
                and k["kernel"].endswith(":sdf_fwd")]
         top = sdf[0] if sdf else (kernels[0] if kernels else None)
         if top is not None:

@@ -150,25 +150,10 @@ int mms_mlp_chain(int prec, int backward, int n_layers, const float* X, int64_t 
                   const void* const* a_hi, const void* const* a_lo, const float* const* bias, const float* const* aux,
                   const int64_t* ldaux, float* const* out, const int64_t* ldo, const int* N, const int* act,
                   float beta, float thr, const float* w2row0, float* tap_part, int64_t ld_tap, void* stream);
-/* The SDF and radiance chains at two waves per SIMD (16x16x32 MFMA tiles, 16 rows per wave, 8 waves per 128-row
- * block): same arguments, semantics and reference interfaces as mms_mlp_chain for the 3-layer SDF chain 71-256-256-257
- * (Softplus hidden layers; forward with or without hidden stores and single-output rows >= rows_full; backward with
- * the taps' tap_part) and the radiance chain 317-256-256-256 (ReLU; forward storing the hidden layers; backward with
- * the input scaled by xaux and stored to xout, >= 32 ceil(K0/32) columns), prec 1 or 2.  Weights packed with permute
- * bit 1 set (the 16x16x32 layout: 16 ceil(N/16) x 32 ceil(K/32)); layers >= 1 with bit 0 too.  Replaces the same
- * weight-normed MLP as mms_mlp_chain (mlp.py:152-209; surface_field.py:99-116, radiance_field.py:72-77). */
-int mms_mlp_chain16(int prec, int backward, int n_layers, const float* X, int64_t ldx, int K0, int64_t M,
-                    int64_t rows_full, const float* xaux, int64_t ldxaux, int xact, float* xout, int64_t ldxout,
-                    const void* const* a_hi, const void* const* a_lo, const float* const* bias,
-                    const float* const* aux, const int64_t* ldaux, float* const* out, const int64_t* ldo,
-                    const int* N, const int* act, float beta, float thr, const float* w2row0, float* tap_part,
-                    int64_t ld_tap, void* stream);
 /* bf16 (hi, and lo = residual if non-NULL) image of W [N, K] (ldw) as an MFMA A operand of rows x cols:
- * transpose = 0 -> A = W, 1 -> A = W^T; permute bit 0 stores each k-step in register-fed order (32x32x16: columns
- * 0-3, 8-11, 4-7, 12-15 of a 16-column step; 16x16x32: K position 8 g + j <- column 4 g + j (j < 4) or 16 + 4 g +
- * j - 4 of a 32-column step).  permute bit 1 selects the 16x16x32 layout (mms_mlp_chain16); bit 2 writes an fp16 image
- * (hi only, fp16 bits in the 16-bit buffer: mms_mlp_chain prec 5).  Zero padded; rows % 32
- * == 0, cols % 16 == 0 (16x16x32: rows % 16, cols % 32).  Fragment-major: the fragment of (k-step s, row tile t) is
+ * transpose = 0 -> A = W, 1 -> A = W^T; permute bit 0 stores each k-step in register-fed order (columns 0-3, 8-11,
+ * 4-7, 12-15 of a 16-column step); bit 2 writes an fp16 image (hi only, fp16 bits in the 16-bit buffer:
+ * mms_mlp_chain prec 5).  Zero padded; rows % 32 == 0, cols % 16 == 0.  Fragment-major: the fragment of (k-step s, row tile t) is
  * one 1 KiB block at element ((s * tiles + t) * 64 + lane) * 8. */
 int mms_mlp_pack(const float* W, int64_t N, int64_t K, int64_t ldw, int transpose, int permute, int64_t rows,
                  int64_t cols, void* hi, void* lo, void* stream);

@@ -1,5 +1,4 @@
-// Shared by the fused MLP chain kernels (mlp_chain.hip: 32x32x16 MFMA, one wave per SIMD; chain16.hip: 16x16x32
-// MFMA, two waves per SIMD): argument structs, activations and their derivatives, split-bf16 conversion, the LDS-DMA
+// Used by the fused MLP chain kernels (mlp_chain.hip: 32x32x16 MFMA, one wave per SIMD): argument structs, activations and their derivatives, split-bf16 conversion, the LDS-DMA
 // weight / input staging and the exact-count wait + barrier.  Reference layers: weight-normed nn.Linear + activation
 // (/root/reference/src/field_components/mlp.py:152-209).
 #pragma once

@@ -994,34 +994,19 @@ __device__ __forceinline__ int64_t perm_col(int64_t c) {
   return (c & ~(int64_t)15) | (q & 3) | ((q & 4) << 1) | ((q & 8) >> 1);
 }
 
-// 16x16x32 layout (chain16.hip): a register-fed 32-unit k-step holds units 4 g + j (j < 4) and 16 + 4 g + j - 4 of the
-// step at K position 8 g + j
-__device__ __forceinline__ int64_t perm_col16(int64_t c) {
-  const int64_t q = c & 31, gq = q >> 3, j = q & 7;
-  return (c & ~(int64_t)31) | (j < 4 ? 4 * gq + j : 16 + 4 * gq + (j - 4));
-}
-
-// one element i of a packed image, fragment-major.  permute bit 0: the register-fed column order; bit 1: the 16x16x32
-// layout ((k-step s of 32 columns, tile t of 16 rows) block, lane r + 16 (q >> 3), element q & 7) instead of 32x32x16
-// ((k-step of 16, tile of 32) block, lane r + 32 (q >> 3))
+// one element i of a packed image, fragment-major ((k-step of 16, tile of 32) block, lane r + 32 (q >> 3)).
+// permute bit 0: the register-fed column order
 __device__ __forceinline__ void pack_elem(const float* __restrict__ W, int64_t N, int64_t K, int64_t ldw, int transpose,
                                           int permute, int64_t rows, int64_t cols, __bf16* __restrict__ hi,
                                           __bf16* __restrict__ lo, int64_t i) {
   const int64_t R = transpose ? K : N, C = transpose ? N : K;
-  const bool l16 = (permute & 2) != 0;
-  const int64_t nt = rows / (l16 ? 16 : 32);
+  const int64_t nt = rows / 32;
   const int64_t row = i / cols, c = i - row * cols;
-  const int64_t src = (permute & 1) ? (l16 ? perm_col16(c) : perm_col(c)) : c;
+  const int64_t src = (permute & 1) ? perm_col(c) : c;
   float v = 0.f;
   if (row < R && src < C) v = transpose ? W[src * ldw + row] : W[row * ldw + src];
-  int64_t o;
-  if (l16) {
-    const int64_t s = c >> 5, q = c & 31, t = row >> 4, r = row & 15;
-    o = ((s * nt + t) * 64 + r + 16 * (q >> 3)) * 8 + (q & 7);
-  } else {
-    const int64_t s = c >> 4, q = c & 15, t = row >> 5, r = row & 31;
-    o = ((s * nt + t) * 64 + r + 32 * (q >> 3)) * 8 + (q & 7);
-  }
+  const int64_t s = c >> 4, q = c & 15, t = row >> 5, r = row & 31;
+  const int64_t o = ((s * nt + t) * 64 + r + 32 * (q >> 3)) * 8 + (q & 7);
   if (permute & 4) {   // fp16 image (bits stored in the bf16 buffer; mms_mlp_chain prec 5)
     hi[o] = __builtin_bit_cast(__bf16, (_Float16)v);
     return;
@@ -1100,8 +1085,8 @@ MMS_EXPORT int mms_mlp_pack(const float* W, int64_t N, int64_t K, int64_t ldw, i
   const char* fn = "mms_mlp_pack";
   MMS_REQUIRE(N > 0 && K > 0 && ldw >= K, fn, "bad weight shape");
   MMS_REQUIRE(rows >= (transpose ? K : N) && cols >= (transpose ? N : K), fn, "packed image smaller than the weight");
-  MMS_REQUIRE((permute & 2) ? (rows % 16 == 0 && cols % 32 == 0) : (rows % 32 == 0 && cols % 16 == 0), fn,
-              "packed image must be [32 x tiles][16 x k-steps] (16x16x32 layout: [16 x tiles][32 x k-steps])");
+  MMS_REQUIRE((permute & ~5) == 0, fn, "permute: bit 0 (register-fed order) and bit 2 (fp16 image) only");
+  MMS_REQUIRE(rows % 32 == 0 && cols % 16 == 0, fn, "packed image must be [32 x tiles][16 x k-steps]");
   MMS_REQUIRE(W && hi, fn, "null pointer");
   hipLaunchKernelGGL(pack_kernel, dim3(mms::grid_for(rows * cols, 256, 4096)), dim3(256), 0, mms::as_stream(stream), W,
                      N, K, ldw, transpose, permute, rows, cols, reinterpret_cast<__bf16*>(hi),

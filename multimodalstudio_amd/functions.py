@@ -372,10 +372,10 @@ def sdf_panel(pos: torch.Tensor, ldp: int, M: int, ntaps: int, delta: float, g: 
     grid_fwd(g, X, X.stride(0), (1 + ntaps) * M, table, active, X, 39, group=1 + ntaps)
 
 
-# hash-grid backward with both gradients: MMS_HASH_SPLIT=1 runs the table walk without position gradients + the
-# gather-style position-gradient kernel (scripts/hash_bench.py: the same 0.52 ms as the walk computing both, whose
-# time is the LDS merge, not its table re-gather), so the walk computes both by default
-HASH_SPLIT = os.environ.get("MMS_HASH_SPLIT", "0") == "1"
+# hash-grid backward with both gradients: the table walk computes both (scripts/hash_bench.py: the walk without
+# position gradients + the gather-style mms_hashgrid_dpos_grouped cost the same as the walk computing both).
+# HASH_SPLIT = True (tests only) routes the position gradient through the gather kernel.
+HASH_SPLIT = False
 
 
 def grid_bwd(g: GridCfg, pos, ldx, M, table, active, dout: torch.Tensor, col: int, dtable, dpos, group: int = 1):
@@ -561,21 +561,6 @@ class SmallRun:
 
 # the SDF taps' weight-gradient row inside the backward chain (MMS_TAP_WGRAD=0: a grouped weight-gradient item)
 TAP_WGRAD_IN_CHAIN = os.environ.get("MMS_TAP_WGRAD", "1") != "0"
-# the SDF / radiance chains at two waves per SIMD (mms_mlp_chain16: 16x16x32 MFMA tiles, 16 rows per wave) instead of
-# the 32x32x16 chain at one (MMS_CHAIN16=1).  Not the default: both kernels issue the same weight-staging VMEM
-# instructions per 128 rows and k-step, which bound them alike (step A/B 610k vs 622k rays/s)
-CHAIN16 = os.environ.get("MMS_CHAIN16", "0") == "1"
-
-
-def _chain16_shape(L: int, K0: int, Ns, acts, cprec: int, bcprec: int) -> bool:
-    """The chains mms_mlp_chain16 serves: the SDF MLP 71-256-256-257 (Softplus hidden layers, identity output) and the
-    radiance MLP 317-256-256-256 (ReLU)."""
-    if not (CHAIN16 and L == 3 and cprec in (1, 2) and bcprec in (1, 2)):
-        return False
-    sdf = 64 < K0 <= 96 and list(Ns) == [256, 256, 257] and list(acts) == [2, 2, 0]
-    rad = 288 < K0 <= 320 and list(Ns) == [256, 256, 256] and list(acts) == [1, 1, 1]
-    return sdf or rad
-
 
 class ChainRun:
     """A weight-normed 3- or 4-layer MLP on the fused chain kernel (mms_mlp_chain: all layers in one launch, bf16 or
@@ -602,7 +587,6 @@ class ChainRun:
         if self.L not in (3, 4):
             raise ValueError("chains of 3 or 4 layers")
         self.beta, self.thr = float(acts[0][1]), float(acts[0][2])
-        self.l16 = False      # set per forward: the shape runs on mms_mlp_chain16
 
     def _pack(self, W, rows: int, cols: int, transpose: bool, permute: int, prec: Optional[int] = None):
         prec = self.cprec if prec is None else prec
@@ -625,7 +609,6 @@ class ChainRun:
                xaux=None, xact: int = 0, xout=None, w2row0=None, tap_part=None):
         prec = self.bcprec if backward else self.cprec
         n = self.L
-        l16 = self.l16
         VP = ctypes.c_void_p * n
         his = VP(*[p[0].data_ptr() for p in packs])
         los = VP(*[(p[1].data_ptr() if p[1] is not None else None) for p in packs])
@@ -637,7 +620,7 @@ class ChainRun:
         ns = (ctypes.c_int * n)(*Ns)
         ac = (ctypes.c_int * n)(*acts)
         cast = lambda a: ctypes.cast(a, ctypes.c_void_p)
-        _lib.call("mms_mlp_chain16" if l16 else "mms_mlp_chain", prec, int(backward), n, X.data_ptr(), X.stride(0), K0,
+        _lib.call("mms_mlp_chain", prec, int(backward), n, X.data_ptr(), X.stride(0), K0,
                   X.shape[0], rows_full,
                   _p(xaux), 0 if xaux is None else xaux.stride(0), int(xact), _p(xout),
                   0 if xout is None else xout.stride(0), cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux),
@@ -660,16 +643,9 @@ class ChainRun:
             self.Ws.append(W)
             self.norms.append(nrm)
         Ns = [W.shape[0] for W in self.Ws]
-        self.l16 = _chain16_shape(L, K0, Ns, [a[0] for a in self.acts], self.cprec, self.bcprec)
-        up = lambda n, k: k * ((n + k - 1) // k)  # noqa: E731
-        if self.l16:
-            # the 16x16x32 layout (permute bit 1): 16-row tiles, 32-column k-steps
-            packs = [self._pack(self.Ws[0], up(Ns[0], 16), up(K0, 32), False, 2)] + \
-                    [self._pack(self.Ws[l], up(Ns[l], 16), up(Ns[l - 1], 32), False, 3) for l in range(1, L)]
-        else:
-            nt = [(n + 31) // 32 for n in Ns]
-            packs = [self._pack(self.Ws[0], 32 * nt[0], 16 * ((K0 + 15) // 16), False, False)] + \
-                    [self._pack(self.Ws[l], 32 * nt[l], 32 * nt[l - 1], False, True) for l in range(1, L)]
+        nt = [(n + 31) // 32 for n in Ns]
+        packs = [self._pack(self.Ws[0], 32 * nt[0], 16 * ((K0 + 15) // 16), False, False)] + \
+                [self._pack(self.Ws[l], 32 * nt[l], 32 * nt[l - 1], False, True) for l in range(1, L)]
         self.rows_full = M if rows_full is None else int(rows_full)
         if dense_col0 and self.rows_full != 0:
             raise ValueError("dense_col0 needs rows_full = 0")
@@ -694,10 +670,6 @@ class ChainRun:
         up = lambda n, k: k * ((n + k - 1) // k)  # noqa: E731
         p = self.bcprec
         p0, pr = (2, 5) if p == 6 else (p, p)     # prec 6: the first layer split-bf16x3, the rest fp16
-        if self.l16:
-            return [self._pack(self.Ws[L - 1], up(Ns[L - 2], 16), up(Ns[L - 1], 32), True, 2, p)] + \
-                   [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 16), up(Ns[l], 32), True, 3, p)
-                    for l in range(L - 2, -1, -1)]
         return [self._pack(self.Ws[L - 1], up(Ns[L - 2], 32), up(Ns[L - 1], 16), True, False, p0)] + \
                [self._pack(self.Ws[l], up(Ns[l - 1] if l > 0 else K0, 32), up(Ns[l], 32), True, True, pr)
                 for l in range(L - 2, -1, -1)]
@@ -733,7 +705,7 @@ class ChainRun:
         tap_part = None
         if tapw:
             n0 = Ns[L - 2]
-            B = 128 if self.l16 else _lib.lib().mms_mlp_chain_block_rows()
+            B = _lib.lib().mms_mlp_chain_block_rows()
             tap_part = torch.empty(-(-M // B) - rf // B, n0 + 4, device=dev)
         self._chain(True, dy, Ns[L - 1], rf, packs, [None] * L, [Y[l] for l in order] + [None],
                     [dZ[l] for l in order] + [dx], [Ns[l] for l in order] + [K0], [acts[l] for l in order] + [0],

@@ -817,7 +817,10 @@ class BaseModel(nn.Module):
                     bg_res.append(background())
         if at == -2:
             issue_bg()
-        if all(m in rng.bins for m in mods):
+        if rng.bins and not all(m in rng.bins for m in mods):
+            raise ValueError(f"injected NeuS bins cover {sorted(rng.bins)} but the batch has modalities {list(mods)}: "
+                             "give every modality's bins or none")
+        if rng.bins:
             # injected samples: each modality's bins, fixed-capacity segments padded with their first ray's bins (the
             # padding rows repeat the first hit ray)
             parts = []

@@ -420,9 +420,6 @@ class TrainConfig:
     own_heads_only: bool = True         # training renders each modality's rays through its own head only
 
 
-# single-process training steps: the main stream's MLP weight-gradient launches deferred to the end of the backward
-# (MMS_DEFER_WGRAD=1; A/B knob, default inline)
-DEFER_WGRAD = os.environ.get("MMS_DEFER_WGRAD", "0") == "1"
 _SEEDS: Dict[tuple, torch.Tensor] = {}
 
 
@@ -452,11 +449,6 @@ def backward_batched(total: torch.Tensor, between=None) -> None:
                 total.backward(_seed(total))
             finally:
                 between()
-            fx.wgrad_flush()
-        elif DEFER_WGRAD:
-            # the main stream's weight gradients after the rest of the backward (the background's stay inline)
-            fx.wgrad_defer_begin(this_stream_only=True)
-            total.backward(_seed(total))
             fx.wgrad_flush()
         else:
             total.backward(_seed(total))

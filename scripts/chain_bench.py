@@ -49,7 +49,7 @@ def kernel_us(fn, reps=10):
     torch.cuda.synchronize()
     sys.path.insert(0, ROOT)
     from bench import chain_work
-    _lib.TIMER.start({"mms_mlp_chain": chain_work, "mms_mlp_chain16": chain_work})
+    _lib.TIMER.start({"mms_mlp_chain": chain_work})
     for _ in range(reps):
         fn()
     torch.cuda.synchronize()

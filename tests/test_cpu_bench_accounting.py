@@ -25,10 +25,13 @@ def test_chain_work_sdf(prec, label):
     M, rf = 5 * 1000, 1000
     if prec == 6:   # a backward mode: the SDF backward 257 -> 256 -> 256 -> 71
         a, keep = _chain_args(prec, 1, [256, 256, 71], 257, M, rf, [True, True, True])
-        name, (flops, nbytes) = bench.chain_work(a)
+        name, (flops, nbytes, eq) = bench.chain_work(a)
         assert name == f"{label}:sdf_bwd"
         # first layer: 257 inputs on the centre rows, 1 on the taps; then 256x256 and 256x71 on every row
-        assert flops == 2.0 * (rf * 257 + (M - rf)) * 256 + 2.0 * M * (256 * 256 + 256 * 71)
+        f0 = 2.0 * (rf * 257 + (M - rf)) * 256
+        assert flops == f0 + 2.0 * M * (256 * 256 + 256 * 71)
+        # its mode ceiling: the first layer split-bf16x3 (three MFMAs per product), the rest one fp16 MFMA
+        assert eq == flops + 2.0 * f0
     else:
         a, keep = _chain_args(prec, 0, [256, 256, 257], 71, M, rf, [True, True, True])
         name, (flops, nbytes) = bench.chain_work(a)
@@ -40,4 +43,14 @@ def test_chain_work_sdf(prec, label):
 
 def test_every_chain_mode_has_a_peak():
     for p, name in bench.PREC_NAMES.items():
-        assert name in bench.MFMA_PEAK_TF, (p, name)
+        assert name in bench.MFMA_PEAK_TF or p == 6, (p, name)    # prec 6 is priced per launch (chain_work)
+
+
+def test_rowscaled_mode_peak_is_priced_per_layer():
+    """a prec-6 backward chain's mode ceiling weights its split-bf16x3 first layer at a third of the peak."""
+    a, keep = _chain_args(6, 1, [256, 256, 256], 256, 4096, 4096, [True, True, True])
+    name, work = bench.chain_work(a)
+    recs = bench.kernel_records({"mms_mlp_chain:" + name: (1, 0.1, work)}, 1, "fast_h16b")
+    r = recs[0]
+    assert abs(r["mode_peak"] - bench.BF16_MFMA_PEAK_TF * 3 / 5) < 0.1      # 3 equal layers: 1/(3/3 + 1/3 + 1/3)
+    assert r["frac_of_mode_peak"] > r["frac"]

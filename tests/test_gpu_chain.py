@@ -19,16 +19,6 @@ CASES = {"geo": [(2, 100.0, 20.0), (2, 100.0, 20.0), (0, 1.0, 20.0)],
 PKEYS = ["parametrizations.weight.original0", "parametrizations.weight.original1", "bias"]
 
 
-@pytest.fixture(params=[True, False], ids=["chain16", "chain32"])
-def chain16(request):
-    """Both SDF chain kernels: mms_mlp_chain16 (16x16x32, two waves per SIMD, the default) and mms_mlp_chain."""
-    from multimodalstudio_amd import functions as fx
-    old = fx.CHAIN16
-    fx.CHAIN16 = request.param
-    yield request.param
-    fx.CHAIN16 = old
-
-
 def rel(actual, ref):
     a = np.asarray(actual, dtype=np.float64)
     r = np.asarray(ref, dtype=np.float64)
@@ -72,7 +62,7 @@ def _masked_ref(x, params, acts, Y, dy):
 
 @pytest.mark.parametrize("prec", [2, 1])
 @pytest.mark.parametrize("name", list(CASES))
-def test_chain_vs_golden(dev, name, prec, chain16):
+def test_chain_vs_golden(dev, name, prec):
     """Forward vs the reference's golden output; backward vs the golden gradients (split bf16x3) or, for plain bf16,
     vs an fp64 backward taken at the kernel's own activations (see _masked_ref)."""
     from multimodalstudio_amd import functions as fx
@@ -81,7 +71,6 @@ def test_chain_vs_golden(dev, name, prec, chain16):
     X = _panel(f["x"], dev)
     run = fx.ChainRun(params, CASES[name], prec)
     y = run.forward(X, keep=True)
-    assert run.l16 == chain16
     Y = [t.detach().clone() for t in run.Y]
     dy = _panel(f["dy"], dev)
     dx = run.backward(dy)
@@ -167,7 +156,7 @@ def _ref_mlp(x, params, acts, leaves=None):
 
 
 @pytest.mark.parametrize("M,rows_full", [(1000, 200), (777, 777), (640, 0), (20000, 4000), (20013, 3990)])
-def test_chain_sdf_tap_rows(dev, M, rows_full, chain16):
+def test_chain_sdf_tap_rows(dev, M, rows_full):
     """SDF chain with tap rows (>= rows_full): column 0 for every row, all 257 columns for the rows below; the
     backward reads only column 0 of the tap rows (the rest of those rows is garbage on purpose).  Parameter gradients
     too: the taps' share of the last layer's row 0 is summed inside the backward chain (dw_row0 / db_row0)."""
@@ -180,7 +169,6 @@ def test_chain_sdf_tap_rows(dev, M, rows_full, chain16):
     run = fx.ChainRun(params, CASES["geo"], 2)
     keep = rows_full > 0
     y = run.forward(X, keep=keep, rows_full=rows_full)
-    assert run.l16 == chain16
     xr = x.double().requires_grad_(True)
     leaves = [p.detach().double().cpu().requires_grad_(True) for p in params]
     ref = _ref_mlp(xr, params, CASES["geo"], leaves)
@@ -206,7 +194,7 @@ def test_chain_sdf_tap_rows(dev, M, rows_full, chain16):
         assert rel(p.grad.cpu(), q.grad) < TOL[2], (i, rel(p.grad.cpu(), q.grad))
 
 
-def test_sdf_only_fast_matches_fp32(dev, chain16):
+def test_sdf_only_fast_matches_fp32(dev):
     """The sampler's inference SDF (functions.sdf_only) on the chain kernel (fast preset) vs the fp32 GEMM path:
     same values, returned as a dense [M] vector (mms_neus_step reads it densely)."""
     from multimodalstudio_amd import functions as fx
@@ -429,7 +417,7 @@ def test_chain_fp16_backward(dev, dims, acts, M, rows_full):
     fx.PRECISION["bwd16"] = 1
     try:
         run = fx.ChainRun(params, acts, prec)
-        assert run.bcprec == 6 and not run.l16
+        assert run.bcprec == 6
         x = torch.randn(M, dims[0], generator=g) * 0.5
         run.forward(_panel(x, dev), keep=True, rows_full=rows_full)
         Y = [t.detach().clone() for t in run.Y]
