@@ -10,9 +10,11 @@ from __future__ import annotations
 
 FULL_SEED = 1234
 FULL_TABLE_SCALE = 50.0
+# the smooth full-size fixture (e2e_full_grid_rgb_l19_smooth): formula tables at 1/500 of the rough fixtures' amplitude
+FULL_SMOOTH_SCALE = 0.1
 
 
-def fullsize_state(mods, log2T: int, seed: int = FULL_SEED, table_scale: float = FULL_TABLE_SCALE):
+def fullsize_state(mods, log2T: int, seed: int = FULL_SEED, table_scale: float = FULL_TABLE_SCALE, bg_kind="nerf"):
     import torch
 
     from multimodalstudio_amd import scene as ms
@@ -21,7 +23,7 @@ def fullsize_state(mods, log2T: int, seed: int = FULL_SEED, table_scale: float =
     rng = torch.random.get_rng_state()
     try:
         torch.manual_seed(seed)
-        m = BaseModel(ModelSpec({k: ms.CHANNELS[k] for k in mods}, log2T=log2T))
+        m = BaseModel(ModelSpec({k: ms.CHANNELS[k] for k in mods}, log2T=log2T, bg_kind=bg_kind))
     finally:
         torch.random.set_rng_state(rng)
     sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
@@ -49,7 +51,8 @@ def with_fullsize_params(f: dict) -> dict:
     if "param_checksum" not in f:
         return f
     mods = [str(m) for m in f["mods"]]
-    sd = fullsize_state(mods, int(f["log2T"]))
+    sd = fullsize_state(mods, int(f["log2T"]), table_scale=float(f.get("state:table_scale", FULL_TABLE_SCALE)),
+                        bg_kind=str(f.get("state:bg_kind", "nerf")))
     ck = param_checksum(sd)
     want = float(f["param_checksum"])
     if abs(ck - want) > 1e-9 * abs(want):

@@ -29,11 +29,14 @@ from test_oracle_golden import e2e_inputs  # noqa: E402
 
 
 def run(f, dtype):
-    from multimodalstudio_amd.scene import CHANNELS
+    from multimodalstudio_amd.scene import CHANNELS, mosaick_mask
     mods = [str(m) for m in f["mods"]]
+    raw = bool(f["raw"])
     T = lambda a: torch.from_numpy(np.asarray(a)).to(dtype if np.asarray(a).dtype.kind == "f" else None)  # noqa
     key = "p:surface_model.surface_field.field.feature_grid.encoding.hash_table"
-    spec = om.spec_grid({m: CHANNELS[m] for m in mods}, log2T=int(np.log2(f[key].shape[0] // 16)))
+    bg = "grid" if "p:background_model.background_field.base_field.feature_grid.encoding.hash_table" in f else "nerf"
+    spec = om.spec_grid({m: CHANNELS[m] for m in mods}, log2T=int(np.log2(f[key].shape[0] // 16)), raw=raw,
+                        bg_kind=bg)
     st = om.StepState(step=int(f["step"]))
     P = {k[2:]: T(v).clone().requires_grad_(True) for k, v in f.items() if k.startswith("p:")}
     torch.set_default_dtype(dtype)      # the oracle's own allocations and constants follow
@@ -43,9 +46,13 @@ def run(f, dtype):
             for m in mods}
     bins = {m: T(f[f"{m}:bins"]) for m in mods}
     orig = orr.neus_sample
+    calls = []
 
     def injected(nears, fars, o, d, sdf_fn, *a, **k):
-        m = mods[0]
+        # the oracle samples the modalities in order (oracle/model.py): the reference's bins of each, injected
+        m = mods[len(calls)]
+        calls.append(m)
+        assert nears.shape[0] == bins[m].shape[0], (m, nears.shape, bins[m].shape)
         return orr.make_samples(bins[m], nears, fars, "uniform"), []
     orr.neus_sample = injected
     om.orr.neus_sample = injected
@@ -56,6 +63,11 @@ def run(f, dtype):
                      pdf={m: draws[nm + 4 * i: nm + 4 * i + 4] for i, m in enumerate(mods)},
                      background={m: draws[5 * nm + i] for i, m in enumerate(mods)})
         outs = om.model_forward(rays, P, spec, st, rng)
+        assert calls == mods, calls
+        if raw:
+            for m in mods:
+                outs[m][m] = om.select_channel(outs[m][m], mosaick_mask(m, int(f["W"]), int(f["H"])),
+                                               T(f[f"{m}:coords"]))
         losses, total = om.compute_loss(outs, {m: T(f[f"{m}:pixels"]) for m in mods}, spec, st)
         total.backward()
     finally:

@@ -30,7 +30,22 @@ from multimodalstudio_amd import scene as mscene  # noqa: E402
 
 OUT = HERE
 sys.path.insert(0, os.path.dirname(HERE))
-from fullsize_state import fullsize_state, param_checksum  # noqa: E402  (tests/fullsize_state.py)
+from fullsize_state import FULL_SMOOTH_SCALE, fullsize_state, param_checksum  # noqa: E402  (tests/fullsize_state.py)
+
+RAW5 = ["rgb", "infrared", "mono", "polarization", "multispectral"]
+
+
+def config5_train_views(n_views=50):
+    """The training views of grid_raw_rgb_all_views_pol_10_views.yaml (:39-48): every view except the eval views, and
+    for polarization also except skip_image_indices_per_modality -- 45 rgb views, 10 polarization views."""
+    import yaml
+    with open("/root/reference/confs/grid_raw_rgb_all_views_pol_10_views.yaml") as fh:
+        dm = yaml.safe_load(fh)["pipeline"]["datamanager"]
+    out = {}
+    for m in dm["modalities"]:
+        drop = set(dm["eval_image_indices_per_modality"][m]) | set(dm["skip_image_indices_per_modality"].get(m, []))
+        out[m] = [v for v in range(n_views) if v not in drop]
+    return out
 
 
 def save(name, **arrays):
@@ -237,11 +252,22 @@ def set_callbacks(model, step, max_iters=100000):
 
 
 def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=False, grid_bg=False, grids=True,
-                   saturate=0.0, W=96, H=80, n_views=12, cam_seed=4, state=None, compact=False):
+                   saturate=0.0, W=96, H=80, n_views=12, cam_seed=4, state=None, compact=False, amp_scale=None,
+                   write=True, keep_table_grads=None, train_views=None, state_meta=None, inject_bins=None):
     """One reference fwd + loss + bwd.  ``saturate``: that fraction of the polarization frame values is set to 1.0,
     so targets above SkipSaturationLoss's 0.998 threshold (losses.py:152-164) are drawn.  ``state``: load these
     parameters (fullsize_state) instead of the seeded reference init; ``compact``: store no parameters and, of the
-    hash-table gradients, per-level norms plus a fixed sample of their nonzero entries (the full-size fixture)."""
+    hash-table gradients, per-level norms plus a fixed sample of their nonzero entries (the full-size fixture).
+    ``amp_scale``: the reference's own "16-mixed" mode (autocast16.py: the model forward under CUDA's fp16 autocast
+    policy, the loss scaled by this power of two before the backward and the gradients unscaled after it, as Fabric's
+    GradScaler; arrays["amp_finite"] = its inf / nan check).  ``write``: save the fixture, else only return it.
+    ``keep_table_grads``: a dict that receives the full hash-table gradients of a compact run.  ``train_views``: per
+    modality, the view ids whose frames the pixel sampler draws from (the datamanager's training split after
+    skip_image_indices_per_modality, datasets.py); default every view.  ``state_meta``: extra scalars stored with a
+    compact fixture so tests/fullsize_state.py regenerates the same parameters (background kind, table scale).
+    ``inject_bins``: per modality, final NeuS spacing bins that replace the up-sampler's (it still runs, so every
+    random draw is made as before), built into RaySamples exactly as merge_ray_samples builds them
+    (ray_samplers.py:58-66) -- the rest of the step then runs on those samples."""
     from cameras.camera_optimizers import CameraOptimizerConfig
     from cameras.pixel_samplers import UniformPixelSamplerConfig
     from model_components.ray_generators import RayGenerator
@@ -282,7 +308,12 @@ def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=F
         imgs = torch.rand(C, H, W, 1 if raw else modalities[m], generator=torch.Generator().manual_seed(9))
         if saturate > 0 and m == "polarization":
             imgs[imgs > 1.0 - saturate] = 1.0
-        frames[m] = {"images": imgs, "indexes": torch.arange(C, dtype=torch.int32)}
+        idx = torch.arange(C, dtype=torch.int32)
+        if train_views is not None and m in train_views:
+            # view ids -> positions in the camera list (make_cameras keeps the train split: eval views absent)
+            idx = torch.tensor([cams[m].view_ids.index(v) for v in sorted(train_views[m])], dtype=torch.int32)
+            imgs = imgs[idx.long()]
+        frames[m] = {"images": imgs, "indexes": idx}
     sampler = UniformPixelSamplerConfig(num_rays_per_modality=n_rays).setup(device=None)
     sampler.generator = torch.Generator()
     sampler.generator.manual_seed(654824)
@@ -319,6 +350,14 @@ def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=F
             return v
         k = dict(k, sdf_fn=sdf_fn)
         out = orig_gen(self, *a, **k)
+        if inject_bins is not None:
+            rsm_out = out["ray_samples_per_modality"]
+            for m, rs in list(rsm_out.items()):
+                b = inject_bins[m].to(rs.spacing_starts.dtype)
+                eb = rs.spacing_to_euclidean_fn(b, bundles[m])
+                rsm_out[m] = bundles[m].get_ray_samples(bin_starts=eb[..., :-1, None], bin_ends=eb[..., 1:, None],
+                                                        spacing_starts=b[..., :-1, None], spacing_ends=b[..., 1:, None],
+                                                        spacing_to_euclidean_fn=rs.spacing_to_euclidean_fn)
         seen["bins"] = {m: torch.cat([rs.spacing_starts[..., 0], rs.spacing_ends[..., -1:, 0]], -1).detach().clone()
                         for m, rs in out["ray_samples_per_modality"].items()}
         return out
@@ -328,7 +367,12 @@ def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=F
     rsm.merge_ray_samples = merge
     try:
         with record_rand() as draws:
-            outputs = model(rb)
+            if amp_scale is not None:
+                import autocast16
+                with autocast16.CudaAutocastFp16():
+                    outputs = model(rb)
+            else:
+                outputs = model(rb)
     finally:
         scm.ColliderInstancer.update_ray_bundles = orig_update
         rsm.NeuSSampler.generate_ray_samples = orig_gen
@@ -341,14 +385,27 @@ def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=F
             band = mm[coords[m][:, 1].long(), coords[m][:, 2].long()].unsqueeze(1).long()
             outputs[m][m] = torch.gather(outputs[m][m], 1, band)
     losses, total = lm.compute_loss(outputs, pixels, coords, step)
-    total.backward()
-    arrays = {"step": step, "level": level, "delta": delta, "W": W, "H": H, "raw": raw,
-              "mods": np.array(mods), "loss": total.detach()}
+    arrays = {}
+    if amp_scale is not None:
+        (total * amp_scale).backward()
+        params = list(model.parameters()) + list(opt.parameters())
+        arrays["amp_finite"] = all(p.grad is None or bool(torch.isfinite(p.grad).all()) for p in params)
+        with torch.no_grad():
+            for p in params:
+                if p.grad is not None:
+                    p.grad.mul_(1.0 / amp_scale)
+        arrays["amp_scale"] = float(amp_scale)
+    else:
+        total.backward()
+    arrays.update({"step": step, "level": level, "delta": delta, "W": W, "H": H, "raw": raw,
+                   "mods": np.array(mods), "loss": total.detach()})
     for k, v in losses.items():
         arrays["loss:" + k] = torch.as_tensor(v).detach()
     if compact:
         arrays["param_checksum"] = param_checksum(model.state_dict())
         arrays["log2T"] = log2T
+        for k, v in (state_meta or {}).items():
+            arrays["state:" + k] = v
     else:
         for k, v in model.state_dict().items():
             arrays["p:" + k] = v
@@ -357,6 +414,8 @@ def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=F
         if p.grad is None:
             continue
         if compact and k.endswith("hash_table"):
+            if keep_table_grads is not None:
+                keep_table_grads[k] = p.grad.detach().clone()
             g = p.grad.detach().reshape(16, -1).double()
             arrays["gtab_level_norm:" + k] = g.norm(dim=1)
             flat = p.grad.detach().reshape(-1)
@@ -394,7 +453,9 @@ def gen_end_to_end(method, yaml_name, mods, step, tag, n_rays=8, log2T=12, raw=F
         for mm in mods:
             if mm in o:
                 arrays[f"{m}:out:{mm}"] = o[mm].detach()
-    save(f"e2e_{tag}", **arrays)
+    if write:
+        save(f"e2e_{tag}", **arrays)
+    return arrays
 
 
 def gen_eval(method="grid", yaml_name="grid.yaml", mods=("rgb",), step=95000, tag="eval_grid_rgb", raw=False):
@@ -702,6 +763,27 @@ if __name__ == "__main__":
         b = {k: v for k, v in b.items() if not k.startswith("p:")}
         b["params_from"] = np.array("e2e_grid_raw_gridbg_s95000")
         np.savez_compressed(os.path.join(OUT, "e2e_grid_raw_gridbg_s30000.npz"), **b)
+    if "e2e_full_raw5" in which:
+        # BASELINE configs[2] at its own size: grid_raw.yaml, five mosaicked modalities x 2048 rays
+        # (/root/reference/confs/grid_raw.yaml:39-67), log2T 19, step 95000, the 50-view 640 x 512 rig
+        gen_end_to_end("grid_raw", "grid_raw.yaml", RAW5, 95000, "full_grid_raw5_l19", n_rays=2048, log2T=19, W=640,
+                       H=512, n_views=50, cam_seed=0, raw=True, state=fullsize_state(RAW5, 19), compact=True)
+    if "e2e_full_bg" in which:
+        # BASELINE configs[4] per GPU at its own size: grid_raw_rgb_all_views_pol_10_views.yaml -- rgb + polarization x
+        # 2048 rays, polarization drawn from its 10 training views (skip_image_indices_per_modality and the eval
+        # views removed, :39-48), hash-grid background, SO3xR3 poses; log2T 19, step 95000
+        bg_mods = ["rgb", "polarization"]
+        gen_end_to_end("grid_raw_grid_bg_unbalanced", "grid_raw_rgb_all_views_pol_10_views.yaml", bg_mods, 95000,
+                       "full_gridbg_l19", n_rays=2048, log2T=19, W=640, H=512, n_views=50, cam_seed=0, raw=True,
+                       grid_bg=True, state=fullsize_state(bg_mods, 19, bg_kind="grid"), compact=True,
+                       train_views=config5_train_views(), state_meta={"bg_kind": "grid"})
+    if "e2e_full_smooth" in which:
+        # the benchmarked configuration with SMOOTH tables (formula tables x FULL_SMOOTH_SCALE instead of x 50): the
+        # SDF is smooth on the scale of a sample step, so the free-running HIP sampler must reproduce the reference's
+        # bins (tests/test_gpu_fullsize.py::test_fullsize_smooth_free_running)
+        gen_end_to_end("grid", "grid.yaml", ["rgb"], 95000, "full_grid_rgb_l19_smooth", n_rays=2048, log2T=19, W=640,
+                       H=512, n_views=50, cam_seed=0, state=fullsize_state(["rgb"], 19, table_scale=FULL_SMOOTH_SCALE),
+                       compact=True, state_meta={"table_scale": FULL_SMOOTH_SCALE})
     if "e2e_full" in which:
         # BASELINE configs[1] at its own size: grid.yaml, rgb, 2048 rays, log2T 19 (confs/grid.yaml:58-59), step 95000,
         # the benchmark's 50-view 640 x 512 camera rig; parameters regenerated on the box (fullsize_state)

@@ -462,3 +462,103 @@ def test_chain_fp16_backward(dev, dims, acts, M, rows_full):
     for k, v in errs.items():
         assert v < 3e-3, (k, v)
     assert row_err < 1e-2
+
+
+def _autocast_sdf_backward(x, params, acts, Y, dyr):
+    """The reference GPU's fp16-autocast backward of the SDF MLP (trainer.py:51: nn.Linear in fp16 -- operands rounded
+    to fp16, fp32 accumulation, fp16 results --, Softplus upcast to fp32 and its input gradient cast back to fp16, the
+    loss scaled by the largest power of two that keeps every fp16 gradient finite, GradScaler-style, and unscaled at
+    the end) restated in float64 with fp16 rounding at those points, at the kernel's own forward activations Y.
+    Returns dx and the (g, v, b) gradients of each layer, like _masked_ref."""
+    h16 = lambda t: t.half().double()    # noqa: E731
+    L = len(params) // 3
+    Ws = []
+    for l in range(L):
+        g64 = params[3 * l].detach().double().cpu()
+        v64 = params[3 * l + 1].detach().double().cpu()
+        Ws.append(torch._weight_norm(v64, g64, 0))
+    ins = [x.double()] + [Y[l].double().cpu() for l in range(L - 1)]
+    # largest |gradient| anywhere in the chain (fp64), to pick the scale
+    d, peak = dyr.clone(), dyr.abs().max().item()
+    for l in range(L - 1, -1, -1):
+        if l < L - 1:
+            d = d * (1 - torch.exp(-acts[l][1] * ins[l + 1]))
+        peak = max(peak, d.abs().max().item(), (d.T @ ins[l]).abs().max().item())
+        d = d @ Ws[l]
+        peak = max(peak, d.abs().max().item())
+    S = 2.0 ** np.floor(np.log2(32768.0 / peak))
+    d = h16(dyr * S)
+    out = [None] * (3 * L)
+    for l in range(L - 1, -1, -1):
+        if l < L - 1:      # Softplus in fp32 on the fp16 pre-activation, its input gradient cast back to fp16
+            d = h16(d * (1 - torch.exp(-acts[l][1] * ins[l + 1])))
+        dW = h16(d.T @ h16(ins[l])) / S
+        g64 = params[3 * l].detach().double().cpu().requires_grad_(True)
+        v64 = params[3 * l + 1].detach().double().cpu().requires_grad_(True)
+        torch._weight_norm(v64, g64, 0).backward(dW)
+        out[3 * l], out[3 * l + 1], out[3 * l + 2] = g64.grad, v64.grad, h16(d.sum(0)) / S
+        d = h16(d @ h16(Ws[l]))
+    return d / S, out
+
+
+@pytest.mark.parametrize("delta", [1e-3, 2.5e-4])
+def test_sdf_backward_fp16_on_antisymmetric_taps(dev, delta):
+    """preset fast_h16b runs the SDF backward-data chain on prec 6 (fp16 register-fed layers with a per-row
+    scale).  The SDF's real dY is not random per row: the eikonal loss puts k_t . g / (4 delta) on the 4 tap rows of a
+    sample and the curvature loss c / (2 delta^2) on each tap and -2 c / delta^2 on the centre
+    (/root/reference/src/model_components/surface_model.py:137-151), and the tap rows' inputs differ from the centre's
+    by O(delta) -- so the weight gradients are sums of large, nearly cancelling per-row terms.  On that pattern the
+    prec-6 dX and parameter gradients (vs fp64 at the kernel's own activations) must stay within 2x the error of the
+    reference GPU's own fp16-autocast backward of the same chain (_autocast_sdf_backward) -- prec 6 rounds each row to
+    fp16 like the autocast does, but with a per-row instead of a global scale.  The split-bf16x3 backward is reported
+    beside it."""
+    from multimodalstudio_amd import functions as fx
+    g = torch.Generator().manual_seed(int(1 / delta))
+    f = dict(np.load(os.path.join(GOLD, "mlp_geo.npz")))
+    params = _params(f, dev)
+    acts = CASES["geo"]
+    C = 2000
+    xc = torch.randn(C, 71, generator=g) * 0.5
+    A = torch.randn(71, 3, generator=g)                      # d panel / d position
+    k = torch.tensor([[1., -1., -1.], [-1., -1., 1.], [-1., 1., -1.], [1., 1., 1.]])
+    x = torch.cat([xc] + [xc + delta * (A @ k[t]) for t in range(4)])
+    M = 5 * C
+    gv = torch.randn(C, 3, generator=g)                      # d loss / d gradient (eikonal)
+    cv = torch.randn(C, 1, generator=g) * 1e-3               # d loss / d hessian (curvature)
+    dy = torch.randn(M, 257, generator=g)
+    dy[:C, :1] += -2.0 * cv / delta ** 2
+    for t in range(4):
+        dy[C * (t + 1): C * (t + 2), :1] = (gv @ k[t])[:, None] / (4 * delta) + cv / (2 * delta ** 2)
+    dyr = dy.double().clone()
+    dyr[C:, 1:] = 0.0
+    dy[C:, 1:] = float("nan")                # never read
+    errs = {}
+    for name, bwd16 in (("x3", 0), ("prec6", 1)):
+        old = dict(fx.PRECISION)
+        fx.PRECISION["bwd16"] = bwd16
+        try:
+            for p in params:
+                p.grad = None
+            run = fx.ChainRun(params, acts, 2)
+            assert run.bcprec == (6 if bwd16 else 2)
+            run.forward(_panel(x, dev), keep=True, rows_full=C)
+            Y = [t.detach().clone() for t in run.Y]
+            dx = run.backward(_panel(dy, dev))
+            torch.cuda.synchronize()
+        finally:
+            fx.PRECISION.clear()
+            fx.PRECISION.update(old)
+        grads = [p.grad.detach().cpu().double().clone() for p in params]
+        ref_dx, ref_g = _masked_ref(x, params, acts, Y, dyr)
+        e = {"dx": rel(dx.cpu(), ref_dx)}
+        e.update({f"p{i}": rel(grads[i], ref_g[i]) for i in range(len(params))})
+        errs[name] = e
+    am_dx, am_g = _autocast_sdf_backward(x, params, acts, Y, dyr)
+    e = {"dx": rel(am_dx, ref_dx)}
+    e.update({f"p{i}": rel(am_g[i], ref_g[i]) for i in range(len(params))})
+    errs["autocast"] = e
+    for q in errs["x3"]:
+        print(f"  delta {delta:.1e} {q:4s} x3 {errs['x3'][q]:.2e}  prec6 {errs['prec6'][q]:.2e}  "
+              f"ref-fp16-autocast {errs['autocast'][q]:.2e}")
+    for q, v in errs["prec6"].items():
+        assert np.isfinite(v) and v <= 2.0 * errs["autocast"][q] + 1e-6, (q, v, errs["autocast"][q])

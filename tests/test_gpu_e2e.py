@@ -231,15 +231,117 @@ def test_e2e_train_step(dev, name):
     assert_e2e_bounds(name, report, mods)
 
 
+def envelope_report(f, mods, model, pose, outs, total, cap=None, sizes=None):
+    """The quantities tests/golden/make_autocast_envelope.py records, same keys and metrics: loss|rel; per modality the
+    rendered radiance (mean_rel / max_rel relative to max(|ref|, 1e-2) per element, max scale-relative), normals /
+    accumulation / depth / SDF gradients / hessians and dpose (scale-relative max), bins|abs; per parameter gradient
+    its relative L2 (|l2) and scale-relative max (|max).  ``cap``: fixed-capacity outputs (first count rows);
+    ``sizes`` (a dict) receives each parameter-gradient key's element count."""
+    rep = {"loss|rel": abs(total.item() - float(f["loss"])) / abs(float(f["loss"]))}
+    for m in mods:
+        o = outs[m]
+        n = int(o["count"].item()) if cap is not None else None
+        got = o[m].detach().cpu().numpy().astype(np.float64)
+        ref = f[f"{m}:out:{m}"].astype(np.float64)
+        rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-2)
+        rep[f"{m}:{m}|mean_rel"], rep[f"{m}:{m}|max_rel"] = float(rel.mean()), float(rel.max())
+        rep[f"{m}:{m}|max"] = rel_err(got, ref)
+        for k in ["normals", "accumulation", "depth", "gradients", "hessians"]:
+            if f"{m}:out:{k}" in f and o.get(k) is not None:
+                v = o[k].detach()
+                if cap is not None and k in ("gradients", "hessians"):
+                    v = v[:n]
+                rep[f"{m}:{k}|max"] = rel_err(v.cpu(), f[f"{m}:out:{k}"])
+        rep[f"{m}:dpose|max"] = rel_err(pose.pose_adjustment[m].grad.cpu(), f[f"{m}:dpose"])
+        bins = o["bins"].cpu().numpy()
+        rep[f"{m}:bins|abs"] = float(np.abs((bins[:n] if cap is not None else bins) - f[f"{m}:bins"]).max())
+    for k, p in model.named_parameters():
+        if sizes is not None:
+            sizes[f"g:{k}|l2"] = p.numel()
+        if "g:" + k in f:
+            rep[f"g:{k}|l2"], rep[f"g:{k}|max"] = rel_l2(p.grad.cpu(), f["g:" + k]), rel_err(p.grad.cpu(), f["g:" + k])
+        elif "gtab_val:" + k in f:
+            g = p.grad.detach().double()
+            val = g.reshape(-1)[torch.from_numpy(f["gtab_idx:" + k].astype(np.int64)).to(g.device)].cpu().numpy()
+            norms = g.reshape(16, -1).norm(dim=1).cpu().numpy()
+            ref_n = f["gtab_level_norm:" + k]
+            rep[f"g:{k}|l2"] = max(rel_l2(val, f["gtab_val:" + k]), float(np.abs(norms - ref_n).max() / ref_n.max()))
+            rep[f"g:{k}|max"] = rel_err(val, f["gtab_val:" + k])
+    return rep
+
+
+_ENVELOPE = {}
+
+
+def autocast_envelope(name):
+    """{quantity: the reference's own fp16-autocast deviation} of fixture ``name`` (tests/golden/autocast_envelope.npz,
+    written by make_autocast_envelope.py from the reference run in "16-mixed", the mode every BASELINE YAML trains
+    in: /root/reference/confs/grid.yaml:17, /root/reference/src/engine/trainer.py:51,57-62)."""
+    if not _ENVELOPE:
+        _ENVELOPE.update(np.load(os.path.join(GOLD, "autocast_envelope.npz")))
+    pre = name + "/"
+    return {k[len(pre):]: float(v) for k, v in _ENVELOPE.items() if k.startswith(pre)}
+
+
+# the quantities held to the envelope: the loss, the rendered radiance, the SDF gradients / hessians, every parameter
+# gradient's relative L2 and every pose gradient (the other recorded ones -- bins, normals, accumulation, depth,
+# per-element maxima -- are printed beside their envelope)
+ENVELOPE_GATED = ("loss|rel", "|mean_rel", ":gradients|max", ":hessians|max", "|l2", ":dpose|max")
+ENVELOPE_FACTOR = 2.0
+# Parameter gradients of fewer elements than this (the narrow layers' weight-norm magnitudes and biases: 1-3 values,
+# the variance) are gated as ONE pool, by the RMS of their relative-L2 distances: a scalar's distance is a single draw
+# of the rounding noise, and for two equally accurate implementations P(|X| > 2 |Y|) = 30 % (X, Y iid normal), so a
+# per-scalar 2x gate would fail a third of its checks by chance.  Pooled over the fixture's ~20 small tensors the RMS
+# ratio is resolved; every tensor of >= SMALL_TENSOR elements keeps its own 2x gate.
+SMALL_TENSOR = 64
+
+
+def check_envelope(name, rep, preset, sizes):
+    """Every gated quantity of ``rep`` within ENVELOPE_FACTOR x the reference's own fp16-autocast deviation (plus 1e-6
+    absolute for quantities the reference's fp16 mode reproduces exactly, e.g. an all-zero table gradient); the
+    parameter gradients of < SMALL_TENSOR elements as one RMS pool."""
+    env = autocast_envelope(name)
+    assert env, f"no autocast envelope for {name}"
+    bad, rows, pool = [], [], []
+    for k, v in rep.items():
+        if k not in env:
+            continue
+        ratio = v / env[k] if env[k] > 0 else (0.0 if v <= 1e-6 else float("inf"))
+        small = k.startswith("g:") and k.endswith("|l2") and sizes.get(k, SMALL_TENSOR) < SMALL_TENSOR
+        gated = k.endswith(ENVELOPE_GATED) and not small
+        rows.append((ratio, k, v, env[k], "*" if gated else ("p" if small else " ")))
+        if small:
+            pool.append((v, env[k]))
+        if gated and v > ENVELOPE_FACTOR * env[k] + 1e-6:
+            bad.append((k, v, env[k]))
+    rows.sort(reverse=True)
+    print(f"{name} {preset}: {len(rows)} quantities vs the reference's fp16 autocast (loss scale "
+          f"2^{int(np.log2(env['amp_scale']))}), largest ratios (* gated at {ENVELOPE_FACTOR}x, p pooled):")
+    for ratio, k, v, e, tag in rows[:16]:
+        print(f"   {tag} {k:100s} ours {v:.3e}  ref-fp16 {e:.3e}  ratio {ratio:.2f}")
+    gr = [r for r in rows if r[4] == "*"]
+    print(f"   worst gated ratio {gr[0][0]:.2f} ({gr[0][1]})")
+    if pool:
+        ours = float(np.sqrt(np.mean([a * a for a, _ in pool])))
+        ref = float(np.sqrt(np.mean([b * b for _, b in pool])))
+        print(f"   small-tensor pool ({len(pool)} tensors): RMS relative L2 ours {ours:.3e}  ref-fp16 {ref:.3e}  "
+              f"ratio {ours / ref if ref > 0 else 0.0:.2f}")
+        if ours > ENVELOPE_FACTOR * ref + 1e-6:
+            bad.append(("small-tensor pool", ours, ref))
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("preset", FAST_PRESETS)
-@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_5mod_s95000", "e2e_grid_raw_5mod_sat_s95000",
-                                  "e2e_grid_raw_gridbg_s95000"])
+@pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_rgb_s30000", "e2e_grid_raw_5mod_s95000",
+                                  "e2e_grid_raw_5mod_sat_s95000", "e2e_grid_raw_gridbg_s95000"])
 def test_e2e_fast_preset_deviation(dev, name, preset):
-    """The benchmarked `fast` preset (every MLP on split-bf16x3 MFMA operands, the narrow background layers fp32 VALU)
-    on the reference's fixture:
-    per-modality rendered-radiance deviation, reported and bounded (bf16 is judged by PSNR parity,
-    tests/test_gpu_train_parity.py, plus this measured deviation; the reference's own fp16 autocast is ~1e-3 mean rel
-    and bf16 5e-3 .. 2.5e-2).  Relative to max(|ref|, 1e-2) per element (polarization channels sit near 0)."""
+    """The throughput presets (the benchmarked fast_h16b: fp16 radiance / head / background forwards and row-scaled
+    fp16 backward-data chains; fast: split-bf16x3 throughout) on the reference's fixture, held to the REFERENCE'S OWN
+    numerics mode: every BASELINE YAML trains in fp16 autocast ("16-mixed"), so each compared quantity -- loss,
+    rendered radiance, SDF gradients and hessians, every parameter gradient (relative L2) and every pose gradient --
+    must stay within 2x the distance between the reference in fp16 autocast and the reference in fp32 (the fixture),
+    measured per quantity on the same inputs (tests/golden/autocast_envelope.npz, make_autocast_envelope.py).  The
+    radiance also keeps its absolute bounds (relative to max(|ref|, 1e-2) per element)."""
     from multimodalstudio_amd import functions as fx
     f = load(name)
     fx.set_precision(preset)
@@ -247,53 +349,22 @@ def test_e2e_fast_preset_deviation(dev, name, preset):
         mods, model, pose, outs, losses, total = run_hip_e2e(f, dev)
     finally:
         fx.set_precision("fp32")
-    loss_rel = abs(total.item() - float(f["loss"])) / abs(float(f["loss"]))
-    print(f"{name} {preset}: loss rel {loss_rel:.3e}")
+    sizes = {}
+    rep = envelope_report(f, mods, model, pose, outs, total, sizes=sizes)
     for m in mods:
-        got = outs[m][m].detach().cpu().numpy().astype(np.float64)
-        ref = f[f"{m}:out:{m}"].astype(np.float64)
-        rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-2)
-        print(f"  {m:14s} radiance rel dev: mean {rel.mean():.3e}  max {rel.max():.3e}")
-        # about 10x the measured deviation (round 3, every MLP split-bf16x3: mean <= 2.4e-5, polarization 3.8e-4 --
-        # its intensities are differences of Stokes terms --, max 2.4e-3; round 5, fast_h16: mean <= 9.0e-5,
-        # polarization 1.1e-3, max 3.4e-3 -- test_e2e_fp16_forward_preset_deviation holds those to 10x)
-        assert rel.mean() < (4e-3 if m == "polarization" else 3e-4), (m, rel.mean())
-        assert rel.max() < 2.5e-2, (m, rel.max())
-        # the geometry the eikonal / curvature losses see: 4-tap SDF gradients and hessians (second differences over
-        # delta^2 ~ 1.3e-6, so any activation rounding that differs between the centre and the tap rows shows here)
-        for k in ("gradients", "hessians"):
-            e = rel_err(outs[m][k].detach().cpu(), f[f"{m}:out:{k}"])
-            print(f"  {m:14s} {k} rel err {e:.3e}")
-            assert e < GEO_TOL_FAST[k], (m, k, e)
-    assert loss_rel < 2e-4   # measured <= 1.6e-5
-    # every parameter and pose gradient against the reference's (the fp16 backward-data chains' rounding shows here)
-    report = e2e_report(f, mods, model, pose, outs, total)
-    dpose = max(report[f"{m}:dpose"] for m in mods)
-    print(f"  worst parameter gradient {report['worst_param']:.3e} (relative L2 {report['worst_l2']:.3e}), "
-          f"worst dpose {dpose:.3e}")
-    l2 = {k: rel_l2(p.grad.cpu(), f["g:" + k]) for k, p in model.named_parameters() if "g:" + k in f}
-    for k in sorted(l2, key=lambda k: -l2[k])[:6]:
-        print(f"    {k:80s} relative L2 {l2[k]:.3e}")
-    bl2, bpose = fast_grad_bounds(preset)
-    assert report["worst_l2"] < bl2 and dpose < bpose, (report["worst_l2"], dpose)
+        print(f"  {m:14s} radiance rel dev: mean {rep[f'{m}:{m}|mean_rel']:.3e}  max {rep[f'{m}:{m}|max_rel']:.3e}")
+        # about 10x the measured deviation (round 5: fast mean <= 2.4e-5, polarization 3.8e-4 -- differences of Stokes
+        # terms --, max 2.4e-3; fast_h16b mean <= 9.0e-5, polarization 1.1e-3, max 3.4e-3)
+        assert rep[f"{m}:{m}|mean_rel"] < (1e-2 if m == "polarization" else 1e-3), m
+        assert rep[f"{m}:{m}|max_rel"] < 3.5e-2, m
+    check_envelope(name, rep, preset, sizes)
 
 
-# fast preset geometry bounds (fp32 mode: gradients 2e-3, hessians 0.15)
+# fast preset geometry bounds on their own (fp32 mode: gradients 2e-3, hessians 0.15)
 # (split-bf16x3 operands carry ~17 significant bits: measured gradients 2.4e-3, hessians 0.9 of the reference's hessian
-# scale on both fixtures; the bf16-weight SDF chain -- preset fast_x2 -- measured 56 and fails)
+# scale on both fixtures; the bf16-weight SDF chain -- preset fast_x2 -- measured 56 and fails; the reference's own fp16
+# autocast: gradients 0.2-0.3, hessians 65-134 of the scale, tests/golden/autocast_envelope.npz)
 GEO_TOL_FAST = {"gradients": 5e-3, "hessians": 1.5}
-# parameter gradients (relative L2 of the worst tensor) and pose gradients (scale-relative max) of the throughput
-# presets against the reference's, about 2x the worst measured over the four fixtures and the full-size one (round 5):
-# fast 1.5e-2 / 3.9e-2; fast_h16 and fast_h16b alike 3.2e-2 / 6.8e-2 -- the fp16 forward operands (2^-11) move
-# near-zero ReLU pre-activations of the background, radiance and head MLPs across zero (the row-scaled fp16 backward adds
-# nothing measurable), and the free-running sampler's bins follow the SDF's rounding.  The fp32 parity mode's bounds
-# are 1e-3 / 5e-3 (test_e2e_train_step).
-FAST_GRAD_BOUNDS = {"fast": (3e-2, 8e-2)}
-FAST_GRAD_BOUNDS_FP16 = (6e-2, 0.14)
-
-
-def fast_grad_bounds(preset):
-    return FAST_GRAD_BOUNDS.get(preset, FAST_GRAD_BOUNDS_FP16)
 
 
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_raw_gridbg_s95000"])
