@@ -111,6 +111,10 @@ class KernelTimer:
 
 
 TIMER = KernelTimer()
+# debugging: synchronise after every entry point and name the first one whose kernel faulted (MMS_SYNC_CALLS=1; the
+# previous calls' argument summaries are printed with it)
+SYNC_CALLS = os.environ.get("MMS_SYNC_CALLS", "0") == "1"
+_RECENT: list = []
 
 
 def call(name: str, *args) -> None:
@@ -136,6 +140,17 @@ def call(name: str, *args) -> None:
     if rc != 0:
         msg = L.mms_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed ({rc}): {msg}")
+    if SYNC_CALLS:
+        import torch
+        _RECENT.append(f"{name}{tuple(a if isinstance(a, (int, float)) else type(a).__name__ for a in args)}")
+        del _RECENT[:-4]
+        try:
+            torch.cuda.synchronize()
+            import time
+            time.sleep(0.02)        # a memory fault can be reported after the faulting kernel's completion
+            torch.cuda.synchronize()
+        except Exception as e:
+            raise RuntimeError(f"kernel fault in or before {name} (last calls: {_RECENT})") from e
 
 
 def exported_symbols():

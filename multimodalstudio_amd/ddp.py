@@ -78,17 +78,20 @@ class DDP:
             g.grad.mul_(1.0 / self.world)
         self.pending = []
 
-    def overlap_exchange(self, ready: List[torch.Tensor], groups: List, middle) -> None:
-        """Graph-replayed data-parallel steps: all-reduce the gradient regions ``ready`` (final now: the hash tables)
-        asynchronously, run ``middle`` (the replay that writes the remaining gradients) while they are in flight,
-        then all-reduce the rest, wait and average (graphs.GraphTrainer)."""
+    def overlap_exchange(self, stages: List, groups: List) -> None:
+        """Graph-replayed data-parallel steps.  ``stages``: [(ready, replay), ...] in order -- all-reduce the gradient
+        regions ``ready`` (final now) asynchronously, then run ``replay`` (the next graph, writing later gradients)
+        while they are in flight; then all-reduce the rest, wait and average (graphs.GraphTrainer: the radiance table
+        during the SDF backward, the SDF table during the weight gradients)."""
         if self.world <= 1:
-            middle()
+            for _, replay in stages:
+                replay()
             return
         self.begin_step()
-        for g in ready:
-            self.grad_ready(g, groups)
-        middle()
+        for ready, replay in stages:
+            for g in ready:
+                self.grad_ready(g, groups)
+            replay()
         self.finish_step(groups)
 
     def allreduce_grads(self, groups: List) -> None:

@@ -376,11 +376,25 @@ def sdf_panel(pos: torch.Tensor, ldp: int, M: int, ntaps: int, delta: float, g: 
 # position gradients + the gather-style mms_hashgrid_dpos_grouped cost the same as the walk computing both).
 # HASH_SPLIT = True (tests only) routes the position gradient through the gather kernel.
 HASH_SPLIT = False
+# groups (1: plain, 5: the SDF [centre | 4 taps] batch) whose TABLE gradient is made by ownership
+# (mms_hashgrid_bwd_owner: workgroup (level, chunk) scans every point and adds its chunk once -- no global atomics),
+# the position gradient then by the gather kernel (mms_hashgrid_dpos_grouped)
+HASH_OWNER = frozenset()
 
 
 def grid_bwd(g: GridCfg, pos, ldx, M, table, active, dout: torch.Tensor, col: int, dtable, dpos, group: int = 1):
     """Table / position gradients; group=5 for the [centre | 4 taps] SDF batch (M = 5 x centres)."""
     Mg = M // group
+    if dtable is not None and group in HASH_OWNER:
+        ws = torch.empty(M * (4 + 2 * g.L), device=dtable.device)
+        _lib.call("mms_hashgrid_bwd_owner", pos.data_ptr(), Mg, group, Mg, ldx, table.data_ptr(), g.L, g.log2T, g.F,
+                  g.interp, g.scales_ptr, g.radius, active, dout.data_ptr() + 4 * col, dout.stride(0),
+                  dtable.data_ptr(), ws.data_ptr(), ws.numel(), _s())
+        if dpos is not None:
+            _lib.call("mms_hashgrid_dpos_grouped", pos.data_ptr(), Mg, group, Mg, ldx, table.data_ptr(), g.L, g.log2T,
+                      g.F, g.interp, g.scales_ptr, g.radius, active, dout.data_ptr() + 4 * col, dout.stride(0),
+                      dpos.data_ptr(), dpos.stride(0), _s())
+        return
     split = HASH_SPLIT and dtable is not None and dpos is not None
     wpos = None if split else dpos
     _lib.call("mms_hashgrid_bwd_grouped", pos.data_ptr(), Mg, group, Mg, ldx, table.data_ptr(), g.L, g.log2T, g.F,
@@ -903,6 +917,23 @@ class _ZeroArena:
 _ARENA = _ZeroArena()
 _ARENA_OFF = os.environ.get("MMS_NO_ZERO_ARENA", "0") == "1"   # debugging: per-function zero fills
 _ALIGN = 64          # floats: every carved buffer starts on a 256-B boundary (vector / GEMM paths)
+# debugging (scripts/fullsize_graph_probe.py): a zero gap of this many floats after every carved buffer, checked by
+# arena_guard_report() -- a kernel that writes past its zeroed buffer shows up as a nonzero gap, named by its carve site
+_ARENA_GUARD = int(os.environ.get("MMS_ARENA_GUARD", "0"))
+_ARENA_SITES: List = []
+
+
+def arena_guard_report() -> List[str]:
+    """Carve sites whose guard gap was written (MMS_ARENA_GUARD builds only); call after a synchronize."""
+    a = _ARENA
+    bad = []
+    for off, n, site in _ARENA_SITES:
+        if a.buf is not None and off + n + _ARENA_GUARD <= a.buf.numel():
+            gap = a.buf[off + n: off + n + _ARENA_GUARD]
+            nz = int((gap != 0).sum())
+            if nz:
+                bad.append(f"{site}: {nz} gap floats written past a {n}-float buffer")
+    return bad
 
 
 def _arena_grow(dev) -> None:
@@ -932,6 +963,7 @@ def zero_arena_begin(dev, zeroed: Optional[torch.Tensor] = None) -> None:
         zeroed = None
     a.dev = dev
     a.need, a.off = 0, 0
+    _ARENA_SITES.clear()
     a.in_step = not _ARENA_OFF
     a.active = a.buf is not None and a.buf.device == torch.device(dev)
     if a.active and zeroed is None:
@@ -958,10 +990,14 @@ def _zeroed_views(shapes, dev) -> List[Optional[torch.Tensor]]:
     total = max(sum(padded), 1)
     a = _ARENA
     if a.in_step:
-        a.need += total     # (counted from the first step on: the buffer is sized at the next begin)
-    if a.active and a.off + total <= a.buf.numel():
+        a.need += total + _ARENA_GUARD     # (counted from the first step on: the buffer is sized at the next begin)
+    if a.active and a.off + total + _ARENA_GUARD <= a.buf.numel():
         buf = a.buf[a.off:a.off + total]
-        a.off += total
+        if _ARENA_GUARD:
+            import traceback
+            site = " <- ".join(f"{fr.name}:{fr.lineno}" for fr in traceback.extract_stack(limit=6)[-6:-1][::-1])
+            _ARENA_SITES.append((a.off, total, f"{shapes} @ {site}"))
+        a.off += total + _ARENA_GUARD
     else:
         buf = torch.zeros(total, device=dev)
     out, off = [], 0
@@ -981,6 +1017,39 @@ def _zeroed_views(shapes, dev) -> List[Optional[torch.Tensor]]:
 # autograd orders them with the main stream and adds them (a shared buffer across the two streams raced on the first
 # step, round 4).  MMS_GRAD_ACC=0: per-consumer buffers everywhere.
 GRAD_ACC = os.environ.get("MMS_GRAD_ACC", "1") != "0"
+
+# Two-phase backward (graph-replayed data-parallel steps, graphs.GraphTrainer): while PHASE_CUT is a list, the model's
+# forward hands every tensor that the SDF side (the surface field, the NeuS samples, the hit rays, the rays) passes to
+# the radiance / rendering / background / loss side through cut(): the consumers get a detached leaf copy and the pair
+# is recorded.  The training backward then runs in two caller-thread phases (pipeline.backward_batched ``mid``):
+# phase 1 from the loss down to the cut leaves -- the radiance field and its hash table, the heads, the composite, the
+# NeuS weights and the background, so the radiance (and grid-background) table gradients are final when it returns --
+# and phase 2 from the cut tensors with the leaves' gradients -- the SDF field, its table, the sampler, the rays and the
+# poses.  Between the two the graph capture ends and restarts on the caller's thread, so the radiance table's
+# all-reduce goes out while the SDF backward replays.  The arithmetic is unchanged: phase 2 delivers each
+# leaf's gradient to its producer as the single backward would (test_gpu_graph.py::test_phase_cut_backward).
+PHASE_CUT: List = [None]
+
+
+def cut(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """Forward: the phase-1 consumers' view of SDF-side tensor ``t`` (a detached leaf while PHASE_CUT is active)."""
+    rec = PHASE_CUT[0]
+    if rec is None or t is None or not t.requires_grad:
+        return t
+    d = t.detach().requires_grad_(True)
+    rec.append((t, d))
+    return d
+
+
+def phase_two(cuts) -> None:
+    """Backward phase 2: the cut tensors' gradients (accumulated on their leaf copies by phase 1) into the SDF side."""
+    ts, gs = [], []
+    for t, d in cuts:
+        if d.grad is not None:
+            ts.append(t)
+            gs.append(d.grad)
+    if ts:
+        torch.autograd.backward(ts, gs)
 
 
 class GradAcc:
@@ -2119,6 +2188,9 @@ class HeadsCompositeFunction(torch.autograd.Function):
                 out = torch.empty(bg.shape, device=bg.device) if hit is not None else bg.detach().clone().contiguous()
             else:
                 out = torch.empty(rays if sidx is None else rows, C, device=feat.device)
+            if _lib.SYNC_CALLS:
+                _composite_extents("fwd", w_c[w0:], v[sub * S:], v.stride(0), C, bg, rays, S, sidx, out.shape[0],
+                                   hit, None, None, 0, None, out)
             _lib.call("mms_composite_fwd", w_c[w0:].data_ptr(), v[sub * S:].data_ptr(), v.stride(0), C,
                       _p(None if bg is None else bg.contiguous()), rays, S, _p(sidx), out.shape[0], _p(hit),
                       out.data_ptr(), _s())
@@ -2155,6 +2227,9 @@ class HeadsCompositeFunction(torch.autograd.Function):
             dout = dout.contiguous()
             dbg = None if bg is None else (torch.empty(dout.shape, device=dev) if hit is not None else dout.clone())
             dwi = dw[w0:] if dw_direct else torch.empty(rays, S, device=dev)
+            if _lib.SYNC_CALLS:
+                _composite_extents("bwd", w[w0:], v[sub * S:], v.stride(0), C, bg, rays, S, sidx, dout.shape[0], hit,
+                                   dout, dvals[j][sub * S:], dvals[j].stride(0), dwi, dbg)
             _lib.call("mms_composite_bwd", w[w0:].data_ptr(), v[sub * S:].data_ptr(), v.stride(0), C, _p(bg), rays, S,
                       _p(sidx), dout.shape[0], _p(hit), dout.data_ptr(), dvals[j][sub * S:].data_ptr(),
                       dvals[j].stride(0), dwi.data_ptr(), _p(dbg), _s())
@@ -2201,6 +2276,28 @@ class HeadsCompositeFunction(torch.autograd.Function):
                 acc_ret(ctx.acc_d, ddirs) if ctx.needs_input_grad[2] else None,
                 acc_ret(ctx.acc_u, dups) if ctx.needs_input_grad[3] else None, None, None, None, None, *dbgs,
                 *([None] * ctx.n_params))
+
+
+def _composite_extents(tag, w, v, ldv, C, bg, R, S, idx, nout, hit, dout, dv, lddv, dw, dbg) -> None:
+    """Debugging (MMS_SYNC_CALLS=1): the elements mms_composite_fwd / _bwd will touch lie inside every operand."""
+    def need(name, t, n):
+        if t is not None and t.numel() < n:
+            raise RuntimeError(f"composite {tag}: {name} has {t.numel()} elements, the launch touches {n} "
+                               f"(R {R}, S {S}, C {C}, nout {nout}, ldv {ldv}, lddv {lddv}, shapes "
+                               f"{None if t is None else tuple(t.shape)})")
+    need("w", w, R * S)
+    need("vals", v, (R * S - 1) * ldv + C)
+    need("dvals", dv, (R * S - 1) * lddv + C)
+    need("dw", dw, R * S)
+    need("dout", dout, nout * C)
+    need("bg", bg, nout * C)
+    need("dbg", dbg, nout * C)
+    need("hit", hit, nout)
+    if idx is not None:
+        need("idx", idx, R)
+        mx = int(idx[:R].max())
+        if mx > nout:
+            raise RuntimeError(f"composite {tag}: scatter index {mx} > nout {nout}")
 
 
 def _partitions(ranges, total: int) -> bool:

@@ -26,12 +26,14 @@ graph is captured once they hold still.  The AdamW scalars (learning-rate schedu
 every step and are read from a device buffer instead (``mms_adamw_dev``).
 
 Multi-GPU: the RCCL gradient all-reduce stays outside the graphs, so each rank may replay a different capacity
-and no collective is ever captured.  The data-parallel step is three graphs: (1) forward + backward with the MLPs'
-weight-gradient GEMMs deferred (functions.wgrad_defer_begin) -- when it ends, every hash-table gradient (97 % of the
-138-205 MB payload) is final, so their bucketed all-reduces are launched right after its replay; (2) the
-deferred weight-gradient GEMMs + weight-norm flush, replayed while those all-reduces run on RCCL's stream; (3) the
-rest of the all-reduce, then clip + AdamW (+ the next step's draws).  The two backward graphs are one capture split
-where pipeline.backward_batched calls ``between``.
+and no collective is ever captured.  The data-parallel step is four graphs: (1a) the forward and the backward's first
+phase (the rendering side, functions.PHASE_CUT) with the MLPs' weight-gradient GEMMs deferred
+(functions.wgrad_defer_begin) -- when it ends the radiance table's gradient (and a grid background's) is final, so its
+bucketed all-reduce is launched right after the replay; (1m) the backward's second phase (the SDF field, its table, the
+sampler, the rays and the poses), replayed while that all-reduce runs -- when it ends the SDF table's gradient is final
+and its all-reduce goes out; (1b) the deferred weight-gradient GEMMs + weight-norm flush, replayed while those run; (2)
+the rest of the all-reduce, then clip + AdamW (+ the next step's draws).  The three backward graphs are one capture
+split on the caller's thread where pipeline.backward_batched calls ``mid`` and ``between``.
 """
 from __future__ import annotations
 
@@ -184,7 +186,7 @@ class GraphTrainer:
         return {m: t.images[m][self.sel[m], self.coords[m][:, 1].long(), self.coords[m][:, 2].long()]
                 for m in t.modalities}
 
-    def _forward_backward(self, cap: int, between=None):
+    def _forward_backward(self, cap: int, between=None, mid=None):
         t = self.t
         targets = self._targets()
         if BANKED_OPTIM:
@@ -200,26 +202,42 @@ class GraphTrainer:
                 t.poses.zero_grad()
             fx.zero_arena_begin(t.device)
         try:
-            return self._forward_backward_body(t, targets, cap, between)
+            return self._forward_backward_body(t, targets, cap, between, mid)
         finally:
             fx.zero_arena_end()
 
-    def _forward_backward_body(self, t, targets, cap: int, between=None):
+    def _forward_backward_body(self, t, targets, cap: int, between=None, mid=None):
         rays = t.raygen(self.coords)
         fx.reset_grad_uses()
-        outputs = t.model(rays, None, cap=cap)
+        cuts = None
+        if mid is not None:
+            # the two-phase backward (functions.PHASE_CUT): the forward records where the SDF side hands over
+            cuts = fx.PHASE_CUT[0] = []
+        try:
+            outputs = t.model(rays, None, cap=cap)
+        finally:
+            fx.PHASE_CUT[0] = None
         if t.raw:
             for m in t.modalities:
                 c = self.coords[m]
                 band = t.masks[m][c[:, 1].long(), c[:, 2].long()].long()[:, None]
                 outputs[m][m] = select_right_channel(outputs[m][m], band)
         losses, total = compute_loss(outputs, targets, t.modalities, t.step, max_iters=t.cfg.max_iters)
-        backward_batched(total, between)
+        backward_batched(total, between, mid, cuts)
         return losses, total
 
-    def table_grads(self):
-        """Flat-buffer views of the hash-table gradients: final when the first data-parallel graph ends."""
-        return [p.grad.view(-1) for name, p in self.t.model.named_parameters() if name.endswith("hash_table")]
+    def table_grads(self, phase: Optional[int] = None):
+        """Flat-buffer views of the hash-table gradients.  ``phase`` 1: those final when the backward's first phase
+        ends (the radiance field's and a grid background's table: functions.PHASE_CUT); 2: the SDF field's, final
+        when the second phase ends; None: all."""
+        out = []
+        for name, p in self.t.model.named_parameters():
+            if not name.endswith("hash_table"):
+                continue
+            sdf = name.startswith("surface_model.")
+            if phase is None or (phase == 2) == sdf:
+                out.append(p.grad.view(-1))
+        return out
 
     @staticmethod
     def _capture_stream():
@@ -230,33 +248,36 @@ class GraphTrainer:
         return torch.cuda.graph.default_capture_stream
 
     def _capture_split(self, cap: int, mode: str):
-        """Data-parallel capture: the forward/backward split into two graphs where the backward has queued all but
-        the deferred weight gradients (pipeline.backward_batched ``between``)."""
-        g1a, g1b = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        """Data-parallel capture: the forward/backward split into three graphs -- (a) the forward and the backward's
+        first phase (the rendering side: the radiance and grid-background table gradients are final when it ends), (m)
+        the second phase (the SDF side: the SDF table gradient is final when it ends), (b) the deferred weight
+        gradients and the weight-norm flush -- at the two caller-thread points of pipeline.backward_batched (``mid``,
+        ``between``)."""
+        gs = [torch.cuda.CUDAGraph() for _ in range(3)]
         pool = () if self.pool is None else (self.pool,)
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        live = [g1a]
+        live = [0]
 
-        def between():
-            live[0].capture_end()
-            live[0] = g1b
-            g1b.capture_begin(g1a.pool(), capture_error_mode=mode)
+        def cut_here():
+            gs[live[0]].capture_end()
+            live[0] += 1
+            gs[live[0]].capture_begin(gs[0].pool(), capture_error_mode=mode)
 
         with torch.cuda.stream(self._capture_stream()):
-            g1a.capture_begin(*pool, capture_error_mode=mode)
+            gs[0].capture_begin(*pool, capture_error_mode=mode)
             try:
-                out = self._forward_backward(cap, between)
+                out = self._forward_backward(cap, cut_here, cut_here)
             except BaseException:
                 try:
-                    live[0].capture_end()
+                    gs[live[0]].capture_end()
                 except Exception:
                     pass
                 raise
-            live[0].capture_end()
-        if live[0] is not g1b:
-            raise RuntimeError("the backward never reached its split point")
-        return g1a, g1b, out
+            gs[live[0]].capture_end()
+        if live[0] != 2:
+            raise RuntimeError(f"the backward reached {live[0]} of its 2 split points")
+        return gs, out
 
     def _optimizer(self):
         t = self.t
@@ -281,8 +302,8 @@ class GraphTrainer:
                     self._tail(captured=True)
             pool = g1.pool()
         else:
-            g1a, g1b, out = self._capture_split(cap, mode)
-            g1, pool = (g1a, g1b), g1a.pool()
+            g1, out = self._capture_split(cap, mode)
+            pool = g1[0].pool()
         if self.pool is None:
             self.pool = pool
         g2 = None
@@ -373,11 +394,12 @@ class GraphTrainer:
         if self.ddp is None:
             g1.replay()
         else:
-            # the hash-table gradients' all-reduce (launched after the first graph) runs while the second graph
-            # replays the deferred weight gradients; the rest follows, then the optimizer graph
+            # the radiance (+ grid background) table's all-reduce, launched after the first graph, runs while the
+            # second replays the SDF backward; the SDF table's while the third replays the deferred weight gradients;
+            # the rest follows, then the optimizer graph
             g1[0].replay()
-            self.ddp.overlap_exchange(self.table_grads(), [t.fields] + ([t.poses] if t.poses is not None else []),
-                                      g1[1].replay)
+            self.ddp.overlap_exchange([(self.table_grads(1), g1[1].replay), (self.table_grads(2), g1[2].replay)],
+                                      [t.fields] + ([t.poses] if t.poses is not None else []))
             g2.replay()
         if self.tail:
             self.count_event.record()

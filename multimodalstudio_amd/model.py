@@ -784,6 +784,10 @@ class BaseModel(nn.Module):
         # the ray's own modality's output reaches the loss, raw_pipeline.py:112-122), just its own
         own = self.own_heads_only and torch.is_grad_enabled()
 
+        # (two-phase backward, functions.PHASE_CUT: the background reads the rays through leaf copies, so phase 1 stops
+        # there and the rays' backward runs once, in phase 2)
+        o_c, d_c, up_c, bn_c, bf_c = fx.cut(o), fx.cut(d), fx.cut(up), fx.cut(bnears), fx.cut(bfars)
+
         def background():
             with torch.cuda.stream(bgs):
                 # the reported 1 / s (an output only, no loss term reads it: compute_metrics' inv_s) off the main stream
@@ -798,10 +802,10 @@ class BaseModel(nn.Module):
                 blin = self._lin_dev(nb, 1.0, dev)
                 bbins = torch.empty(nm * N, nb, device=dev)
                 _lib.call("mms_stratified_bins", blin.data_ptr(), nb, fx._p(bt), nb, nm * N, bbins.data_ptr(), fx._s())
-                bpos, bdeltas, _, _ = fx.SamplesFunction.apply(bbins, bnears, bfars, o, d, 1)
-                density, bfeat = self.background_model.field(bpos, d, sp.bg_samples)
+                bpos, bdeltas, _, _ = fx.SamplesFunction.apply(bbins, bn_c, bf_c, o_c, d_c, 1)
+                density, bfeat = self.background_model.field(bpos, d_c, sp.bg_samples)
                 bw = fx.DensityWeightsFunction.apply(density, bdeltas, sp.bg_samples)
-                bg_out = self._heads_composite(self.background_model.modality_heads, mods, own, bfeat, bw, d, up,
+                bg_out = self._heads_composite(self.background_model.modality_heads, mods, own, bfeat, bw, d_c, up_c,
                                                sp.bg_samples, [i * N for i in range(nm)], [N] * nm)
             return inv_s, bg_out
         # NeuS sampling (ray_samplers.py:448-514) -- latency-bound launches the background work overlaps; the
@@ -840,8 +844,11 @@ class BaseModel(nn.Module):
         # surface + radiance
         sdf, geo, grads, hess, normals = self.surface_model(pos)
         vr = self.surface_model.volume_rendering
-        w = fx.NeusWeightsFunction.apply(sdf, grads, d_h, deltas, s_param, vr._cos_anneal_ratio, S)
-        feat = self.radiance_model.features(pos, d_h, normals.detach(), geo, S)
+        # the SDF side's tensors as the rendering side reads them (leaf copies under functions.PHASE_CUT)
+        sdf, geo, grads, hess = fx.cut(sdf), fx.cut(geo), fx.cut(grads), fx.cut(hess)
+        pos_c, d_hc, up_hc, deltas = fx.cut(pos), fx.cut(d_h), fx.cut(up_h), fx.cut(deltas)
+        w = fx.NeusWeightsFunction.apply(sdf, grads, d_hc, deltas, s_param, vr._cos_anneal_ratio, S)
+        feat = self.radiance_model.features(pos_c, d_hc, normals.detach(), geo, S)
         # padded batches: the statistics scatter their padding rays into a dummy row N (cut off below); the composite
         # discards them (mms_composite nout = N), so its outputs need no cut -- no slice in the autograd graph, no
         # padded copy of the background
@@ -853,7 +860,7 @@ class BaseModel(nn.Module):
                 bg_out[k].record_stream(cur)    # made on the background stream, read (and freed) on this one
                 if torch.is_grad_enabled() and bg_out[k].requires_grad:
                     bg_out[k] = _JoinBackground.apply(bg_out[k], torch.device(dev).index or 0)
-        fg = self._heads_composite(self.radiance_model.modality_heads, mods, own, feat, w, d_h, up_h, S, off[:-1], Rm,
+        fg = self._heads_composite(self.radiance_model.modality_heads, mods, own, feat, w, d_hc, up_hc, S, off[:-1], Rm,
                                    sidx=sidx_m, bgs=bg_out, rows=N, hits=[mask[i * N:(i + 1) * N] for i in range(nm)])
         # accumulation / normals / depth renderers (renderers.py:176-242, no grad): one launch pair for all modalities
         stats = _render_stats_segments(w, normals, starts, ends, off, S, sidx_cat, rows, dev)

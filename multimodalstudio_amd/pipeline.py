@@ -435,23 +435,32 @@ def _seed(total: torch.Tensor) -> torch.Tensor:
     return one
 
 
-def backward_batched(total: torch.Tensor, between=None) -> None:
+def backward_batched(total: torch.Tensor, between=None, mid=None, cuts=None) -> None:
     """total.backward() with the layers' weight-norm gradients applied in one batched launch at its end.
 
     ``between`` (data-parallel graph steps): the MLPs' weight-gradient GEMMs are deferred, ``between()`` runs once the
     backward has queued everything else -- the hash-table gradients are final there -- and the deferred launches and
-    the weight-norm flush follow it (graphs.GraphTrainer ends one captured graph and begins the next there)."""
+    the weight-norm flush follow it (graphs.GraphTrainer ends one captured graph and begins the next there).
+    ``cuts`` (the forward ran under functions.PHASE_CUT): the backward runs in two caller-thread phases, the rendering
+    side first, then ``mid()`` -- the radiance table gradient is final there --, then the SDF side from the cut
+    tensors (functions.phase_two)."""
     fx.wn_bwd_begin()
     try:
+        def run():
+            total.backward(_seed(total))
+            if cuts is not None:
+                if mid is not None:
+                    mid()
+                fx.phase_two(cuts)
         if between is not None:
             fx.wgrad_defer_begin()
             try:
-                total.backward(_seed(total))
+                run()
             finally:
                 between()
             fx.wgrad_flush()
         else:
-            total.backward(_seed(total))
+            run()
     finally:
         fx._WGRAD_DEFER[0] = None
         fx._WGRAD_DEFER_STREAM[0] = None

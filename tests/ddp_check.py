@@ -2,9 +2,10 @@
 ``python -m torch.distributed.run --nproc-per-node 2 tests/ddp_check.py <out.json>`` (both ranks on cuda:0, gloo
 collectives: RCCL needs one GPU per rank).  Not a pytest module.
 
-0. GraphTrainer(ddp) x 5 (graph replays: the hash-table all-reduce launched after the first backward graph, overlapping
-   the replay of the deferred weight gradients, the rest after it): averaged gradients, parameters identical on both
-   ranks, and the steps were replayed.
+0. GraphTrainer(ddp) x 5 (graph replays: the radiance and background tables' all-reduce launched after the backward's
+   first phase, overlapping the SDF backward graph, the SDF table's after the second, overlapping the deferred weight
+   gradients, the rest after them): averaged gradients, parameters identical on both ranks, the regions launched in
+   that order, and the steps were replayed.
 1. Trainer.compute_grads(ddp) -- hash-table gradients all-reduced while the backward still runs, the rest after --
    equals the average of the two ranks' local gradients (local pass = same batch, same device RNG seed, no ddp).
 2. Trainer.train_step(ddp) x 2: parameters identical on both ranks.
@@ -42,8 +43,10 @@ def main():
     from multimodalstudio_amd.graphs import GraphTrainer
     from multimodalstudio_amd.pipeline import TrainConfig, Trainer
     fx.set_precision("fp32")
-    cfg = TrainConfig(method="grid_raw", modalities=("rgb", "polarization"), num_rays_per_modality=256, log2T=14,
-                      width=64, height=48)
+    # config 5's method: three hash tables (surface, radiance, grid background) -- the radiance and background tables'
+    # all-reduce goes out after the backward's first phase, the surface table's after its second
+    cfg = TrainConfig(method="grid_raw_grid_bg_unbalanced", modalities=("rgb", "polarization"),
+                      num_rays_per_modality=256, log2T=14, width=64, height=48)
     ddp = mddp.DDP(world, bucket_bytes=1 << 20)
     res = {"world": world}
     # graph-replayed data-parallel steps on a fresh trainer (as bench.py drives it: no eager default-stream steps
@@ -56,16 +59,33 @@ def main():
     # (split path: the hash-table regions are launched while the second backward graph replays, so their local values
     # are snapshotted at launch -- ordered before the collective on the stream -- and the rest when the exchange
     # finishes the step)
-    seen = {"local": [], "reduced": [], "early": [], "overlapped": 0}
+    seen = {"local": [], "reduced": [], "early": [], "overlapped": 0, "stage_ok": True}
     orig_ready, orig_finish = ddp.grad_ready, ddp.finish_step
 
+    in_graph = [False]
+    orig_ox = ddp.overlap_exchange
+
+    def spy_ox(stages, groups):
+        in_graph[0] = True
+        try:
+            orig_ox(stages, groups)
+        finally:
+            in_graph[0] = False
+    ddp.overlap_exchange = spy_ox
+
     def spy_ready(grad, groups):
-        seen["early"].append((grad.data_ptr(), grad.detach().reshape(-1).clone()))
+        # replayed steps: the surface table goes out second (after the backward's second phase), the others first
+        names = [n for n, p in tg.model.named_parameters() if p.grad is not None and p.grad.data_ptr() == grad.data_ptr()]
+        second = bool(names) and names[0].startswith("surface_model.")
+        early_second = [e for e in seen["early"] if e[2]]
+        if in_graph[0] and not second and early_second:
+            seen["stage_ok"] = False
+        seen["early"].append((grad.data_ptr(), grad.detach().reshape(-1).clone(), second))
         orig_ready(grad, groups)
 
     def spy_finish(groups):
         local = [gr.grad.clone() for gr in groups]
-        for ptr, early in seen["early"]:
+        for ptr, early, _ in seen["early"]:
             for gr, lg in zip(groups, local):
                 off = (ptr - gr.grad.data_ptr()) // 4
                 if 0 <= off < gr.grad.numel():
@@ -81,6 +101,7 @@ def main():
         g.step()
     torch.cuda.synchronize()
     ddp.grad_ready, ddp.finish_step = orig_ready, orig_finish
+    ddp.overlap_exchange = orig_ox
     if seen["local"]:
         errs = []
         for local, red in zip(seen["local"], seen["reduced"]):
@@ -90,6 +111,7 @@ def main():
         res["graph_grad_err"] = max(errs)
         res["graph_allreduces"] = len(seen["local"])
         res["graph_overlapped_regions"] = seen["overlapped"]
+        res["graph_stage_order_ok"] = seen["stage_ok"]
     p = gather(tg.fields.flat)
     q = gather(tg.poses.flat)
     res["graph_params_equal"] = bool(torch.equal(p[0], p[1]) and torch.equal(q[0], q[1]))

@@ -60,3 +60,24 @@ def with_fullsize_params(f: dict) -> dict:
     f = dict(f)
     f.update({"p:" + k: v.numpy() for k, v in sd.items()})
     return f
+
+
+def sorted_index_equal_up_to_ties(got, ref, final_bins=None) -> bool:
+    """An up-sampler iteration's sorted_index against the reference's, up to the order of TIED keys: torch.sort is not
+    stable, so where a new sample lands exactly on an existing bin the reference's own CPU runs order the two indices
+    either way (measured on the full-size fixtures: a few swapped pairs per modality, at bins equal to the last bit).
+    Every maximal run of differing columns in a row must hold the same indices in both; with ``final_bins`` (the last
+    iteration's sorted bins) the run's bins must also be equal."""
+    import numpy as np
+    got, ref = np.asarray(got, np.int64), np.asarray(ref, np.int64)
+    if got.shape != ref.shape:
+        return False
+    for r in np.nonzero((got != ref).any(1))[0]:
+        cols = np.nonzero(got[r] != ref[r])[0]
+        runs = np.split(cols, np.nonzero(np.diff(cols) > 1)[0] + 1)
+        for run in runs:
+            if sorted(got[r, run]) != sorted(ref[r, run]):
+                return False
+            if final_bins is not None and not np.all(final_bins[r, run] == final_bins[r, run[0]]):
+                return False
+    return True

@@ -39,5 +39,8 @@ def test_two_rank_training(tmp_path):
     # the graph path's exchange (hash tables overlapped with the weight-gradient graph, the rest after it) averages the
     # ranks' gradients, as the eager path does
     assert res["graph_allreduces"] >= 1 and res["graph_grad_err"] < 1e-6, res
-    # the hash-table regions went out before the weight-gradient graph replayed (2 tables per replayed step)
-    assert res["graph_overlapped_regions"] >= 2 * res["graph_stats"]["replays"], res
+    # the hash-table regions went out early, in two stages: the radiance and background tables after the backward's
+    # first phase (overlapping the SDF backward graph), the SDF table after the second (overlapping the weight
+    # gradients) -- 3 tables per replayed step
+    assert res["graph_overlapped_regions"] >= 3 * res["graph_stats"]["replays"], res
+    assert res["graph_stage_order_ok"], res

@@ -56,7 +56,7 @@ from test_gpu_e2e import (FAST_PRESETS, GEO_TOL_FAST, GOLD, E2ECase, check_envel
 pytestmark = pytest.mark.gpu
 NAME = "e2e_full_grid_rgb_l19"
 # every full-size fixture with a float64 truth (tests/golden/make_fullsize_truth.py)
-FULL = [NAME]
+FULL = [NAME, "e2e_full_grid_raw5_l19", "e2e_full_gridbg_l19"]
 SMOOTH = "e2e_full_grid_rgb_l19_smooth"
 
 
@@ -66,16 +66,24 @@ def truth_check(f, case, outs, total, cap, tag, name=NAME):
     t = dict(np.load(os.path.join(GOLD, name + "_f64.npz")))
     rows, worst = [], 0.0
 
-    def check(key, hip, ref, tru, l2=False):
+    def check(key, hip, ref, tru, l2=False, nulls=None):
         nonlocal worst
         hip, ref, tru = (np.asarray(x, np.float64) for x in (hip, ref, tru))
         d = rel_l2 if l2 else rel_err
-        d_ref, d_hip = d(ref, tru), d(hip, tru)
+        d_hip = d(hip, tru)
+        # the reference algorithm's own float32 scatter about the truth: the reference's distance and the stored null
+        # draws' (make_fullsize_truth.py: float32 oracle runs on fp32-reordering-size parameter perturbations)
+        d_ref = d(ref, tru)
+        if nulls is not None:
+            nk = ("nulll2:" if l2 else "nullmax:") + nulls
+            if nk in t:
+                d_ref = max([d_ref] + [float(x) for x in np.asarray(t[nk]).reshape(-1)])
         # a single element's max error varies more between two float32 orderings than an L2 or a norm does
         bound = (2.0 if l2 or key.startswith("gtabnorm") else 3.0) * d_ref + 1e-5
         rows.append((d_hip / bound, key, d_hip, d_ref))
         worst = max(worst, d_hip / bound)
     assert abs(total.item() - float(f["loss"])) / abs(float(f["loss"])) < 1e-4
+    nul = lambda key: key  # noqa: E731   (the truth fixture's null-draw distances of this quantity)
     for m in case.mods:
         o = outs[m]
         n = int(o["count"].item()) if cap is not None else int(f[f"{m}:mask"].sum())
@@ -86,20 +94,21 @@ def truth_check(f, case, outs, total, cap, tag, name=NAME):
             v = o[k].detach()
             if k in ("gradients", "hessians"):
                 v = v[:n]
-            check(f"{m}:{k}", v.cpu(), f[f"{m}:out:{k}"], t[f"{m}:out:{k}"])
-        check(f"{m}:dpose", case.pose.pose_adjustment[m].grad.cpu(), f[f"{m}:dpose"], t[f"{m}:dpose"])
+            check(f"{m}:{k}", v.cpu(), f[f"{m}:out:{k}"], t[f"{m}:out:{k}"], nulls=nul(f"{m}:out:{k}"))
+        check(f"{m}:dpose", case.pose.pose_adjustment[m].grad.cpu(), f[f"{m}:dpose"], t[f"{m}:dpose"],
+              nulls=nul(f"{m}:dpose"))
     for k, p in case.model.named_parameters():
         g = p.grad.detach()
         if "g:" + k in f:
-            check("g:" + k, g.cpu(), f["g:" + k], t["g:" + k])
-            check("gL2:" + k, g.cpu(), f["g:" + k], t["g:" + k], l2=True)
+            check("g:" + k, g.cpu(), f["g:" + k], t["g:" + k], nulls=nul("g:" + k))
+            check("gL2:" + k, g.cpu(), f["g:" + k], t["g:" + k], l2=True, nulls=nul("g:" + k))
         elif "gtab_val:" + k in f:
             idx = torch.from_numpy(f["gtab_idx:" + k].astype(np.int64)).to(g.device)
             v = g.reshape(-1)[idx].cpu()
-            check("gtab:" + k, v, f["gtab_val:" + k], t["gtab_val:" + k])
-            check("gtabL2:" + k, v, f["gtab_val:" + k], t["gtab_val:" + k], l2=True)
+            check("gtab:" + k, v, f["gtab_val:" + k], t["gtab_val:" + k], nulls=nul("gtab_val:" + k))
+            check("gtabL2:" + k, v, f["gtab_val:" + k], t["gtab_val:" + k], l2=True, nulls=nul("gtab_val:" + k))
             check("gtabnorm:" + k, g.double().reshape(16, -1).norm(dim=1).cpu(), f["gtab_level_norm:" + k],
-                  t["gtab_level_norm:" + k])
+                  t["gtab_level_norm:" + k], nulls=nul("gtab_level_norm:" + k))
     rows.sort(reverse=True)
     print(f"{tag}: worst d_hip / bound {worst:.3f}")
     for r, key, dh, dr in rows[:10]:
@@ -114,10 +123,11 @@ def granule_cap(f):
     return bucket_capacity([int(np.asarray(f[f"{m}:mask"]).sum()) for m in mods], 64, n)
 
 
-@pytest.mark.parametrize("name", FULL)
+@pytest.mark.parametrize("name", FULL + [SMOOTH])
 def test_fullsize_sampler_bit_exact(dev, name):
     """Per modality: the HIP up-sampler fed the reference's hit rays, uniforms and per-iteration SDFs reproduces the
-    final bins and all four sorted_index tensors bit for bit."""
+    final bins bit for bit and all four sorted_index tensors up to the order of tied keys."""
+    from fullsize_state import sorted_index_equal_up_to_ties
     from multimodalstudio_amd import model as mm
     f = load(name)
     mods = [str(m) for m in f["mods"]]
@@ -147,8 +157,10 @@ def test_fullsize_sampler_bit_exact(dev, name):
               f"{np.abs(got - ref).max():.3e}")
         assert np.array_equal(got, ref), m
         for k in range(4):
-            assert np.array_equal(hist[k].cpu().numpy().astype(np.int64),
-                                  f[f"{m}:sampler:sorted_index{k}"].astype(np.int64)), (m, k)
+            # up to the order of tied keys: the reference's torch.sort is not stable (the HIP merge is; the
+            # reference's own CPU runs order exactly tied bins either way, fullsize_state.sorted_index_equal_up_to_ties)
+            assert sorted_index_equal_up_to_ties(hist[k].cpu().numpy(), f[f"{m}:sampler:sorted_index{k}"],
+                                                 ref[:, :-1] if k == 3 else None), (m, k)
 
 
 @pytest.mark.parametrize("which", ["dynamic", "granule", "all_rays"])

@@ -130,3 +130,59 @@ def test_tail_count_after_eager_steps(dev):
             assert 0 < ref[0] <= 512
     finally:
         graphs.FUSED_COUNT = old
+
+
+@pytest.mark.parametrize("name", ["e2e_grid_raw_5mod_s95000", "e2e_grid_raw_gridbg_s95000"])
+@pytest.mark.parametrize("cap", [None, "granule"])
+def test_phase_cut_backward(dev, name, cap):
+    """The two-phase backward of the graph-replayed data-parallel step (functions.PHASE_CUT, pipeline.backward_batched
+    ``cuts``: the rendering side first, then the SDF side from the cut tensors) gives the single backward's results:
+    the loss, the outputs and every parameter and pose gradient to float-atomic summation order; phase 1 alone has
+    already finished the radiance (and grid-background) table gradients and left the SDF table's untouched."""
+    from multimodalstudio_amd import functions as fx
+    from multimodalstudio_amd import pipeline as pl
+    from test_gpu_e2e import E2ECase, rel_err
+    from test_gpu_fullsize import granule_cap
+    f = load(name)
+    c = None if cap is None else granule_cap(f)
+    runs = []
+    for split in (False, True):
+        case = E2ECase(f, dev)
+        rays = case.gen(case.coords)
+        cuts = None
+        if split:
+            cuts = fx.PHASE_CUT[0] = []
+        try:
+            outs = case.model(rays, case.rng, cap=c)
+        finally:
+            fx.PHASE_CUT[0] = None
+        for m, band in case.band.items():
+            outs[m][m] = pl.select_right_channel(outs[m][m], band)
+        losses, total = pl.compute_loss(outs, case.targets, case.mods, int(f["step"]))
+        phase1 = {}
+
+        def mid():
+            torch.cuda.synchronize()
+            for k, p in case.model.named_parameters():
+                if k.endswith("hash_table"):
+                    phase1[k] = None if p.grad is None else p.grad.detach().clone()
+        pl.backward_batched(total, mid=mid if split else None, cuts=cuts)
+        torch.cuda.synchronize()
+        if split:
+            assert len(cuts) >= 8, len(cuts)
+        grads = {k: p.grad.detach().cpu().clone() for k, p in case.model.named_parameters() if p.grad is not None}
+        grads.update({f"pose:{k}": p.grad.detach().cpu().clone() for k, p in case.pose.named_parameters()
+                      if p.grad is not None})
+        runs.append((float(total), {m: outs[m][m].detach().cpu().clone() for m in case.mods}, grads, phase1))
+    (l0, o0, g0, _), (l1, o1, g1, p1) = runs
+    assert abs(l0 - l1) <= 1e-6 * abs(l0)
+    for m in o0:
+        assert rel_err(o1[m], o0[m]) < 1e-6, m
+    assert g0.keys() == g1.keys()
+    for k in g0:
+        assert rel_err(g1[k], g0[k]) < 1e-4, (k, rel_err(g1[k], g0[k]))
+    for k, g in p1.items():
+        if k.startswith("surface_model."):
+            assert g is None or float(g.abs().max()) == 0.0, k       # the SDF table: phase 2
+        else:
+            assert g is not None and rel_err(g.cpu(), g0[k]) < 1e-6, k   # final after phase 1

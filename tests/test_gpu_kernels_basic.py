@@ -38,14 +38,16 @@ def test_hashgrid_fwd_bwd(dev, log2T, active, radius):
     np.testing.assert_allclose(xd.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("split", [True, False])
+@pytest.mark.parametrize("split", [True, False, "owner"])
 @pytest.mark.parametrize("group", [1, 5])
 def test_hashgrid_smoothstep(dev, group, split, monkeypatch):
     """interpolation "Smoothstep" (HashEncodingConfig, encodings.py:64-67; tcnn's mode, parity-unpinned): forward,
     table and position gradients of the plain and the [centre | 4 taps] kernels vs the oracle's restatement of the
     smoothstep weights, whose position gradient autograd derives (d S / dt = 6 t (1 - t))."""
     from multimodalstudio_amd import functions as F
-    monkeypatch.setattr(F, "HASH_SPLIT", split)    # position gradient by the gather kernel / by the table walk
+    monkeypatch.setattr(F, "HASH_SPLIT", split is True)    # position gradient by the gather kernel / by the table walk
+    # the table gradient by ownership (mms_hashgrid_bwd_owner) or by the walk
+    monkeypatch.setattr(F, "HASH_OWNER", frozenset({1, 5}) if split == "owner" else frozenset())
     L, Mc, log2T = 16, 1500, 14
     scales = ohg.level_scales(16, 1024, L)
     g = torch.Generator().manual_seed(11)
@@ -74,13 +76,14 @@ def test_hashgrid_smoothstep(dev, group, split, monkeypatch):
     np.testing.assert_allclose(dpos.cpu().numpy(), xr.grad.numpy(), rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("split", [True, False])
+@pytest.mark.parametrize("split", [True, False, "owner"])
 @pytest.mark.parametrize("log2T", [12, 19])
 def test_hashgrid_bwd_grouped_taps(dev, log2T, split, monkeypatch):
     """[centre | 4 taps] batch: the grouped backward (LDS merge of shared-cell corners; position gradient by the
-    gather kernel or by the walk) vs the oracle."""
+    gather kernel or by the walk; or the table gradient by ownership, mms_hashgrid_bwd_owner) vs the oracle."""
     from multimodalstudio_amd import functions as F
-    monkeypatch.setattr(F, "HASH_SPLIT", split)
+    monkeypatch.setattr(F, "HASH_SPLIT", split is True)
+    monkeypatch.setattr(F, "HASH_OWNER", frozenset({1, 5}) if split == "owner" else frozenset())
     L, Mc, delta = 16, 2000, 2.0 / 1024 / 3 ** 0.5
     scales = ohg.level_scales(16, 2048, L)
     g = torch.Generator().manual_seed(7)

@@ -165,7 +165,8 @@ def run_oracle_e2e(f):
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_rgb_s30000", "e2e_grid_raw_5mod_s95000",
                                   "e2e_grid_raw_5mod_sat_s95000", "e2e_mlp_raw_rgb_s95000",
                                   "e2e_grid_raw_gridbg_s95000", "e2e_grid_raw_gridbg_s30000",
-                                  "e2e_full_grid_rgb_l19"])
+                                  "e2e_full_grid_rgb_l19", "e2e_full_grid_rgb_l19_smooth", "e2e_full_gridbg_l19",
+                                  "e2e_full_grid_raw5_l19"])
 def test_end_to_end(name):
     f = e2e_inputs(name)
     mods, outs, losses, total, P, poses = run_oracle_e2e(f)
@@ -264,21 +265,29 @@ def test_train_parity_window_resolves_the_bound(name):
         assert float(f[f"eval:{m}:psnr"]) > float(f[f"eval0:{m}:psnr"]) + 0.25, m
 
 
-def test_fullsize_sampler_bit_exact():
-    """The oracle's NeuS up-sampler on the full-size fixture's hit rays, uniforms and per-iteration reference SDFs
-    reproduces the reference's final bins and every iteration's sorted_index bit for bit."""
-    f = load("e2e_full_grid_rgb_l19")
-    m = "rgb"
-    sdfs = [T(f[f"{m}:sampler:sdf{i}"]) for i in range(4)]
-    calls = []
+@pytest.mark.parametrize("name", ["e2e_full_grid_rgb_l19", "e2e_full_grid_rgb_l19_smooth", "e2e_full_gridbg_l19",
+                                  "e2e_full_grid_raw5_l19"])
+def test_fullsize_sampler_bit_exact(name):
+    from fullsize_state import sorted_index_equal_up_to_ties
+    """The oracle's NeuS up-sampler on each full-size fixture's hit rays, uniforms and per-iteration reference SDFs
+    reproduces the reference's final bins bit for bit and every iteration's sorted_index up to the order of tied keys,
+    per modality."""
+    f = load(name)
+    mods = [str(m) for m in f["mods"]]
+    nm = len(mods)
+    for i, m in enumerate(mods):
+        sdfs = [T(f[f"{m}:sampler:sdf{k}"]) for k in range(4)]
+        calls = []
 
-    def sdf_fn(pts):
-        calls.append(1)
-        return sdfs[len(calls) - 1]
-    smp, hist = orr.neus_sample(T(f[f"{m}:hit:nears"]), T(f[f"{m}:hit:fars"]), T(f[f"{m}:hit:origins"]),
-                                T(f[f"{m}:hit:directions"]), sdf_fn, T(f["rand:0"]),
-                                [T(f[f"rand:{1 + i}"]) for i in range(4)])
-    assert len(calls) == 4
-    assert np.array_equal(smp.spacing_bins.numpy(), f[f"{m}:bins"])
-    for i in range(4):
-        assert np.array_equal(hist[i].numpy(), f[f"{m}:sampler:sorted_index{i}"].astype(np.int64)), i
+        def sdf_fn(pts):
+            calls.append(1)
+            return sdfs[len(calls) - 1]
+        smp, hist = orr.neus_sample(T(f[f"{m}:hit:nears"]), T(f[f"{m}:hit:fars"]), T(f[f"{m}:hit:origins"]),
+                                    T(f[f"{m}:hit:directions"]), sdf_fn, T(f[f"rand:{i}"]),
+                                    [T(f[f"rand:{nm + 4 * i + k}"]) for k in range(4)])
+        assert len(calls) == 4
+        assert np.array_equal(smp.spacing_bins.numpy(), f[f"{m}:bins"]), m
+        for k in range(4):
+            # up to the order of tied keys (torch.sort is not stable; fullsize_state.sorted_index_equal_up_to_ties)
+            assert sorted_index_equal_up_to_ties(hist[k].numpy(), f[f"{m}:sampler:sorted_index{k}"],
+                                                 f[f"{m}:bins"][:, :-1] if k == 3 else None), (m, k)
