@@ -60,16 +60,6 @@ int mms_hashgrid_dpos_grouped(const float* pos, int64_t Mg, int group, int64_t g
                               const float* table, int L, int log2T, int F, int interp, const float* scales,
                               float radius, int active_levels, const float* dout, int64_t ldd, float* dpos,
                               int64_t lddx, void* stream);
-/* The table gradient alone (dtable +=, the same values as mms_hashgrid_bwd_grouped's to float summation order) by
- * ownership instead of global atomics (HashEncoding backward, encodings.py:263-304 under autograd): workgroup (level,
- * 2^14-entry chunk) scans every point, accumulates the corners that land in its chunk in LDS and adds the chunk to
- * dtable once.  `workspace` (16-B aligned, >= Mg * group * (4 + 2 L) floats) holds the points' x_hat and level-major
- * output gradients.  Same arguments and grouping as mms_hashgrid_bwd_grouped; the position gradient comes from
- * mms_hashgrid_dpos_grouped. */
-int mms_hashgrid_bwd_owner(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx, const float* table,
-                           int L, int log2T, int F, int interp, const float* scales, float radius, int active_levels,
-                           const float* dout, int64_t ldd, float* dtable, float* workspace, int64_t workspace_floats,
-                           void* stream);
 /* The SDF field's MLP input panel in one launch: rows [x(3) | PE(6 pe_freqs) | hash grid(2L)] of ldx floats, for the M
  * centre positions cpos [M, ldp] and (ntaps = 4) their tap points centre + k_t delta, rows t * M + i (t = 0 centre).
  * Replaces SDFField.forward's input stage (surface_field.py:99-116: NeRFEncoding encodings.py:161-182 + FeatureGrid

@@ -654,111 +654,6 @@ __global__ __launch_bounds__(256) void hashgrid_dpos_kernel(const float* __restr
   }
 }
 
-// Table gradient by ownership (mms_hashgrid_bwd_owner): the walk above adds every fine-level corner gradient with a
-// float atomic of its own -- at the fine levels each of a point's 8 corners is its own table line (the hash scatters
-// neighbouring cells), and over a step every line of a fine level's 4 MB table is hit ~14 times by unrelated samples
-// (scripts/hash_line_floor.py), so the walk is bound by memory-side atomic requests.  Here workgroup (level l, chunk c)
-// OWNS table entries [c 2^CB, (c + 1) 2^CB) of level l: it scans every point, recomputes the point's 8 corner indices
-// at level l (the forward's arithmetic: same corners, contraction off in this file), and accumulates the corners that
-// fall in its chunk into a 2^CB-entry LDS array (ds_add_f32), which it then adds to the table gradient once, with
-// coalesced plain read-modify-writes -- no global atomics, every table line written by exactly one workgroup.
-// The scan reads compact per-point rows made by hashgrid_owner_prep_kernel (x_hat as float4, the output gradient
-// level-major as float2) instead of the strided panel rows.
-constexpr int kOwnBits = 14;     // entries per chunk: 2^14 float2 = 128 KB of LDS
-constexpr int kOwnThreads = 1024;
-
-// p -> row of point p: rows g + j * gstride, p = j * Mg + g (all centres, then each tap block)
-__device__ __forceinline__ int64_t owner_row(int64_t p, int64_t Mg, int64_t gstride) {
-  const int64_t j = p / Mg;
-  return p - j * Mg + j * gstride;
-}
-
-__global__ __launch_bounds__(256) void hashgrid_owner_prep_kernel(const float* __restrict__ pos, int64_t P, int64_t Mg,
-                                                                  int64_t gstride, int64_t ldx, GridParams p,
-                                                                  const float* __restrict__ dout, int64_t ldd,
-                                                                  float4* __restrict__ xh, float2* __restrict__ dl) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= P) return;
-  const int64_t r = owner_row(i, Mg, gstride);
-  const float* xp = pos + r * ldx;
-  const float two_r = 2.0f * p.radius;
-  const bool norm = p.radius > 0.f;
-  // make_corners' rounding of x_hat (bit-exact corner indices)
-  xh[i] = make_float4(norm ? (xp[0] + p.radius) / two_r : xp[0], norm ? (xp[1] + p.radius) / two_r : xp[1],
-                      norm ? (xp[2] + p.radius) / two_r : xp[2], 0.f);
-  const float* dr = dout + r * ldd;
-  const int nlv = p.levels < p.active_levels ? p.levels : p.active_levels;
-  for (int l = 0; l < nlv; ++l) dl[(int64_t)l * P + i] = make_float2(dr[2 * l], dr[2 * l + 1]);
-}
-
-__global__ __launch_bounds__(kOwnThreads) void hashgrid_bwd_owner_kernel(const float4* __restrict__ xh,
-                                                                         const float2* __restrict__ dl, int64_t P,
-                                                                         GridParams p, float* __restrict__ dtable) {
-  __shared__ float acc[2 << kOwnBits];
-  const int cb = p.log2T < kOwnBits ? p.log2T : kOwnBits;     // chunk bits
-  const int nchunk = 1 << (p.log2T - cb);
-  const int level = blockIdx.x / nchunk, chunk = blockIdx.x - level * nchunk;
-  const int nlv = p.levels < p.active_levels ? p.levels : p.active_levels;
-  if (level >= nlv) return;     // the whole block: no barrier reached
-  const int t = threadIdx.x;
-  const int n2 = 2 << cb;
-  for (int i = t; i < n2; i += kOwnThreads) acc[i] = 0.f;
-  __syncthreads();
-  const float s = p.scale[level];
-  const uint32_t hmask = (1u << p.log2T) - 1u;
-  const uint32_t cmask = (1u << cb) - 1u;
-  const uint32_t mine = (uint32_t)chunk;
-  const bool sm = p.smooth != 0;
-  const float2* dlev = dl + (int64_t)level * P;
-  for (int64_t i = t; i < P; i += kOwnThreads) {
-    const float4 h = xh[i];
-    const float sx = h.x * s, sy = h.y * s, sz = h.z * s;
-    const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
-    const int xf = (int)fx, yf = (int)fy, zf = (int)fz;
-    const int xc = (int)ceilf(sx), yc = (int)ceilf(sy), zc = (int)ceilf(sz);
-    // hash3 = x ^ y P1 ^ z P2 (mod 2^log2T): the y and z products once per side
-    const uint32_t yc1 = (uint32_t)yc * kP1, yf1 = (uint32_t)yf * kP1;
-    const uint32_t zc2 = (uint32_t)zc * kP2, zf2 = (uint32_t)zf * kP2;
-    uint32_t idx[8];
-    idx[0] = ((uint32_t)xc ^ yc1 ^ zc2) & hmask;   // corner order of make_corners
-    idx[1] = ((uint32_t)xc ^ yf1 ^ zc2) & hmask;
-    idx[2] = ((uint32_t)xf ^ yf1 ^ zc2) & hmask;
-    idx[3] = ((uint32_t)xf ^ yc1 ^ zc2) & hmask;
-    idx[4] = ((uint32_t)xc ^ yc1 ^ zf2) & hmask;
-    idx[5] = ((uint32_t)xc ^ yf1 ^ zf2) & hmask;
-    idx[6] = ((uint32_t)xf ^ yf1 ^ zf2) & hmask;
-    idx[7] = ((uint32_t)xf ^ yc1 ^ zf2) & hmask;
-    uint32_t hit = 0u;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) hit |= (uint32_t)((idx[k] >> cb) == mine) << k;
-    if (hit == 0u) continue;
-    const float2 dE = dlev[i];
-    const float tx = sx - fx, ty = sy - fy, tz = sz - fz;
-    const float ox = sm ? smoothstep(tx) : tx, oy = sm ? smoothstep(ty) : ty, oz = sm ? smoothstep(tz) : tz;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if ((hit >> k) & 1u) {
-        // corner k's sides (0 ccc, 1 cfc, 2 ffc, 3 fcc, 4 ccf, 5 cff, 6 fff, 7 fcf); autograd's order of
-        // encodings.py:292-302 reversed, as the walk: ((dE * w_z) * w_y) * w_x
-        const bool cxk = k == 0 || k == 1 || k == 4 || k == 5;
-        const bool cyk = k == 0 || k == 3 || k == 4 || k == 7;
-        const bool czk = k < 4;
-        const float wx = cxk ? ox : 1.0f - ox, wy = cyk ? oy : 1.0f - oy, wz = czk ? oz : 1.0f - oz;
-        const uint32_t e = idx[k] & cmask;
-        atomicAdd(&acc[2 * e], ((dE.x * wz) * wy) * wx);
-        atomicAdd(&acc[2 * e + 1], ((dE.y * wz) * wy) * wx);
-      }
-    }
-  }
-  __syncthreads();
-  // the chunk's gradient added to the table gradient once: consecutive floats per thread, coalesced
-  float* dst = dtable + 2 * (((int64_t)level << p.log2T) + ((int64_t)chunk << cb));
-  for (int i = t; i < n2; i += kOwnThreads) {
-    const float v = acc[i];
-    if (v != 0.f) dst[i] += v;
-  }
-}
-
 int fill_params(const char* fn, GridParams& p, int L, int log2T, int interp, const float* scales, float radius,
                 int active_levels) {
   if (L < 1 || L > kMaxLevels) return mms::set_error(fn, "num_levels must be in [1, 16]");
@@ -954,35 +849,5 @@ MMS_EXPORT int mms_hashgrid_dpos_grouped(const float* pos, int64_t Mg, int group
   else
     hipLaunchKernelGGL((hashgrid_dpos_kernel<1>), dim3(blocks), dim3(256), 0, s, pos, Mg, Mg, ldx, t2, p, dout, ldd,
                        dpos, lddx);
-  return mms::check_launch(fn);
-}
-
-MMS_EXPORT int mms_hashgrid_bwd_owner(const float* pos, int64_t Mg, int group, int64_t gstride, int64_t ldx,
-                                      const float* table, int L, int log2T, int F, int interp, const float* scales,
-                                      float radius, int active_levels, const float* dout, int64_t ldd, float* dtable,
-                                      float* workspace, int64_t workspace_floats, void* stream) {
-  const char* fn = "mms_hashgrid_bwd_owner";
-  MMS_REQUIRE(F == 2, fn, "features_per_level must be 2");
-  MMS_REQUIRE(Mg >= 0 && ldx >= 3 && ldd >= 2 * L, fn, "bad shapes");
-  MMS_REQUIRE(group == 1 || group == 5, fn, "group must be 1 (plain) or 5 (centre + 4 taps)");
-  MMS_REQUIRE(group == 1 || gstride >= Mg, fn, "group rows overlap (gstride < groups)");
-  GridParams p;
-  int rc = fill_params(fn, p, L, log2T, interp, scales, radius, active_levels);
-  if (rc) return rc;
-  if (Mg == 0) return 0;
-  (void)table;
-  MMS_REQUIRE(pos && dout && dtable && workspace, fn, "null pointer");
-  const int64_t P = Mg * group;
-  MMS_REQUIRE(workspace_floats >= P * (4 + 2 * (int64_t)L), fn, "workspace smaller than Mg * group * (4 + 2 L)");
-  MMS_REQUIRE(((uintptr_t)workspace & 15) == 0, fn, "workspace must be 16-B aligned");
-  MMS_REQUIRE(P <= INT32_MAX, fn, "too many points");
-  float4* xh = reinterpret_cast<float4*>(workspace);
-  float2* dl = reinterpret_cast<float2*>(workspace + 4 * P);
-  hipStream_t s = mms::as_stream(stream);
-  hipLaunchKernelGGL(hashgrid_owner_prep_kernel, dim3(mms::grid_for(P, 256, INT32_MAX)), dim3(256), 0, s, pos, P, Mg,
-                     group == 1 ? Mg : gstride, ldx, p, dout, ldd, xh, dl);
-  const int cb = log2T < kOwnBits ? log2T : kOwnBits;
-  const int blocks = L << (log2T - cb);
-  hipLaunchKernelGGL(hashgrid_bwd_owner_kernel, dim3(blocks), dim3(kOwnThreads), 0, s, xh, dl, P, p, dtable);
   return mms::check_launch(fn);
 }

@@ -273,7 +273,8 @@ __global__ __launch_bounds__(256) void composite_bwd_kernel(const float* __restr
     if (lane < S) {
       if (dvals) dvals[i * lddv + c] = g * wi;
       gw += g * vals[i * ldv + c];
-      if (bg) gw -= g * bg[orow * C + c];
+      // (a padding ray's orow is nout, one row past bg: no read -- its gradients are zero)
+      if (bg && live) gw -= g * bg[orow * C + c];
     }
     if (lane == 0 && bg && dbg && live) dbg[orow * C + c] = g * (1.0f - acc);  // hit rows: overwrite the pass-through dout
   }

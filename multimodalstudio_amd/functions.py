@@ -376,25 +376,11 @@ def sdf_panel(pos: torch.Tensor, ldp: int, M: int, ntaps: int, delta: float, g: 
 # position gradients + the gather-style mms_hashgrid_dpos_grouped cost the same as the walk computing both).
 # HASH_SPLIT = True (tests only) routes the position gradient through the gather kernel.
 HASH_SPLIT = False
-# groups (1: plain, 5: the SDF [centre | 4 taps] batch) whose TABLE gradient is made by ownership
-# (mms_hashgrid_bwd_owner: workgroup (level, chunk) scans every point and adds its chunk once -- no global atomics),
-# the position gradient then by the gather kernel (mms_hashgrid_dpos_grouped)
-HASH_OWNER = frozenset()
 
 
 def grid_bwd(g: GridCfg, pos, ldx, M, table, active, dout: torch.Tensor, col: int, dtable, dpos, group: int = 1):
     """Table / position gradients; group=5 for the [centre | 4 taps] SDF batch (M = 5 x centres)."""
     Mg = M // group
-    if dtable is not None and group in HASH_OWNER:
-        ws = torch.empty(M * (4 + 2 * g.L), device=dtable.device)
-        _lib.call("mms_hashgrid_bwd_owner", pos.data_ptr(), Mg, group, Mg, ldx, table.data_ptr(), g.L, g.log2T, g.F,
-                  g.interp, g.scales_ptr, g.radius, active, dout.data_ptr() + 4 * col, dout.stride(0),
-                  dtable.data_ptr(), ws.data_ptr(), ws.numel(), _s())
-        if dpos is not None:
-            _lib.call("mms_hashgrid_dpos_grouped", pos.data_ptr(), Mg, group, Mg, ldx, table.data_ptr(), g.L, g.log2T,
-                      g.F, g.interp, g.scales_ptr, g.radius, active, dout.data_ptr() + 4 * col, dout.stride(0),
-                      dpos.data_ptr(), dpos.stride(0), _s())
-        return
     split = HASH_SPLIT and dtable is not None and dpos is not None
     wpos = None if split else dpos
     _lib.call("mms_hashgrid_bwd_grouped", pos.data_ptr(), Mg, group, Mg, ldx, table.data_ptr(), g.L, g.log2T, g.F,
@@ -2281,8 +2267,10 @@ class HeadsCompositeFunction(torch.autograd.Function):
 def _composite_extents(tag, w, v, ldv, C, bg, R, S, idx, nout, hit, dout, dv, lddv, dw, dbg) -> None:
     """Debugging (MMS_SYNC_CALLS=1): the elements mms_composite_fwd / _bwd will touch lie inside every operand."""
     def need(name, t, n):
-        if t is not None and t.numel() < n:
-            raise RuntimeError(f"composite {tag}: {name} has {t.numel()} elements, the launch touches {n} "
+        # elements reachable from the view's first one in its storage (a strided view may reach past its numel)
+        avail = None if t is None else t.untyped_storage().nbytes() // t.element_size() - t.storage_offset()
+        if t is not None and avail < n:
+            raise RuntimeError(f"composite {tag}: {name} reaches {avail} elements, the launch touches {n} "
                                f"(R {R}, S {S}, C {C}, nout {nout}, ldv {ldv}, lddv {lddv}, shapes "
                                f"{None if t is None else tuple(t.shape)})")
     need("w", w, R * S)

@@ -83,13 +83,3 @@ def main():
 
 if __name__ == "__main__":
     main()
-    F.HASH_OWNER = frozenset({1, 5})
-    rep("owner G=5  (dtable + dpos gather)", timeit(lambda: F.grid_bwd(cfg, x, 3, 5 * M, table, L, dout, 0, dtable,
-                                                                       dpos, group=5)), 2188)
-    rep("owner G=5  (dtable only)", timeit(lambda: F.grid_bwd(cfg, x, 3, 5 * M, table, L, dout, 0, dtable, None,
-                                                              group=5)), 2188)
-    rep("owner plain 1/5 rows (dtable + dpos) x5", timeit(lambda: F.grid_bwd(cfg, x, 3, M, table, L, dout, 0, dtable,
-                                                                             dpos)) * 5, 2188)
-    rep("owner plain 1/5 rows (dtable only) x5", timeit(lambda: F.grid_bwd(cfg, x, 3, M, table, L, dout, 0, dtable,
-                                                                           None)) * 5, 2188)
-    F.HASH_OWNER = frozenset()

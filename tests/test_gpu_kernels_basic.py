@@ -38,16 +38,14 @@ def test_hashgrid_fwd_bwd(dev, log2T, active, radius):
     np.testing.assert_allclose(xd.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("split", [True, False, "owner"])
+@pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("group", [1, 5])
 def test_hashgrid_smoothstep(dev, group, split, monkeypatch):
     """interpolation "Smoothstep" (HashEncodingConfig, encodings.py:64-67; tcnn's mode, parity-unpinned): forward,
     table and position gradients of the plain and the [centre | 4 taps] kernels vs the oracle's restatement of the
     smoothstep weights, whose position gradient autograd derives (d S / dt = 6 t (1 - t))."""
     from multimodalstudio_amd import functions as F
-    monkeypatch.setattr(F, "HASH_SPLIT", split is True)    # position gradient by the gather kernel / by the table walk
-    # the table gradient by ownership (mms_hashgrid_bwd_owner) or by the walk
-    monkeypatch.setattr(F, "HASH_OWNER", frozenset({1, 5}) if split == "owner" else frozenset())
+    monkeypatch.setattr(F, "HASH_SPLIT", split)    # position gradient by the gather kernel / by the table walk
     L, Mc, log2T = 16, 1500, 14
     scales = ohg.level_scales(16, 1024, L)
     g = torch.Generator().manual_seed(11)
@@ -76,14 +74,13 @@ def test_hashgrid_smoothstep(dev, group, split, monkeypatch):
     np.testing.assert_allclose(dpos.cpu().numpy(), xr.grad.numpy(), rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("split", [True, False, "owner"])
+@pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("log2T", [12, 19])
 def test_hashgrid_bwd_grouped_taps(dev, log2T, split, monkeypatch):
     """[centre | 4 taps] batch: the grouped backward (LDS merge of shared-cell corners; position gradient by the
-    gather kernel or by the walk; or the table gradient by ownership, mms_hashgrid_bwd_owner) vs the oracle."""
+    gather kernel or by the walk) vs the oracle."""
     from multimodalstudio_amd import functions as F
-    monkeypatch.setattr(F, "HASH_SPLIT", split is True)
-    monkeypatch.setattr(F, "HASH_OWNER", frozenset({1, 5}) if split == "owner" else frozenset())
+    monkeypatch.setattr(F, "HASH_SPLIT", split)
     L, Mc, delta = 16, 2000, 2.0 / 1024 / 3 ** 0.5
     scales = ohg.level_scales(16, 2048, L)
     g = torch.Generator().manual_seed(7)
@@ -359,9 +356,11 @@ def test_small_linear(dev, C, K, act):
     rdx = dX0.double() + dz @ Wd
     rdw = 1 + dz.T @ Xd
     rdb = 1 + dz.sum(0)
-    for got, want, name in ((dX, rdx, "dX"), (dW, rdw, "dW"), (db, rdb, "db")):
+    # dW / db are sums over 70,001 rows whose per-block partials meet in float atomics (the order varies run to run):
+    # db measured 0.4-1.1e-5 of its scale, so 3e-5 for the reductions, 1e-5 for the row-local dX
+    for got, want, name, tol in ((dX, rdx, "dX", 1e-5), (dW, rdw, "dW", 3e-5), (db, rdb, "db", 3e-5)):
         e = ((got.double().cpu() - want).abs().max() / want.abs().max()).item()
-        assert e < 1e-5, f"{name}: rel err {e:.2e}"
+        assert e < tol, f"{name}: rel err {e:.2e}"
 
 
 @pytest.mark.parametrize("ntaps,M", [(4, 5000), (0, 7001), (4, 1)])
