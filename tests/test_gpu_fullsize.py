@@ -163,13 +163,11 @@ def test_fullsize_sampler_bit_exact(dev, name):
                                                  ref[:, :-1] if k == 3 else None), (m, k)
 
 
-@pytest.mark.parametrize("which", ["dynamic", "granule", "all_rays"])
-@pytest.mark.parametrize("name", FULL)
+# (cap = N, "all_rays", on the rgb fixture only: the multi-modality fixtures cover the dynamic and granule paths)
+@pytest.mark.parametrize("name,which", [(n, w) for n in FULL for w in ["dynamic", "granule"]] + [(NAME, "all_rays")])
 def test_fullsize_step_on_reference_samples(dev, name, which):
     f = load(name)
     mods = [str(m) for m in f["mods"]]
-    if which == "all_rays" and name != NAME:
-        pytest.skip("cap = N is covered on the rgb fixture")
     cap = {"dynamic": None, "granule": granule_cap(f), "all_rays": f[f"{mods[0]}:coords"].shape[0]}[which]
     case = E2ECase(f, dev, inject_bins=True)
     outs, losses, total = case.run_step(cap, batched=which != "dynamic")
