@@ -63,7 +63,12 @@ DTYPES = {"fp32": "fp32",
                        "scaled), split-bf16x3 for the SDF MLP forward, the chains' first backward layer and the weight "
                        "gradients, fp32 elsewhere",
           "fast_h16bw": "as fast_h16b with bf16 MFMA (fp32 accumulate) for the MLP weight gradients -- not the "
-                        "benchmarked preset, fp32 elsewhere"}
+                        "benchmarked preset, fp32 elsewhere",
+          "fast_h16c": "fp16 MFMA (fp32 accumulate: the reference's autocast) for the radiance / head / background MLP "
+                       "forwards, for every MLP's backward-data chain after its first layer (per-row power-of-two "
+                       "scaled) and for the hidden layers' weight gradients (fp16 dZ rows in their row scale, fp16 X in "
+                       "a per-launch scale); split-bf16x3 for the SDF MLP forward, the chains' first backward layer and "
+                       "the output layers' weight gradients, fp32 elsewhere"}
 # the benchmarked preset (tests/test_cpu_host.py::test_benchmarked_preset_* guard its numerics)
 DEFAULT_PRECISION = "fast_h16b"
 HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per lookup, forward
@@ -93,6 +98,15 @@ def gemm_grouped_work(a):
     return f"{PREC_NAMES[prec]}:TN_grouped", (flops, nbytes)
 
 
+def gemm_wide16_work(a):
+    """(label, (flops, bytes)) of one mms_gemm_tn_wide16 launch: 2 M N K flops per item; bytes = the fp16 dZ rows
+    (2 B per element + the row's 4-B inverse scale), the fp32 X rows once, dW read and written."""
+    n, M, N, K = a[0], a[1], a[2], a[3]
+    flops = sum(2.0 * M[i] * N[i] * K[i] for i in range(n))
+    nbytes = sum(2.0 * K[i] * M[i] + 4.0 * K[i] + 4.0 * K[i] * N[i] + 8.0 * M[i] * N[i] for i in range(n))
+    return "fp16:TN_grouped", (flops, nbytes)
+
+
 def chain_work(a):
     """(precision label, (algorithmic flops, algorithmic HBM bytes)) of one mms_mlp_chain launch (include/mms_hip.h
     argument order): every layer's 2MNK, narrowed on the SDF tap rows (rows >= rows_full: one output column of the
@@ -104,7 +118,10 @@ def chain_work(a):
     Np = ctypes.cast(a[20], ctypes.POINTER(ctypes.c_int))
     outs = ctypes.cast(a[18], ctypes.POINTER(ctypes.c_void_p))
     n = [Np[i] for i in range(nl)]
-    st = [outs[i] is not None for i in range(nl)]
+    # bytes per stored element: 4 (fp32), or 2 + 4 / n (a prec-6 hidden layer's fp16 dZ rows and their inverse scale)
+    rinv = ctypes.cast(a[27], ctypes.POINTER(ctypes.c_void_p)) if len(a) > 27 and a[27] else None
+    st = [0.0 if outs[i] is None else (0.5 + 1.0 / n[i] if (rinv is not None and rinv[i]) else 1.0)
+          for i in range(nl)]
     mid = sum(n[l - 1] * n[l] for l in range(1, nl - 1))
     if bwd:
         f0 = 2.0 * (rf * K0 + (M - rf)) * n[0]       # the first backward layer (B = dY from memory)
@@ -167,6 +184,7 @@ def work_fns():
         "mms_gemm": gemm_work,
         "mms_gemm_tn_grouped": gemm_grouped_work,
         "mms_gemm_tn_wide": gemm_grouped_work,
+        "mms_gemm_tn_wide16": gemm_wide16_work,
         "mms_mlp_chain": chain_work,
         "mms_hashgrid_fwd_grouped": hash_fwd_work,
         "mms_sdf_panel_fwd": sdf_panel_work,

@@ -116,6 +116,16 @@ int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const 
                      const int64_t* lda, const float* const* B, const int64_t* ldb, float* const* C,
                      const int64_t* ldc, float* const* colsum, int target_blocks, int stage_rows, float* workspace,
                      int64_t workspace_floats, void* stream);
+/* The same weight gradients on fp16 operands (fp32 accumulate: the reference GPU's fp16-autocast nn.Linear backward,
+ * trainer.py:51,57-62): A16_i = the dZ rows as mms_mlp_chain prec 6 stores them (fp16 [K_i rows][lda_i], 8-B aligned,
+ * row k scaled by 1 / ainv_i[k]), emax_i = that launch's largest biased row exponent; B_i = X fp32 (16-B rows), each
+ * row scaled by ainv_i[k] 2^(14 - e_max) <= 1 and rounded to fp16 (no overflow, the scale undone on the fp32
+ * accumulators); colsum_i[m] += sum_k A16_i[k][m] ainv_i[k].  One fp16 MFMA per product (vs three for split bf16x3)
+ * and half the dZ bytes. */
+int mms_gemm_tn_wide16(int n, const int64_t* M, const int64_t* N, const int64_t* K, const void* const* A16,
+                       const int64_t* lda, const float* const* ainv, const unsigned* const* emax, const float* const* B,
+                       const int64_t* ldb, float* const* C, const int64_t* ldc, float* const* colsum, int target_blocks,
+                       void* stream);
 
 /* ---- fused MLP chains (MLP.forward mlp.py:152-171 under weight norm :206-209, all layers in one launch) for the
  * SDF field (71-256-256-257, Softplus(100), surface_field.py:99-116), the radiance field (317-256-256-256, ReLU,
@@ -140,7 +150,12 @@ int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const 
  *   the last forward layer's
  *   weight-gradient row 0, sum over its rows >= rows_full of X[m, 0] * aux[0][m, :] (columns < N[0]), and of the bias
  *   gradient, sum of X[m, 0] (column N[0]) -- the taps' sdf column, surface_model.py:137-153 (reduce with
- *   mms_rowsum_add); NULL: not computed. 
+ *   mms_rowsum_add); NULL: not computed.
+ * prec 6 backward, hidden layers l < n_layers - 1: rinv[l] non-NULL stores out[l] as fp16 [rows][ldo] (8-B aligned,
+ *   ldo >= 32 ceil(N/32)) holding the ROW-SCALED dZ the next layer's fp16 operands are made of (each row's largest
+ *   |dZ| in [2^13, 2^14)), rinv[l][row] = the row's inverse scale 2^(e - 14), and atomically raises emax[l] to the
+ *   largest e + 1000 of its rows (emax zeroed by the caller; 0 = every row zero): the fp16 weight-gradient operands of
+ *   mms_gemm_tn_wide16.  rinv NULL (or rinv[l] NULL): fp32 dZ as before. 
  * a_hi / a_lo: per-layer packed weights from mms_mlp_pack (bf16, 32 ceil(N/32) x 16 ceil(K/16)); layers >= 1 are
  * register-fed and must be packed with permute = 1.  All row pitches multiples of 4 floats, 16-B aligned. */
 /* Rows per mms_mlp_chain block (128; 64 in a build with two blocks per CU): the tap_part row granularity. */
@@ -149,7 +164,8 @@ int mms_mlp_chain(int prec, int backward, int n_layers, const float* X, int64_t 
                   int64_t rows_full, const float* xaux, int64_t ldxaux, int xact, float* xout, int64_t ldxout,
                   const void* const* a_hi, const void* const* a_lo, const float* const* bias, const float* const* aux,
                   const int64_t* ldaux, float* const* out, const int64_t* ldo, const int* N, const int* act,
-                  float beta, float thr, const float* w2row0, float* tap_part, int64_t ld_tap, void* stream);
+                  float beta, float thr, const float* w2row0, float* tap_part, int64_t ld_tap, float* const* rinv,
+                  unsigned* emax, void* stream);
 /* bf16 (hi, and lo = residual if non-NULL) image of W [N, K] (ldw) as an MFMA A operand of rows x cols:
  * transpose = 0 -> A = W, 1 -> A = W^T; permute bit 0 stores each k-step in register-fed order (columns 0-3, 8-11,
  * 4-7, 12-15 of a 16-column step); bit 2 writes an fp16 image (hi only, fp16 bits in the 16-bit buffer:

@@ -24,10 +24,16 @@ struct ChainLayer {
   const float* bias;   // forward: [N], or null
   const float* aux;    // backward: forward output Y [rows][ldaux] whose act' scales the product, or null
   int64_t ldaux;
-  float* out;          // fp32 store [rows][ldo] of the layer result, or null
+  float* out;          // fp32 store [rows][ldo] of the layer result, or null; with rinv: fp16 store (see rinv)
   int64_t ldo;
   int N;               // valid output columns
   int act;             // forward: activation; backward: derivative taken at aux
+  // backward prec 6, hidden layers: non-null -> `out` holds the layer's dZ as fp16 [rows][ldo] in the row scale of the
+  // next layer's fp16 operands (each row's largest |dZ| in [2^13, 2^14)), rinv[row] = the inverse scale 2^(e - 14),
+  // and *emax = max over rows of e + 1000 (0: every row zero) -- the weight gradients' fp16 operands
+  // (mms_gemm_tn_wide16)
+  float* rinv;
+  unsigned* emax;
 };
 
 struct ChainArgs {

@@ -52,7 +52,7 @@ typedef short short4_ __attribute__((ext_vector_type(4)));
 typedef short short8_ __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) short4_ lds_short4;
 
-enum Prec { P_F32 = 0, P_BF16 = 1, P_BF16X3 = 2 };
+enum Prec { P_F32 = 0, P_BF16 = 1, P_BF16X3 = 2, P_F16 = 5 };   // P_F16: the wide weight-gradient kernel only
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SOFTPLUS = 2, ACT_SIGMOID = 3 };
 
 constexpr int BM = 128, BN = 128;
@@ -460,8 +460,10 @@ constexpr int kWLD = kWT + 32;      // image row pitch (elements): 576-B rows, c
 
 struct WideItem {
   int64_t M, N, K;   // C[M, N] += A^T B: A [K rows, M] (lda), B [K rows, N] (ldb)
-  const float* A;
+  const float* A;    // P_F16: fp16 rows (lda in halves), row k scaled by 1 / ainv[k]
   int64_t lda;
+  const float* ainv;       // P_F16: per-row inverse scales of A (powers of two)
+  const unsigned* emax;    // P_F16: max over rows of log2(ainv) + 14 + 1000 (0: A is all zero)
   const float* B;
   int64_t ldb;
   float* C;
@@ -484,6 +486,12 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
   constexpr int NLD = WK / 8;         // float4 loads per thread per operand and stage
   constexpr int NIMG = PREC == P_BF16X3 ? 2 : 1;
   constexpr int IMG = kWK * kWLD;                        // elements per image
+  // P_F16 (mms_gemm_tn_wide16): A = fp16 dZ rows in their row scale (1 / ainv[k]) and B = X scaled per row by
+  // ainv[k] 2^(14 - emax) <= 1 (then rounded to fp16), so each product carries the common factor 2^(14 - emax),
+  // undone on the accumulators before they are added to C; one fp16 MFMA per product, one image per operand
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+  typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   __shared__ __attribute__((aligned(16))) __bf16 lds[2][2 * NIMG * IMG];   // [buffer][A hi, (A lo), B hi, (B lo)]
   __shared__ float scs[8][kWT];                           // bias-gradient partials per wave
   int id = blockIdx.x, ii = 0;
@@ -507,6 +515,22 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
   const int vb = (int)(t.N - cb < 0 ? 0 : (t.N - cb > 4 ? 4 : t.N - cb));
   const bool do_cs = t.colsum != nullptr && n0 == 0;
   float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+  float bsc = 1.f, osc = 1.f;
+  if constexpr (PREC == P_F16) {
+    const unsigned eb = *t.emax;
+    const int emx = eb > 0u ? (int)eb - 1000 : 14;
+    bsc = __builtin_amdgcn_ldexpf(1.f, 14 - emx);
+    osc = __builtin_amdgcn_ldexpf(1.f, emx - 14);
+  }
+  // one A load: float4, or (P_F16) the 4 fp16 values' bits in .x / .y and the row's inverse scale in .z
+  auto ldA = [&](int64_t rc) {
+    if constexpr (PREC == P_F16) {
+      const uint2 hv = *reinterpret_cast<const uint2*>(reinterpret_cast<const unsigned short*>(t.A) + rc * t.lda + ca_c);
+      return make_float4(__uint_as_float(hv.x), __uint_as_float(hv.y), t.ainv[rc], 0.f);
+    } else {
+      return *reinterpret_cast<const float4*>(t.A + rc * t.lda + ca_c);
+    }
+  };
 #if MMS_WIDE_PIPE
   // two register sets: stage s + 2's loads are issued before stage s's MFMAs, and stage s + 1's image stores sit in
   // the same basic block as those MFMAs (no branch between them), so the scheduler can interleave the conversions and
@@ -525,7 +549,7 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
         rset[Q][0][i] = make_float4((float)rc, 1.f, 2.f, 3.f);
         rset[Q][1][i] = make_float4(1.f, (float)rc, 3.f, 4.f);
       } else {
-        rset[Q][0][i] = *reinterpret_cast<const float4*>(t.A + rc * t.lda + ca_c);
+        rset[Q][0][i] = ldA(rc);
         rset[Q][1][i] = *reinterpret_cast<const float4*>(t.B + rc * t.ldb + cb_c);
       }
     }
@@ -544,7 +568,7 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
         ra[i] = make_float4((float)rc, 1.f, 2.f, 3.f);
         rb[i] = make_float4(1.f, (float)rc, 3.f, 4.f);
       } else {
-        ra[i] = *reinterpret_cast<const float4*>(t.A + rc * t.lda + ca_c);
+        ra[i] = ldA(rc);
         rb[i] = *reinterpret_cast<const float4*>(t.B + rc * t.ldb + cb_c);
       }
     }
@@ -563,6 +587,25 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const bool ok = w + 8 * i < nr;
+      if constexpr (PREC == P_F16) {
+        // A: the fp16 bits as loaded (invalid columns / rows zeroed); B: scaled by the row's factor, rounded to fp16
+        const uint32_t k0 = !ok ? 0u : (va > 1 ? 0xffffffffu : (va > 0 ? 0xffffu : 0u));
+        const uint32_t k1 = !ok ? 0u : (va > 3 ? 0xffffffffu : (va > 2 ? 0xffffu : 0u));
+        const uint32_t u0 = __float_as_uint(xa[i].x) & k0, u1 = __float_as_uint(xa[i].y) & k1;
+        const float rin = xa[i].z;
+        if (do_cs) {
+          const f16x2 p0 = __builtin_bit_cast(f16x2, u0), p1 = __builtin_bit_cast(f16x2, u1);
+          cs.x += (float)p0[0] * rin; cs.y += (float)p0[1] * rin;
+          cs.z += (float)p1[0] * rin; cs.w += (float)p1[1] * rin;
+        }
+        const float4 b = mask4(xb[i], vb, ok);
+        const float f = rin * bsc;
+        const f16x4 bh = {(_Float16)(b.x * f), (_Float16)(b.y * f), (_Float16)(b.z * f), (_Float16)(b.w * f)};
+        const int off = (w + 8 * i) * kWLD + 4 * lane;
+        *reinterpret_cast<uint2*>(base + off) = make_uint2(u0, u1);
+        *reinterpret_cast<f16x4*>(base + NIMG * IMG + off) = bh;
+        continue;
+      }
       const float4 a = mask4(xa[i], va, ok), b = mask4(xb[i], vb, ok);
       if (do_cs) { cs.x += a.x; cs.y += a.y; cs.z += a.z; cs.w += a.w; }
       const int off = (w + 8 * i) * kWLD + 4 * lane;
@@ -612,6 +655,11 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
           if (!ALL && !act_j[j]) continue;
           if constexpr ((MMS_WIDE_ABLATE & 2) != 0) {
             acc[i][j][0] += (float)ah[i][0] + (float)bh[j][0];   // keeps the fragment reads live
+            continue;
+          }
+          if constexpr (PREC == P_F16) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, ah[i]),
+                                                               __builtin_bit_cast(f16x8, bh[j]), acc[i][j], 0, 0, 0);
             continue;
           }
           if constexpr (PREC == P_BF16X3) {
@@ -693,10 +741,11 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
       for (int e = 0; e < 16; ++e) {
         const int tr = tr0 + (e & 3) + 8 * (e >> 2);
         if ((MMS_WIDE_ABLATE & 1) != 0 && acc[i][j][e] != 1234.5f) continue;
+        const float v = PREC == P_F16 ? acc[i][j][e] * osc : acc[i][j][e];
         if (part != nullptr) {
-          part[tr * kWT + tc] = acc[i][j][e];    // 128-B row segments per instruction: plain, coalesced stores
+          part[tr * kWT + tc] = v;    // 128-B row segments per instruction: plain, coalesced stores
         } else if (m0 + tr < t.M && n0 + tc < t.N) {
-          atomicAdd(t.C + (m0 + tr) * t.ldc + n0 + tc, acc[i][j][e]);
+          atomicAdd(t.C + (m0 + tr) * t.ldc + n0 + tc, v);
         }
       }
     }
@@ -860,38 +909,20 @@ MMS_EXPORT int mms_gemm_tn_grouped(int prec, int n, const int64_t* M, const int6
   return mms::check_launch(fn);
 }
 
-MMS_EXPORT int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const int64_t* K,
-                                const float* const* A, const int64_t* lda, const float* const* B, const int64_t* ldb,
-                                float* const* C, const int64_t* ldc, float* const* colsum, int target_blocks,
-                                int stage_rows, float* workspace, int64_t workspace_floats, void* stream) {
-  const char* fn = "mms_gemm_tn_wide";
-  MMS_REQUIRE(stage_rows == 16 || stage_rows == 32, fn, "stage_rows must be 16 or 32");
-  MMS_REQUIRE(prec == 1 || prec == 2, fn, "prec must be 1 (bf16) or 2 (bf16x3)");
-  MMS_REQUIRE(n >= 1 && n <= kMaxTnItems, fn, "1 to 5 weight-gradient items per launch");
-  MMS_REQUIRE(M && N && K && A && lda && B && ldb && C && ldc, fn, "null argument array");
+namespace {
+
+// K slices of each item (g.it[0 .. g.n) with M, N, K set) in proportion to its share of the work, so every block
+// streams about the same rows (>= 1024 rows per slice); returns the total block count
+int64_t plan_wide(WideGroup& g, int target_blocks) {
   if (target_blocks < 1) target_blocks = 256;
   double work = 0.0;
-  for (int i = 0; i < n; ++i) {
-    MMS_REQUIRE(M[i] >= 0 && N[i] >= 0 && K[i] >= 0, fn, "negative size");
-    if (M[i] == 0 || N[i] == 0 || K[i] == 0) continue;
-    MMS_REQUIRE(A[i] && B[i] && C[i], fn, "null operand");
-    MMS_REQUIRE(aligned16(A[i]) && aligned16(B[i]) && lda[i] % 4 == 0 && ldb[i] % 4 == 0, fn,
-                "operand rows must be 16-B aligned");
-    MMS_REQUIRE(lda[i] >= M[i] && ldb[i] >= N[i], fn, "leading dimension smaller than the row");
-    work += (double)((M[i] + kWT - 1) / kWT) * ((N[i] + kWT - 1) / kWT) * (double)K[i];
-  }
-  WideGroup g{};
+  for (int i = 0; i < g.n; ++i)
+    work += (double)((g.it[i].M + kWT - 1) / kWT) * ((g.it[i].N + kWT - 1) / kWT) * (double)g.it[i].K;
   int64_t total = 0;
-  int m = 0;
-  for (int i = 0; i < n; ++i) {
-    if (M[i] == 0 || N[i] == 0 || K[i] == 0) continue;   // nothing to add
-    WideItem& t = g.it[m++];
-    t.M = M[i]; t.N = N[i]; t.K = K[i];
-    t.A = A[i]; t.lda = lda[i]; t.B = B[i]; t.ldb = ldb[i]; t.C = C[i]; t.ldc = ldc[i];
-    t.colsum = colsum ? colsum[i] : nullptr;
+  for (int i = 0; i < g.n; ++i) {
+    WideItem& t = g.it[i];
     t.mt = (int)((t.M + kWT - 1) / kWT);
     t.nt = (int)((t.N + kWT - 1) / kWT);
-    // K slices in proportion to the item's share of the work (every block streams about the same rows), >= 1024 rows
     const double share = (double)t.mt * t.nt * (double)t.K / work;
     int64_t zs = (int64_t)(share * target_blocks / (t.mt * t.nt) + 0.5);
     if (zs > t.K / 1024) zs = t.K / 1024;
@@ -903,23 +934,84 @@ MMS_EXPORT int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t
     t.blocks = t.mt * t.nt * t.zs;
     total += t.blocks;
   }
-  g.n = m;
-  if (m == 0) return 0;
-  MMS_REQUIRE(total <= INT32_MAX, fn, "grid too large");
-  hipStream_t s = mms::as_stream(stream);
+  return total;
+}
+
+template <int PREC>
+void launch_wide(WideGroup& g, int64_t total, int stage_rows, float* workspace, int64_t workspace_floats,
+                 hipStream_t s) {
   // partial tiles through the workspace when it holds them all (else float atomics into C)
   g.ws = (workspace != nullptr && workspace_floats >= total * (int64_t)(kWT * kWT)) ? workspace : nullptr;
   int all_tiles = 0;
-  for (int i = 0; i < m; ++i) all_tiles += g.it[i].mt * g.it[i].nt;
+  for (int i = 0; i < g.n; ++i) all_tiles += g.it[i].mt * g.it[i].nt;
   const dim3 grid((unsigned)total), blk(512);
-  if (stage_rows == 32) {
-    if (prec == P_BF16) hipLaunchKernelGGL((gemm_tn_wide_kernel<P_BF16, 32>), grid, blk, 0, s, g);
-    else hipLaunchKernelGGL((gemm_tn_wide_kernel<P_BF16X3, 32>), grid, blk, 0, s, g);
-  } else {
-    if (prec == P_BF16) hipLaunchKernelGGL((gemm_tn_wide_kernel<P_BF16, 16>), grid, blk, 0, s, g);
-    else hipLaunchKernelGGL((gemm_tn_wide_kernel<P_BF16X3, 16>), grid, blk, 0, s, g);
-  }
+  if (stage_rows == 32) hipLaunchKernelGGL((gemm_tn_wide_kernel<PREC, 32>), grid, blk, 0, s, g);
+  else hipLaunchKernelGGL((gemm_tn_wide_kernel<PREC, 16>), grid, blk, 0, s, g);
   if (g.ws != nullptr)
     hipLaunchKernelGGL(gemm_tn_wide_reduce_kernel, dim3(kWT * kWT / 256, all_tiles), dim3(256), 0, s, g);
+}
+
+}  // namespace
+
+MMS_EXPORT int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const int64_t* K,
+                                const float* const* A, const int64_t* lda, const float* const* B, const int64_t* ldb,
+                                float* const* C, const int64_t* ldc, float* const* colsum, int target_blocks,
+                                int stage_rows, float* workspace, int64_t workspace_floats, void* stream) {
+  const char* fn = "mms_gemm_tn_wide";
+  MMS_REQUIRE(stage_rows == 16 || stage_rows == 32, fn, "stage_rows must be 16 or 32");
+  MMS_REQUIRE(prec == 1 || prec == 2, fn, "prec must be 1 (bf16) or 2 (bf16x3)");
+  MMS_REQUIRE(n >= 1 && n <= kMaxTnItems, fn, "1 to 5 weight-gradient items per launch");
+  MMS_REQUIRE(M && N && K && A && lda && B && ldb && C && ldc, fn, "null argument array");
+  WideGroup g{};
+  int m = 0;
+  for (int i = 0; i < n; ++i) {
+    MMS_REQUIRE(M[i] >= 0 && N[i] >= 0 && K[i] >= 0, fn, "negative size");
+    if (M[i] == 0 || N[i] == 0 || K[i] == 0) continue;   // nothing to add
+    MMS_REQUIRE(A[i] && B[i] && C[i], fn, "null operand");
+    MMS_REQUIRE(aligned16(A[i]) && aligned16(B[i]) && lda[i] % 4 == 0 && ldb[i] % 4 == 0, fn,
+                "operand rows must be 16-B aligned");
+    MMS_REQUIRE(lda[i] >= M[i] && ldb[i] >= N[i], fn, "leading dimension smaller than the row");
+    WideItem& t = g.it[m++];
+    t.M = M[i]; t.N = N[i]; t.K = K[i];
+    t.A = A[i]; t.lda = lda[i]; t.B = B[i]; t.ldb = ldb[i]; t.C = C[i]; t.ldc = ldc[i];
+    t.colsum = colsum ? colsum[i] : nullptr;
+  }
+  g.n = m;
+  if (m == 0) return 0;
+  const int64_t total = plan_wide(g, target_blocks);
+  MMS_REQUIRE(total <= INT32_MAX, fn, "grid too large");
+  hipStream_t s = mms::as_stream(stream);
+  if (prec == P_BF16) launch_wide<P_BF16>(g, total, stage_rows, workspace, workspace_floats, s);
+  else launch_wide<P_BF16X3>(g, total, stage_rows, workspace, workspace_floats, s);
+  return mms::check_launch(fn);
+}
+
+MMS_EXPORT int mms_gemm_tn_wide16(int n, const int64_t* M, const int64_t* N, const int64_t* K, const void* const* A16,
+                                  const int64_t* lda, const float* const* ainv, const unsigned* const* emax,
+                                  const float* const* B, const int64_t* ldb, float* const* C, const int64_t* ldc,
+                                  float* const* colsum, int target_blocks, void* stream) {
+  const char* fn = "mms_gemm_tn_wide16";
+  MMS_REQUIRE(n >= 1 && n <= kMaxTnItems, fn, "1 to 5 weight-gradient items per launch");
+  MMS_REQUIRE(M && N && K && A16 && lda && ainv && emax && B && ldb && C && ldc, fn, "null argument array");
+  WideGroup g{};
+  int m = 0;
+  for (int i = 0; i < n; ++i) {
+    MMS_REQUIRE(M[i] >= 0 && N[i] >= 0 && K[i] >= 0, fn, "negative size");
+    if (M[i] == 0 || N[i] == 0 || K[i] == 0) continue;
+    MMS_REQUIRE(A16[i] && ainv[i] && emax[i] && B[i] && C[i], fn, "null operand");
+    MMS_REQUIRE(((uintptr_t)A16[i] & 7) == 0 && lda[i] % 4 == 0 && aligned16(B[i]) && ldb[i] % 4 == 0, fn,
+                "fp16 rows must be 8-B aligned, fp32 rows 16-B aligned");
+    MMS_REQUIRE(lda[i] >= M[i] && ldb[i] >= N[i], fn, "leading dimension smaller than the row");
+    WideItem& t = g.it[m++];
+    t.M = M[i]; t.N = N[i]; t.K = K[i];
+    t.A = reinterpret_cast<const float*>(A16[i]); t.lda = lda[i]; t.ainv = ainv[i]; t.emax = emax[i];
+    t.B = B[i]; t.ldb = ldb[i]; t.C = C[i]; t.ldc = ldc[i];
+    t.colsum = colsum ? colsum[i] : nullptr;
+  }
+  g.n = m;
+  if (m == 0) return 0;
+  const int64_t total = plan_wide(g, target_blocks);
+  MMS_REQUIRE(total <= INT32_MAX, fn, "grid too large");
+  launch_wide<P_F16>(g, total, 16, nullptr, 0, mms::as_stream(stream));
   return mms::check_launch(fn);
 }

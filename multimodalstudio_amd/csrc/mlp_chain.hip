@@ -361,6 +361,7 @@ __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const C
   // are free, so the layer's epilogue waits out the HBM latency about once instead of once per tile (one wave per
   // SIMD: no other wave hides it)
   constexpr int YA = NT < YMAX ? NT : YMAX;
+  const bool st32 = Ly.rinv == nullptr;   // fp32 dZ stored here; fp16 dZ after the row scale (store_dz16)
   f32x4 y[YA][4];
   auto load = [&](int t, f32x4* dst) {
 #pragma unroll
@@ -407,13 +408,18 @@ __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const C
         v[i] = acc[t][4 * g + i] * act_grad_out<ACT>(yv[i], beta, thr);
         acc[t][4 * g + i] = v[i];
       }
-      if constexpr (kScrRT) *reinterpret_cast<f32x4*>(scr + r * kScr + 8 * g + 4 * h) = v;
-      else ycopy[g] = v;
+      if constexpr (kScrRT) {
+        if (st32) *reinterpret_cast<f32x4*>(scr + r * kScr + 8 * g + 4 * h) = v;
+      } else {
+        ycopy[g] = v;
+      }
     }
+    if (st32) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const f32x4 v = kScrRT ? *reinterpret_cast<const f32x4*>(scr + (8 * j + (lane >> 3)) * kScr + 4 * q) : ycopy[j];
-      if constexpr ((MMS_CHAIN_EPI_ABL & 2) == 0) st_nt4(Ly.out + rows[j] * Ly.ldo + 32 * t + 4 * q, v);
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 v = kScrRT ? *reinterpret_cast<const f32x4*>(scr + (8 * j + (lane >> 3)) * kScr + 4 * q) : ycopy[j];
+        if constexpr ((MMS_CHAIN_EPI_ABL & 2) == 0) st_nt4(Ly.out + rows[j] * Ly.ldo + 32 * t + 4 * q, v);
+      }
     }
   }
   if constexpr (TAPW) {
@@ -567,8 +573,9 @@ __device__ __forceinline__ void lazy_fwd_b(int s, floatx16 (&accp)[NT], bf16x8* 
 // to [2^13, 2^14) -- fp16's 11 significant bits for every value within 2^-27 of the row maximum, no overflow -- in
 // place, before the B split; returns the inverse scale the next layer's accumulators (same data row on the lane) are
 // multiplied by (exact: powers of two).
+// eb: the row's e + 1000 (> 0), or 0 for an all-zero row -- the biased exponent store_dz16 reduces into *emax.
 template <int NT>
-__device__ __forceinline__ float row_scale(floatx16 (&acc)[NT]) {
+__device__ __forceinline__ float row_scale(floatx16 (&acc)[NT], int& eb) {
   float mx = 0.f;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
@@ -577,11 +584,45 @@ __device__ __forceinline__ float row_scale(floatx16 (&acc)[NT]) {
   mx = fmaxf(mx, __shfl_xor(mx, 32));
   int e = __builtin_amdgcn_frexp_expf(mx);  // mx < 2^e (0 for mx = 0)
   e = e < -100 ? -100 : (e > 100 ? 100 : e);
+  eb = mx > 0.f ? e + 1000 : 0;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = __builtin_amdgcn_ldexpf(acc[t][i], 14 - e);
   return __builtin_amdgcn_ldexpf(1.f, e - 14);
+}
+
+// The row-scaled dZ of a hidden layer (after row_scale: the values the next layer's fp16 B operands are made of) as
+// fp16 rows for the weight gradients (ChainLayer::rinv non-null): each tile through the wave's LDS scratch like the
+// fp32 stores (8-B pieces of 64-B row segments), the row's inverse scale, and the wave's largest biased exponent
+// into *emax (one vector atomic per wave).  Rows past M are not written.
+template <int NT>
+__device__ __forceinline__ void store_dz16(const floatx16 (&acc)[NT], const ChainLayer& Ly, int64_t m0, int64_t M,
+                                           float* scr, int lane, float inv, int eb) {
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+  const int r = lane & 31, h = lane >> 5, q = lane & 7;
+  _Float16* o16 = reinterpret_cast<_Float16*>(Ly.out);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(scr + r * kScr + 8 * g + 4 * h) =
+          f32x4{acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = 8 * j + (lane >> 3);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(scr + row * kScr + 4 * q);
+      const f16x4 hv = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+      if (m0 + row < M)
+        __builtin_nontemporal_store(hv, reinterpret_cast<f16x4*>(o16 + (m0 + row) * Ly.ldo + 32 * t + 4 * q));
+    }
+  }
+  const bool valid = m0 + r < M;
+  if (h == 0 && valid) Ly.rinv[m0 + r] = inv;
+  int e = valid ? eb : 0;
+#pragma unroll
+  for (int d = 1; d < 32; d <<= 1) e = max(e, __shfl_xor(e, d));
+  if (lane == 0 && e > 0) atomicMax(Ly.emax, (unsigned)e);
 }
 
 template <int NT>
@@ -736,7 +777,11 @@ __global__ __launch_bounds__(64 * kNW) void chain_kernel(ChainArgs a) {
     else
       epilogue_bwd_staged<NT0, A0, false, NL == 4 ? MMS_CHAIN_YAHEAD4 : MMS_CHAIN_YAHEAD>(acc0, a.L[0], m0, a.M, scr,
                                                                                         lane, a.beta, a.thr);
-    if constexpr (PREC == 6) inv1 = row_scale<NT0>(acc0);
+    if constexpr (PREC == 6) {
+      int eb;
+      inv1 = row_scale<NT0>(acc0, eb);
+      if (a.L[0].rinv != nullptr) store_dz16<NT0>(acc0, a.L[0], m0, a.M, scr, lane, inv1, eb);
+    }
     to_b<PR, NT0>(acc0, b1h, b1l);
   }
 
@@ -763,7 +808,11 @@ __global__ __launch_bounds__(64 * kNW) void chain_kernel(ChainArgs a) {
       if constexpr (PREC == 6) unscale<NT1>(accp, invp);
       epilogue_bwd_staged<NT1, A1, false, NL == 4 ? MMS_CHAIN_YAHEAD4 : MMS_CHAIN_YAHEAD>(accp, a.L[LP], m0, a.M, scr,
                                                                                         lane, a.beta, a.thr);
-      if constexpr (PREC == 6) inv2 = row_scale<NT1>(accp);
+      if constexpr (PREC == 6) {
+        int eb;
+        inv2 = row_scale<NT1>(accp, eb);
+        if (a.L[LP].rinv != nullptr) store_dz16<NT1>(accp, a.L[LP], m0, a.M, scr, lane, inv2, eb);
+      }
       to_b<PR, NT1>(accp, b2h, b2l);
     }
     floatx16 acc2[NT2];
@@ -819,7 +868,11 @@ __global__ __launch_bounds__(64 * kNW) void chain_kernel(ChainArgs a) {
     if constexpr (BWD) {
       if constexpr (PREC == 6) unscale<NT1>(acc1, inv1);
       epilogue_bwd_staged<NT1, A1, false, MMS_CHAIN_YAHEAD4>(acc1, a.L[1], m0, a.M, scr, lane, a.beta, a.thr);
-      if constexpr (PREC == 6) invm = row_scale<NT1>(acc1);
+      if constexpr (PREC == 6) {
+        int eb;
+        invm = row_scale<NT1>(acc1, eb);
+        if (a.L[1].rinv != nullptr) store_dz16<NT1>(acc1, a.L[1], m0, a.M, scr, lane, invm, eb);
+      }
       to_b<PR, NT1>(acc1, bmh, bml);
     }
     floatx16 accm[NT1];
@@ -1101,7 +1154,8 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
                              int64_t ldxout, const void* const* a_hi, const void* const* a_lo,
                              const float* const* bias, const float* const* aux, const int64_t* ldaux,
                              float* const* out, const int64_t* ldo, const int* N, const int* act, float beta,
-                             float thr, const float* w2row0, float* tap_part, int64_t ld_tap, void* stream) {
+                             float thr, const float* w2row0, float* tap_part, int64_t ld_tap, float* const* rinv,
+                             unsigned* emax, void* stream) {
   const char* fn = "mms_mlp_chain";
   MMS_REQUIRE((prec >= 1 && prec <= 3) || prec == 5 || (prec == 6 && backward), fn,
               "prec must be 1 (bf16), 2 (split bf16x3), 3 (split activations), 5 (fp16, forward chains) or 6 (backward: "
@@ -1142,10 +1196,19 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
     MMS_REQUIRE(L.aux == nullptr || (aligned16(L.aux) && L.ldaux % 4 == 0), fn, "aux rows must be 16-B aligned");
     L.out = out[l];
     L.ldo = ldo[l];
+    L.rinv = rinv ? rinv[l] : nullptr;
+    L.emax = L.rinv ? emax + l : nullptr;
+    if (L.rinv != nullptr) {
+      // fp16 dZ rows of a hidden layer (prec 6 backward): 8-B stores of whole 32-column tiles
+      MMS_REQUIRE(prec == 6 && backward && l < n_layers - 1 && emax != nullptr, fn,
+                  "fp16 dZ stores (rinv) are a prec-6 backward hidden-layer feature and need emax");
+      MMS_REQUIRE(L.out != nullptr && ((uintptr_t)L.out & 7) == 0 && L.ldo % 4 == 0 && L.ldo >= 32 * ((N[l] + 31) / 32),
+                  fn, "fp16 dZ rows must be 8-B aligned and hold whole 32-column tiles");
+    }
     // a forward whose rows all take the single-output path (rows_full = 0, the sampler's SDF queries) stores only
     // column 0 of the last layer, one scalar per row: any pitch >= 1 (a dense [M] sdf vector with ldo = 1)
     const bool col0_only = !backward && l == n_layers - 1 && a.rows_full == 0;
-    MMS_REQUIRE(L.out == nullptr || (col0_only && L.ldo >= 1) ||
+    MMS_REQUIRE(L.out == nullptr || L.rinv != nullptr || (col0_only && L.ldo >= 1) ||
                     (aligned16(L.out) && L.ldo % 4 == 0 && L.ldo >= N[l]), fn, "output rows must be 16-B aligned");
     L.N = N[l];
     L.act = act[l];

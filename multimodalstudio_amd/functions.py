@@ -27,7 +27,8 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from . import _lib
-from .hip_ops import NN, NT, TN, _splits_for, act_bwd, gemm, gemm_tn_grouped, weight_norm_bwd, weight_norm_fwd
+from .hip_ops import (NN, NT, TN, _splits_for, act_bwd, gemm, gemm_tn_grouped, gemm_tn_wide16, weight_norm_bwd,
+                      weight_norm_fwd)
 
 ACT = {None: 0, "None": 0, "ReLU": 1, "Softplus": 2, "Sigmoid": 3}
 
@@ -65,10 +66,17 @@ PRESETS["fast_h16b"] = dict(PRESETS["fast_h16"], bwd16=1)
 # NOT the benchmarked preset (its weight gradients have bf16's 8 significant bits, the reference's autocast keeps 11):
 # fast_h16b with bf16 weight gradients, priced in converged PSNR (+0.007 +- 0.085 dB vs fp32, 9 seeds) and rays/s
 PRESETS["fast_h16bw"] = dict(PRESETS["fast_h16b"], wgrad=1)
+# ... and the reference's fp16 weight gradients too: the prec-6 backward chains store each hidden layer's dZ as the
+# fp16 row-scaled values their next layer already multiplies (half the bytes of the fp32 panels), and the weight
+# gradients of those layers run one fp16 MFMA per product on them and on X rounded to fp16 in a common per-launch scale
+# (mms_gemm_tn_wide16: the autocast nn.Linear backward's operand precision, fp32 accumulation); the layers whose dZ is
+# the chain's input (the SDF / background output layers, the radiance field's last layer) stay split-bf16x3
+PRESETS["fast_h16c"] = dict(PRESETS["fast_h16b"], wgrad16=1)
 for _p in PRESETS.values():
     _p.setdefault("sdf_chain", 0)      # 0: the chain runs on the "sdf" GEMM precision
     _p.setdefault("wgrad", 0)          # 0: the weight gradients on the family's backward operand mode
     _p.setdefault("bwd16", 0)          # 1: split-bf16x3 backward-data chains run prec 6
+    _p.setdefault("wgrad16", 0)        # 1: prec-6 chains' hidden-layer weight gradients on fp16 dZ (gemm_tn_wide16)
 # NOT a parity preset: the SDF chain on bf16 weights x split activations (mms_mlp_chain prec 3, two MFMAs per product;
 # with bf16-ROUNDED weights the SDF is a different, rippled function: 56x the reference's hessian scale off on the
 # e2e fixtures and a 24x larger curvature loss over the rgb training trajectory), kept to measure what the curvature
@@ -606,7 +614,7 @@ class ChainRun:
         return hi, lo
 
     def _chain(self, backward: bool, X, K0: int, rows_full: int, packs, bias, aux, outs, Ns, acts,
-               xaux=None, xact: int = 0, xout=None, w2row0=None, tap_part=None):
+               xaux=None, xact: int = 0, xout=None, w2row0=None, tap_part=None, rinv=None, emax=None):
         prec = self.bcprec if backward else self.cprec
         n = self.L
         VP = ctypes.c_void_p * n
@@ -625,7 +633,8 @@ class ChainRun:
                   _p(xaux), 0 if xaux is None else xaux.stride(0), int(xact), _p(xout),
                   0 if xout is None else xout.stride(0), cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux),
                   cast(os_), cast(ldo), cast(ns), cast(ac), self.beta, self.thr, _p(w2row0), _p(tap_part),
-                  0 if tap_part is None else tap_part.stride(0), _s())
+                  0 if tap_part is None else tap_part.stride(0),
+                  None if rinv is None else cast(VP(*[_p(r) for r in rinv])), _p(emax), _s())
 
     def forward(self, x: torch.Tensor, keep: bool, rows_full: Optional[int] = None,
                 dense_col0: bool = False, last_out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -686,10 +695,20 @@ class ChainRun:
         packs = self.bwd_packs if self.bwd_packs is not None else self._bwd_packs(K0)
         # the scaled input's store writes 16 ceil(N/16) columns per row (zeros past N)
         dZl = _alloc(M, 32 * ((Ns[L - 1] + 31) // 32), dev)[:, :Ns[L - 1]] if acts[L - 1] != 0 else None
-        dZ = [_alloc(M, Ns[l], dev) for l in range(L - 1)]
+        order = list(range(L - 2, -1, -1))           # hidden layers, last first
+        # preset wgrad16: the hidden layers' dZ as the chain's fp16 row-scaled values (whole 32-column tiles per row),
+        # their inverse row scales and per-layer largest exponents (chain slot order), for gemm_tn_wide16
+        w16 = bool(PRECISION.get("wgrad16", 0)) and self.bcprec == 6 and min(Ns[:L - 1]) >= 128
+        rinv = emax = None
+        if w16:
+            dZ = [torch.empty(M, 32 * ((Ns[l] + 31) // 32), dtype=torch.float16, device=dev)[:, :Ns[l]]
+                  for l in range(L - 1)]
+            rinv = [torch.empty(M, device=dev) for _ in range(L - 1)]
+            emax = torch.zeros(L, dtype=torch.int32, device=dev)
+        else:
+            dZ = [_alloc(M, Ns[l], dev) for l in range(L - 1)]
         dx = dx_out if dx_out is not None else _alloc(M, K0, dev)
         dy = dy if dy.stride(1) == 1 and dy.stride(0) % 4 == 0 else _copy_aligned(dy)
-        order = list(range(L - 2, -1, -1))           # hidden layers, last first
         rf = self.rows_full
         dWs = _dw_views([self.params[3 * l + 1] for l in range(L)], dev)
         dbs = []
@@ -709,14 +728,15 @@ class ChainRun:
             tap_part = torch.empty(-(-M // B) - rf // B, n0 + 4, device=dev)
         self._chain(True, dy, Ns[L - 1], rf, packs, [None] * L, [Y[l] for l in order] + [None],
                     [dZ[l] for l in order] + [dx], [Ns[l] for l in order] + [K0], [acts[l] for l in order] + [0],
-                    xaux=Y[L - 1] if acts[L - 1] != 0 else None, xact=acts[L - 1], xout=dZl, tap_part=tap_part)
+                    xaux=Y[L - 1] if acts[L - 1] != 0 else None, xact=acts[L - 1], xout=dZl, tap_part=tap_part,
+                    rinv=None if rinv is None else [rinv[l] for l in order] + [None], emax=emax)
         if tapw:
             _lib.call("mms_rowsum_add", tap_part.data_ptr(), tap_part.shape[0], n0 + 1, tap_part.stride(0),
                       dWs[L - 1].data_ptr(), n0, dbs[L - 1].data_ptr(), _s())
         dZ = dZ + [dZl if dZl is not None else dy]
         Xin = [x] + Y[:L - 1]
         # every layer's weight gradient dW_l += dZ_l^T X_l (+ bias column sums) in ONE grouped launch
-        items, wn = [], []
+        items, items16, wn = [], [], []
         for l in range(L):
             g, v, b = self.params[3 * l: 3 * l + 3]
             N, K = v.shape
@@ -726,7 +746,11 @@ class ChainRun:
             dW = dWs[l]
             db = dbs[l]
             A, B = dZ[l], Xin[l]
-            if l == L - 1 and rf < M:
+            if w16 and l < L - 1:
+                c = order.index(l)                   # the layer's chain slot (rinv / emax)
+                B = B if (B.data_ptr() % 16 == 0 and B.stride(0) % 4 == 0 and B.stride(1) == 1) else _copy_aligned(B)
+                items16.append((N, K, M, A, rinv[l], emax[c:c + 1], B, dW, db))
+            elif l == L - 1 and rf < M:
                 # rows past rows_full carry only the output column 0 (summed by the chain above when tapw)
                 items.append((N, K, rf, A, B, dW, db))
                 if not tapw:
@@ -734,14 +758,20 @@ class ChainRun:
             else:
                 items.append((N, K, M, A, B, dW, db))
             wn.append((g, v, l, dW, gt, vt, N, K))
-        if items:
+        if items or items16:
             wp = PRECISION.get("wgrad", 0) or self.prec     # the weight gradients' operand mode (preset "wgrad")
+
+            def launch(items=items, items16=items16, prec=wp):
+                if items16:
+                    gemm_tn_wide16(items16)
+                if items:
+                    gemm_tn_grouped(items, prec)
             if _WGRAD_DEFER[0] is not None:
-                _wgrad(lambda items=items, prec=wp: gemm_tn_grouped(items, prec))
-            elif ASYNC_WGRAD and _WN_BWD[0] is not None:
+                _wgrad(launch)
+            elif ASYNC_WGRAD and _WN_BWD[0] is not None and not items16:
                 _wgrad_async(items, wp, dev)
             else:
-                gemm_tn_grouped(items, wp)
+                launch()
         for g, v, l, dW, gt, vt, N, K in wn:
             _wn_bwd(g.reshape(-1), v, self.norms[l], dW, gt.reshape(-1) if gt is not None else
                     torch.zeros(N, device=dev), vt if vt is not None else torch.zeros(N, K, device=dev))

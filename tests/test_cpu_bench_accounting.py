@@ -10,14 +10,19 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 
-def _chain_args(prec, bwd, Ns, K0, M, rows_full, stored):
-    """mms_mlp_chain's positional arguments (include/mms_hip.h), pointers as truthy placeholders."""
+def _chain_args(prec, bwd, Ns, K0, M, rows_full, stored, fp16=None):
+    """mms_mlp_chain's positional arguments (include/mms_hip.h), pointers as truthy placeholders; ``fp16``: per layer,
+    whether its out is a prec-6 fp16 dZ store (rinv[l] set)."""
     n = len(Ns)
     outs = (ctypes.c_void_p * n)(*[(1 if s else None) for s in stored])
     ns = (ctypes.c_int * n)(*Ns)
+    rinv = None if fp16 is None else (ctypes.c_void_p * n)(*[(1 if f else None) for f in fp16])
     a = [prec, bwd, n, 1, K0, K0, M, rows_full] + [None] * 10 + [ctypes.cast(outs, ctypes.c_void_p).value, None,
                                                                  ctypes.cast(ns, ctypes.c_void_p).value]
-    return a, (outs, ns)
+    a += [None] * 6 + [None if rinv is None else ctypes.cast(rinv, ctypes.c_void_p).value, None if fp16 is None else 1,
+                       None]
+    assert len(a) == 30       # ... tap_part, ld_tap, rinv, emax, stream
+    return a, (outs, ns, rinv)
 
 
 @pytest.mark.parametrize("prec,label", [(2, "bf16x3"), (5, "fp16"), (6, "fp16-rowscaled")])
@@ -54,3 +59,24 @@ def test_rowscaled_mode_peak_is_priced_per_layer():
     r = recs[0]
     assert abs(r["mode_peak"] - bench.BF16_MFMA_PEAK_TF * 3 / 5) < 0.1      # 3 equal layers: 1/(3/3 + 1/3 + 1/3)
     assert r["frac_of_mode_peak"] > r["frac"]
+
+
+def test_fp16_dz_stores_and_wide16_bytes():
+    """Preset fast_h16c: a prec-6 backward chain's fp16 hidden-layer dZ stores count 2 B per element + the row's 4-B
+    inverse scale; mms_gemm_tn_wide16 counts its fp16 A rows the same way and fp32 X."""
+    M = 4096
+    a32, k32 = _chain_args(6, 1, [256, 256, 71], 257, M, M, [True, True, True])
+    a16, k16 = _chain_args(6, 1, [256, 256, 71], 257, M, M, [True, True, True], fp16=[True, True, False])
+    _, (f32, b32, _) = bench.chain_work(a32)
+    _, (f16, b16, _) = bench.chain_work(a16)
+    assert f16 == f32
+    assert b32 - b16 == 2 * (M * 256 * 2.0 - M * 4.0)
+    n = 2
+    I64 = ctypes.c_int64 * n
+    w = [n, I64(256, 256), I64(71, 256), I64(M, M)] + [None] * 11
+    name, (flops, nbytes) = bench.gemm_wide16_work(w)
+    assert name == "fp16:TN_grouped"
+    assert flops == 2.0 * M * (256 * 71 + 256 * 256)
+    assert nbytes == sum(2.0 * M * 256 + 4.0 * M + 4.0 * M * k + 8.0 * 256 * k for k in (71, 256))
+    rec = bench.kernel_records({"mms_gemm_tn_wide16:" + name: (1, 0.1, (flops, nbytes))}, 1, "fast_h16c")[0]
+    assert rec["peak"] == bench.BF16_MFMA_PEAK_TF

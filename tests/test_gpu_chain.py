@@ -396,10 +396,13 @@ def test_chain_fp16_forward(dev, dims, acts):
     ([39, 256, 256, 256, 256], [(1, 1.0, 20.0)] * 4, 3000, None),                  # background base
     ([283, 256, 256, 256, 128], [(1, 1.0, 20.0)] * 4, 3000, None)],                # background head
     ids=["sdf", "sdf_taps", "radiance", "head", "pol_head", "bg_base", "bg_head"])
-def test_chain_fp16_backward(dev, dims, acts, M, rows_full):
+@pytest.mark.parametrize("w16", [0, 1], ids=["wgrad_x3", "wgrad16"])
+def test_chain_fp16_backward(dev, dims, acts, M, rows_full, w16):
     """Preset fast_h16b: every backward-data chain on mms_mlp_chain prec 6 -- its first layer (B = dY from memory)
     split-bf16x3, the register-fed layers on fp16 operands with a per-row power-of-two scale (the reference GPU's fp16
-    autocast backward, without its global loss scale).  dX and every parameter gradient vs the fp64 backward taken at
+    autocast backward, without its global loss scale); w16 (preset fast_h16c): the hidden layers' weight gradients
+    from the chain's fp16 row-scaled dZ stores (mms_gemm_tn_wide16; the 64-wide heads keep the fp32 panels).  dX and
+    every parameter gradient vs the fp64 backward taken at
     the kernel's own forward activations within 3e-3 of each tensor's scale (fp16's 11-bit operands over K <= 256;
     split-bf16x3 measures ~1e-5 here), finite everywhere; rows of very different magnitude (1e-6 .. 1e3 in dY) keep
     that relative accuracy per row (the row scale), and the tap rows read only column 0."""
@@ -415,6 +418,7 @@ def test_chain_fp16_backward(dev, dims, acts, M, rows_full):
     prec = 2 if sdf else 5
     old = dict(fx.PRECISION)
     fx.PRECISION["bwd16"] = 1
+    fx.PRECISION["wgrad16"] = w16
     try:
         run = fx.ChainRun(params, acts, prec)
         assert run.bcprec == 6
@@ -503,7 +507,7 @@ def _autocast_sdf_backward(x, params, acts, Y, dyr):
 
 @pytest.mark.parametrize("delta", [1e-3, 2.5e-4])
 def test_sdf_backward_fp16_on_antisymmetric_taps(dev, delta):
-    """preset fast_h16b runs the SDF backward-data chain on prec 6 (fp16 register-fed layers with a per-row
+    """presets fast_h16b / fast_h16c run the SDF backward-data chain on prec 6 (fp16 register-fed layers with a per-row
     scale).  The SDF's real dY is not random per row: the eikonal loss puts k_t . g / (4 delta) on the 4 tap rows of a
     sample and the curvature loss c / (2 delta^2) on each tap and -2 c / delta^2 on the centre
     (/root/reference/src/model_components/surface_model.py:137-151), and the tap rows' inputs differ from the centre's
@@ -533,9 +537,10 @@ def test_sdf_backward_fp16_on_antisymmetric_taps(dev, delta):
     dyr[C:, 1:] = 0.0
     dy[C:, 1:] = float("nan")                # never read
     errs = {}
-    for name, bwd16 in (("x3", 0), ("prec6", 1)):
+    for name, bwd16, w16 in (("x3", 0, 0), ("prec6", 1, 0), ("prec6w16", 1, 1)):
         old = dict(fx.PRECISION)
         fx.PRECISION["bwd16"] = bwd16
+        fx.PRECISION["wgrad16"] = w16
         try:
             for p in params:
                 p.grad = None
@@ -559,6 +564,7 @@ def test_sdf_backward_fp16_on_antisymmetric_taps(dev, delta):
     errs["autocast"] = e
     for q in errs["x3"]:
         print(f"  delta {delta:.1e} {q:4s} x3 {errs['x3'][q]:.2e}  prec6 {errs['prec6'][q]:.2e}  "
-              f"ref-fp16-autocast {errs['autocast'][q]:.2e}")
-    for q, v in errs["prec6"].items():
-        assert np.isfinite(v) and v <= 2.0 * errs["autocast"][q] + 1e-6, (q, v, errs["autocast"][q])
+              f"prec6 + fp16 wgrad {errs['prec6w16'][q]:.2e}  ref-fp16-autocast {errs['autocast'][q]:.2e}")
+    for mode in ("prec6", "prec6w16"):
+        for q, v in errs[mode].items():
+            assert np.isfinite(v) and v <= 2.0 * errs["autocast"][q] + 1e-6, (mode, q, v, errs["autocast"][q])

@@ -318,6 +318,63 @@ def test_gemm_tn_grouped(dev, prec, tol, engine, ws, monkeypatch):
     assert err < tol, f"unaligned item prec={prec}: rel err {err:.2e}"
 
 
+def _rowscaled16(dZ: torch.Tensor):
+    """dZ [rows, N] fp32 -> (fp16 [rows, 32 ceil(N/32)] row-scaled values, rinv [rows], emax) as the prec-6 backward chain
+    stores them (mms_mlp_chain with rinv): each row's largest |dZ| brought to [2^13, 2^14)."""
+    mx = dZ.abs().amax(1)
+    e = torch.frexp(mx)[1].clamp(-100, 100)           # mx < 2^e
+    e = torch.where(mx > 0, e, torch.zeros_like(e))
+    h = torch.zeros(dZ.shape[0], 32 * ((dZ.shape[1] + 31) // 32), dtype=torch.float16)
+    h[:, :dZ.shape[1]] = torch.ldexp(dZ.double(), (14 - e)[:, None].double()).half()
+    rinv = torch.ldexp(torch.ones(dZ.shape[0], dtype=torch.float64), (e - 14).double()).float()
+    eb = int((e[mx > 0] + 1000).max()) if bool((mx > 0).any()) else 0
+    return h, rinv, eb
+
+
+def test_gemm_tn_wide16(dev):
+    """mms_gemm_tn_wide16 (preset fast_h16c's hidden-layer weight gradients): fp16 dZ rows in their row scale x fp32 X
+    rounded to fp16 in the launch's common scale, fp32 accumulation, vs fp64 of EXACTLY those fp16 operands (the
+    scaling and the MFMA path: fp32 accumulation, 3e-5) and vs the fp32 operands (fp16's operand precision: 3e-3); ragged
+    widths (257 outputs, 317 inputs, the SDF input layer's 71), rows of very different magnitude (1e-6 .. 1e3), an
+    all-zero item (emax 0), the bias column sums."""
+    from multimodalstudio_amd import hip_ops
+    g = torch.Generator().manual_seed(16)
+    specs = [(256, 71, 30011), (256, 256, 20000), (257, 256, 9000), (130, 317, 12000), (256, 256, 5000)]
+    items, refs = [], []
+    for i, (N, K, M) in enumerate(specs):
+        dZ = torch.randn(M, N, generator=g) * 10.0 ** torch.randint(-6, 4, (M, 1), generator=g).float()
+        if i == 4:
+            dZ.zero_()
+        X = torch.randn(M, K, generator=g) * 3.0
+        h, rinv, eb = _rowscaled16(dZ)
+        em = torch.tensor([eb], dtype=torch.int32, device=dev)
+        Xd = torch.zeros(M, (K + 3) // 4 * 4, device=dev)[:, :K]
+        Xd.copy_(X.to(dev))
+        dW = torch.zeros(N, K, device=dev)
+        db = torch.zeros(N, device=dev)
+        items.append((N, K, M, h.to(dev)[:, :N], rinv.to(dev), em, Xd, dW, db))
+        # the kernel's operands exactly: A = h * rinv, B = fp16(X 2^(e_r - e_max)) 2^(e_max - e_r)
+        A = h[:, :N].double() * rinv.double()[:, None]
+        if eb > 0:
+            f = rinv.double() * 2.0 ** (14 - (eb - 1000))
+            Bq = (X.double() * f[:, None]).float().half().double() / f[:, None]
+        else:
+            Bq = X.double()
+        refs.append((A.T @ Bq, A.sum(0), dZ.double().T @ X.double()))
+    hip_ops.gemm_tn_wide16(items)
+    torch.cuda.synchronize()
+    for (N, K, M, *_, dW, db), (rq, rb, rt) in zip(items, refs):
+        got = dW.cpu().double()
+        if rt.abs().max() == 0:
+            assert got.abs().max() == 0 and db.abs().max() == 0
+            continue
+        eq = ((got - rq).abs().max() / rq.abs().max()).item()
+        et = ((got - rt).abs().max() / rt.abs().max()).item()
+        eb_ = ((db.cpu().double() - rb).abs().max() / rb.abs().max()).item()
+        print(f"wide16 {N}x{K} rows {M}: vs fp16 operands {eq:.1e}, vs fp32 {et:.1e}, db {eb_:.1e}")
+        assert eq < 3e-5 and et < 3e-3 and eb_ < 1e-5, (N, K, eq, et, eb_)
+
+
 @pytest.mark.parametrize("C,K,act", [(1, 256, 2), (9, 128, 3), (3, 128, 0), (4, 512, 1), (1, 128, 3), (5, 256, 0)])
 def test_small_linear(dev, C, K, act):
     """mms_small_linear_fwd / _bwd (the background density head and 1-layer modality heads) vs fp64: a column view of
