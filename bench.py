@@ -99,11 +99,19 @@ def gemm_grouped_work(a):
 
 
 def gemm_wide16_work(a):
-    """(label, (flops, bytes)) of one mms_gemm_tn_wide16 launch: 2 M N K flops per item; bytes = the fp16 dZ rows
-    (2 B per element + the row's 4-B inverse scale), the fp32 X rows once, dW read and written."""
+    """(label, (flops, bytes)) of one mms_gemm_tn_wide16 launch (one MLP's weight gradients, items of mixed operand
+    modes): 2 M N K flops per item; bytes = the dZ rows (fp16: 2 B per element + the row's 4-B inverse scale; fp32: 4 B),
+    the X rows (2 or 4 B per element) once, dW read and written."""
+    import ctypes
     n, M, N, K = a[0], a[1], a[2], a[3]
+    ainv = ctypes.cast(a[6], ctypes.POINTER(ctypes.c_void_p)) if a[6] else None
+    b16 = ctypes.cast(a[10], ctypes.POINTER(ctypes.c_int)) if a[10] else None
     flops = sum(2.0 * M[i] * N[i] * K[i] for i in range(n))
-    nbytes = sum(2.0 * K[i] * M[i] + 4.0 * K[i] + 4.0 * K[i] * N[i] + 8.0 * M[i] * N[i] for i in range(n))
+    nbytes = 0.0
+    for i in range(n):
+        a16 = ainv is not None and bool(ainv[i])
+        nbytes += (2.0 * M[i] + 4.0 if a16 else 4.0 * M[i]) * K[i] + (2.0 if (b16 is not None and b16[i]) else 4.0) * \
+            K[i] * N[i] + 8.0 * M[i] * N[i]
     return "fp16:TN_grouped", (flops, nbytes)
 
 
@@ -215,7 +223,7 @@ def kernel_records(summ, timing_steps: int, precision: str):
             if mode in ("bf16x3", "bf16x2"):
                 rec.update({"mode_peak": round(MFMA_PEAK_TF[mode], 1),
                             "frac_of_mode_peak": round(ach / MFMA_PEAK_TF[mode], 4)})
-            elif mode == "fp16-rowscaled" and len(work) > 2:
+            elif mode == "fp16-rowscaled" and len(work) > 2 and work[2] > 0:
                 # priced per layer: the split-bf16x3 first layer at a third of the peak, the fp16 layers at the peak
                 mp = BF16_MFMA_PEAK_TF * flops / work[2]
                 rec.update({"mode_peak": round(mp, 1), "frac_of_mode_peak": round(ach / mp, 4)})

@@ -116,16 +116,19 @@ int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const 
                      const int64_t* lda, const float* const* B, const int64_t* ldb, float* const* C,
                      const int64_t* ldc, float* const* colsum, int target_blocks, int stage_rows, float* workspace,
                      int64_t workspace_floats, void* stream);
-/* The same weight gradients on fp16 operands (fp32 accumulate: the reference GPU's fp16-autocast nn.Linear backward,
- * trainer.py:51,57-62): A16_i = the dZ rows as mms_mlp_chain prec 6 stores them (fp16 [K_i rows][lda_i], 8-B aligned,
- * row k scaled by 1 / ainv_i[k]), emax_i = that launch's largest biased row exponent; B_i = X fp32 (16-B rows), each
- * row scaled by ainv_i[k] 2^(14 - e_max) <= 1 and rounded to fp16 (no overflow, the scale undone on the fp32
- * accumulators); colsum_i[m] += sum_k A16_i[k][m] ainv_i[k].  One fp16 MFMA per product (vs three for split bf16x3)
- * and half the dZ bytes. */
-int mms_gemm_tn_wide16(int n, const int64_t* M, const int64_t* N, const int64_t* K, const void* const* A16,
-                       const int64_t* lda, const float* const* ainv, const unsigned* const* emax, const float* const* B,
-                       const int64_t* ldb, float* const* C, const int64_t* ldc, float* const* colsum, int target_blocks,
-                       void* stream);
+/* The same weight gradients with fp16 operands where the producers stored them (preset fast_h16c; fp32 accumulate: the
+ * reference GPU's fp16-autocast nn.Linear backward, trainer.py:51,57-62), items of mixed modes in ONE launch:
+ *  - ainv[i] non-NULL: A_i = the dZ rows as mms_mlp_chain prec 6 stores them (fp16 [K_i rows][lda_i], 8-B aligned, row
+ *    k scaled by 1 / ainv_i[k]; ainv 0 for an all-zero row), emax[i] = that launch's largest biased row exponent; B_i
+ *    rows scaled by ainv_i[k] 2^(14 - e_max) <= 1 and rounded to fp16 (the scale undone on the fp32 accumulators): one
+ *    fp16 MFMA per product;
+ *  - ainv NULL (or ainv[i] NULL): A_i fp32 rows (16-B aligned), split bf16x3 as mms_gemm_tn_wide;
+ *  - b16[i] non-zero: B_i holds fp16 rows (8-B aligned, ldb in halves), else fp32 rows (16-B aligned).
+ * colsum_i[m] += sum_k dZ_i[k][m] (the bias gradient). */
+int mms_gemm_tn_wide16(int n, const int64_t* M, const int64_t* N, const int64_t* K, const void* const* A,
+                       const int64_t* lda, const float* const* ainv, const unsigned* const* emax, const void* const* B,
+                       const int64_t* ldb, const int* b16, float* const* C, const int64_t* ldc, float* const* colsum,
+                       int target_blocks, void* stream);
 
 /* ---- fused MLP chains (MLP.forward mlp.py:152-171 under weight norm :206-209, all layers in one launch) for the
  * SDF field (71-256-256-257, Softplus(100), surface_field.py:99-116), the radiance field (317-256-256-256, ReLU,
@@ -153,7 +156,8 @@ int mms_gemm_tn_wide16(int n, const int64_t* M, const int64_t* N, const int64_t*
  *   mms_rowsum_add); NULL: not computed.
  * prec 6 backward, hidden layers l < n_layers - 1: rinv[l] non-NULL stores out[l] as fp16 [rows][ldo] (8-B aligned,
  *   ldo >= 32 ceil(N/32)) holding the ROW-SCALED dZ the next layer's fp16 operands are made of (each row's largest
- *   |dZ| in [2^13, 2^14)), rinv[l][row] = the row's inverse scale 2^(e - 14), and atomically raises emax[l] to the
+ *   |dZ| in [2^13, 2^14)), rinv[l][row] = the row's inverse scale 2^(e - 14) (0 for an all-zero row), and
+ *   atomically raises emax[l] to the
  *   largest e + 1000 of its rows (emax zeroed by the caller; 0 = every row zero): the fp16 weight-gradient operands of
  *   mms_gemm_tn_wide16.  rinv NULL (or rinv[l] NULL): fp32 dZ as before. 
  * a_hi / a_lo: per-layer packed weights from mms_mlp_pack (bf16, 32 ceil(N/32) x 16 ceil(K/16)); layers >= 1 are

@@ -29,9 +29,9 @@ struct ChainLayer {
   int N;               // valid output columns
   int act;             // forward: activation; backward: derivative taken at aux
   // backward prec 6, hidden layers: non-null -> `out` holds the layer's dZ as fp16 [rows][ldo] in the row scale of the
-  // next layer's fp16 operands (each row's largest |dZ| in [2^13, 2^14)), rinv[row] = the inverse scale 2^(e - 14),
-  // and *emax = max over rows of e + 1000 (0: every row zero) -- the weight gradients' fp16 operands
-  // (mms_gemm_tn_wide16)
+  // next layer's fp16 operands (each row's largest |dZ| in [2^13, 2^14)), rinv[row] = the inverse scale 2^(e - 14)
+  // (0 for an all-zero row), and *emax = max over rows of e + 1000 (0: every row zero) -- the weight gradients' fp16
+  // operands (mms_gemm_tn_wide16)
   float* rinv;
   unsigned* emax;
 };

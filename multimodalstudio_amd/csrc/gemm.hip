@@ -464,8 +464,9 @@ struct WideItem {
   int64_t lda;
   const float* ainv;       // P_F16: per-row inverse scales of A (powers of two)
   const unsigned* emax;    // P_F16: max over rows of log2(ainv) + 14 + 1000 (0: A is all zero)
-  const float* B;
+  const float* B;    // fp32 rows, or (b16) fp16 rows (ldb in halves, 8-B aligned)
   int64_t ldb;
+  int b16;
   float* C;
   int64_t ldc;
   float* colsum;
@@ -480,8 +481,12 @@ struct WideGroup {
                      // instead of adding it to C with float atomics
 };
 
-template <int PREC, int WK>
-__global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
+// One block's tile and K slice of item t.  PREC: the item's operand mode (P_BF16 / P_BF16X3: fp32 A rows; P_F16: fp16
+// A rows, see WideItem); B16: fp16 B rows (their values widened exactly, then split or scaled like fp32 rows).  lds:
+// the kernel's image buffers, scs: [8][256] floats.
+template <int PREC, int WK, bool B16>
+__device__ __forceinline__ void wide_block(const WideItem& t, int id, float* part, __bf16 (*lds)[4 * WK * kWLD],
+                                           float (*scs)[kWT]) {
   constexpr int kWK = WK;             // rows per stage (16 or 32)
   constexpr int NLD = WK / 8;         // float4 loads per thread per operand and stage
   constexpr int NIMG = PREC == P_BF16X3 ? 2 : 1;
@@ -492,14 +497,6 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
   typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2][2 * NIMG * IMG];   // [buffer][A hi, (A lo), B hi, (B lo)]
-  __shared__ float scs[8][kWT];                           // bias-gradient partials per wave
-  int id = blockIdx.x, ii = 0;
-  while (ii + 1 < g.n && id >= g.it[ii].blocks) {
-    id -= g.it[ii].blocks;
-    ++ii;
-  }
-  const WideItem& t = g.it[ii];
   const int tiles = t.mt * t.nt;
   const int tile = id % tiles, slice = id / tiles;
   const int64_t m0 = (int64_t)(tile % t.mt) * kWT, n0 = (int64_t)(tile / t.mt) * kWT;
@@ -522,6 +519,25 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
     bsc = __builtin_amdgcn_ldexpf(1.f, 14 - emx);
     osc = __builtin_amdgcn_ldexpf(1.f, emx - 14);
   }
+  // one B load: float4, or (B16) the 4 fp16 values' bits in .x / .y
+  auto ldB = [&](int64_t rc) {
+    if constexpr (B16) {
+      const uint2 hv = *reinterpret_cast<const uint2*>(reinterpret_cast<const unsigned short*>(t.B) + rc * t.ldb + cb_c);
+      return make_float4(__uint_as_float(hv.x), __uint_as_float(hv.y), 0.f, 0.f);
+    } else {
+      return *reinterpret_cast<const float4*>(t.B + rc * t.ldb + cb_c);
+    }
+  };
+  // B16 rows widened to float4 (exact)
+  auto widenB = [](float4 v) {
+    if constexpr (B16) {
+      const f16x2 p0 = __builtin_bit_cast(f16x2, __float_as_uint(v.x));
+      const f16x2 p1 = __builtin_bit_cast(f16x2, __float_as_uint(v.y));
+      return make_float4((float)p0[0], (float)p0[1], (float)p1[0], (float)p1[1]);
+    } else {
+      return v;
+    }
+  };
   // one A load: float4, or (P_F16) the 4 fp16 values' bits in .x / .y and the row's inverse scale in .z
   auto ldA = [&](int64_t rc) {
     if constexpr (PREC == P_F16) {
@@ -550,7 +566,7 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
         rset[Q][1][i] = make_float4(1.f, (float)rc, 3.f, 4.f);
       } else {
         rset[Q][0][i] = ldA(rc);
-        rset[Q][1][i] = *reinterpret_cast<const float4*>(t.B + rc * t.ldb + cb_c);
+        rset[Q][1][i] = ldB(rc);
       }
     }
   };
@@ -569,7 +585,7 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
         rb[i] = make_float4(1.f, (float)rc, 3.f, 4.f);
       } else {
         ra[i] = ldA(rc);
-        rb[i] = *reinterpret_cast<const float4*>(t.B + rc * t.ldb + cb_c);
+        rb[i] = ldB(rc);
       }
     }
   };
@@ -598,7 +614,7 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
           cs.x += (float)p0[0] * rin; cs.y += (float)p0[1] * rin;
           cs.z += (float)p1[0] * rin; cs.w += (float)p1[1] * rin;
         }
-        const float4 b = mask4(xb[i], vb, ok);
+        const float4 b = mask4(widenB(xb[i]), vb, ok);
         const float f = rin * bsc;
         const f16x4 bh = {(_Float16)(b.x * f), (_Float16)(b.y * f), (_Float16)(b.z * f), (_Float16)(b.w * f)};
         const int off = (w + 8 * i) * kWLD + 4 * lane;
@@ -606,7 +622,7 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
         *reinterpret_cast<f16x4*>(base + NIMG * IMG + off) = bh;
         continue;
       }
-      const float4 a = mask4(xa[i], va, ok), b = mask4(xb[i], vb, ok);
+      const float4 a = mask4(xa[i], va, ok), b = mask4(widenB(xb[i]), vb, ok);
       if (do_cs) { cs.x += a.x; cs.y += a.y; cs.z += a.z; cs.w += a.w; }
       const int off = (w + 8 * i) * kWLD + 4 * lane;
       const bf16x4 ah = cvt4(a), bh = cvt4(b);
@@ -728,7 +744,6 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
     }
   }
   // C/D map: column = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
-  float* part = g.ws != nullptr ? g.ws + (int64_t)blockIdx.x * (kWT * kWT) : nullptr;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     if (!act_i[i]) continue;
@@ -749,6 +764,32 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
         }
       }
     }
+  }
+}
+
+// P_F16 launches (mms_gemm_tn_wide16) mix modes per item: fp16 A rows (ainv set) run P_F16, fp32 A rows split bf16x3;
+// B rows fp16 or fp32 per item.  The image buffers are sized for split bf16x3 (4 images).
+template <int PREC, int WK>
+__global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2][4 * WK * kWLD];   // [buffer][A hi, (A lo), B hi, (B lo)]
+  __shared__ float scs[8][kWT];                                             // bias-gradient partials per wave
+  int id = blockIdx.x, ii = 0;
+  while (ii + 1 < g.n && id >= g.it[ii].blocks) {
+    id -= g.it[ii].blocks;
+    ++ii;
+  }
+  const WideItem& t = g.it[ii];
+  float* part = g.ws != nullptr ? g.ws + (int64_t)blockIdx.x * (kWT * kWT) : nullptr;
+  if constexpr (PREC == P_F16) {
+    if (t.ainv != nullptr) {
+      if (t.b16) wide_block<P_F16, WK, true>(t, id, part, lds, scs);
+      else wide_block<P_F16, WK, false>(t, id, part, lds, scs);
+    } else {
+      if (t.b16) wide_block<P_BF16X3, WK, true>(t, id, part, lds, scs);
+      else wide_block<P_BF16X3, WK, false>(t, id, part, lds, scs);
+    }
+  } else {
+    wide_block<PREC, WK, false>(t, id, part, lds, scs);
   }
 }
 
@@ -911,19 +952,23 @@ MMS_EXPORT int mms_gemm_tn_grouped(int prec, int n, const int64_t* M, const int6
 
 namespace {
 
-// K slices of each item (g.it[0 .. g.n) with M, N, K set) in proportion to its share of the work, so every block
-// streams about the same rows (>= 1024 rows per slice); returns the total block count
+// K slices of each item (g.it[0 .. g.n) with M, N, K set) in proportion to its share of the work -- tiles x rows x the
+// operand bytes per row element (the kernel streams its operands from HBM) -- so every block takes about the same time
+// (>= 1024 rows per slice); returns the total block count
 int64_t plan_wide(WideGroup& g, int target_blocks) {
   if (target_blocks < 1) target_blocks = 256;
+  auto cost = [](const WideItem& t) {
+    return (double)((t.M + kWT - 1) / kWT) * ((t.N + kWT - 1) / kWT) * (double)t.K *
+           ((t.ainv ? 2.0 : 4.0) + (t.b16 ? 2.0 : 4.0));
+  };
   double work = 0.0;
-  for (int i = 0; i < g.n; ++i)
-    work += (double)((g.it[i].M + kWT - 1) / kWT) * ((g.it[i].N + kWT - 1) / kWT) * (double)g.it[i].K;
+  for (int i = 0; i < g.n; ++i) work += cost(g.it[i]);
   int64_t total = 0;
   for (int i = 0; i < g.n; ++i) {
     WideItem& t = g.it[i];
     t.mt = (int)((t.M + kWT - 1) / kWT);
     t.nt = (int)((t.N + kWT - 1) / kWT);
-    const double share = (double)t.mt * t.nt * (double)t.K / work;
+    const double share = cost(t) / work;
     int64_t zs = (int64_t)(share * target_blocks / (t.mt * t.nt) + 0.5);
     if (zs > t.K / 1024) zs = t.K / 1024;
     if (zs < 1) zs = 1;
@@ -986,26 +1031,29 @@ MMS_EXPORT int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t
   return mms::check_launch(fn);
 }
 
-MMS_EXPORT int mms_gemm_tn_wide16(int n, const int64_t* M, const int64_t* N, const int64_t* K, const void* const* A16,
+MMS_EXPORT int mms_gemm_tn_wide16(int n, const int64_t* M, const int64_t* N, const int64_t* K, const void* const* A,
                                   const int64_t* lda, const float* const* ainv, const unsigned* const* emax,
-                                  const float* const* B, const int64_t* ldb, float* const* C, const int64_t* ldc,
-                                  float* const* colsum, int target_blocks, void* stream) {
+                                  const void* const* B, const int64_t* ldb, const int* b16, float* const* C,
+                                  const int64_t* ldc, float* const* colsum, int target_blocks, void* stream) {
   const char* fn = "mms_gemm_tn_wide16";
   MMS_REQUIRE(n >= 1 && n <= kMaxTnItems, fn, "1 to 5 weight-gradient items per launch");
-  MMS_REQUIRE(M && N && K && A16 && lda && ainv && emax && B && ldb && C && ldc, fn, "null argument array");
+  MMS_REQUIRE(M && N && K && A && lda && B && ldb && C && ldc, fn, "null argument array");
   WideGroup g{};
   int m = 0;
   for (int i = 0; i < n; ++i) {
     MMS_REQUIRE(M[i] >= 0 && N[i] >= 0 && K[i] >= 0, fn, "negative size");
     if (M[i] == 0 || N[i] == 0 || K[i] == 0) continue;
-    MMS_REQUIRE(A16[i] && ainv[i] && emax[i] && B[i] && C[i], fn, "null operand");
-    MMS_REQUIRE(((uintptr_t)A16[i] & 7) == 0 && lda[i] % 4 == 0 && aligned16(B[i]) && ldb[i] % 4 == 0, fn,
-                "fp16 rows must be 8-B aligned, fp32 rows 16-B aligned");
+    const bool a16 = ainv && ainv[i], bh = b16 && b16[i];
+    MMS_REQUIRE(A[i] && B[i] && C[i] && (!a16 || (emax && emax[i])), fn, "null operand");
+    MMS_REQUIRE(((uintptr_t)A[i] & (a16 ? 7 : 15)) == 0 && lda[i] % 4 == 0 && ((uintptr_t)B[i] & (bh ? 7 : 15)) == 0 &&
+                    ldb[i] % 4 == 0, fn, "fp16 rows must be 8-B aligned, fp32 rows 16-B aligned");
     MMS_REQUIRE(lda[i] >= M[i] && ldb[i] >= N[i], fn, "leading dimension smaller than the row");
     WideItem& t = g.it[m++];
     t.M = M[i]; t.N = N[i]; t.K = K[i];
-    t.A = reinterpret_cast<const float*>(A16[i]); t.lda = lda[i]; t.ainv = ainv[i]; t.emax = emax[i];
-    t.B = B[i]; t.ldb = ldb[i]; t.C = C[i]; t.ldc = ldc[i];
+    t.A = reinterpret_cast<const float*>(A[i]); t.lda = lda[i];
+    t.ainv = a16 ? ainv[i] : nullptr; t.emax = a16 ? emax[i] : nullptr;
+    t.B = reinterpret_cast<const float*>(B[i]); t.ldb = ldb[i]; t.b16 = bh ? 1 : 0;
+    t.C = C[i]; t.ldc = ldc[i];
     t.colsum = colsum ? colsum[i] : nullptr;
   }
   g.n = m;

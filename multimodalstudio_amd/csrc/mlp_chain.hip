@@ -618,7 +618,9 @@ __device__ __forceinline__ void store_dz16(const floatx16 (&acc)[NT], const Chai
     }
   }
   const bool valid = m0 + r < M;
-  if (h == 0 && valid) Ly.rinv[m0 + r] = inv;
+  // an all-zero row stores rinv 0: the weight gradients scale its X row by rinv (a zero row's row scale, 2^-14, would
+  // lift X above fp16's range in a launch whose largest exponent is negative -- e.g. fixed-capacity padding rows)
+  if (h == 0 && valid) Ly.rinv[m0 + r] = eb > 0 ? inv : 0.f;
   int e = valid ? eb : 0;
 #pragma unroll
   for (int d = 1; d < 32; d <<= 1) e = max(e, __shfl_xor(e, d));

@@ -746,10 +746,17 @@ class ChainRun:
             dW = dWs[l]
             db = dbs[l]
             A, B = dZ[l], Xin[l]
-            if w16 and l < L - 1:
-                c = order.index(l)                   # the layer's chain slot (rinv / emax)
-                B = B if (B.data_ptr() % 16 == 0 and B.stride(0) % 4 == 0 and B.stride(1) == 1) else _copy_aligned(B)
-                items16.append((N, K, M, A, rinv[l], emax[c:c + 1], B, dW, db))
+            if w16:
+                # one mixed launch: the hidden layers' fp16 dZ (chain slot c's rinv / emax), the output layer's fp32 dY
+                B = B if _aligned16(B) else _copy_aligned(B)
+                if l < L - 1:
+                    c = order.index(l)
+                    items16.append((N, K, M, A, rinv[l], emax[c:c + 1], B, dW, db))
+                else:
+                    A = A if _aligned16(A) else _copy_aligned(A)
+                    items16.append((N, K, rf if rf < M else M, A, None, None, B, dW, db))
+                    if rf < M and not tapw:
+                        items16.append((1, K, M - rf, A[rf:], None, None, B[rf:], dW, db))
             elif l == L - 1 and rf < M:
                 # rows past rows_full carry only the output column 0 (summed by the chain above when tapw)
                 items.append((N, K, rf, A, B, dW, db))
@@ -1121,6 +1128,11 @@ def acc_ret(acc: Optional[GradAcc], g):
 
 def _capturing(dev) -> bool:
     return torch.device(dev).type == "cuda" and torch.cuda.is_current_stream_capturing()
+
+
+def _aligned16(t: torch.Tensor) -> bool:
+    """16-B aligned rows of unit column stride (the wide weight-gradient engine's fp32 operands)."""
+    return t.data_ptr() % 16 == 0 and t.stride(1) == 1 and t.stride(0) % 4 == 0
 
 
 def _copy_aligned(t: torch.Tensor) -> torch.Tensor:

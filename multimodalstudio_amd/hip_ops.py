@@ -198,17 +198,23 @@ def gemm_tn_grouped(items, prec: int, target_blocks: Optional[int] = None, engin
 
 
 def gemm_tn_wide16(items, target_blocks: Optional[int] = None):
-    """items = [(N_out, K_in, rows, dZ16 [rows, >=N_out] fp16 (row-scaled, mms_mlp_chain prec 6 with rinv), rinv [rows],
-    emax (a 1-element int32 view), X [rows, >=K_in] fp32, dW [N_out, K_in], db [N_out] or None)]: dW += dZ^T X and
-    db += colsum(dZ) on fp16 operands, fp32 accumulation (mms_gemm_tn_wide16), <= 5 items per launch."""
+    """items = [(N_out, K_in, rows, dZ, rinv or None, emax or None, X, dW, db or None)] in ONE launch
+    (mms_gemm_tn_wide16): dW += dZ^T X and db += colsum(dZ).  dZ fp16 row-scaled with rinv / emax (mms_mlp_chain prec
+    6 with rinv; emax a 1-element int32 view): one fp16 MFMA per product; dZ fp32 (rinv None): split bf16x3.  X fp32 or
+    fp16 rows (its dtype).  <= 5 items."""
     n = len(items)
     I64 = ctypes.c_int64 * n
     VP = ctypes.c_void_p * n
     target = int(os.environ.get("MMS_TN_BLOCKS", "0")) or target_blocks or _WIDE_BLOCKS
     _lib.call("mms_gemm_tn_wide16", n, I64(*[it[0] for it in items]), I64(*[it[1] for it in items]),
               I64(*[it[2] for it in items]), VP(*[it[3].data_ptr() for it in items]),
-              I64(*[it[3].stride(0) for it in items]), VP(*[it[4].data_ptr() for it in items]),
-              VP(*[it[5].data_ptr() for it in items]), VP(*[it[6].data_ptr() for it in items]),
-              I64(*[it[6].stride(0) for it in items]), VP(*[it[7].data_ptr() for it in items]),
-              I64(*[it[7].stride(0) for it in items]),
-              VP(*[(it[8].data_ptr() if it[8] is not None else None) for it in items]), target, _stream())
+              I64(*[it[3].stride(0) for it in items]), VP(*[_ptr(it[4]) for it in items]),
+              VP(*[_ptr(it[5]) for it in items]), VP(*[it[6].data_ptr() for it in items]),
+              I64(*[it[6].stride(0) for it in items]),
+              (ctypes.c_int * n)(*[int(it[6].dtype == torch.float16) for it in items]),
+              VP(*[it[7].data_ptr() for it in items]), I64(*[it[7].stride(0) for it in items]),
+              VP(*[_ptr(it[8]) for it in items]), target, _stream())
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()

@@ -71,12 +71,17 @@ def test_fp16_dz_stores_and_wide16_bytes():
     _, (f16, b16, _) = bench.chain_work(a16)
     assert f16 == f32
     assert b32 - b16 == 2 * (M * 256 * 2.0 - M * 4.0)
-    n = 2
+    n = 3
     I64 = ctypes.c_int64 * n
-    w = [n, I64(256, 256), I64(71, 256), I64(M, M)] + [None] * 11
+    ainv = (ctypes.c_void_p * n)(1, 1, None)          # two fp16-dZ items and an fp32 one (the output layer)
+    b16 = (ctypes.c_int * n)(0, 1, 1)                 # the input panel fp32, hidden activations fp16
+    w = [n, I64(256, 256, 257), I64(71, 256, 256), I64(M, M, M), None, None,
+         ctypes.cast(ainv, ctypes.c_void_p).value, None, None, None, ctypes.cast(b16, ctypes.c_void_p).value] + \
+        [None] * 5
     name, (flops, nbytes) = bench.gemm_wide16_work(w)
     assert name == "fp16:TN_grouped"
-    assert flops == 2.0 * M * (256 * 71 + 256 * 256)
-    assert nbytes == sum(2.0 * M * 256 + 4.0 * M + 4.0 * M * k + 8.0 * 256 * k for k in (71, 256))
+    assert flops == 2.0 * M * (256 * 71 + 256 * 256 + 257 * 256)
+    assert nbytes == (2.0 * M * 256 + 4.0 * M + 4.0 * M * 71 + 8.0 * 256 * 71) + \
+        (2.0 * M * 256 + 4.0 * M + 2.0 * M * 256 + 8.0 * 256 * 256) + (4.0 * M * 257 + 2.0 * M * 256 + 8.0 * 257 * 256)
     rec = bench.kernel_records({"mms_gemm_tn_wide16:" + name: (1, 0.1, (flops, nbytes))}, 1, "fast_h16c")[0]
     assert rec["peak"] == bench.BF16_MFMA_PEAK_TF

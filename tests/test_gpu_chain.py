@@ -427,6 +427,7 @@ def test_chain_fp16_backward(dev, dims, acts, M, rows_full, w16):
         Y = [t.detach().clone() for t in run.Y]
         dy = torch.randn(M, dims[-1], generator=g)
         dy *= 10.0 ** torch.randint(-6, 4, (M, 1), generator=g).double().float()    # per-row magnitudes
+        dy[1::17] = 0.0           # all-zero rows (fixed-capacity padding rows: fp16 weight gradients' rinv 0)
         rf = M if rows_full is None else rows_full
         dyr = dy.double().clone()
         dyr[rf:, 1:] = 0.0

@@ -33,10 +33,12 @@ def test_e2e_fixed_capacity(dev, name):
 
 
 @pytest.mark.parametrize("precision,max_iters,start", [("fp32", 100000, 95000), ("fast", 100000, 95000),
+                                                       ("fast_h16b", 100000, 95000), ("fast_h16c", 100000, 95000),
                                                        ("fp32", 50000, 45000)])
 def test_graph_trainer_matches_eager(dev, precision, max_iters, start):
     """max_iters 50000: the curvature factor (and every other schedule) follow the run's num_iterations in the
-    graph key and in the loss alike."""
+    graph key and in the loss alike.  The fp16 presets replay the padding rows of fixed capacity through
+    their row-scaled fp16 paths (all-zero dZ rows beside the real ones)."""
     from multimodalstudio_amd import functions as fx
     from multimodalstudio_amd import graphs
     from multimodalstudio_amd import pipeline as pl

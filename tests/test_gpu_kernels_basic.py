@@ -327,52 +327,72 @@ def _rowscaled16(dZ: torch.Tensor):
     h = torch.zeros(dZ.shape[0], 32 * ((dZ.shape[1] + 31) // 32), dtype=torch.float16)
     h[:, :dZ.shape[1]] = torch.ldexp(dZ.double(), (14 - e)[:, None].double()).half()
     rinv = torch.ldexp(torch.ones(dZ.shape[0], dtype=torch.float64), (e - 14).double()).float()
+    rinv[mx == 0] = 0.0                                 # all-zero rows: rinv 0
     eb = int((e[mx > 0] + 1000).max()) if bool((mx > 0).any()) else 0
     return h, rinv, eb
 
 
 def test_gemm_tn_wide16(dev):
-    """mms_gemm_tn_wide16 (preset fast_h16c's hidden-layer weight gradients): fp16 dZ rows in their row scale x fp32 X
-    rounded to fp16 in the launch's common scale, fp32 accumulation, vs fp64 of EXACTLY those fp16 operands (the
-    scaling and the MFMA path: fp32 accumulation, 3e-5) and vs the fp32 operands (fp16's operand precision: 3e-3); ragged
+    """mms_gemm_tn_wide16 (preset fast_h16c's weight gradients, one mixed launch per MLP): fp16 dZ rows in their row
+    scale x X rounded to fp16 in the launch's common scale (fp32 or fp16 X rows), fp32 accumulation, vs fp64 of
+    EXACTLY those fp16 operands (the scaling and the MFMA path: fp32 accumulation, 3e-5) and vs the unrounded operands
+    (fp16's operand precision: 3e-3); an fp32-dZ item in the same launch runs split bf16x3 (2e-5 of fp64); ragged
     widths (257 outputs, 317 inputs, the SDF input layer's 71), rows of very different magnitude (1e-6 .. 1e3), an
-    all-zero item (emax 0), the bias column sums."""
+    all-zero item (emax 0), an item of small gradients (largest exponent < 0) with all-zero rows beside large X rows
+    (fixed-capacity padding rows: their X row must not be lifted past fp16's range), the bias column sums."""
     from multimodalstudio_amd import hip_ops
     g = torch.Generator().manual_seed(16)
-    specs = [(256, 71, 30011), (256, 256, 20000), (257, 256, 9000), (130, 317, 12000), (256, 256, 5000)]
-    items, refs = [], []
-    for i, (N, K, M) in enumerate(specs):
-        dZ = torch.randn(M, N, generator=g) * 10.0 ** torch.randint(-6, 4, (M, 1), generator=g).float()
-        if i == 4:
-            dZ.zero_()
-        X = torch.randn(M, K, generator=g) * 3.0
-        h, rinv, eb = _rowscaled16(dZ)
-        em = torch.tensor([eb], dtype=torch.int32, device=dev)
-        Xd = torch.zeros(M, (K + 3) // 4 * 4, device=dev)[:, :K]
-        Xd.copy_(X.to(dev))
-        dW = torch.zeros(N, K, device=dev)
-        db = torch.zeros(N, device=dev)
-        items.append((N, K, M, h.to(dev)[:, :N], rinv.to(dev), em, Xd, dW, db))
-        # the kernel's operands exactly: A = h * rinv, B = fp16(X 2^(e_r - e_max)) 2^(e_max - e_r)
-        A = h[:, :N].double() * rinv.double()[:, None]
-        if eb > 0:
-            f = rinv.double() * 2.0 ** (14 - (eb - 1000))
-            Bq = (X.double() * f[:, None]).float().half().double() / f[:, None]
-        else:
-            Bq = X.double()
-        refs.append((A.T @ Bq, A.sum(0), dZ.double().T @ X.double()))
-    hip_ops.gemm_tn_wide16(items)
-    torch.cuda.synchronize()
-    for (N, K, M, *_, dW, db), (rq, rb, rt) in zip(items, refs):
-        got = dW.cpu().double()
-        if rt.abs().max() == 0:
-            assert got.abs().max() == 0 and db.abs().max() == 0
-            continue
-        eq = ((got - rq).abs().max() / rq.abs().max()).item()
-        et = ((got - rt).abs().max() / rt.abs().max()).item()
-        eb_ = ((db.cpu().double() - rb).abs().max() / rb.abs().max()).item()
-        print(f"wide16 {N}x{K} rows {M}: vs fp16 operands {eq:.1e}, vs fp32 {et:.1e}, db {eb_:.1e}")
-        assert eq < 3e-5 and et < 3e-3 and eb_ < 1e-5, (N, K, eq, et, eb_)
+    # (N_out, K_in, rows, kind): kind 0 fp16 dZ / fp32 X, 1 fp16 dZ / fp16 X, 2 fp32 dZ (split bf16x3) / fp16 X,
+    # 3 all-zero fp16 dZ, 4 small fp16 dZ with zero rows and large X rows
+    launches = [[(256, 71, 30011, 0), (256, 256, 20000, 1), (257, 256, 9000, 2), (130, 317, 12000, 0)],
+                [(256, 256, 5000, 3), (256, 256, 7000, 4), (257, 256, 6000, 2)]]
+    for specs in launches:
+        items, refs = [], []
+        for N, K, M, kind in specs:
+            dZ = torch.randn(M, N, generator=g) * 10.0 ** torch.randint(-6, 4, (M, 1), generator=g).float()
+            X = torch.randn(M, K, generator=g) * 3.0
+            if kind == 3:
+                dZ.zero_()
+            if kind == 4:
+                dZ = torch.randn(M, N, generator=g) * 1e-7
+                dZ[M // 2:] = 0.0
+                X[M // 2:] *= 1e4
+            x16 = kind in (1, 2)
+            Xd = torch.zeros(M, (K + 3) // 4 * 4, device=dev, dtype=torch.float16 if x16 else torch.float32)[:, :K]
+            Xd.copy_(X.to(dev))
+            Xv = Xd.cpu().double()                      # X as the kernel reads it
+            dW = torch.zeros(N, K, device=dev)
+            db = torch.zeros(N, device=dev)
+            if kind == 2:
+                Ad = torch.zeros(M, (N + 3) // 4 * 4, device=dev)[:, :N]
+                Ad.copy_(dZ.to(dev))
+                items.append((N, K, M, Ad, None, None, Xd, dW, db))
+                r = dZ.double().T @ Xv
+                refs.append((r, dZ.double().sum(0), r, 2e-5))
+                continue
+            h, rinv, eb = _rowscaled16(dZ)
+            em = torch.tensor([eb], dtype=torch.int32, device=dev)
+            items.append((N, K, M, h.to(dev)[:, :N], rinv.to(dev), em, Xd, dW, db))
+            # the kernel's operands exactly: A = h * rinv, B = fp16(X 2^(e_r - e_max)) 2^(e_max - e_r)
+            A = h[:, :N].double() * rinv.double()[:, None]
+            if eb > 0:
+                f = rinv.double() * 2.0 ** (14 - (eb - 1000))
+                Bq = (Xv * f[:, None]).float().half().double() / f.clamp_min(1e-300)[:, None]
+            else:
+                Bq = Xv
+            refs.append((A.T @ Bq, A.sum(0), dZ.double().T @ X.double(), 3e-5))
+        hip_ops.gemm_tn_wide16(items)
+        torch.cuda.synchronize()
+        for (N, K, M, *_, dW, db), (rq, rb, rt, tq) in zip(items, refs):
+            got = dW.cpu().double()
+            if rt.abs().max() == 0:
+                assert got.abs().max() == 0 and db.abs().max() == 0
+                continue
+            eq = ((got - rq).abs().max() / rq.abs().max()).item()
+            et = ((got - rt).abs().max() / rt.abs().max()).item()
+            eb_ = ((db.cpu().double() - rb).abs().max() / rb.abs().max()).item()
+            print(f"wide16 {N}x{K} rows {M}: vs the kernel's operands {eq:.1e}, vs fp32 {et:.1e}, db {eb_:.1e}")
+            assert eq < tq and et < 3e-3 and eb_ < 1e-5, (N, K, eq, et, eb_)
 
 
 @pytest.mark.parametrize("C,K,act", [(1, 256, 2), (9, 128, 3), (3, 128, 0), (4, 512, 1), (1, 128, 3), (5, 256, 0)])
