@@ -68,9 +68,11 @@ DTYPES = {"fp32": "fp32",
                        "forwards, for every MLP's backward-data chain after its first layer (per-row power-of-two "
                        "scaled) and for the hidden layers' weight gradients (fp16 dZ rows in their row scale, fp16 X in "
                        "a per-launch scale); split-bf16x3 for the SDF MLP forward, the chains' first backward layer and "
-                       "the output layers' weight gradients, fp32 elsewhere"}
+                       "the output layers' weight gradients, fp32 elsewhere",
+          "fast_h16d": "as fast_h16c with those MLPs' hidden activations stored as fp16 rows (the reference autocast's "
+                       "fp16 activations: the backward's act' and the weight gradients read them), fp32 elsewhere"}
 # the benchmarked preset (tests/test_cpu_host.py::test_benchmarked_preset_* guard its numerics)
-DEFAULT_PRECISION = "fast_h16b"
+DEFAULT_PRECISION = "fast_h16d"
 HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per lookup, forward
 HASH_BWD_B = 128 + 12 + 16 * 8 * 2 * (4 + 4)    # bytes per lookup, backward (table grads)
 HASH_BWD_ATOMIC_B = 16 * 8 * 2 * 4              # the float-atomic bytes one backward lookup adds into the table
@@ -126,15 +128,20 @@ def chain_work(a):
     Np = ctypes.cast(a[20], ctypes.POINTER(ctypes.c_int))
     outs = ctypes.cast(a[18], ctypes.POINTER(ctypes.c_void_p))
     n = [Np[i] for i in range(nl)]
-    # bytes per stored element: 4 (fp32), or 2 + 4 / n (a prec-6 hidden layer's fp16 dZ rows and their inverse scale)
+    # bytes per stored element: 4 (fp32), or 2 + 4 / n (a prec-6 hidden layer's fp16 dZ rows and their inverse scale),
+    # or 2 (fp16 hidden activations, f16); the backward's activation rows (aux) 2 B per element when f16
     rinv = ctypes.cast(a[27], ctypes.POINTER(ctypes.c_void_p)) if len(a) > 27 and a[27] else None
-    st = [0.0 if outs[i] is None else (0.5 + 1.0 / n[i] if (rinv is not None and rinv[i]) else 1.0)
-          for i in range(nl)]
+    f16 = ctypes.cast(a[29], ctypes.POINTER(ctypes.c_int)) if len(a) > 29 and a[29] else None
+    h = [bool(f16 is not None and f16[i]) for i in range(nl)]
+    st = [0.0 if outs[i] is None else (0.5 + 1.0 / n[i] if (rinv is not None and rinv[i]) else
+                                       (0.5 if (h[i] and not bwd) else 1.0)) for i in range(nl)]
+    ya = [0.5 if h[i] else 1.0 for i in range(nl)]      # backward: bytes factor of layer i's activation rows
     mid = sum(n[l - 1] * n[l] for l in range(1, nl - 1))
     if bwd:
         f0 = 2.0 * (rf * K0 + (M - rf)) * n[0]       # the first backward layer (B = dY from memory)
         flops = f0 + 2.0 * M * (mid + n[nl - 2] * n[nl - 1])
-        nbytes = 4.0 * ((rf * K0 + (M - rf)) + M * sum(n[l] * st[l] for l in range(nl)) + M * sum(n[:nl - 1]))
+        nbytes = 4.0 * ((rf * K0 + (M - rf)) + M * sum(n[l] * st[l] for l in range(nl)) +
+                        M * sum(n[l] * ya[l] for l in range(nl - 1)))
     else:
         flops = 2.0 * M * (K0 * n[0] + mid) + 2.0 * (rf * n[nl - 1] + (M - rf)) * n[nl - 2]
         nbytes = 4.0 * (M * K0 + M * sum(n[l] * st[l] for l in range(nl - 1)) + (rf * n[nl - 1] + (M - rf)) * st[nl - 1])

@@ -159,7 +159,10 @@ int mms_gemm_tn_wide16(int n, const int64_t* M, const int64_t* N, const int64_t*
  *   |dZ| in [2^13, 2^14)), rinv[l][row] = the row's inverse scale 2^(e - 14) (0 for an all-zero row), and
  *   atomically raises emax[l] to the
  *   largest e + 1000 of its rows (emax zeroed by the caller; 0 = every row zero): the fp16 weight-gradient operands of
- *   mms_gemm_tn_wide16.  rinv NULL (or rinv[l] NULL): fp32 dZ as before. 
+ *   mms_gemm_tn_wide16.  rinv NULL (or rinv[l] NULL): fp32 dZ as before.
+ * f16 (NULL: none): per layer, hidden layers l < n_layers - 1 only -- forward: out[l] holds fp16 activation rows
+ *   (8-B aligned, ldo >= 32 ceil(N/32)), the reference autocast's fp16 activations; backward: aux[l] is such an fp16
+ *   row buffer (act' evaluated from the fp16 values). 
  * a_hi / a_lo: per-layer packed weights from mms_mlp_pack (bf16, 32 ceil(N/32) x 16 ceil(K/16)); layers >= 1 are
  * register-fed and must be packed with permute = 1.  All row pitches multiples of 4 floats, 16-B aligned. */
 /* Rows per mms_mlp_chain block (128; 64 in a build with two blocks per CU): the tap_part row granularity. */
@@ -169,7 +172,7 @@ int mms_mlp_chain(int prec, int backward, int n_layers, const float* X, int64_t 
                   const void* const* a_hi, const void* const* a_lo, const float* const* bias, const float* const* aux,
                   const int64_t* ldaux, float* const* out, const int64_t* ldo, const int* N, const int* act,
                   float beta, float thr, const float* w2row0, float* tap_part, int64_t ld_tap, float* const* rinv,
-                  unsigned* emax, void* stream);
+                  unsigned* emax, const int* f16, void* stream);
 /* bf16 (hi, and lo = residual if non-NULL) image of W [N, K] (ldw) as an MFMA A operand of rows x cols:
  * transpose = 0 -> A = W, 1 -> A = W^T; permute bit 0 stores each k-step in register-fed order (columns 0-3, 8-11,
  * 4-7, 12-15 of a 16-column step); bit 2 writes an fp16 image (hi only, fp16 bits in the 16-bit buffer:

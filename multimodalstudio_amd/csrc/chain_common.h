@@ -34,7 +34,30 @@ struct ChainLayer {
   // operands (mms_gemm_tn_wide16)
   float* rinv;
   unsigned* emax;
+  // hidden layers: forward -> `out` holds fp16 rows [rows][ldo] of the activations (the backward's act' source and the
+  // weight gradients' X); backward -> `aux` is such an fp16 row buffer
+  int f16;
 };
+
+typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+// 4 floats -> 4 fp16 values, stored as one 8-B (non-temporal) write
+__device__ __forceinline__ void st_nt4h(float* base_as_half, int64_t off, f32x4 v) {
+  const f16x4_t h = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+  __builtin_nontemporal_store(h, reinterpret_cast<f16x4_t*>(reinterpret_cast<_Float16*>(base_as_half) + off));
+}
+// 4 fp16 values loaded as 8 B, carried in .x / .y of an f32x4 until widened (the load stays in flight)
+__device__ __forceinline__ f32x4 ld_nt4h(const float* base_as_half, int64_t off) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 v = __builtin_nontemporal_load(
+      reinterpret_cast<const u32x2*>(reinterpret_cast<const _Float16*>(base_as_half) + off));
+  return f32x4{__uint_as_float(v[0]), __uint_as_float(v[1]), 0.f, 0.f};
+}
+__device__ __forceinline__ f32x4 widen4h(f32x4 v) {
+  const f16x2_t p0 = __builtin_bit_cast(f16x2_t, __float_as_uint(v[0]));
+  const f16x2_t p1 = __builtin_bit_cast(f16x2_t, __float_as_uint(v[1]));
+  return f32x4{(float)p0[0], (float)p0[1], (float)p1[0], (float)p1[1]};
+}
 
 struct ChainArgs {
   const float* X;      // layer-0 input [rows][ldx], K0 valid columns (16-B aligned rows)

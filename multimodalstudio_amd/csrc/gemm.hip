@@ -957,9 +957,11 @@ namespace {
 // (>= 1024 rows per slice); returns the total block count
 int64_t plan_wide(WideGroup& g, int target_blocks) {
   if (target_blocks < 1) target_blocks = 256;
+  // (a split-bf16x3 item's rows cost 1.5x their bytes' share beside fp16 items: its three MFMAs and four images per
+  // product; fast_h16d A/B, 1.0 / 1.5 / 2.2: the launch 154 / 141 / 143 us)
   auto cost = [](const WideItem& t) {
     return (double)((t.M + kWT - 1) / kWT) * ((t.N + kWT - 1) / kWT) * (double)t.K *
-           ((t.ainv ? 2.0 : 4.0) + (t.b16 ? 2.0 : 4.0));
+           ((t.ainv ? 2.0 : 4.0) + (t.b16 ? 2.0 : 4.0)) * (t.ainv ? 1.0 : 1.5);
   };
   double work = 0.0;
   for (int i = 0; i < g.n; ++i) work += cost(g.it[i]);

@@ -264,7 +264,8 @@ constexpr int kScr = 36;  // scratch row pitch (floats)
 
 template <int ACT, bool KEEP>
 __device__ __forceinline__ void epi_tile_full(floatx16& acc, int t, const float* sb, float* obase, int64_t ldo,
-                                              int64_t m0, int64_t M, float* scr, int lane, float beta, float thr) {
+                                              int64_t m0, int64_t M, float* scr, int lane, float beta, float thr,
+                                              bool o16) {
   const int r = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -285,7 +286,8 @@ __device__ __forceinline__ void epi_tile_full(floatx16& acc, int t, const float*
       const int row = 8 * j + (lane >> 3);
       const f32x4 v = *reinterpret_cast<const f32x4*>(scr + row * kScr + 4 * q);
       const int64_t mr = m0 + row < M ? m0 + row : M - 1;
-      st_nt4(obase + mr * ldo + 32 * t + 4 * q, v);
+      if (o16) st_nt4h(obase, mr * ldo + 32 * t + 4 * q, v);
+      else st_nt4(obase + mr * ldo + 32 * t + 4 * q, v);
     }
   }
 }
@@ -304,7 +306,7 @@ __device__ __forceinline__ void epi_tile_act(floatx16& acc, int t, const float* 
 // ... and (KEEP) the staged row-contiguous store of the activated tile (4 vector-memory instructions per lane)
 template <bool KEEP>
 __device__ __forceinline__ void epi_tile_store(const floatx16& acc, int t, float* obase, int64_t ldo, int64_t m0,
-                                               int64_t M, float* scr, int lane) {
+                                               int64_t M, float* scr, int lane, bool o16) {
   if constexpr (KEEP) {
     const int r = lane & 31, h = lane >> 5, q = lane & 7;
 #pragma unroll
@@ -316,7 +318,8 @@ __device__ __forceinline__ void epi_tile_store(const floatx16& acc, int t, float
       const int row = 8 * j + (lane >> 3);
       const f32x4 v = *reinterpret_cast<const f32x4*>(scr + row * kScr + 4 * q);
       const int64_t mr = m0 + row < M ? m0 + row : M - 1;
-      st_nt4(obase + mr * ldo + 32 * t + 4 * q, v);
+      if (o16) st_nt4h(obase, mr * ldo + 32 * t + 4 * q, v);   // (one store instruction either way)
+      else st_nt4(obase + mr * ldo + 32 * t + 4 * q, v);
     }
   }
 }
@@ -363,10 +366,12 @@ __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const C
   constexpr int YA = NT < YMAX ? NT : YMAX;
   const bool st32 = Ly.rinv == nullptr;   // fp32 dZ stored here; fp16 dZ after the row scale (store_dz16)
   f32x4 y[YA][4];
+  const bool y16 = Ly.f16 != 0;           // fp16 Y rows: 8-B loads, widened when used
   auto load = [&](int t, f32x4* dst) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if constexpr ((MMS_CHAIN_EPI_ABL & 1) != 0) dst[j] = f32x4{0.3f, 0.2f, 0.1f, 0.4f};
+      else if (y16) dst[j] = ld_nt4h(Ly.aux, rows[j] * Ly.ldaux + 32 * t + 4 * q);
       else dst[j] = ld_nt4(Ly.aux + rows[j] * Ly.ldaux + 32 * t + 4 * q);
     }
   };
@@ -375,6 +380,10 @@ __device__ __forceinline__ void epilogue_bwd_staged(floatx16 (&acc)[NT], const C
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     f32x4 (&yt)[4] = y[t % YA];
+    if (y16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) yt[j] = widen4h(yt[j]);
+    }
     if constexpr (TAPW) {
       f32x4 sw = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -549,7 +558,7 @@ __device__ __forceinline__ void to_b(const floatx16 (&acc)[NT], bf16x8 (&bh)[2 *
 template <int PREC, int ACT, bool KEEP, int NT>
 __device__ __forceinline__ void lazy_fwd_b(int s, floatx16 (&accp)[NT], bf16x8* bh, bf16x8* bl, const float* sb,
                                            float* obase, int64_t ldo, int64_t m0, int64_t M, float* scr, int lane,
-                                           float beta, float thr) {
+                                           float beta, float thr, bool o16) {
   if ((s & 1) != 0) return;
   const int t = s >> 1;
 #if MMS_CHAIN_AHEAD
@@ -557,13 +566,13 @@ __device__ __forceinline__ void lazy_fwd_b(int s, floatx16 (&accp)[NT], bf16x8* 
     epi_tile_act<ACT>(accp[0], 0, sb, lane, beta, thr);
     tile_to_b<PREC>(accp[0], &bh[0], &bl[0]);
   }
-  epi_tile_store<KEEP>(accp[t], t, obase, ldo, m0, M, scr, lane);
+  epi_tile_store<KEEP>(accp[t], t, obase, ldo, m0, M, scr, lane, o16);
   if (t + 1 < NT) {
     epi_tile_act<ACT>(accp[t + 1], t + 1, sb, lane, beta, thr);
     tile_to_b<PREC>(accp[t + 1], &bh[2 * t + 2], &bl[2 * t + 2]);
   }
 #else
-  epi_tile_full<ACT, KEEP>(accp[t], t, sb, obase, ldo, m0, M, scr, lane, beta, thr);
+  epi_tile_full<ACT, KEEP>(accp[t], t, sb, obase, ldo, m0, M, scr, lane, beta, thr, o16);
   tile_to_b<PREC>(accp[t], &bh[s], &bl[s]);
 #endif
 }
@@ -796,7 +805,7 @@ __global__ __launch_bounds__(64 * kNW) void chain_kernel(ChainArgs a) {
                                        [&](int s, bf16x8& bh, bf16x8& bl) {
       if constexpr (!BWD)
         lazy_fwd_b<PREC, A0, KEEP, NT0>(s, acc0, b1h, b1l, sbias[0], a.L[0].out, a.L[0].ldo, m0, a.M, scr, lane, a.beta,
-                                        a.thr);
+                                        a.thr, a.L[0].f16 != 0);
       bh = b1h[s]; bl = b1l[s];
     } MMS_ST(1));
   }
@@ -824,7 +833,7 @@ __global__ __launch_bounds__(64 * kNW) void chain_kernel(ChainArgs a) {
     auto get_b2 = [&](int s, bf16x8& bh, bf16x8& bl) {
       if constexpr (!BWD)
         lazy_fwd_b<PREC, A1, KEEP, NT1>(s, accp, b2h, b2l, sbias[LP], a.L[LP].out, a.L[LP].ldo, m0, a.M, scr, lane,
-                                        a.beta, a.thr);
+                                        a.beta, a.thr, a.L[LP].f16 != 0);
       bh = b2h[s]; bl = b2l[s];
     };
     if (BWD || blockfull) {
@@ -837,7 +846,8 @@ __global__ __launch_bounds__(64 * kNW) void chain_kernel(ChainArgs a) {
       float p = 0.f;
 #pragma unroll
       for (int t = 0; t < NT1; ++t) {
-        epi_tile_full<A1, KEEP>(accp[t], t, sbias[LP], a.L[LP].out, a.L[LP].ldo, m0, a.M, scr, lane, a.beta, a.thr);
+        epi_tile_full<A1, KEEP>(accp[t], t, sbias[LP], a.L[LP].out, a.L[LP].ldo, m0, a.M, scr, lane, a.beta, a.thr,
+                                a.L[LP].f16 != 0);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const f32x4 w = *reinterpret_cast<const f32x4*>(sw0 + 32 * t + 8 * g + 4 * h);
@@ -884,7 +894,7 @@ __global__ __launch_bounds__(64 * kNW) void chain_kernel(ChainArgs a) {
                                                   [&](int s, bf16x8& bh, bf16x8& bl) {
       if constexpr (!BWD)
         lazy_fwd_b<PREC, A1, KEEP, NT1>(s, acc1, bmh, bml, sbias[1], a.L[1].out, a.L[1].ldo, m0, a.M, scr, lane, a.beta,
-                                        a.thr);
+                                        a.thr, a.L[1].f16 != 0);
       bh = bmh[s]; bl = bml[s];
     } MMS_ST(2));
     last_layer(accm, std::integral_constant<int, 2>{}, invm);
@@ -1157,7 +1167,7 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
                              const float* const* bias, const float* const* aux, const int64_t* ldaux,
                              float* const* out, const int64_t* ldo, const int* N, const int* act, float beta,
                              float thr, const float* w2row0, float* tap_part, int64_t ld_tap, float* const* rinv,
-                             unsigned* emax, void* stream) {
+                             unsigned* emax, const int* f16, void* stream) {
   const char* fn = "mms_mlp_chain";
   MMS_REQUIRE((prec >= 1 && prec <= 3) || prec == 5 || (prec == 6 && backward), fn,
               "prec must be 1 (bf16), 2 (split bf16x3), 3 (split activations), 5 (fp16, forward chains) or 6 (backward: "
@@ -1195,7 +1205,17 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
     L.bias = (!backward && bias) ? bias[l] : nullptr;
     L.aux = (backward && aux) ? aux[l] : nullptr;
     L.ldaux = (backward && ldaux) ? ldaux[l] : 0;
-    MMS_REQUIRE(L.aux == nullptr || (aligned16(L.aux) && L.ldaux % 4 == 0), fn, "aux rows must be 16-B aligned");
+    L.f16 = (f16 && f16[l]) ? 1 : 0;
+    if (L.f16) {
+      // fp16 hidden activations: the forward's stored rows, the backward's act' source
+      MMS_REQUIRE(l < n_layers - 1 && (backward ? L.aux != nullptr : out[l] != nullptr), fn,
+                  "fp16 rows (f16) are a hidden-layer feature: forward out / backward aux");
+      const void* p = backward ? (const void*)L.aux : (const void*)out[l];
+      const int64_t ld = backward ? L.ldaux : ldo[l];
+      MMS_REQUIRE(((uintptr_t)p & 7) == 0 && ld % 4 == 0 && ld >= 32 * ((N[l] + 31) / 32),
+                  fn, "fp16 rows must be 8-B aligned and hold whole 32-column tiles");
+    }
+    MMS_REQUIRE(L.aux == nullptr || L.f16 || (aligned16(L.aux) && L.ldaux % 4 == 0), fn, "aux rows must be 16-B aligned");
     L.out = out[l];
     L.ldo = ldo[l];
     L.rinv = rinv ? rinv[l] : nullptr;
@@ -1210,7 +1230,7 @@ MMS_EXPORT int mms_mlp_chain(int prec, int backward, int n_layers, const float* 
     // a forward whose rows all take the single-output path (rows_full = 0, the sampler's SDF queries) stores only
     // column 0 of the last layer, one scalar per row: any pitch >= 1 (a dense [M] sdf vector with ldo = 1)
     const bool col0_only = !backward && l == n_layers - 1 && a.rows_full == 0;
-    MMS_REQUIRE(L.out == nullptr || L.rinv != nullptr || (col0_only && L.ldo >= 1) ||
+    MMS_REQUIRE(L.out == nullptr || L.rinv != nullptr || (L.f16 && !backward) || (col0_only && L.ldo >= 1) ||
                     (aligned16(L.out) && L.ldo % 4 == 0 && L.ldo >= N[l]), fn, "output rows must be 16-B aligned");
     L.N = N[l];
     L.act = act[l];

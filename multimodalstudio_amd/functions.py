@@ -72,11 +72,16 @@ PRESETS["fast_h16bw"] = dict(PRESETS["fast_h16b"], wgrad=1)
 # (mms_gemm_tn_wide16: the autocast nn.Linear backward's operand precision, fp32 accumulation); the layers whose dZ is
 # the chain's input (the SDF / background output layers, the radiance field's last layer) stay split-bf16x3
 PRESETS["fast_h16c"] = dict(PRESETS["fast_h16b"], wgrad16=1)
+# ... and the reference's fp16 activations: those chains' hidden-layer outputs stored as fp16 rows (the backward's act'
+# source and the weight gradients' X: half the bytes written by the forward, read by the backward and the weight
+# gradients); the forward itself still feeds each layer from its fp32 accumulators
+PRESETS["fast_h16d"] = dict(PRESETS["fast_h16c"], y16=1)
 for _p in PRESETS.values():
     _p.setdefault("sdf_chain", 0)      # 0: the chain runs on the "sdf" GEMM precision
     _p.setdefault("wgrad", 0)          # 0: the weight gradients on the family's backward operand mode
     _p.setdefault("bwd16", 0)          # 1: split-bf16x3 backward-data chains run prec 6
     _p.setdefault("wgrad16", 0)        # 1: prec-6 chains' hidden-layer weight gradients on fp16 dZ (gemm_tn_wide16)
+    _p.setdefault("y16", 0)            # 1 (with wgrad16): those chains' hidden activations stored as fp16 rows
 # NOT a parity preset: the SDF chain on bf16 weights x split activations (mms_mlp_chain prec 3, two MFMAs per product;
 # with bf16-ROUNDED weights the SDF is a different, rippled function: 56x the reference's hessian scale off on the
 # e2e fixtures and a 24x larger curvature loss over the rgb training trajectory), kept to measure what the curvature
@@ -614,7 +619,7 @@ class ChainRun:
         return hi, lo
 
     def _chain(self, backward: bool, X, K0: int, rows_full: int, packs, bias, aux, outs, Ns, acts,
-               xaux=None, xact: int = 0, xout=None, w2row0=None, tap_part=None, rinv=None, emax=None):
+               xaux=None, xact: int = 0, xout=None, w2row0=None, tap_part=None, rinv=None, emax=None, f16=None):
         prec = self.bcprec if backward else self.cprec
         n = self.L
         VP = ctypes.c_void_p * n
@@ -634,7 +639,8 @@ class ChainRun:
                   0 if xout is None else xout.stride(0), cast(his), cast(los), cast(bs), cast(auxs), cast(ldaux),
                   cast(os_), cast(ldo), cast(ns), cast(ac), self.beta, self.thr, _p(w2row0), _p(tap_part),
                   0 if tap_part is None else tap_part.stride(0),
-                  None if rinv is None else cast(VP(*[_p(r) for r in rinv])), _p(emax), _s())
+                  None if rinv is None else cast(VP(*[_p(r) for r in rinv])), _p(emax),
+                  None if f16 is None else cast((ctypes.c_int * n)(*[int(bool(f)) for f in f16])), _s())
 
     def forward(self, x: torch.Tensor, keep: bool, rows_full: Optional[int] = None,
                 dense_col0: bool = False, last_out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -662,14 +668,25 @@ class ChainRun:
             last = torch.empty(M, device=dev).view(M, 1)
         else:
             last = last_out if last_out is not None else _alloc(M, Ns[-1], dev)
-        Y = [_alloc(M, Ns[l], dev) if keep else None for l in range(L - 1)] + [last]
+        y16 = keep and self._fp16_panels(Ns) and bool(PRECISION.get("y16", 0))
+        if y16:   # (whole 32-column tiles per row)
+            Y = [torch.empty(M, 32 * ((Ns[l] + 31) // 32), dtype=torch.float16, device=dev)[:, :Ns[l]]
+                 for l in range(L - 1)] + [last]
+        else:
+            Y = [_alloc(M, Ns[l], dev) if keep else None for l in range(L - 1)] + [last]
         self._chain(False, x, K0, self.rows_full, packs, [self.params[3 * l + 2] for l in range(L)], [None] * L, Y,
-                    Ns, [a[0] for a in self.acts], w2row0=self.Ws[-1])
+                    Ns, [a[0] for a in self.acts], w2row0=self.Ws[-1],
+                    f16=[y16] * (L - 1) + [False] if y16 else None)
         self.Y = Y
         # a training forward fetches the backward's transposed images too, so a model forward prepares them in the
         # same batched launch (WeightPrep) instead of one pack launch each in the backward
         self.bwd_packs = self._bwd_packs(K0) if keep else None
         return Y[-1].view(M) if dense_col0 else Y[-1]
+
+    def _fp16_panels(self, Ns) -> bool:
+        """Presets fast_h16c / d: this MLP's hidden-layer weight gradients take fp16 panels (a prec-6 backward chain
+        whose hidden layers feed the wide weight-gradient engine)."""
+        return bool(PRECISION.get("wgrad16", 0)) and self.bcprec == 6 and min(Ns[:self.L - 1]) >= 128
 
     def _bwd_packs(self, K0: int):
         """Backward chain images: W_last^T (natural: B = dy from memory), then the earlier layers' W^T (register-fed,
@@ -698,7 +715,7 @@ class ChainRun:
         order = list(range(L - 2, -1, -1))           # hidden layers, last first
         # preset wgrad16: the hidden layers' dZ as the chain's fp16 row-scaled values (whole 32-column tiles per row),
         # their inverse row scales and per-layer largest exponents (chain slot order), for gemm_tn_wide16
-        w16 = bool(PRECISION.get("wgrad16", 0)) and self.bcprec == 6 and min(Ns[:L - 1]) >= 128
+        w16 = self._fp16_panels(Ns)
         rinv = emax = None
         if w16:
             dZ = [torch.empty(M, 32 * ((Ns[l] + 31) // 32), dtype=torch.float16, device=dev)[:, :Ns[l]]
@@ -729,7 +746,8 @@ class ChainRun:
         self._chain(True, dy, Ns[L - 1], rf, packs, [None] * L, [Y[l] for l in order] + [None],
                     [dZ[l] for l in order] + [dx], [Ns[l] for l in order] + [K0], [acts[l] for l in order] + [0],
                     xaux=Y[L - 1] if acts[L - 1] != 0 else None, xact=acts[L - 1], xout=dZl, tap_part=tap_part,
-                    rinv=None if rinv is None else [rinv[l] for l in order] + [None], emax=emax)
+                    rinv=None if rinv is None else [rinv[l] for l in order] + [None], emax=emax,
+                    f16=[Y[l].dtype == torch.float16 for l in order] + [False])
         if tapw:
             _lib.call("mms_rowsum_add", tap_part.data_ptr(), tap_part.shape[0], n0 + 1, tap_part.stride(0),
                       dWs[L - 1].data_ptr(), n0, dbs[L - 1].data_ptr(), _s())

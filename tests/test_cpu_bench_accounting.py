@@ -10,19 +10,21 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 
-def _chain_args(prec, bwd, Ns, K0, M, rows_full, stored, fp16=None):
+def _chain_args(prec, bwd, Ns, K0, M, rows_full, stored, fp16=None, f16=None):
     """mms_mlp_chain's positional arguments (include/mms_hip.h), pointers as truthy placeholders; ``fp16``: per layer,
-    whether its out is a prec-6 fp16 dZ store (rinv[l] set)."""
+    whether its out is a prec-6 fp16 dZ store (rinv[l] set); ``f16``: per layer, fp16 activation rows (forward out /
+    backward aux)."""
     n = len(Ns)
     outs = (ctypes.c_void_p * n)(*[(1 if s else None) for s in stored])
     ns = (ctypes.c_int * n)(*Ns)
     rinv = None if fp16 is None else (ctypes.c_void_p * n)(*[(1 if f else None) for f in fp16])
     a = [prec, bwd, n, 1, K0, K0, M, rows_full] + [None] * 10 + [ctypes.cast(outs, ctypes.c_void_p).value, None,
                                                                  ctypes.cast(ns, ctypes.c_void_p).value]
+    fl = None if f16 is None else (ctypes.c_int * n)(*[int(f) for f in f16])
     a += [None] * 6 + [None if rinv is None else ctypes.cast(rinv, ctypes.c_void_p).value, None if fp16 is None else 1,
-                       None]
-    assert len(a) == 30       # ... tap_part, ld_tap, rinv, emax, stream
-    return a, (outs, ns, rinv)
+                       None if fl is None else ctypes.cast(fl, ctypes.c_void_p).value, None]
+    assert len(a) == 31       # ... tap_part, ld_tap, rinv, emax, f16, stream
+    return a, (outs, ns, rinv, fl)
 
 
 @pytest.mark.parametrize("prec,label", [(2, "bf16x3"), (5, "fp16"), (6, "fp16-rowscaled")])
@@ -85,3 +87,16 @@ def test_fp16_dz_stores_and_wide16_bytes():
         (2.0 * M * 256 + 4.0 * M + 2.0 * M * 256 + 8.0 * 256 * 256) + (4.0 * M * 257 + 2.0 * M * 256 + 8.0 * 257 * 256)
     rec = bench.kernel_records({"mms_gemm_tn_wide16:" + name: (1, 0.1, (flops, nbytes))}, 1, "fast_h16c")[0]
     assert rec["peak"] == bench.BF16_MFMA_PEAK_TF
+
+
+def test_fp16_activation_rows_bytes():
+    """Preset fast_h16d: the forward's fp16 hidden activation rows count 2 B per element, and so do the backward's
+    activation (aux) reads of them."""
+    M = 4096
+    f32, _ = _chain_args(2, 0, [256, 256, 257], 71, M, M, [True, True, True])
+    f16, _ = _chain_args(2, 0, [256, 256, 257], 71, M, M, [True, True, True], f16=[True, True, False])
+    assert bench.chain_work(f32)[1][1] - bench.chain_work(f16)[1][1] == 2 * M * 256 * 2.0
+    b32, _ = _chain_args(6, 1, [256, 256, 71], 257, M, M, [True, True, True], fp16=[True, True, False])
+    b16, _ = _chain_args(6, 1, [256, 256, 71], 257, M, M, [True, True, True], fp16=[True, True, False],
+                         f16=[True, True, False])
+    assert bench.chain_work(b32)[1][1] - bench.chain_work(b16)[1][1] == 2 * M * 256 * 2.0

@@ -222,14 +222,16 @@ def test_benchmarked_preset_keeps_the_sdf_forward_split_bf16x3():
     """The preset bench.py benchmarks by default (bench.DEFAULT_PRECISION, VERDICT r5: this guard used to check `fast`
     while the bench ran `fast_h16b`) keeps the SDF MLP forward on split-bf16x3 -- the bf16-weight SDF chain (prec 3,
     preset fast_x2) moved the hessians 56x the reference's hessian scale (tests/test_gpu_e2e.py) --, its weight
-    gradients on split-bf16x3, the radiance / head / background forwards on split-bf16x3 or fp16 (the reference GPU's
-    autocast precision; bf16 there cost 0.56 dB of converged PSNR, profiles/round3_converged_psnr.json), and the mlp
-    methods' analytic-gradient fields on fp32."""
+    gradients on split-bf16x3 or, for the hidden layers, fp16 (wgrad16, with fp16 activation rows y16 only beside
+    it: the reference GPU's autocast precision), the radiance / head / background forwards on split-bf16x3 or fp16
+    (bf16 there cost 0.56 dB of converged PSNR, profiles/round3_converged_psnr.json), and the mlp methods'
+    analytic-gradient fields on fp32."""
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     from multimodalstudio_amd import functions as fx
     p = fx.PRESETS[bench.DEFAULT_PRECISION]
     assert p["sdf"] == 2 and p["sdf_chain"] in (0, 2) and p["mlp"] == 0 and p["wgrad"] == 0
+    assert p["wgrad16"] in (0, 1) and (p["y16"] == 0 or (p["wgrad16"] == 1 and p["bwd16"] == 1))
     assert all(p[k] in (2, 5) for k in ("radiance", "heads", "pol_head", "background"))
     assert fx.PRESETS["fast_x2"]["sdf_chain"] == 3
     assert fx.fwd_prec(4) == 2 and fx.bwd_prec(4) == 1 and fx.fwd_prec(2) == fx.bwd_prec(2) == 2

@@ -396,12 +396,13 @@ def test_chain_fp16_forward(dev, dims, acts):
     ([39, 256, 256, 256, 256], [(1, 1.0, 20.0)] * 4, 3000, None),                  # background base
     ([283, 256, 256, 256, 128], [(1, 1.0, 20.0)] * 4, 3000, None)],                # background head
     ids=["sdf", "sdf_taps", "radiance", "head", "pol_head", "bg_base", "bg_head"])
-@pytest.mark.parametrize("w16", [0, 1], ids=["wgrad_x3", "wgrad16"])
+@pytest.mark.parametrize("w16", [0, 1, 2], ids=["wgrad_x3", "wgrad16", "wgrad16_y16"])
 def test_chain_fp16_backward(dev, dims, acts, M, rows_full, w16):
     """Preset fast_h16b: every backward-data chain on mms_mlp_chain prec 6 -- its first layer (B = dY from memory)
     split-bf16x3, the register-fed layers on fp16 operands with a per-row power-of-two scale (the reference GPU's fp16
     autocast backward, without its global loss scale); w16 (preset fast_h16c): the hidden layers' weight gradients
-    from the chain's fp16 row-scaled dZ stores (mms_gemm_tn_wide16; the 64-wide heads keep the fp32 panels).  dX and
+    from the chain's fp16 row-scaled dZ stores (mms_gemm_tn_wide16; the 64-wide heads keep the fp32 panels); w16 = 2
+    (fast_h16d): the forward's hidden activations stored as fp16 rows too (the reference below is taken at them).  dX and
     every parameter gradient vs the fp64 backward taken at
     the kernel's own forward activations within 3e-3 of each tensor's scale (fp16's 11-bit operands over K <= 256;
     split-bf16x3 measures ~1e-5 here), finite everywhere; rows of very different magnitude (1e-6 .. 1e3 in dY) keep
@@ -418,7 +419,8 @@ def test_chain_fp16_backward(dev, dims, acts, M, rows_full, w16):
     prec = 2 if sdf else 5
     old = dict(fx.PRECISION)
     fx.PRECISION["bwd16"] = 1
-    fx.PRECISION["wgrad16"] = w16
+    fx.PRECISION["wgrad16"] = int(w16 > 0)
+    fx.PRECISION["y16"] = int(w16 == 2)
     try:
         run = fx.ChainRun(params, acts, prec)
         assert run.bcprec == 6
@@ -538,10 +540,11 @@ def test_sdf_backward_fp16_on_antisymmetric_taps(dev, delta):
     dyr[C:, 1:] = 0.0
     dy[C:, 1:] = float("nan")                # never read
     errs = {}
-    for name, bwd16, w16 in (("x3", 0, 0), ("prec6", 1, 0), ("prec6w16", 1, 1)):
+    for name, bwd16, w16 in (("x3", 0, 0), ("prec6", 1, 0), ("prec6w16", 1, 1), ("prec6y16", 1, 2)):
         old = dict(fx.PRECISION)
         fx.PRECISION["bwd16"] = bwd16
-        fx.PRECISION["wgrad16"] = w16
+        fx.PRECISION["wgrad16"] = int(w16 > 0)
+        fx.PRECISION["y16"] = int(w16 == 2)
         try:
             for p in params:
                 p.grad = None
@@ -565,7 +568,8 @@ def test_sdf_backward_fp16_on_antisymmetric_taps(dev, delta):
     errs["autocast"] = e
     for q in errs["x3"]:
         print(f"  delta {delta:.1e} {q:4s} x3 {errs['x3'][q]:.2e}  prec6 {errs['prec6'][q]:.2e}  "
-              f"prec6 + fp16 wgrad {errs['prec6w16'][q]:.2e}  ref-fp16-autocast {errs['autocast'][q]:.2e}")
-    for mode in ("prec6", "prec6w16"):
+              f"prec6 + fp16 wgrad {errs['prec6w16'][q]:.2e}  + fp16 Y {errs['prec6y16'][q]:.2e}  "
+              f"ref-fp16-autocast {errs['autocast'][q]:.2e}")
+    for mode in ("prec6", "prec6w16", "prec6y16"):
         for q, v in errs[mode].items():
             assert np.isfinite(v) and v <= 2.0 * errs["autocast"][q] + 1e-6, (mode, q, v, errs["autocast"][q])

@@ -16,9 +16,10 @@ import numpy as np
 import pytest
 import torch
 
-# the throughput presets under test: the benchmarked one (fast_h16b: fp16 radiance / head / background forwards and
-# row-scaled fp16 backward-data chains) and the all-split-bf16x3 one (MMS_FAST_PRESET picks one alone)
-FAST_PRESETS = [os.environ["MMS_FAST_PRESET"]] if "MMS_FAST_PRESET" in os.environ else ["fast_h16b", "fast"]
+# the throughput presets under test: the benchmarked one (fast_h16d: fp16 radiance / head / background forwards,
+# row-scaled fp16 backward-data chains, fp16 hidden-layer weight gradients and fp16 hidden activation rows -- the
+# reference GPU's autocast precision) and the all-split-bf16x3 one (MMS_FAST_PRESET picks one alone)
+FAST_PRESETS = [os.environ["MMS_FAST_PRESET"]] if "MMS_FAST_PRESET" in os.environ else ["fast_h16d", "fast"]
 FAST = FAST_PRESETS[0]
 
 pytestmark = pytest.mark.gpu
@@ -335,8 +336,9 @@ def check_envelope(name, rep, preset, sizes):
 @pytest.mark.parametrize("name", ["e2e_grid_rgb_s95000", "e2e_grid_rgb_s30000", "e2e_grid_raw_5mod_s95000",
                                   "e2e_grid_raw_5mod_sat_s95000", "e2e_grid_raw_gridbg_s95000"])
 def test_e2e_fast_preset_deviation(dev, name, preset):
-    """The throughput presets (the benchmarked fast_h16b: fp16 radiance / head / background forwards and row-scaled
-    fp16 backward-data chains; fast: split-bf16x3 throughout) on the reference's fixture, held to the REFERENCE'S OWN
+    """The throughput presets (the benchmarked fast_h16d: fp16 radiance / head / background forwards, row-scaled fp16
+    backward-data chains, fp16 hidden-layer weight gradients and activation rows; fast: split-bf16x3 throughout) on the
+    reference's fixture, held to the REFERENCE'S OWN
     numerics mode: every BASELINE YAML trains in fp16 autocast ("16-mixed"), so each compared quantity -- loss,
     rendered radiance, SDF gradients and hessians, every parameter gradient (relative L2) and every pose gradient --
     must stay within 2x the distance between the reference in fp16 autocast and the reference in fp32 (the fixture),

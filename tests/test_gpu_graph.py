@@ -34,6 +34,7 @@ def test_e2e_fixed_capacity(dev, name):
 
 @pytest.mark.parametrize("precision,max_iters,start", [("fp32", 100000, 95000), ("fast", 100000, 95000),
                                                        ("fast_h16b", 100000, 95000), ("fast_h16c", 100000, 95000),
+                                                       ("fast_h16d", 100000, 95000),
                                                        ("fp32", 50000, 45000)])
 def test_graph_trainer_matches_eager(dev, precision, max_iters, start):
     """max_iters 50000: the curvature factor (and every other schedule) follow the run's num_iterations in the
