@@ -69,8 +69,12 @@ DTYPES = {"fp32": "fp32",
                        "scaled) and for the hidden layers' weight gradients (fp16 dZ rows in their row scale, fp16 X in "
                        "a per-launch scale); split-bf16x3 for the SDF MLP forward, the chains' first backward layer and "
                        "the output layers' weight gradients, fp32 elsewhere",
-          "fast_h16d": "as fast_h16c with those MLPs' hidden activations stored as fp16 rows (the reference autocast's "
-                       "fp16 activations: the backward's act' and the weight gradients read them), fp32 elsewhere"}
+          "fast_h16d": "fp16 MFMA (fp32 accumulate: the reference's autocast) for the radiance / head / background MLP "
+                       "forwards, for every MLP's backward-data chain after its first layer (per-row power-of-two "
+                       "scaled) and for the hidden layers' weight gradients; fp16 storage of those MLPs' hidden "
+                       "activations and dZ rows (the reference autocast's fp16 activations); split-bf16x3 for the SDF "
+                       "MLP forward, the chains' first backward layer and the output layers' weight gradients, fp32 "
+                       "elsewhere"}
 # the benchmarked preset (tests/test_cpu_host.py::test_benchmarked_preset_* guard its numerics)
 DEFAULT_PRECISION = "fast_h16d"
 HASH_FWD_B = 16 * 8 * 2 * 4 + 12 + 128          # bytes per lookup, forward
