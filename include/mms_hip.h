@@ -119,9 +119,10 @@ int mms_gemm_tn_wide(int prec, int n, const int64_t* M, const int64_t* N, const 
 /* The same weight gradients with fp16 operands where the producers stored them (preset fast_h16c; fp32 accumulate: the
  * reference GPU's fp16-autocast nn.Linear backward, trainer.py:51,57-62), items of mixed modes in ONE launch:
  *  - ainv[i] non-NULL: A_i = the dZ rows as mms_mlp_chain prec 6 stores them (fp16 [K_i rows][lda_i], 8-B aligned, row
- *    k scaled by 1 / ainv_i[k]; ainv 0 for an all-zero row), emax[i] = that launch's largest biased row exponent; B_i
- *    rows scaled by ainv_i[k] 2^(14 - e_max) <= 1 and rounded to fp16 (the scale undone on the fp32 accumulators): one
- *    fp16 MFMA per product;
+ *    k scaled by 1 / ainv_i[k]; ainv 0 for an all-zero row), emax[i] = that launch's largest biased row exponent;
+ *    each A row rescaled by ainv_i[k] 2^(14 - e_max) <= 1 to one common scale (the largest |dZ| at 2^14: the
+ *    reference's loss-scaled fp16 dZ) and rounded to fp16, B_i rounded to fp16 (the autocast's fp16 activations), the
+ *    common scale undone on the fp32 accumulators: one fp16 MFMA per product;
  *  - ainv NULL (or ainv[i] NULL): A_i fp32 rows (16-B aligned), split bf16x3 as mms_gemm_tn_wide;
  *  - b16[i] non-zero: B_i holds fp16 rows (8-B aligned, ldb in halves), else fp32 rows (16-B aligned).
  * colsum_i[m] += sum_k dZ_i[k][m] (the bias gradient). */

@@ -481,6 +481,9 @@ struct WideGroup {
                      // instead of adding it to C with float atomics
 };
 
+__device__ __forceinline__ float4 ld_f4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ uint2 ld_u2(const unsigned short* p) { return *reinterpret_cast<const uint2*>(p); }
+
 // One block's tile and K slice of item t.  PREC: the item's operand mode (P_BF16 / P_BF16X3: fp32 A rows; P_F16: fp16
 // A rows, see WideItem); B16: fp16 B rows (their values widened exactly, then split or scaled like fp32 rows).  lds:
 // the kernel's image buffers, scs: [8][256] floats.
@@ -491,9 +494,10 @@ __device__ __forceinline__ void wide_block(const WideItem& t, int id, float* par
   constexpr int NLD = WK / 8;         // float4 loads per thread per operand and stage
   constexpr int NIMG = PREC == P_BF16X3 ? 2 : 1;
   constexpr int IMG = kWK * kWLD;                        // elements per image
-  // P_F16 (mms_gemm_tn_wide16): A = fp16 dZ rows in their row scale (1 / ainv[k]) and B = X scaled per row by
-  // ainv[k] 2^(14 - emax) <= 1 (then rounded to fp16), so each product carries the common factor 2^(14 - emax),
-  // undone on the accumulators before they are added to C; one fp16 MFMA per product, one image per operand
+  // P_F16 (mms_gemm_tn_wide16): A = fp16 dZ rows in their row scale (1 / ainv[k]), rescaled per row by
+  // ainv[k] 2^(14 - emax) <= 1 to the launch's common scale 2^(14 - emax) and rounded to fp16 again, B = X rounded to
+  // fp16; the common factor is undone on the accumulators before they are added to C; one fp16 MFMA per product, one
+  // image per operand
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
   typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -522,10 +526,10 @@ __device__ __forceinline__ void wide_block(const WideItem& t, int id, float* par
   // one B load: float4, or (B16) the 4 fp16 values' bits in .x / .y
   auto ldB = [&](int64_t rc) {
     if constexpr (B16) {
-      const uint2 hv = *reinterpret_cast<const uint2*>(reinterpret_cast<const unsigned short*>(t.B) + rc * t.ldb + cb_c);
+      const uint2 hv = ld_u2(reinterpret_cast<const unsigned short*>(t.B) + rc * t.ldb + cb_c);
       return make_float4(__uint_as_float(hv.x), __uint_as_float(hv.y), 0.f, 0.f);
     } else {
-      return *reinterpret_cast<const float4*>(t.B + rc * t.ldb + cb_c);
+      return ld_f4(t.B + rc * t.ldb + cb_c);
     }
   };
   // B16 rows widened to float4 (exact)
@@ -541,10 +545,10 @@ __device__ __forceinline__ void wide_block(const WideItem& t, int id, float* par
   // one A load: float4, or (P_F16) the 4 fp16 values' bits in .x / .y and the row's inverse scale in .z
   auto ldA = [&](int64_t rc) {
     if constexpr (PREC == P_F16) {
-      const uint2 hv = *reinterpret_cast<const uint2*>(reinterpret_cast<const unsigned short*>(t.A) + rc * t.lda + ca_c);
+      const uint2 hv = ld_u2(reinterpret_cast<const unsigned short*>(t.A) + rc * t.lda + ca_c);
       return make_float4(__uint_as_float(hv.x), __uint_as_float(hv.y), t.ainv[rc], 0.f);
     } else {
-      return *reinterpret_cast<const float4*>(t.A + rc * t.lda + ca_c);
+      return ld_f4(t.A + rc * t.lda + ca_c);
     }
   };
 #if MMS_WIDE_PIPE
@@ -609,16 +613,24 @@ __device__ __forceinline__ void wide_block(const WideItem& t, int id, float* par
         const uint32_t k1 = !ok ? 0u : (va > 3 ? 0xffffffffu : (va > 2 ? 0xffffu : 0u));
         const uint32_t u0 = __float_as_uint(xa[i].x) & k0, u1 = __float_as_uint(xa[i].y) & k1;
         const float rin = xa[i].z;
+        const f16x2 p0 = __builtin_bit_cast(f16x2, u0), p1 = __builtin_bit_cast(f16x2, u1);
         if (do_cs) {
-          const f16x2 p0 = __builtin_bit_cast(f16x2, u0), p1 = __builtin_bit_cast(f16x2, u1);
           cs.x += (float)p0[0] * rin; cs.y += (float)p0[1] * rin;
           cs.z += (float)p1[0] * rin; cs.w += (float)p1[1] * rin;
         }
-        const float4 b = mask4(widenB(xb[i]), vb, ok);
+        // A: the row-scaled values brought to the launch's common scale (each row by 2^(e_r - e_max) <= 1: the
+        // largest |dZ| at 2^14, rows down to 2^-28 of it keep fp16's full precision -- the reference's loss-scaled
+        // fp16 dZ); B: X rounded to fp16 as it is (the autocast's fp16 activations)
         const float f = rin * bsc;
-        const f16x4 bh = {(_Float16)(b.x * f), (_Float16)(b.y * f), (_Float16)(b.z * f), (_Float16)(b.w * f)};
+        const f16x4 ah = {(_Float16)((float)p0[0] * f), (_Float16)((float)p0[1] * f), (_Float16)((float)p1[0] * f),
+                          (_Float16)((float)p1[1] * f)};
+        // (an all-zero dZ row -- rinv 0, e.g. a fixed-capacity padding row -- contributes nothing, whatever its X row
+        // holds; X beyond fp16's range saturates instead of turning 0 x inf into NaN)
+        const float4 b = mask4(widenB(xb[i]), vb, ok && rin != 0.f);
+        auto sat = [](float v) { return fminf(fmaxf(v, -65504.f), 65504.f); };
+        const f16x4 bh = {(_Float16)sat(b.x), (_Float16)sat(b.y), (_Float16)sat(b.z), (_Float16)sat(b.w)};
         const int off = (w + 8 * i) * kWLD + 4 * lane;
-        *reinterpret_cast<uint2*>(base + off) = make_uint2(u0, u1);
+        *reinterpret_cast<f16x4*>(base + off) = ah;
         *reinterpret_cast<f16x4*>(base + NIMG * IMG + off) = bh;
         continue;
       }

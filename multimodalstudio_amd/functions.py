@@ -793,8 +793,8 @@ class ChainRun:
                     gemm_tn_grouped(items, prec)
             if _WGRAD_DEFER[0] is not None:
                 _wgrad(launch)
-            elif ASYNC_WGRAD and _WN_BWD[0] is not None and not items16:
-                _wgrad_async(items, wp, dev)
+            elif ASYNC_WGRAD and _WN_BWD[0] is not None:
+                _wgrad_async(launch, [t for it in items + items16 for t in it[3:] if isinstance(t, torch.Tensor)], dev)
             else:
                 launch()
         for g, v, l, dW, gt, vt, N, K in wn:
@@ -863,18 +863,19 @@ def join_wgrad(i: int) -> None:
         torch.cuda.current_stream(i).wait_stream(_WGRAD_STREAMS[i])
 
 
-def _wgrad_async(items, prec, dev) -> None:
+def _wgrad_async(launch, tensors, dev) -> None:
+    """launch() (an MLP's weight-gradient launch) on the side stream, forked from the caller's; ``tensors``: what it
+    reads or writes (made or freed on the caller's stream)."""
     cur = torch.cuda.current_stream(dev)
     side = wgrad_stream(dev)
     side.wait_stream(cur)
     with torch.cuda.stream(side):
-        gemm_tn_grouped(items, prec)
+        launch()
     seen = set()
-    for it in items:
-        for t in it[3:]:          # A, B, dW, db: made (or freed) on the caller's stream, read / written on the side
-            if t is not None and t.data_ptr() not in seen:
-                seen.add(t.data_ptr())
-                t.record_stream(side)
+    for t in tensors:
+        if t.data_ptr() not in seen:
+            seen.add(t.data_ptr())
+            t.record_stream(side)
     i = torch.device(dev).index or 0
     torch.autograd.Variable._execution_engine.queue_callback(lambda: join_wgrad(i))
 

@@ -333,19 +333,21 @@ def _rowscaled16(dZ: torch.Tensor):
 
 
 def test_gemm_tn_wide16(dev):
-    """mms_gemm_tn_wide16 (preset fast_h16c's weight gradients, one mixed launch per MLP): fp16 dZ rows in their row
-    scale x X rounded to fp16 in the launch's common scale (fp32 or fp16 X rows), fp32 accumulation, vs fp64 of
+    """mms_gemm_tn_wide16 (presets fast_h16c / d's weight gradients, one mixed launch per MLP): fp16 dZ rows brought
+    from their row scale to the launch's common scale x X rounded to fp16 (fp32 or fp16 X rows), fp32 accumulation,
+    vs fp64 of
     EXACTLY those fp16 operands (the scaling and the MFMA path: fp32 accumulation, 3e-5) and vs the unrounded operands
     (fp16's operand precision: 3e-3); an fp32-dZ item in the same launch runs split bf16x3 (2e-5 of fp64); ragged
     widths (257 outputs, 317 inputs, the SDF input layer's 71), rows of very different magnitude (1e-6 .. 1e3), an
     all-zero item (emax 0), an item of small gradients (largest exponent < 0) with all-zero rows beside large X rows
-    (fixed-capacity padding rows: their X row must not be lifted past fp16's range), the bias column sums."""
+    (fixed-capacity padding rows), the bias column sums; and rows 2^-20 below the launch's largest keep their
+    contribution (the common scale sits on dZ, whose row values have 2^14 of headroom, not on X)."""
     from multimodalstudio_amd import hip_ops
     g = torch.Generator().manual_seed(16)
     # (N_out, K_in, rows, kind): kind 0 fp16 dZ / fp32 X, 1 fp16 dZ / fp16 X, 2 fp32 dZ (split bf16x3) / fp16 X,
     # 3 all-zero fp16 dZ, 4 small fp16 dZ with zero rows and large X rows
     launches = [[(256, 71, 30011, 0), (256, 256, 20000, 1), (257, 256, 9000, 2), (130, 317, 12000, 0)],
-                [(256, 256, 5000, 3), (256, 256, 7000, 4), (257, 256, 6000, 2)]]
+                [(256, 256, 5000, 3), (256, 256, 7000, 4), (257, 256, 6000, 2), (256, 256, 8000, 5)]]
     for specs in launches:
         items, refs = [], []
         for N, K, M, kind in specs:
@@ -357,6 +359,15 @@ def test_gemm_tn_wide16(dev):
                 dZ = torch.randn(M, N, generator=g) * 1e-7
                 dZ[M // 2:] = 0.0
                 X[M // 2:] *= 1e4
+            if kind == 5:
+                # pairs of rows 2^16 above the rest whose contributions cancel exactly (same X, opposite dZ), small
+                # activations: what remains is the many small rows' sum, which must not vanish (with the common
+                # scale on X those rows' fp16 X fell to 2-3 significant bits)
+                dZ = torch.randn(M, N, generator=g)
+                X = torch.randn(M, K, generator=g) * 1e-2
+                dZ[::1000] *= 2.0 ** 16
+                dZ[1::1000] = -dZ[::1000]
+                X[1::1000] = X[::1000]
             x16 = kind in (1, 2)
             Xd = torch.zeros(M, (K + 3) // 4 * 4, device=dev, dtype=torch.float16 if x16 else torch.float32)[:, :K]
             Xd.copy_(X.to(dev))
@@ -373,14 +384,13 @@ def test_gemm_tn_wide16(dev):
             h, rinv, eb = _rowscaled16(dZ)
             em = torch.tensor([eb], dtype=torch.int32, device=dev)
             items.append((N, K, M, h.to(dev)[:, :N], rinv.to(dev), em, Xd, dW, db))
-            # the kernel's operands exactly: A = h * rinv, B = fp16(X 2^(e_r - e_max)) 2^(e_max - e_r)
+            # the kernel's operands exactly: A = fp16(h rinv 2^(14 - e_max)) 2^(e_max - 14), B = fp16(X)
             A = h[:, :N].double() * rinv.double()[:, None]
-            if eb > 0:
-                f = rinv.double() * 2.0 ** (14 - (eb - 1000))
-                Bq = (Xv * f[:, None]).float().half().double() / f.clamp_min(1e-300)[:, None]
-            else:
-                Bq = Xv
-            refs.append((A.T @ Bq, A.sum(0), dZ.double().T @ X.double(), 3e-5))
+            S = 2.0 ** (14 - (eb - 1000)) if eb > 0 else 1.0
+            Aq = (A * S).float().half().double() / S
+            Bq = Xv.clamp(-65504, 65504).float().half().double()
+            Bq[rinv == 0] = 0.0                         # all-zero dZ rows: X ignored (padding rows)
+            refs.append((Aq.T @ Bq, A.sum(0), dZ.double().T @ X.double(), 3e-5 if kind != 5 else 1e-3))
         hip_ops.gemm_tn_wide16(items)
         torch.cuda.synchronize()
         for (N, K, M, *_, dW, db), (rq, rb, rt, tq) in zip(items, refs):
@@ -392,7 +402,9 @@ def test_gemm_tn_wide16(dev):
             et = ((got - rt).abs().max() / rt.abs().max()).item()
             eb_ = ((db.cpu().double() - rb).abs().max() / rb.abs().max()).item()
             print(f"wide16 {N}x{K} rows {M}: vs the kernel's operands {eq:.1e}, vs fp32 {et:.1e}, db {eb_:.1e}")
-            assert eq < tq and et < 3e-3 and eb_ < 1e-5, (N, K, eq, et, eb_)
+            # (kind 5: the fp32 accumulators' rounding of the 2^16-larger pairs before they cancel, ~1e-4 / 1e-3 of the
+            # small rows' sum)
+            assert eq < tq and et < 3e-3 and eb_ < (1e-5 if tq < 1e-4 else 5e-3), (N, K, eq, et, eb_)
 
 
 @pytest.mark.parametrize("C,K,act", [(1, 256, 2), (9, 128, 3), (3, 128, 0), (4, 512, 1), (1, 128, 3), (5, 256, 0)])
