@@ -34,8 +34,8 @@ def label(name, grid=0):
     if m:
         return f"mms_gemm_tn_grouped:{PREC[m.group(1)]}:TN_grouped"
     m = re.search(r"gemm_tn_wide_kernel<(\d), \d+>", name)
-    if m:
-        return f"mms_gemm_tn_wide:{PREC[m.group(1)]}:TN_grouped"
+    if m:   # (prec 5: the mixed fp16 launch, mms_gemm_tn_wide16)
+        return f"mms_gemm_tn_wide{'16' if m.group(1) == '5' else ''}:{PREC[m.group(1)]}:TN_grouped"
     m = re.search(r"gemm_kernel<(\d), (true|false), (true|false), (true|false)>", name)
     if m:
         return f"mms_gemm:{PREC[m.group(1)]}:{MODE.get((m.group(2), m.group(3)), '??')}"
