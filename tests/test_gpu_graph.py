@@ -140,8 +140,10 @@ def test_tail_count_after_eager_steps(dev):
 def test_phase_cut_backward(dev, name, cap):
     """The two-phase backward of the graph-replayed data-parallel step (functions.PHASE_CUT, pipeline.backward_batched
     ``cuts``: the rendering side first, then the SDF side from the cut tensors) gives the single backward's results:
-    the loss, the outputs and every parameter and pose gradient to float-atomic summation order; phase 1 alone has
-    already finished the radiance (and grid-background) table gradients and left the SDF table's untouched."""
+    the loss, the outputs and every parameter and pose gradient to float-atomic summation order (1e-4, or 4x the
+    spread of two single backwards of the same step where float-atomic order alone moves a cancelling sum -- e.g. a
+    bias gradient -- further); phase 1 alone has already finished the radiance (and grid-background) table gradients
+    and left the SDF table's untouched."""
     from multimodalstudio_amd import functions as fx
     from multimodalstudio_amd import pipeline as pl
     from test_gpu_e2e import E2ECase, rel_err
@@ -149,7 +151,7 @@ def test_phase_cut_backward(dev, name, cap):
     f = load(name)
     c = None if cap is None else granule_cap(f)
     runs = []
-    for split in (False, True):
+    for split in (False, False, True):
         case = E2ECase(f, dev)
         rays = case.gen(case.coords)
         cuts = None
@@ -177,13 +179,14 @@ def test_phase_cut_backward(dev, name, cap):
         grads.update({f"pose:{k}": p.grad.detach().cpu().clone() for k, p in case.pose.named_parameters()
                       if p.grad is not None})
         runs.append((float(total), {m: outs[m][m].detach().cpu().clone() for m in case.mods}, grads, phase1))
-    (l0, o0, g0, _), (l1, o1, g1, p1) = runs
+    (l0, o0, g0, _), (_, _, gn, _), (l1, o1, g1, p1) = runs
     assert abs(l0 - l1) <= 1e-6 * abs(l0)
     for m in o0:
         assert rel_err(o1[m], o0[m]) < 1e-6, m
     assert g0.keys() == g1.keys()
     for k in g0:
-        assert rel_err(g1[k], g0[k]) < 1e-4, (k, rel_err(g1[k], g0[k]))
+        noise = rel_err(gn[k], g0[k])          # two single backwards: float-atomic order alone
+        assert rel_err(g1[k], g0[k]) < max(1e-4, 4.0 * noise), (k, rel_err(g1[k], g0[k]), noise)
     for k, g in p1.items():
         if k.startswith("surface_model."):
             assert g is None or float(g.abs().max()) == 0.0, k       # the SDF table: phase 2
