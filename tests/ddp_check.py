@@ -1,6 +1,7 @@
 """Two-rank check of the real data-parallel training paths, run by tests/test_gpu_ddp.py as
-``python -m torch.distributed.run --nproc-per-node 2 tests/ddp_check.py <out.json>`` (both ranks on cuda:0, gloo
-collectives: RCCL needs one GPU per rank).  Not a pytest module.
+``python -m torch.distributed.run --nproc-per-node 2 tests/ddp_check.py <out.json> [precision]`` (both ranks on
+cuda:0, gloo collectives: RCCL needs one GPU per rank; precision: a functions.PRESETS name, fp32 by default).  Not a
+pytest module.
 
 0. GraphTrainer(ddp) x 5 (graph replays: the radiance and background tables' all-reduce launched after the backward's
    first phase, overlapping the SDF backward graph, the SDF table's after the second, overlapping the deferred weight
@@ -34,6 +35,7 @@ def main():
     import faulthandler
     faulthandler.enable()
     out_path = sys.argv[1]
+    precision = sys.argv[2] if len(sys.argv) > 2 else "fp32"
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
@@ -42,7 +44,7 @@ def main():
     from multimodalstudio_amd import functions as fx
     from multimodalstudio_amd.graphs import GraphTrainer
     from multimodalstudio_amd.pipeline import TrainConfig, Trainer
-    fx.set_precision("fp32")
+    fx.set_precision(precision)
     # config 5's method: three hash tables (surface, radiance, grid background) -- the radiance and background tables'
     # all-reduce goes out after the backward's first phase, the surface table's after its second
     cfg = TrainConfig(method="grid_raw_grid_bg_unbalanced", modalities=("rgb", "polarization"),

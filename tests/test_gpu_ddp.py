@@ -13,7 +13,16 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def test_two_rank_training(tmp_path):
+def _bench_default():
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    return bench.DEFAULT_PRECISION
+
+
+@pytest.mark.parametrize("precision", ["fp32", _bench_default()])
+def test_two_rank_training(tmp_path, precision):
+    """fp32 and the benchmarked preset (its fp16 weight-gradient launches deferred into the third graph, the fp16
+    panels they read made in the first two)."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -21,7 +30,7 @@ def test_two_rank_training(tmp_path):
     out = tmp_path / "ddp.json"
     env = dict(os.environ, OMP_NUM_THREADS="4")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(HERE, "ddp_check.py"), str(out)]
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(HERE, "ddp_check.py"), str(out), precision]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     ranks = "\n".join(l for l in r.stderr.splitlines() if l.startswith("[rank"))
     assert r.returncode == 0, r.stdout[-2000:] + ranks[-6000:]
