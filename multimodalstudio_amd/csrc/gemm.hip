@@ -25,6 +25,7 @@
 #include "common.h"
 
 #include <type_traits>
+#include <utility>
 
 // Diagnostic ablation builds only (scripts/gemm_ablate.py compiles them separately; the product library is
 // built with 0): bit 0 drops the epilogue stores, bit 1 the MFMAs, bit 2 the global loads.
@@ -481,6 +482,18 @@ struct WideGroup {
                      // instead of adding it to C with float atomics
 };
 
+#ifndef MMS_WIDE_DEPTH16
+#define MMS_WIDE_DEPTH16 3   // register sets of the fp16 items' pipeline (split-bf16x3 items: 2)
+#endif
+template <typename F, int... I>
+__device__ __forceinline__ void wide_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void wide_for(F&& f) {   // f(integral_constant<i>) for i < N, unrolled
+  wide_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 __device__ __forceinline__ float4 ld_f4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ uint2 ld_u2(const unsigned short* p) { return *reinterpret_cast<const uint2*>(p); }
 
@@ -555,8 +568,11 @@ __device__ __forceinline__ void wide_block(const WideItem& t, int id, float* par
   // two register sets: stage s + 2's loads are issued before stage s's MFMAs, and stage s + 1's image stores sit in
   // the same basic block as those MFMAs (no branch between them), so the scheduler can interleave the conversions and
   // LDS writes with the MFMAs and one whole stage of MFMA time covers each load's latency
-  float4 rset[2][2][NLD];
-  int nset[2] = {0, 0};
+  // DEPTH register sets: stage s + DEPTH's loads are issued at stage s (the fp16 items' short stages need more loads
+  // in flight than split-bf16x3's: their global loads were half the launch time, MMS_WIDE_ABLATE=4 A/B)
+  constexpr int DEPTH = PREC == P_F16 ? MMS_WIDE_DEPTH16 : 2;
+  float4 rset[DEPTH][2][NLD];
+  int nset[DEPTH] = {};
   auto load2 = [&](int s, auto setc) {
     constexpr int Q = decltype(setc)::value;
     const int64_t r0 = kbeg + (int64_t)s * kWK;
@@ -701,29 +717,26 @@ __device__ __forceinline__ void wide_block(const WideItem& t, int id, float* par
   };
   const int S = (int)((kend - kbeg + kWK - 1) / kWK);
 #if MMS_WIDE_PIPE
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
   if (S > 0) {
-    load2(0, I0{});
+    load2(0, std::integral_constant<int, 0>{});
     store_from(0, rset[0][0], rset[0][1], nset[0]);
-    load2(1, I1{});
+    wide_for<DEPTH - 1>([&](auto dc) { load2(decltype(dc)::value + 1, std::integral_constant<int, decltype(dc)::value + 1>{}); });
   }
   __syncthreads();
   // one branch per wave for the whole loop: a wave whose tiles are all active runs the branch-free body (its MFMAs,
   // conversions and LDS stores one basic block the scheduler interleaves)
   auto loop = [&](auto allc) {
-    for (int s = 0; s < S; s += 2) {
-      // even stage s: set 1 holds stage s + 1; set 0 takes stage s + 2
-      load2(s + 2, I0{});
-      compute(0, allc);
-      store_from(1, rset[1][0], rset[1][1], nset[1]);
-      __syncthreads();
-      if (s + 1 >= S) break;
-      // odd stage s + 1: set 0 holds stage s + 2; set 1 takes stage s + 3
-      load2(s + 3, I1{});
-      compute(1, allc);
-      store_from(0, rset[0][0], rset[0][1], nset[0]);
-      __syncthreads();
+    for (int s = 0; s < S; s += DEPTH) {
+      // stage s + j: set j held it (already in LDS buffer (s + j) & 1) and takes stage s + j + DEPTH; set (j + 1) % DEPTH
+      // holds stage s + j + 1, stored into buffer (s + j + 1) & 1 (s, S block-uniform: every thread skips alike)
+      wide_for<DEPTH>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, jn = (j + 1) % DEPTH;
+        if (s + j >= S) return;
+        load2(s + j + DEPTH, std::integral_constant<int, j>{});
+        compute((s + j) & 1, allc);
+        store_from((s + j + 1) & 1, rset[jn][0], rset[jn][1], nset[jn]);
+        __syncthreads();
+      });
     }
   };
   const bool all_act = act_i[0] && act_i[1] && act_j[0] && act_j[1] && act_j[2] && act_j[3];
@@ -790,7 +803,8 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
     id -= g.it[ii].blocks;
     ++ii;
   }
-  const WideItem& t = g.it[ii];
+  // (a copy: the item's fields in registers once, not re-read from the kernel arguments inside the stage loop)
+  const WideItem t = g.it[ii];
   float* part = g.ws != nullptr ? g.ws + (int64_t)blockIdx.x * (kWT * kWT) : nullptr;
   if constexpr (PREC == P_F16) {
     if (t.ainv != nullptr) {
