@@ -482,8 +482,14 @@ struct WideGroup {
                      // instead of adding it to C with float atomics
 };
 
+// the fp16 items' stages: 32 rows (2 images of 32 rows in the LDS split bf16x3's 4 images of 16 take; one barrier per
+// 32 rows; 0.141 -> 0.138 ms per launch, 3 x 2 A/B) with two register sets (16-row stages with 2, 3 or 4 sets measured
+// equal: the loads are not latency-bound)
+#ifndef MMS_WIDE_WK16
+#define MMS_WIDE_WK16 32
+#endif
 #ifndef MMS_WIDE_DEPTH16
-#define MMS_WIDE_DEPTH16 3   // register sets of the fp16 items' pipeline (split-bf16x3 items: 2)
+#define MMS_WIDE_DEPTH16 2   // register sets of the fp16 items' pipeline (split-bf16x3 items: 2)
 #endif
 template <typename F, int... I>
 __device__ __forceinline__ void wide_for_impl(F&& f, std::integer_sequence<int, I...>) {
@@ -501,12 +507,12 @@ __device__ __forceinline__ uint2 ld_u2(const unsigned short* p) { return *reinte
 // A rows, see WideItem); B16: fp16 B rows (their values widened exactly, then split or scaled like fp32 rows).  lds:
 // the kernel's image buffers, scs: [8][256] floats.
 template <int PREC, int WK, bool B16>
-__device__ __forceinline__ void wide_block(const WideItem& t, int id, float* part, __bf16 (*lds)[4 * WK * kWLD],
-                                           float (*scs)[kWT]) {
+__device__ __forceinline__ void wide_block(const WideItem& t, int id, float* part, __bf16* lds, float (*scs)[kWT]) {
   constexpr int kWK = WK;             // rows per stage (16 or 32)
   constexpr int NLD = WK / 8;         // float4 loads per thread per operand and stage
   constexpr int NIMG = PREC == P_BF16X3 ? 2 : 1;
   constexpr int IMG = kWK * kWLD;                        // elements per image
+  constexpr int BUF = 2 * NIMG * IMG;                     // elements per image set (A hi, (A lo), B hi, (B lo))
   // P_F16 (mms_gemm_tn_wide16): A = fp16 dZ rows in their row scale (1 / ainv[k]), rescaled per row by
   // ainv[k] 2^(14 - emax) <= 1 to the launch's common scale 2^(14 - emax) and rounded to fp16 again, B = X rounded to
   // fp16; the common factor is undone on the accumulators before they are added to C; one fp16 MFMA per product, one
@@ -619,7 +625,7 @@ __device__ __forceinline__ void wide_block(const WideItem& t, int id, float* par
   };
   auto store_from = [&](int buf, const float4* xa, const float4* xb, int nr) {
     if constexpr ((MMS_WIDE_ABLATE & 8) != 0) return;
-    __bf16* base = &lds[buf][0];
+    __bf16* base = lds + buf * BUF;
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       const bool ok = w + 8 * i < nr;
@@ -676,8 +682,8 @@ __device__ __forceinline__ void wide_block(const WideItem& t, int id, float* par
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx16{};
   auto compute = [&](int buf, auto allc) {
     constexpr bool ALL = decltype(allc)::value;   // every wave-tile active: no per-tile branches around the MFMAs
-    const __bf16* Ai = &lds[buf][0];
-    const __bf16* Bi = &lds[buf][NIMG * IMG];
+    const __bf16* Ai = lds + buf * BUF;
+    const __bf16* Bi = lds + buf * BUF + NIMG * IMG;
 #pragma unroll
     for (int ks = 0; ks < kWK; ks += 16) {
       bf16x8 ah[2], al[2], bh[4], bl[4];
@@ -793,7 +799,7 @@ __device__ __forceinline__ void wide_block(const WideItem& t, int id, float* par
 }
 
 // P_F16 launches (mms_gemm_tn_wide16) mix modes per item: fp16 A rows (ainv set) run P_F16, fp32 A rows split bf16x3;
-// B rows fp16 or fp32 per item.  The image buffers are sized for split bf16x3 (4 images).
+// B rows fp16 or fp32 per item.  The image buffers are sized for split bf16x3 (4 images of WK rows = 2 of 2 WK).
 template <int PREC, int WK>
 __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[2][4 * WK * kWLD];   // [buffer][A hi, (A lo), B hi, (B lo)]
@@ -808,14 +814,15 @@ __global__ __launch_bounds__(512) void gemm_tn_wide_kernel(WideGroup g) {
   float* part = g.ws != nullptr ? g.ws + (int64_t)blockIdx.x * (kWT * kWT) : nullptr;
   if constexpr (PREC == P_F16) {
     if (t.ainv != nullptr) {
-      if (t.b16) wide_block<P_F16, WK, true>(t, id, part, lds, scs);
-      else wide_block<P_F16, WK, false>(t, id, part, lds, scs);
+      // (MMS_WIDE_WK16 rows per stage for the fp16 items: the same LDS holds 2 images of 2 WK rows)
+      if (t.b16) wide_block<P_F16, MMS_WIDE_WK16, true>(t, id, part, &lds[0][0], scs);
+      else wide_block<P_F16, MMS_WIDE_WK16, false>(t, id, part, &lds[0][0], scs);
     } else {
-      if (t.b16) wide_block<P_BF16X3, WK, true>(t, id, part, lds, scs);
-      else wide_block<P_BF16X3, WK, false>(t, id, part, lds, scs);
+      if (t.b16) wide_block<P_BF16X3, WK, true>(t, id, part, &lds[0][0], scs);
+      else wide_block<P_BF16X3, WK, false>(t, id, part, &lds[0][0], scs);
     }
   } else {
-    wide_block<PREC, WK, false>(t, id, part, lds, scs);
+    wide_block<PREC, WK, false>(t, id, part, &lds[0][0], scs);
   }
 }
 

@@ -35,6 +35,7 @@ VARIANTS = {  # name: (translation unit, macro definitions)
 # 8 no LDS image stores; results wrong, timing only -- round 6's fp16 mixed launch)
 VARIANTS.update({f"wabl{n}": ("gemm", {"MMS_WIDE_ABLATE": n}) for n in (2, 4, 8, 12)})
 VARIANTS.update({f"wd{n}": ("gemm", {"MMS_WIDE_DEPTH16": n}) for n in (2, 4)})   # the fp16 items' register sets
+VARIANTS["wk16"] = ("gemm", {"MMS_WIDE_WK16": 16, "MMS_WIDE_DEPTH16": 3})   # 16-row stages for the fp16 items
 # the backward epilogue's ablations on the stamp build (MMS_CHAIN_EPI_ABL bits: 1 no Y loads, 2 no dZ stores, 4 no
 # scratch round trips)
 VARIANTS.update({f"stampsE{n}": ("mlp_chain", {"MMS_CHAIN_STAMPS": 1, "MMS_CHAIN_EPI_ABL": n}) for n in (1, 2, 4, 3, 7)})
