@@ -985,16 +985,21 @@ MMS_EXPORT int mms_gemm_tn_grouped(int prec, int n, const int64_t* M, const int6
 
 namespace {
 
+// a split-bf16x3 item's per-row cost beside fp16 items, relative to its bytes' share (with 32-row fp16 stages, same-box
+// step A/B 1.2 / 1.5 / 2.0: 3.150 / 3.167 / 3.176 ms; with 16-row stages 1.5 was best for the launch alone)
+#ifndef MMS_WIDE_X3COST
+#define MMS_WIDE_X3COST 1.2
+#endif
 // K slices of each item (g.it[0 .. g.n) with M, N, K set) in proportion to its share of the work -- tiles x rows x the
 // operand bytes per row element (the kernel streams its operands from HBM) -- so every block takes about the same time
 // (>= 1024 rows per slice); returns the total block count
 int64_t plan_wide(WideGroup& g, int target_blocks) {
   if (target_blocks < 1) target_blocks = 256;
-  // (a split-bf16x3 item's rows cost 1.5x their bytes' share beside fp16 items: its three MFMAs and four images per
-  // product; fast_h16d A/B, 1.0 / 1.5 / 2.2: the launch 154 / 141 / 143 us)
+  // (a split-bf16x3 item's rows cost more than their bytes' share beside fp16 items: its three MFMAs and four images
+  // per product; 16-row fp16 stages, A/B 1.0 / 1.5 / 2.2: the launch 154 / 141 / 143 us)
   auto cost = [](const WideItem& t) {
     return (double)((t.M + kWT - 1) / kWT) * ((t.N + kWT - 1) / kWT) * (double)t.K *
-           ((t.ainv ? 2.0 : 4.0) + (t.b16 ? 2.0 : 4.0)) * (t.ainv ? 1.0 : 1.5);
+           ((t.ainv ? 2.0 : 4.0) + (t.b16 ? 2.0 : 4.0)) * (t.ainv ? 1.0 : MMS_WIDE_X3COST);
   };
   double work = 0.0;
   for (int i = 0; i < g.n; ++i) work += cost(g.it[i]);
