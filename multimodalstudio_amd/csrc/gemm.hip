@@ -986,7 +986,8 @@ MMS_EXPORT int mms_gemm_tn_grouped(int prec, int n, const int64_t* M, const int6
 namespace {
 
 // a split-bf16x3 item's per-row cost beside fp16 items, relative to its bytes' share (with 32-row fp16 stages, same-box
-// step A/B 1.2 / 1.5 / 2.0: 3.150 / 3.167 / 3.176 ms; with 16-row stages 1.5 was best for the launch alone)
+// step A/B 1.0 / 1.2 / 1.5 / 2.0: 3.155 / 3.146-3.150 / 3.167 / 3.176 ms; with 16-row stages 1.5 was best for the launch
+// alone; 320 blocks instead of 256: 3.213 ms)
 #ifndef MMS_WIDE_X3COST
 #define MMS_WIDE_X3COST 1.2
 #endif

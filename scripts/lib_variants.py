@@ -36,7 +36,7 @@ VARIANTS = {  # name: (translation unit, macro definitions)
 VARIANTS.update({f"wabl{n}": ("gemm", {"MMS_WIDE_ABLATE": n}) for n in (2, 4, 8, 12)})
 VARIANTS.update({f"wd{n}": ("gemm", {"MMS_WIDE_DEPTH16": n}) for n in (2, 4)})   # the fp16 items' register sets
 VARIANTS["wk16"] = ("gemm", {"MMS_WIDE_WK16": 16, "MMS_WIDE_DEPTH16": 3})   # 16-row stages for the fp16 items
-VARIANTS.update({f"x3c{int(10 * c)}": ("gemm", {"MMS_WIDE_X3COST": c}) for c in (1.5, 2.0)})   # slice cost weights
+VARIANTS.update({f"x3c{int(10 * c)}": ("gemm", {"MMS_WIDE_X3COST": c}) for c in (1.0, 1.5, 2.0)})   # slice cost weights
 # the backward epilogue's ablations on the stamp build (MMS_CHAIN_EPI_ABL bits: 1 no Y loads, 2 no dZ stores, 4 no
 # scratch round trips)
 VARIANTS.update({f"stampsE{n}": ("mlp_chain", {"MMS_CHAIN_STAMPS": 1, "MMS_CHAIN_EPI_ABL": n}) for n in (1, 2, 4, 3, 7)})
